@@ -1,0 +1,294 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X checksum path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
+
+One step = one pass of the element over one device-resident batch
+(inputs generated in HBM before timing).  Default workload C3: SetUDPChecksum
+over 16M x 1500 B UDP/IPv4 packets in 1536 B slots per GPU; the 64 B
+min-size batch (C2: SetIPChecksum over 16M packets in 64 B slots) is measured
+in the same run and reported under "c2_64b" because the metric names both.
+Multi-GPU (torchrun, one process per GPU): every rank generates and
+processes its own shard of global packet indices -- packets are independent,
+so there is no collective in the data path (weak scaling); one RCCL
+all-reduce after the timed region takes the max time and a result digest.
+
+Rank 0 prints ONE JSON line.  roofline.achieved = algorithmic bytes per
+launch / mean kernel time from HIP events recorded on the stream the kernel
+runs on; roofline.traffic = HBM bytes per launch from the committed
+rocprofv3 PMC summary (profiles/pmc_<workload>.json) when present.
+cpu_baseline: the oracle restatement of lib/in_cksum.c + the element (-O2 -g)
+on the host cores, on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s checksummed (device-resident) + Mpps, 64B and 1500B packet batches"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+GIB = float(1 << 30)
+
+# workload: (proto, element, packet bytes L, slot stride, packets per GPU,
+#            bytes "checksummed" per packet (metric), algorithmic HBM bytes per packet)
+WORKLOADS = {
+    "c3": dict(proto=17, element="SetUDPChecksum", L=1500, stride=1536, n=16 << 20, ck=1500, alg=1500 + 2 + 1,
+               desc="C3: SetUDPChecksum, 1500 B UDP/IPv4 packets, 16M-packet batch per GPU, 1536 B slots"),
+    "c2": dict(proto=17, element="SetIPChecksum", L=46, stride=64, n=16 << 20, ck=20, alg=20 + 2 + 1,
+               desc="C2: SetIPChecksum, 64 B min-size slots (IP length 46), 16M-packet batch per GPU"),
+    "c5": dict(proto=6, element="SetTCPChecksum", L=9000, stride=9024, n=16 << 20, ck=9000, alg=9000 + 2 + 1,
+               desc="C5: SetTCPChecksum, 9000 B jumbo TCP/IPv4, 16M packets per GPU (128M over 8 GPUs)"),
+    "c4": dict(proto=17, element="SetUDPChecksum", L=0, stride=0, n=64 << 20, ck=None, alg=None,
+               desc="C4: SetUDPChecksum, IMIX 64/576/1500 (7:4:1), 64M packets, 64 B-aligned packing"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def imix_layout(torch, n, seed, first_idx):
+    """Packet sizes 64/576/1500 with P = 7/12, 4/12, 1/12 by hash; packed at
+    64 B-aligned offsets.  Returns (off int64, len int32, arena bytes, sum L)."""
+    import numpy as np
+    i = np.arange(first_idx, first_idx + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = i * np.uint64(0x9E3779B97F4A7C15) + np.uint64(seed)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+    r = (x % np.uint64(12)).astype(np.int64)
+    L = np.where(r < 7, 64, np.where(r < 11, 576, 1500)).astype(np.int64)
+    slot = (L + 63) // 64 * 64
+    off = np.zeros(n, np.int64)
+    np.cumsum(slot[:-1], out=off[1:])
+    total = int(off[-1] + slot[-1])
+    return (torch.from_numpy(off).cuda(), torch.from_numpy(L.astype(np.int32)).cuda(), total, int(L.sum()))
+
+
+def run_element(ctx, w, b, status):
+    if w["element"] == "SetUDPChecksum":
+        ctx.set_udp_checksum(b, status=status, want_sums=False)
+    elif w["element"] == "SetTCPChecksum":
+        ctx.set_tcp_checksum(b, status=status, want_sums=False)
+    elif w["element"] == "SetIPChecksum":
+        ctx.set_ip_checksum(b, status=status, want_sums=False)
+    else:
+        raise ValueError(w["element"])
+
+
+def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
+    """Generate the shard, run warmup + timed steps; returns a dict."""
+    import click_amd
+    w = dict(WORKLOADS[wname])
+    n = w["n"]
+    first = rank * n
+    if wname == "c4":
+        off, ln, total, sum_l = imix_layout(torch, n, seed, first)
+        arena = torch.empty(total, dtype=torch.uint8, device="cuda")
+        b = click_amd.Batch(arena, n, off=off, length=ln, max_len=1500)
+        ck_bytes = sum_l
+        alg_bytes = sum_l + 3 * n + 12 * n      # + field write + status + descriptor (off u64, len u32)
+    else:
+        arena = torch.empty(n * w["stride"], dtype=torch.uint8, device="cuda")
+        b = click_amd.Batch(arena, n, stride=w["stride"], fixed_len=w["L"])
+        ck_bytes = w["ck"] * n
+        alg_bytes = w["alg"] * n
+    status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ctx.gen_packets(b, proto=w["proto"], seed=seed, first_idx=first)
+    ctx.set_ip_checksum(b, status=status, want_sums=False)
+    stream = torch.cuda.current_stream()
+    for _ in range(warmup):
+        run_element(ctx, w, b, status)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        run_element(ctx, w, b, status)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    kms = [a.elapsed_time(z) for a, z in ev]
+    kernel_ms = sum(kms) / len(kms)
+    ok = int(ctx.count_codes(status)[0])
+    res = dict(wall=wall, kernel_ms=kernel_ms, kernel_ms_min=min(kms), n=n, ck_bytes=ck_bytes,
+               alg_bytes=alg_bytes, ok=ok, w=w)
+    if dist:
+        t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        d = torch.tensor([ok, n], dtype=torch.int64, device="cuda")
+        dist.all_reduce(d, op=dist.ReduceOp.SUM)
+        res["wall"], res["kernel_ms"] = float(t[0]), float(t[1])
+        res["ok_total"], res["n_total"] = int(d[0]), int(d[1])
+    else:
+        res["ok_total"], res["n_total"] = ok, n
+    del arena, status, b
+    torch.cuda.empty_cache()
+    return res
+
+
+def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5):
+    """Measured HBM read-stream ceiling (16 B loads, grid-stride)."""
+    buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    buf.fill_(1)
+    out = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.read_stream(buf, out=out)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = 1e30
+    for _ in range(reps):
+        s.record()
+        ctx.read_stream(buf, out=out)
+        e.record()
+        torch.cuda.synchronize()
+        best = min(best, s.elapsed_time(e))
+    del buf
+    torch.cuda.empty_cache()
+    return nbytes / (best * 1e-3) / 1e9
+
+
+def cpu_baseline(wname, seconds=8.0):
+    """Oracle (restated lib/in_cksum.c + element, -O2 -g) over a bounded
+    sample of the same workload, on the host cores; single thread and
+    `threads` threads on disjoint shards."""
+    import numpy as np
+    from tests import oracle_lib
+    w = WORKLOADS[wname]
+    L_ = oracle_lib.load_oracle()
+    op = {"SetUDPChecksum": oracle_lib.OP_SET_UDP, "SetTCPChecksum": oracle_lib.OP_SET_TCP,
+          "SetIPChecksum": oracle_lib.OP_SET_IP}[w["element"]]
+    n = max(1, min(w["n"], (256 << 20) // w["stride"]))      # <= 256 MB sample
+    arena = np.zeros(n * w["stride"], np.uint8)
+    oracle_lib.gen(arena, n, stride=w["stride"], fixed_len=w["L"], proto=w["proto"])
+    oracle_lib.batch("set_ip", arena, n, stride=w["stride"], fixed_len=w["L"])
+    ptr = arena.ctypes.data
+    L_.oracle_bench(op, ptr, w["stride"], w["L"], n, 1, 1)                 # warm
+    one = L_.oracle_bench(op, ptr, w["stride"], w["L"], n, 1, 1)
+    reps1 = max(1, int(seconds / 2 / max(one, 1e-6)))
+    t1 = L_.oracle_bench(op, ptr, w["stride"], w["L"], n, reps1, 1)
+    threads = int(os.environ.get("CLK_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    tn_one = L_.oracle_bench(op, ptr, w["stride"], w["L"], n, 1, threads)
+    repsn = max(1, int(seconds / 2 / max(tn_one, 1e-6)))
+    tn = L_.oracle_bench(op, ptr, w["stride"], w["L"], n, repsn, threads)
+    pk1 = n * reps1 / t1
+    pkn = n * repsn / tn
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {
+        "value": round(pkn * w["ck"] / GIB, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "mpps": round(pkn / 1e6, 3),
+        "single_thread": {"value": round(pk1 * w["ck"] / GIB, 3), "mpps": round(pk1 / 1e6, 3), "cores": 1},
+        "sample": "%d x %d B packets (%s, %d B slots) in host DRAM, %d+%d passes; oracle/cksum_oracle.c -O2 -g"
+                  % (n, w["L"], w["element"], w["stride"], reps1, repsn),
+        "cpu": model,
+    }
+
+
+def load_traffic(wname):
+    p = os.path.join(ROOT, "profiles", "pmc_%s.json" % wname)
+    try:
+        with open(p) as f:
+            d = json.load(f)
+        return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+    except (OSError, ValueError):
+        return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--no-c2", action="store_true", help="skip the extra 64 B (C2) measurement")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--no-peak", action="store_true", help="skip the read-stream ceiling")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    args = ap.parse_args()
+
+    import torch
+    import click_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    ctx = click_amd.Context(local)
+
+    main_res = measure(torch, ctx, dist, rank, world, args.workload, args.steps, args.warmup)
+    c2 = None
+    if args.workload != "c2" and not args.no_c2:
+        c2 = measure(torch, ctx, dist, rank, world, "c2", args.steps, args.warmup)
+    peak_meas = None if args.no_peak else read_stream_peak(torch, ctx)
+
+    if rank == 0:
+        r = main_res
+        w = r["w"]
+        n_total = r["n_total"]
+        step_s = r["wall"] / args.steps
+        pps = n_total / step_s
+        value = pps * (r["ck_bytes"] / r["n"]) / GIB
+        achieved = r["alg_bytes"] / (r["kernel_ms"] * 1e-3) / 1e9
+        traffic, traffic_src = load_traffic(args.workload)
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s",
+            "mpps": round(pps / 1e6, 1),
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic (splitmix64 packets generated in HBM)",
+            "config": {"workload": w["desc"], "element": w["element"], "packets_per_gpu": r["n"],
+                       "packet_bytes": w["L"] or "imix", "slot_bytes": w["stride"] or "64B-aligned",
+                       "parallelism": "dp%d (disjoint packet shards, no data-path collective)" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel_ms": round(r["kernel_ms"], 4), "kernel_ms_min": round(r["kernel_ms_min"], 4),
+                         "alg_bytes_per_launch": r["alg_bytes"], "traffic_source": traffic_src,
+                         "read_stream_measured_GBs": round(peak_meas, 1) if peak_meas else None},
+            "verify": {"ok": r["ok_total"], "packets": n_total},
+        }
+        if c2:
+            s2 = c2["wall"] / args.steps
+            pps2 = c2["n_total"] / s2
+            a2 = c2["alg_bytes"] / (c2["kernel_ms"] * 1e-3) / 1e9
+            t2, t2src = load_traffic("c2")
+            line["c2_64b"] = {"workload": c2["w"]["desc"], "mpps": round(pps2 / 1e6, 1),
+                              "value": round(pps2 * 20 / GIB, 2), "unit": "GiB/s (20 B IP header per packet)",
+                              "ms_per_step": round(s2 * 1e3, 4), "kernel_ms": round(c2["kernel_ms"], 4),
+                              "roofline": {"bound": "hbm", "achieved": round(a2, 1), "peak": HBM_PEAK_GBS,
+                                           "unit": "GB/s", "frac": round(a2 / HBM_PEAK_GBS, 4),
+                                           "slot_GBs": round((64 + 3) * c2["n"] / (c2["kernel_ms"] * 1e-3) / 1e9, 1),
+                                           "traffic": t2, "traffic_source": t2src},
+                              "verify": {"ok": c2["ok_total"], "packets": c2["n_total"]}}
+        if world == 1 and not args.no_cpu and args.workload != "c4":
+            try:
+                line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)
+            except Exception as e:        # reported, not fatal
+                line["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

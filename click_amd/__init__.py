@@ -1,0 +1,196 @@
+"""click_amd -- MI355X (gfx950) HIP implementation of Click's Internet-checksum path.
+
+The product is the C ABI in include/click_amd_cksum.h, implemented by the
+hand-written kernels in click_amd/csrc and built into
+click_amd/libclick_amd_cksum.so.  This package is the thin Python host side
+over that ABI: torch provides device memory and streams (plumbing only).
+
+    ctx = click_amd.Context(0)
+    b = click_amd.Batch(arena, stride=1536, fixed_len=1500, n=N)
+    status, sums = ctx.set_udp_checksum(b)
+
+There is no CPU fallback: every call goes to the HIP library and raises
+ClickAmdError when the library reports an error.
+"""
+from . import _abi
+from ._abi import (CLK_OK, CLK_IP_MINISCULE_PACKET, CLK_IP_BAD_VERSION, CLK_IP_BAD_HLEN,  # noqa: F401
+                   CLK_IP_BAD_IP_LEN, CLK_IP_BAD_CHECKSUM, CLK_IP_BAD_SADDR, CLK_L4_NOT_PROTO,
+                   CLK_L4_BAD_LENGTH, CLK_L4_BAD_CHECKSUM, CLK_SET_OK, CLK_SET_OUTPUT1, CLK_SET_KILL)
+import ctypes
+
+__all__ = ["Context", "Batch", "ClickAmdError", "lib"]
+
+
+class ClickAmdError(RuntimeError):
+    pass
+
+
+def lib():
+    return _abi.load()
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+class Batch:
+    """Struct-of-arrays packet batch resident on the device.
+
+    base: uint8 device tensor (the byte arena); off: int64/uint64 device
+    tensor of byte offsets or None (then packet i is at i*stride); length:
+    int32/uint32 device tensor or None (then every packet has fixed_len
+    bytes).  See clk_batch in include/click_amd_cksum.h."""
+
+    def __init__(self, base, n, stride=0, fixed_len=0, off=None, length=None, max_len=0):
+        self.base, self.off, self.length = base, off, length
+        self.n, self.stride, self.fixed_len, self.max_len = int(n), int(stride), int(fixed_len), int(max_len)
+        if n and off is None and stride and (n - 1) * stride + fixed_len > base.numel():
+            raise ValueError("batch exceeds its arena")
+
+    def c(self):
+        b = _abi.clk_batch()
+        b.base = self.base.data_ptr() if self.base is not None else None
+        b.off = self.off.data_ptr() if self.off is not None else None
+        b.stride = self.stride
+        b.len = self.length.data_ptr() if self.length is not None else None
+        b.fixed_len = self.fixed_len
+        b.max_len = self.max_len
+        b.n = self.n
+        return b
+
+
+class Context:
+    """One clk_ctx (device + HIP stream).  Not re-entrant; one per thread.
+
+    stream: "torch" (default) launches on torch's current stream of the
+    device, so the kernels are ordered with the torch ops that fill and read
+    the tensors; "own" uses the context's own non-blocking stream; or any
+    torch stream / raw hipStream_t handle."""
+
+    def __init__(self, device=0, stream="torch"):
+        import torch
+        self._torch = torch
+        self.lib = lib()
+        self.device = device
+        h = ctypes.c_void_p()
+        self._check(self.lib.clk_ctx_create(device, ctypes.byref(h)), None)
+        self.h = h
+        if isinstance(stream, str) and stream == "torch":
+            stream = torch.cuda.current_stream(device)
+        if not (isinstance(stream, str) and stream == "own"):
+            self.set_stream(stream)
+
+    def _check(self, rc, h=True):
+        if rc != 0:
+            msg = self.lib.clk_last_error(self.h if h else None)
+            raise ClickAmdError("click_amd error %d: %s" % (rc, (msg or b"").decode()))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.clk_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- streams ---------------------------------------------------------------
+    def set_stream(self, stream):
+        """stream: a torch.cuda.Stream / ExternalStream, a raw handle, or None
+        (HIP's null stream)."""
+        raw = getattr(stream, "cuda_stream", stream)
+        self._check(self.lib.clk_ctx_set_stream(self.h, ctypes.c_void_p(raw) if raw else None))
+
+    def use_own_stream(self):
+        self._check(self.lib.clk_ctx_set_stream(self.h, self.lib.clk_ctx_own_stream(self.h)))
+
+    def stream_handle(self):
+        return self.lib.clk_ctx_stream(self.h)
+
+    def torch_stream(self):
+        return self._torch.cuda.ExternalStream(self.stream_handle(), device="cuda:%d" % self.device)
+
+    def sync(self):
+        self._check(self.lib.clk_ctx_sync(self.h))
+
+    # -- helpers ---------------------------------------------------------------
+    def _out(self, n, dtype):
+        return self._torch.empty(max(n, 1), dtype=dtype, device="cuda:%d" % self.device)
+
+    # -- checksum path (include/click_amd_cksum.h) -----------------------------
+    def in_cksum(self, b, out=None):
+        out = self._out(b.n, self._torch.uint16) if out is None else out
+        cb = b.c()
+        self._check(self.lib.clk_in_cksum(self.h, ctypes.byref(cb), _ptr(out)))
+        return out[:b.n]
+
+    def check_ip_header(self, b, offset=0, checksum=True, badsrc=None, gooddst=None, out=None):
+        out = self._out(b.n, self._torch.uint8) if out is None else out
+        cfg = _abi.clk_ip_check_cfg()
+        cfg.offset, cfg.checksum = offset, 1 if checksum else 0
+        cfg.badsrc, cfg.nbadsrc = (badsrc.data_ptr(), badsrc.numel()) if badsrc is not None else (None, 0)
+        cfg.gooddst, cfg.ngooddst = (gooddst.data_ptr(), gooddst.numel()) if gooddst is not None else (None, 0)
+        cb = b.c()
+        self._check(self.lib.clk_check_ip_header(self.h, ctypes.byref(cb), ctypes.byref(cfg), _ptr(out)))
+        return out[:b.n]
+
+    def set_ip_checksum(self, b, status=None, sums=None, want_sums=True):
+        status = self._out(b.n, self._torch.uint8) if status is None else status
+        if sums is None and want_sums:
+            sums = self._out(b.n, self._torch.uint16)
+        cb = b.c()
+        self._check(self.lib.clk_set_ip_checksum(self.h, ctypes.byref(cb), _ptr(status), _ptr(sums)))
+        return status[:b.n], (sums[:b.n] if sums is not None else None)
+
+    def check_udp_header(self, b, out=None):
+        out = self._out(b.n, self._torch.uint8) if out is None else out
+        cb = b.c()
+        self._check(self.lib.clk_check_udp_header(self.h, ctypes.byref(cb), _ptr(out)))
+        return out[:b.n]
+
+    def set_udp_checksum(self, b, status=None, sums=None, want_sums=True):
+        status = self._out(b.n, self._torch.uint8) if status is None else status
+        if sums is None and want_sums:
+            sums = self._out(b.n, self._torch.uint16)
+        cb = b.c()
+        self._check(self.lib.clk_set_udp_checksum(self.h, ctypes.byref(cb), _ptr(status), _ptr(sums)))
+        return status[:b.n], (sums[:b.n] if sums is not None else None)
+
+    def check_tcp_header(self, b, out=None):
+        out = self._out(b.n, self._torch.uint8) if out is None else out
+        cb = b.c()
+        self._check(self.lib.clk_check_tcp_header(self.h, ctypes.byref(cb), _ptr(out)))
+        return out[:b.n]
+
+    def set_tcp_checksum(self, b, fixoff=False, status=None, sums=None, want_sums=True):
+        status = self._out(b.n, self._torch.uint8) if status is None else status
+        if sums is None and want_sums:
+            sums = self._out(b.n, self._torch.uint16)
+        cb = b.c()
+        self._check(self.lib.clk_set_tcp_checksum(self.h, ctypes.byref(cb), 1 if fixoff else 0,
+                                                  _ptr(status), _ptr(sums)))
+        return status[:b.n], (sums[:b.n] if sums is not None else None)
+
+    # -- utilities ---------------------------------------------------------------
+    def count_codes(self, codes, ncounts=8, counts=None):
+        if counts is None:
+            counts = self._torch.zeros(ncounts, dtype=self._torch.int64, device="cuda:%d" % self.device)
+        self._check(self.lib.clk_count_codes(self.h, _ptr(codes), codes.numel(), _ptr(counts), ncounts))
+        return counts
+
+    def gen_packets(self, b, proto=17, seed=0x5EED, first_idx=0):
+        cb = b.c()
+        self._check(self.lib.clk_gen_packets(self.h, ctypes.byref(cb), proto, seed, first_idx))
+
+    def gen_corrupt(self, b, seed=0xBAD, rate_log2=10):
+        cb = b.c()
+        self._check(self.lib.clk_gen_corrupt(self.h, ctypes.byref(cb), seed, rate_log2))
+
+    def read_stream(self, t, nbytes=None, out=None):
+        if out is None:
+            out = self._torch.zeros(1, dtype=self._torch.int64, device="cuda:%d" % self.device)
+        nbytes = t.numel() * t.element_size() if nbytes is None else nbytes
+        self._check(self.lib.clk_read_stream(self.h, _ptr(t), nbytes, _ptr(out)))
+        return out

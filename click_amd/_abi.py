@@ -1,0 +1,102 @@
+"""ctypes binding of include/click_amd_cksum.h (the product C ABI).
+
+This is the Python equivalent of the binding a host program adds for the
+library; the Click-side C++ binding is in INTEGRATION.md.  No CPU fallback:
+if the shared library is missing or cannot be loaded this module raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libclick_amd_cksum.so")
+
+# return codes / verdicts (include/click_amd_cksum.h)
+CLK_SUCCESS = 0
+CLK_EINVAL = -1
+CLK_EHIP = -2
+CLK_ENODEV = -3
+
+CLK_OK = 0
+CLK_IP_MINISCULE_PACKET = 1
+CLK_IP_BAD_VERSION = 2
+CLK_IP_BAD_HLEN = 3
+CLK_IP_BAD_IP_LEN = 4
+CLK_IP_BAD_CHECKSUM = 5
+CLK_IP_BAD_SADDR = 6
+CLK_L4_NOT_PROTO = 1
+CLK_L4_BAD_LENGTH = 2
+CLK_L4_BAD_CHECKSUM = 3
+CLK_SET_OK = 0
+CLK_SET_OUTPUT1 = 1
+CLK_SET_KILL = 2
+
+
+class clk_batch(ctypes.Structure):
+    _fields_ = [
+        ("base", ctypes.c_void_p),
+        ("off", ctypes.c_void_p),
+        ("stride", ctypes.c_uint64),
+        ("len", ctypes.c_void_p),
+        ("fixed_len", ctypes.c_uint32),
+        ("max_len", ctypes.c_uint32),
+        ("n", ctypes.c_uint64),
+    ]
+
+
+class clk_ip_check_cfg(ctypes.Structure):
+    _fields_ = [
+        ("offset", ctypes.c_uint32),
+        ("checksum", ctypes.c_int32),
+        ("badsrc", ctypes.c_void_p),
+        ("nbadsrc", ctypes.c_uint32),
+        ("ngooddst", ctypes.c_uint32),
+        ("gooddst", ctypes.c_void_p),
+    ]
+
+
+_P = ctypes.c_void_p
+_BP = ctypes.POINTER(clk_batch)
+
+# name -> (restype, argtypes); every symbol include/click_amd_cksum.h declares
+SIGNATURES = {
+    "clk_abi_version": (ctypes.c_int, []),
+    "clk_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
+    "clk_ctx_destroy": (ctypes.c_int, [_P]),
+    "clk_ctx_set_stream": (ctypes.c_int, [_P, _P]),
+    "clk_ctx_stream": (_P, [_P]),
+    "clk_ctx_own_stream": (_P, [_P]),
+    "clk_ctx_sync": (ctypes.c_int, [_P]),
+    "clk_ctx_device": (ctypes.c_int, [_P]),
+    "clk_last_error": (ctypes.c_char_p, [_P]),
+    "clk_in_cksum": (ctypes.c_int, [_P, _BP, _P]),
+    "clk_check_ip_header": (ctypes.c_int, [_P, _BP, ctypes.POINTER(clk_ip_check_cfg), _P]),
+    "clk_set_ip_checksum": (ctypes.c_int, [_P, _BP, _P, _P]),
+    "clk_check_udp_header": (ctypes.c_int, [_P, _BP, _P]),
+    "clk_set_udp_checksum": (ctypes.c_int, [_P, _BP, _P, _P]),
+    "clk_check_tcp_header": (ctypes.c_int, [_P, _BP, _P]),
+    "clk_set_tcp_checksum": (ctypes.c_int, [_P, _BP, ctypes.c_int, _P, _P]),
+    "clk_count_codes": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P, ctypes.c_uint32]),
+    "clk_gen_packets": (ctypes.c_int, [_P, _BP, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
+    "clk_gen_corrupt": (ctypes.c_int, [_P, _BP, ctypes.c_uint64, ctypes.c_uint32]),
+    "clk_read_stream": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P]),
+}
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load the HIP library (raises OSError if it is missing: no fallback)."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError("click_amd: %s is missing; run `python -m click_amd.build` "
+                      "(there is no CPU fallback)" % path)
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path == LIB_PATH:
+        _lib = lib
+    return lib

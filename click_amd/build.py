@@ -1,0 +1,61 @@
+"""Build the gfx950 shared library (and the test oracle) in-tree.
+
+    python -m click_amd.build            # product library only
+    python -m click_amd.build --oracle   # also oracle/libcksum_oracle.so
+
+The product library is click_amd/libclick_amd_cksum.so: the C ABI of
+include/click_amd_cksum.h over the hand-written kernels in click_amd/csrc.
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "click_amd")
+LIB = os.path.join(PKG, "libclick_amd_cksum.so")
+SOURCES = [os.path.join(PKG, "csrc", "cksum_api.hip")]
+DEPS = SOURCES + [os.path.join(PKG, "csrc", f) for f in ("cksum_kernels.hh", "cksum_device.hh")] + [
+    os.path.join(ROOT, "include", "click_amd_cksum.h")]
+ARCH = "gfx950"
+
+
+def _hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.sep not in c or os.path.exists(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_library(force=False, verbose=False):
+    if not force and not _stale(LIB, DEPS):
+        return LIB
+    cmd = [_hipcc(), "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wall", "-I" + os.path.join(ROOT, "include"), "-o", LIB + ".tmp"] + SOURCES
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+def build_oracle(force=False):
+    odir = os.path.join(ROOT, "oracle")
+    target = os.path.join(odir, "libcksum_oracle.so")
+    deps = [os.path.join(odir, f) for f in ("cksum_oracle.c", "cksum_oracle.h", "Makefile")]
+    if force or _stale(target, deps):
+        subprocess.run(["make", "-s", "-C", odir, "-B" if force else "all"], check=True)
+    return target
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    print(build_library(force=force, verbose=True))
+    if "--oracle" in sys.argv:
+        print(build_oracle(force=force))

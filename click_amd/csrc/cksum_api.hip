@@ -1,0 +1,343 @@
+// cksum_api.hip -- the C ABI (include/click_amd_cksum.h) over the gfx950
+// kernels in cksum_kernels.hh.  Host side: argument checks, geometry
+// selection (lanes per packet), launches on the context's stream.
+#include "cksum_kernels.hh"
+#include "../../include/click_amd_cksum.h"
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+struct clk_ctx {
+    int device;
+    hipStream_t own;
+    hipStream_t cur;
+    int max_blocks;
+    char err[512];
+};
+
+namespace {
+
+thread_local char tls_err[512];
+
+int fail(clk_ctx *ctx, int code, const char *fmt, ...)
+{
+    char *buf = ctx ? ctx->err : tls_err;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, 512, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int hip_fail(clk_ctx *ctx, hipError_t e, const char *what)
+{
+    return fail(ctx, CLK_EHIP, "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+}
+
+int enter(clk_ctx *ctx)
+{
+    if (!ctx)
+        return fail(nullptr, CLK_EINVAL, "null context");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess)
+        return hip_fail(ctx, e, "hipSetDevice");
+    return CLK_SUCCESS;
+}
+
+int check_launch(clk_ctx *ctx, const char *what)
+{
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess)
+        return hip_fail(ctx, e, what);
+    return CLK_SUCCESS;
+}
+
+int check_batch(clk_ctx *ctx, const clk_batch *b, const char *fn)
+{
+    if (!b)
+        return fail(ctx, CLK_EINVAL, "%s: null batch", fn);
+    if (b->n && !b->base)
+        return fail(ctx, CLK_EINVAL, "%s: null batch base", fn);
+    if (b->n && !b->off && b->stride == 0 && b->n > 1)
+        return fail(ctx, CLK_EINVAL, "%s: off == NULL needs a nonzero stride", fn);
+    return CLK_SUCCESS;
+}
+
+clk::BatchArgs args_of(const clk_batch *b)
+{
+    clk::BatchArgs a;
+    a.base = b->base;
+    a.off = b->off;
+    a.stride = b->stride;
+    a.len = b->len;
+    a.fixed_len = b->fixed_len;
+    a.n = b->n;
+    return a;
+}
+
+constexpr int BLOCK = 256;
+constexpr int K = 8;   // 16-byte chunk loads in flight per lane per pass
+
+// Lanes per packet: the fewest (of 1, 4, 16, 64) whose K-deep pass covers
+// the largest packet in one pass; 64 beyond that (multi-pass).
+int pick_group(const clk_batch *b)
+{
+    uint32_t ml = b->len ? b->max_len : b->fixed_len;
+    if (b->len && ml == 0)
+        return 16;
+    const uint64_t nch = (uint64_t)ml / 16 + 2;
+    if (nch <= (uint64_t)K * 1) return 1;
+    if (nch <= (uint64_t)K * 4) return 4;
+    if (nch <= (uint64_t)K * 16) return 16;
+    return 64;
+}
+
+unsigned grid_for(const clk_ctx *ctx, uint64_t threads)
+{
+    uint64_t g = (threads + BLOCK - 1) / BLOCK;
+    if (g > (uint64_t)ctx->max_blocks)
+        g = (uint64_t)ctx->max_blocks;
+    return g ? (unsigned)g : 1u;
+}
+
+template <int G>
+void launch_range(clk_ctx *ctx, const clk_batch *b, uint16_t *out)
+{
+    hipLaunchKernelGGL((clk::range_kernel<G, K>), dim3(grid_for(ctx, b->n * G)), dim3(BLOCK), 0,
+                       ctx->cur, args_of(b), out);
+}
+
+template <int PROTO, bool SET, int G>
+void launch_l4_g(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint16_t *sum)
+{
+    hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K>), dim3(grid_for(ctx, b->n * G)), dim3(BLOCK), 0,
+                       ctx->cur, args_of(b), fixoff, code, sum);
+}
+
+template <int PROTO, bool SET>
+int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint16_t *sum, const char *fn)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, fn))) return r;
+    if (b->n == 0) return CLK_SUCCESS;
+    if (!code) return fail(ctx, CLK_EINVAL, "%s: null output", fn);
+    switch (pick_group(b)) {
+    case 1: launch_l4_g<PROTO, SET, 1>(ctx, b, fixoff, code, sum); break;
+    case 4: launch_l4_g<PROTO, SET, 4>(ctx, b, fixoff, code, sum); break;
+    case 16: launch_l4_g<PROTO, SET, 16>(ctx, b, fixoff, code, sum); break;
+    default: launch_l4_g<PROTO, SET, 64>(ctx, b, fixoff, code, sum); break;
+    }
+    return check_launch(ctx, fn);
+}
+
+bool is_gfx950(int device)
+{
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, device) != hipSuccess)
+        return false;
+    return std::strncmp(p.gcnArchName, "gfx950", 6) == 0;
+}
+
+} // namespace
+
+extern "C" {
+
+int clk_abi_version(void) { return CLK_ABI_VERSION; }
+
+int clk_ctx_create(int device, clk_ctx **out)
+{
+    if (!out)
+        return fail(nullptr, CLK_EINVAL, "clk_ctx_create: null out");
+    *out = nullptr;
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess)
+        return hip_fail(nullptr, e, "hipGetDeviceCount");
+    if (device < 0 || device >= ndev)
+        return fail(nullptr, CLK_ENODEV, "clk_ctx_create: device %d of %d", device, ndev);
+    if (!is_gfx950(device))
+        return fail(nullptr, CLK_ENODEV, "clk_ctx_create: device %d is not gfx950", device);
+    e = hipSetDevice(device);
+    if (e != hipSuccess)
+        return hip_fail(nullptr, e, "hipSetDevice");
+    clk_ctx *c = new (std::nothrow) clk_ctx;
+    if (!c)
+        return fail(nullptr, CLK_EINVAL, "clk_ctx_create: out of memory");
+    c->device = device;
+    c->err[0] = 0;
+    c->max_blocks = 8192;
+    if (const char *mb = std::getenv("CLK_MAX_BLOCKS")) {
+        int v = std::atoi(mb);
+        if (v > 0)
+            c->max_blocks = v;
+    }
+    e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete c;
+        return hip_fail(nullptr, e, "hipStreamCreateWithFlags");
+    }
+    c->cur = c->own;
+    *out = c;
+    return CLK_SUCCESS;
+}
+
+int clk_ctx_destroy(clk_ctx *ctx)
+{
+    if (!ctx)
+        return CLK_SUCCESS;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->cur);
+    (void)hipStreamDestroy(ctx->own);
+    delete ctx;
+    return CLK_SUCCESS;
+}
+
+int clk_ctx_set_stream(clk_ctx *ctx, void *hip_stream)
+{
+    if (!ctx)
+        return fail(nullptr, CLK_EINVAL, "null context");
+    ctx->cur = (hipStream_t)hip_stream;
+    return CLK_SUCCESS;
+}
+
+void *clk_ctx_stream(clk_ctx *ctx) { return ctx ? (void *)ctx->cur : nullptr; }
+void *clk_ctx_own_stream(clk_ctx *ctx) { return ctx ? (void *)ctx->own : nullptr; }
+int clk_ctx_device(clk_ctx *ctx) { return ctx ? ctx->device : -1; }
+
+int clk_ctx_sync(clk_ctx *ctx)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    hipError_t e = hipStreamSynchronize(ctx->cur);
+    if (e != hipSuccess)
+        return hip_fail(ctx, e, "hipStreamSynchronize");
+    return CLK_SUCCESS;
+}
+
+const char *clk_last_error(clk_ctx *ctx) { return ctx ? ctx->err : tls_err; }
+
+int clk_in_cksum(clk_ctx *ctx, const clk_batch *b, uint16_t *out_sum)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, "clk_in_cksum"))) return r;
+    if (b->n == 0) return CLK_SUCCESS;
+    if (!out_sum) return fail(ctx, CLK_EINVAL, "clk_in_cksum: null output");
+    switch (pick_group(b)) {
+    case 1: launch_range<1>(ctx, b, out_sum); break;
+    case 4: launch_range<4>(ctx, b, out_sum); break;
+    case 16: launch_range<16>(ctx, b, out_sum); break;
+    default: launch_range<64>(ctx, b, out_sum); break;
+    }
+    return check_launch(ctx, "clk_in_cksum");
+}
+
+int clk_check_ip_header(clk_ctx *ctx, const clk_batch *b, const clk_ip_check_cfg *cfg, uint8_t *out_verdict)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, "clk_check_ip_header"))) return r;
+    if (!cfg) return fail(ctx, CLK_EINVAL, "clk_check_ip_header: null cfg");
+    if ((cfg->nbadsrc && !cfg->badsrc) || (cfg->ngooddst && !cfg->gooddst))
+        return fail(ctx, CLK_EINVAL, "clk_check_ip_header: null address list");
+    if (b->n == 0) return CLK_SUCCESS;
+    if (!out_verdict) return fail(ctx, CLK_EINVAL, "clk_check_ip_header: null output");
+    const unsigned grid = grid_for(ctx, b->n);
+    if (cfg->checksum)
+        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
+                           args_of(b), cfg->offset, cfg->badsrc, cfg->nbadsrc, cfg->gooddst, cfg->ngooddst,
+                           out_verdict, (uint16_t *)nullptr);
+    else
+        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK_NOCKSUM>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
+                           args_of(b), cfg->offset, cfg->badsrc, cfg->nbadsrc, cfg->gooddst, cfg->ngooddst,
+                           out_verdict, (uint16_t *)nullptr);
+    return check_launch(ctx, "clk_check_ip_header");
+}
+
+int clk_set_ip_checksum(clk_ctx *ctx, const clk_batch *b, uint8_t *out_status, uint16_t *out_sum)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, "clk_set_ip_checksum"))) return r;
+    if (b->n == 0) return CLK_SUCCESS;
+    if (!out_status) return fail(ctx, CLK_EINVAL, "clk_set_ip_checksum: null output");
+    hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_SET>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0, ctx->cur,
+                       args_of(b), 0u, (const uint32_t *)nullptr, 0u, (const uint32_t *)nullptr, 0u,
+                       out_status, out_sum);
+    return check_launch(ctx, "clk_set_ip_checksum");
+}
+
+int clk_check_udp_header(clk_ctx *ctx, const clk_batch *b, uint8_t *out_verdict)
+{
+    return launch_l4<clk::UDP, false>(ctx, b, 0, out_verdict, nullptr, "clk_check_udp_header");
+}
+
+int clk_set_udp_checksum(clk_ctx *ctx, const clk_batch *b, uint8_t *out_status, uint16_t *out_sum)
+{
+    return launch_l4<clk::UDP, true>(ctx, b, 0, out_status, out_sum, "clk_set_udp_checksum");
+}
+
+int clk_check_tcp_header(clk_ctx *ctx, const clk_batch *b, uint8_t *out_verdict)
+{
+    return launch_l4<clk::TCP, false>(ctx, b, 0, out_verdict, nullptr, "clk_check_tcp_header");
+}
+
+int clk_set_tcp_checksum(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *out_status, uint16_t *out_sum)
+{
+    return launch_l4<clk::TCP, true>(ctx, b, fixoff ? 1 : 0, out_status, out_sum, "clk_set_tcp_checksum");
+}
+
+int clk_count_codes(clk_ctx *ctx, const uint8_t *codes, uint64_t n, uint64_t *counts, uint32_t ncounts)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if (n == 0) return CLK_SUCCESS;
+    if (!codes || !counts || ncounts == 0 || ncounts > 256)
+        return fail(ctx, CLK_EINVAL, "clk_count_codes: bad arguments");
+    unsigned grid = grid_for(ctx, n);
+    if (grid > 1024) grid = 1024;
+    hipLaunchKernelGGL(clk::count_codes_kernel, dim3(grid), dim3(BLOCK), 0, ctx->cur, codes, n,
+                       (unsigned long long *)counts, ncounts);
+    return check_launch(ctx, "clk_count_codes");
+}
+
+int clk_gen_packets(clk_ctx *ctx, const clk_batch *b, int proto, uint64_t seed, uint64_t first_idx)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, "clk_gen_packets"))) return r;
+    if (b->n == 0) return CLK_SUCCESS;
+    hipLaunchKernelGGL(clk::gen_kernel, dim3(grid_for(ctx, b->n * 64)), dim3(BLOCK), 0, ctx->cur,
+                       args_of(b), proto, seed, first_idx);
+    return check_launch(ctx, "clk_gen_packets");
+}
+
+int clk_gen_corrupt(clk_ctx *ctx, const clk_batch *b, uint64_t seed, uint32_t rate_log2)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, "clk_gen_corrupt"))) return r;
+    if (b->n == 0) return CLK_SUCCESS;
+    hipLaunchKernelGGL(clk::corrupt_kernel, dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0, ctx->cur,
+                       args_of(b), seed, rate_log2);
+    return check_launch(ctx, "clk_gen_corrupt");
+}
+
+int clk_read_stream(clk_ctx *ctx, const void *base, uint64_t bytes, uint64_t *out_sum)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if (!base || !out_sum || ((uint64_t)base & 15))
+        return fail(ctx, CLK_EINVAL, "clk_read_stream: bad arguments");
+    const uint64_t n16 = bytes / 16;
+    if (n16 == 0) return CLK_SUCCESS;
+    hipLaunchKernelGGL(clk::read_stream_kernel, dim3(grid_for(ctx, n16 / 4 + 1)), dim3(BLOCK), 0, ctx->cur,
+                       (const clk::u32x4 *)base, n16, (unsigned long long *)out_sum);
+    return check_launch(ctx, "clk_read_stream");
+}
+
+} // extern "C"

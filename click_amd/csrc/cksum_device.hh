@@ -1,0 +1,160 @@
+// cksum_device.hh -- gfx950 device arithmetic for Click's Internet checksum.
+//
+// The reference sums native (little-endian) 16-bit words into a uint32_t that
+// silently wraps (lib/in_cksum.c:25,33-36), so the result is the sum taken
+// mod 2^32 and ANY reduction order reproduces it as long as partial sums are
+// never end-around folded.  For a byte range [s, e) with A = sum of the bytes
+// at even absolute addresses and B = sum of the bytes at odd absolute
+// addresses (both mod 2^32), the reference's word sum is
+//     S = A + 256*B   when s is even   (word k = b[s+2k] | b[s+2k+1] << 8)
+//     S = B + 256*A   when s is odd,
+// and an odd trailing byte lands in the low half as in_cksum.c:39-42 adds it.
+// Lanes therefore load 16-byte-aligned chunks, mask the bytes outside the
+// range, and accumulate A/B; any alignment of s is exact.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace clk {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+
+__device__ __forceinline__ uint32_t bswap16(uint32_t v)
+{
+    return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu);
+}
+
+// lib/in_cksum.c:45-49: two-step carry fold of the u32 sum, complement.
+__device__ __forceinline__ uint32_t in_cksum_fold(uint32_t sum)
+{
+    sum = (sum & 0xffffu) + (sum >> 16);
+    sum += sum >> 16;
+    return (~sum) & 0xffffu;
+}
+
+// lib/in_cksum.c:53-80, portable branch 74-78 (htons truncates to 16 bits).
+__device__ __forceinline__ uint32_t pseudohdr_raw(uint32_t csum, uint32_t src, uint32_t dst,
+                                                  uint32_t proto, uint32_t packet_len)
+{
+    csum = ~csum & 0xFFFFu;
+    csum += (src & 0xffffu) + (src >> 16);
+    csum += (dst & 0xffffu) + (dst >> 16);
+    csum += bswap16(packet_len & 0xFFFFu) + bswap16(proto & 0xFFFFu);
+    csum = (csum & 0xffffu) + (csum >> 16);
+    return ~(csum + (csum >> 16)) & 0xFFFFu;
+}
+
+// Bytes of a dword at absolute address a that lie in [s, e): mask of the
+// bytes j with lo <= j < hi, lo = s - a, hi = e - a (clamped to [0, 4]).
+__device__ __forceinline__ uint32_t lowmask(int k)
+{
+    k = k < 0 ? 0 : (k > 4 ? 4 : k);
+    return k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
+}
+
+// Accumulate one 16-byte chunk whose first byte is at relative position rel
+// (chunk address - range start, may be negative) against a range of length
+// len.  A gets the even-address bytes, B the odd-address bytes (the chunk is
+// 16-aligned, so byte j of the chunk has the parity of j).
+__device__ __forceinline__ void chunk_accumulate(const u32x4 v, int rel, int len,
+                                                 uint32_t &A, uint32_t &B)
+{
+    uint32_t xe = 0, xo = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int lo = -rel - 4 * j;
+        const int hi = len - rel - 4 * j;
+        const uint32_t m = lowmask(hi) & ~lowmask(lo);
+        const uint32_t d = v[j] & m;
+        xe += d & 0x00FF00FFu;
+        xo += (d >> 8) & 0x00FF00FFu;
+    }
+    A += (xe & 0xFFFFu) + (xe >> 16);
+    B += (xo & 0xFFFFu) + (xo >> 16);
+}
+
+// Word sum of a range from its A/B byte sums and start parity.
+__device__ __forceinline__ uint32_t word_sum(uint32_t A, uint32_t B, uint64_t start)
+{
+    return (start & 1) ? (B + (A << 8)) : (A + (B << 8));
+}
+
+// Contribution of byte value b at relative offset r to the word sum.
+__device__ __forceinline__ uint32_t byte_term(uint32_t b, int r)
+{
+    return (r & 1) ? (b << 8) : b;
+}
+
+__device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }
+
+__device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t *p)
+{
+    const uint64_t a = (uint64_t)p;
+    const uint32_t *q = (const uint32_t *)(a & ~3ull);
+    const uint32_t sh = (uint32_t)(a & 3);
+    if (sh == 0)
+        return q[0];
+    return __builtin_amdgcn_alignbyte(q[1], q[0], sh);
+}
+
+__device__ __forceinline__ void st_u16(uint8_t *p, uint32_t v)
+{
+    if (((uint64_t)p & 1) == 0) {
+        *(uint16_t *)p = (uint16_t)v;
+    } else {
+        p[0] = (uint8_t)v;
+        p[1] = (uint8_t)(v >> 8);
+    }
+}
+
+// lib/in_cksum.c:83-111: option walk for the SSRR/LSRR final destination,
+// then pseudohdr_raw.  Only reached when ip_hl != 5 (ip.h:152-160).
+__device__ __noinline__ uint32_t pseudohdr_hard(uint32_t csum, const uint8_t *iph, uint32_t packet_len)
+{
+    const uint32_t hl = (ld_u8(iph) & 0xF) << 2;
+    const uint32_t src = ld_u32_unaligned(iph + 12);
+    const uint32_t proto = ld_u8(iph + 9);
+    uint32_t dst = ld_u32_unaligned(iph + 16);
+    uint32_t o = 20;
+    while (o < hl) {
+        const uint32_t t = ld_u8(iph + o);
+        if (t == 1) {               // IPOPT_NOP
+            o++;
+            continue;
+        } else if (t == 0)          // IPOPT_EOL
+            break;
+        if (o + 1 >= hl)
+            break;
+        const uint32_t l = ld_u8(iph + o + 1);
+        if (l < 2 || o + l > hl)
+            break;
+        if ((t == 137 || t == 131) && l >= 7) {   // IPOPT_SSRR / IPOPT_LSRR
+            dst = ld_u32_unaligned(iph + o + l - 4);
+            break;
+        }
+        o += l;
+    }
+    return pseudohdr_raw(csum, src, dst, proto, packet_len);
+}
+
+// include/clicknet/ip.h:152-160
+__device__ __forceinline__ uint32_t pseudohdr(uint32_t csum, const uint8_t *iph, uint32_t b0,
+                                              uint32_t src, uint32_t dst, uint32_t proto,
+                                              uint32_t transport_len)
+{
+    if ((b0 & 0xF) == 5)
+        return pseudohdr_raw(csum, src, dst, proto, transport_len);
+    return pseudohdr_hard(csum, iph, transport_len);
+}
+
+// splitmix64 finalizer (synthetic traffic; identical to oracle_splitmix64).
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+} // namespace clk

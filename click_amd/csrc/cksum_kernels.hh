@@ -1,0 +1,517 @@
+// cksum_kernels.hh -- hand-written gfx950 kernels for Click's checksum path.
+//
+// Two geometries (DESIGN.md "Kernels"):
+//   * lane-per-packet  (ip_header_kernel): IP header check/set, 20-60 bytes
+//     per packet; each lane reads its header with a dwordx4 + dwordx2 from
+//     the dword-aligned address below it and realigns with v_alignbyte.
+//   * group-per-packet (l4_kernel, range_kernel): G lanes (G | 64) share one
+//     packet; lane l of the group loads 16-byte chunks l, l+G, ... of the
+//     packet with K loads in flight per pass, masks the bytes outside the
+//     summed range, keeps even/odd-address byte sums (cksum_device.hh), and
+//     the group reduces them with xor shuffles.  Loads of a wave instruction
+//     cover 16*G contiguous bytes of each of its 64/G packets.
+// Every kernel is a grid-stride loop over packets whose exit condition every
+// lane reaches; no inter-workgroup communication.
+#pragma once
+#include "cksum_device.hh"
+
+namespace clk {
+
+struct BatchArgs {
+    uint8_t *base;
+    const uint64_t *off;
+    uint64_t stride;
+    const uint32_t *len;
+    uint32_t fixed_len;
+    uint64_t n;
+};
+
+__device__ __forceinline__ uint64_t pkt_off(const BatchArgs &b, uint64_t i)
+{
+    return b.off ? b.off[i] : i * b.stride;
+}
+__device__ __forceinline__ uint32_t pkt_len(const BatchArgs &b, uint64_t i)
+{
+    return b.len ? b.len[i] : b.fixed_len;
+}
+
+enum Proto { UDP = 17, TCP = 6 };
+
+// codes (include/click_amd_cksum.h)
+constexpr uint32_t OK = 0;
+constexpr uint32_t IP_MINISCULE = 1, IP_BAD_VERSION = 2, IP_BAD_HLEN = 3, IP_BAD_IP_LEN = 4,
+                   IP_BAD_CHECKSUM = 5, IP_BAD_SADDR = 6;
+constexpr uint32_t L4_NOT_PROTO = 1, L4_BAD_LENGTH = 2, L4_BAD_CHECKSUM = 3;
+constexpr uint32_t SET_OUTPUT1 = 1, SET_KILL = 2;
+
+// ---------------------------------------------------------------------------
+// IP header: CheckIPHeader (checkipheader.cc:161-226) and SetIPChecksum
+// (setipchecksum.cc:74-95), one lane per packet.
+// ---------------------------------------------------------------------------
+enum IpMode { IP_CHECK = 0, IP_CHECK_NOCKSUM = 1, IP_SET = 2 };
+
+template <int MODE>
+__global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t offset,
+                                                        const uint32_t *badsrc, uint32_t nbadsrc,
+                                                        const uint32_t *gooddst, uint32_t ngooddst,
+                                                        uint8_t *out_code, uint16_t *out_sum)
+{
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += nthreads) {
+        uint8_t *ip = b.base + pkt_off(b, i);
+        uint32_t plen = pkt_len(b, i);
+        if (MODE != IP_SET) {           // data() + OFFSET, length() - OFFSET (checkipheader.cc:163-164)
+            ip += offset;
+            plen -= offset;
+        }
+        uint32_t code = OK, stored = 0;
+        if ((int)plen < 20) {           // checkipheader.cc:168-170 / setipchecksum.cc:82
+            code = MODE == IP_SET ? SET_KILL : IP_MINISCULE;
+        } else {
+            // bytes [ip, ip+20): dwordx4 + dwordx2 from the dword below ip
+            const uint64_t a = (uint64_t)ip;
+            const uint32_t sh = (uint32_t)(a & 3);
+            const uint8_t *q = (const uint8_t *)(a & ~3ull);
+            const u32x4 d0 = *(const u32x4_a4 *)q;
+            uint32_t d4 = *(const uint32_t *)(q + 16);
+            uint32_t d5 = sh ? *(const uint32_t *)(q + 20) : 0u;
+            uint32_t h[5];
+            h[0] = __builtin_amdgcn_alignbyte(d0[1], d0[0], sh);
+            h[1] = __builtin_amdgcn_alignbyte(d0[2], d0[1], sh);
+            h[2] = __builtin_amdgcn_alignbyte(d0[3], d0[2], sh);
+            h[3] = __builtin_amdgcn_alignbyte(d4, d0[3], sh);
+            h[4] = __builtin_amdgcn_alignbyte(d5, d4, sh);
+            const uint32_t b0 = h[0] & 0xFF;
+            const uint32_t hlen = (b0 & 0xF) << 2;
+            uint32_t sum = 0;
+#pragma unroll
+            for (int k = 0; k < 5; k++)
+                sum += (h[k] & 0xFFFF) + (h[k] >> 16);
+            if (MODE == IP_SET) {
+                if (hlen < 20 || hlen > plen) {
+                    code = SET_KILL;
+                } else {
+                    for (uint32_t o = 20; o < hlen; o += 4) {
+                        const uint32_t w = ld_u32_unaligned(ip + o);
+                        sum += (w & 0xFFFF) + (w >> 16);
+                    }
+                    sum -= h[2] >> 16;                 // ip_sum = 0 (setipchecksum.cc:85)
+                    stored = in_cksum_fold(sum);       // setipchecksum.cc:86
+                    st_u16(ip + 10, stored);
+                }
+            } else {
+                const uint32_t len = bswap16(h[0] >> 16);
+                if ((b0 >> 4) != 4)
+                    code = IP_BAD_VERSION;
+                else if (hlen < 20)
+                    code = IP_BAD_HLEN;
+                else if (len > plen || len < hlen)
+                    code = IP_BAD_IP_LEN;
+                else {
+                    if (MODE == IP_CHECK) {
+                        for (uint32_t o = 20; o < hlen; o += 4) {
+                            const uint32_t w = ld_u32_unaligned(ip + o);
+                            sum += (w & 0xFFFF) + (w >> 16);
+                        }
+                        if (in_cksum_fold(sum) != 0)
+                            code = IP_BAD_CHECKSUM;
+                    }
+                    if (code == OK && nbadsrc) {       // checkipheader.cc:204-206
+                        bool bad = false, good = false;
+                        for (uint32_t k = 0; k < nbadsrc; k++)
+                            bad |= badsrc[k] == h[3];
+                        if (bad) {
+                            for (uint32_t k = 0; k < ngooddst; k++)
+                                good |= gooddst[k] == h[4];
+                            if (!good)
+                                code = IP_BAD_SADDR;
+                        }
+                    }
+                }
+            }
+        }
+        out_code[i] = (uint8_t)code;
+        if (MODE == IP_SET && out_sum)
+            out_sum[i] = (uint16_t)stored;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Group-per-packet range sum: G lanes, K chunk loads per lane per pass.
+// Returns the A/B byte sums of [s, s+len) (len <= 0: empty), reduced over the
+// group.  `first` holds the chunks of pass 0, already loaded by the caller
+// so that they were in flight while the caller parsed the header.
+// ---------------------------------------------------------------------------
+template <int G, int K>
+__device__ __forceinline__ void load_pass(const uint8_t *c0, uint32_t nch, uint32_t pass, uint32_t gl,
+                                          u32x4 (&v)[K])
+{
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t idx = pass * (G * K) + (uint32_t)k * G + gl;
+        v[k] = idx < nch ? *(const u32x4 *)(c0 + 16ull * idx) : u32x4{0, 0, 0, 0};
+    }
+}
+
+template <int G, int K>
+__device__ __forceinline__ void group_range_ab(const uint8_t *c0, uint32_t nch, uint32_t gl,
+                                               const u32x4 (&first)[K], uint64_t s, int len,
+                                               uint32_t &A, uint32_t &B)
+{
+    A = 0;
+    B = 0;
+    const int rel0 = (int)((uint64_t)c0 - s);       // chunk 0 relative to s (<= 0)
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        const uint32_t idx = (uint32_t)k * G + gl;
+        chunk_accumulate(first[k], rel0 + 16 * (int)idx, len, A, B);
+    }
+    const uint32_t npass = (nch + G * K - 1) / (G * K);
+    for (uint32_t p = 1; p < npass; p++) {
+        u32x4 v[K];
+        load_pass<G, K>(c0, nch, p, gl, v);
+#pragma unroll
+        for (int k = 0; k < K; k++) {
+            const uint32_t idx = p * (G * K) + (uint32_t)k * G + gl;
+            chunk_accumulate(v[k], rel0 + 16 * (int)idx, len, A, B);
+        }
+    }
+#pragma unroll
+    for (int m = 1; m < G; m <<= 1) {
+        A += __shfl_xor(A, m, 64);
+        B += __shfl_xor(B, m, 64);
+    }
+}
+
+// clk_in_cksum: click_in_cksum(base+off_i, len_i) (lib/in_cksum.c:20-51).
+template <int G, int K>
+__global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_sum)
+{
+    const uint32_t lane = threadIdx.x & 63, gl = lane & (G - 1);
+    const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; i < b.n; i += groups) {
+        const uint8_t *p = b.base + pkt_off(b, i);
+        const int len = (int)pkt_len(b, i);
+        const uint64_t s = (uint64_t)p;
+        const uint8_t *c0 = (const uint8_t *)(s & ~15ull);
+        const uint32_t nch = len > 0 ? (uint32_t)(((s + (uint64_t)len + 15) & ~15ull) - (uint64_t)c0) / 16 : 0;
+        u32x4 v[K];
+        load_pass<G, K>(c0, nch, 0, gl, v);
+        uint32_t A, B;
+        group_range_ab<G, K>(c0, nch, gl, v, s, len, A, B);
+        if (gl == 0)
+            out_sum[i] = (uint16_t)in_cksum_fold(word_sum(A, B, s));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// UDP / TCP check and set (checkudpheader.cc:84-107, setudpchecksum.cc:37-69,
+// checktcpheader.cc:85-107, settcpchecksum.cc:44-75).  Every lane of a group
+// issues the packet's chunk loads for [nh, nh+caplen) AND loads the first 40
+// header bytes (same addresses across the group: one request per wave
+// instruction), so one memory round trip serves the parse and the sum.
+// Header parse is speculative on ip_hl = 5; options are re-read.
+// ---------------------------------------------------------------------------
+template <int PROTO, bool SET, int G, int K>
+__global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
+                                                 uint16_t *out_sum)
+{
+    constexpr int HDR_DW = PROTO == TCP ? 11 : 8;   // aligned dwords covering bytes [0, 40) / [0, 28)
+    constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16; // uh_sum / th_sum offset in the transport header
+    const uint32_t lane = threadIdx.x & 63, gl = lane & (G - 1);
+    const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; i < b.n; i += groups) {
+        uint8_t *nh = b.base + pkt_off(b, i);
+        const uint32_t caplen = pkt_len(b, i);
+        const uint64_t a = (uint64_t)nh;
+        const uint8_t *c0 = (const uint8_t *)(a & ~15ull);
+        const uint32_t nch = (uint32_t)((((a + caplen + 15) & ~15ull) - (uint64_t)c0) / 16);
+        // issue: chunk loads for pass 0, then the header dwords
+        u32x4 v[K];
+        load_pass<G, K>(c0, nch, 0, gl, v);
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint8_t *q = (const uint8_t *)(a & ~3ull);
+        const uint64_t end = a + caplen;
+        uint32_t d[HDR_DW];
+#pragma unroll
+        for (int k = 0; k < HDR_DW; k++)
+            d[k] = (uint64_t)(q + 4 * k) < end ? *(const uint32_t *)(q + 4 * k) : 0u;
+        uint32_t h[HDR_DW - 1];                 // h[k] = bytes [4k, 4k+4) of the header, LE
+#pragma unroll
+        for (int k = 0; k < HDR_DW - 1; k++)
+            h[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+
+        const uint32_t b0 = h[0] & 0xFF;
+        const uint32_t hl = (b0 & 0xF) << 2;
+        const uint32_t ip_len = bswap16(h[0] >> 16);
+        const uint32_t proto = (h[2] >> 8) & 0xFF;
+        const uint32_t src = h[3], dst = h[4];
+        const bool isfrag = (bswap16(h[1] >> 16) & 0x3FFF) != 0;   // IP_ISFRAG, ip.h:121
+        // transport fields at nh + hl (speculated hl = 20)
+        auto tbyte = [&](uint32_t r) -> uint32_t {    // byte hl + r
+            if (hl == 20) {
+                const uint32_t o = 20 + r;
+                return (h[o >> 2] >> (8 * (o & 3))) & 0xFF;
+            }
+            return ld_u8(nh + hl + r);
+        };
+        uint32_t code = OK, stored = 0;
+        int rlen = 0;             // summed range length (int, as click_in_cksum's)
+        uint32_t plen_ph = 0;     // packet_len passed to the pseudo-header
+        uint32_t fix_delta = 0;   // set TCP FIXOFF: new byte 12 - old byte 12 (mod 2^32)
+        uint32_t new_b12 = 0;
+        bool fix = false;
+        if (caplen < 20) {
+            code = PROTO == UDP ? (SET ? SET_OUTPUT1 : L4_BAD_LENGTH) : (SET ? SET_KILL : L4_BAD_LENGTH);
+        } else if (PROTO == UDP && !SET) {
+            if (proto != 17)
+                code = L4_NOT_PROTO;
+            else if (caplen < hl + 8)
+                code = L4_BAD_LENGTH;
+            else {
+                const uint32_t ulen = (tbyte(4) << 8) | tbyte(5);
+                if (ulen < 8 || caplen < ulen + hl)
+                    code = L4_BAD_LENGTH;
+                else if ((tbyte(6) | tbyte(7)) == 0)
+                    code = OK;                      // uh_sum == 0: not checked (checkudpheader.cc:100)
+                else {
+                    rlen = (int)ulen;
+                    plen_ph = ulen;
+                }
+            }
+        } else if (PROTO == UDP && SET) {
+            const int tlen = (int)caplen - (int)hl;
+            if (isfrag || tlen < 8)
+                code = SET_OUTPUT1;
+            else {
+                const uint32_t ulen = (tbyte(4) << 8) | tbyte(5);
+                if (tlen < (int)ulen)
+                    code = SET_OUTPUT1;
+                else {
+                    rlen = (int)ulen;
+                    plen_ph = ulen;
+                }
+            }
+        } else if (PROTO == TCP && !SET) {
+            if (proto != 6)
+                code = L4_NOT_PROTO;
+            else if (caplen < hl + 13)
+                code = L4_BAD_LENGTH;
+            else {
+                const uint32_t len = ip_len - hl;
+                const uint32_t thl = (tbyte(12) >> 4) << 2;
+                if (thl < 20 || len < thl || caplen < len + hl)
+                    code = L4_BAD_LENGTH;
+                else {
+                    rlen = (int)len;
+                    plen_ph = len;
+                }
+            }
+        } else {   // TCP set
+            if (hl > caplen)
+                code = SET_KILL;
+            else {
+                const uint32_t plen = ip_len - hl, tlen = caplen - hl;
+                if (plen < 20 || plen > tlen)
+                    code = SET_KILL;
+                else {
+                    rlen = (int)plen;
+                    plen_ph = plen;
+                    if (fixoff) {                   // settcpchecksum.cc:57-63
+                        const uint32_t ob = tbyte(12);
+                        const uint32_t off = (ob >> 4) << 2;
+                        if (off < 20) {
+                            new_b12 = (ob & 0x0F) | (5u << 4);
+                            fix = true;
+                        } else if (off > plen && !isfrag) {
+                            new_b12 = (ob & 0x0F) | (((plen >> 2) & 0xF) << 4);
+                            fix = true;
+                        }
+                        if (fix)
+                            fix_delta = new_b12 - ob;
+                    }
+                }
+            }
+        }
+        const bool summing = (code == OK) && (rlen != 0 || plen_ph != 0 || SET);
+        const uint64_t s = a + hl;
+        uint32_t A, B;
+        // a lane whose packet needs no sum masks everything (len 0)
+        group_range_ab<G, K>(c0, nch, gl, v, s, summing ? rlen : 0, A, B);
+        if (gl == 0 && code == OK && summing) {
+            uint32_t sum = word_sum(A, B, s);
+            if (SET) {
+                // the field was zeroed before summing (setudpchecksum.cc:64,
+                // settcpchecksum.cc:65): remove its bytes that lie in range
+                if ((int)FIELD < rlen)
+                    sum -= tbyte(FIELD);
+                if ((int)FIELD + 1 < rlen)
+                    sum -= tbyte(FIELD + 1) << 8;
+                if (fix && 12 < rlen)
+                    sum += fix_delta;
+            }
+            const uint32_t csum = in_cksum_fold(sum);
+            const uint32_t r = pseudohdr(csum, nh, b0, src, dst, proto, plen_ph);
+            if (SET) {
+                if (fix)
+                    nh[hl + 12] = (uint8_t)new_b12;
+                st_u16(nh + hl + FIELD, r);
+                stored = r;
+            } else if (r != 0) {
+                code = L4_BAD_CHECKSUM;
+            }
+        }
+        if (gl == 0) {
+            out_code[i] = (uint8_t)code;
+            if (SET && out_sum)
+                out_sum[i] = (uint16_t)stored;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Utilities: verdict histogram, synthetic traffic, corruption, read stream.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) count_codes_kernel(const uint8_t *codes, uint64_t n,
+                                                          unsigned long long *counts, uint32_t nc)
+{
+    __shared__ unsigned int hist[256];
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += nthreads)
+        atomicAdd(&hist[codes[i]], 1u);
+    __syncthreads();
+    if (threadIdx.x < nc && hist[threadIdx.x])
+        atomicAdd(&counts[threadIdx.x], (unsigned long long)hist[threadIdx.x]);
+}
+
+__device__ __forceinline__ uint64_t gen_word(uint64_t seed, uint64_t idx, uint64_t w)
+{
+    return splitmix64(seed ^ ((idx << 13) | (w & 0x1FFF)));
+}
+
+// Same bytes as oracle_gen_packet (oracle/cksum_oracle.c): 64 lanes per
+// packet, lane l writes 8-byte words l, l+64, ... masked to [0, len).
+__global__ void __launch_bounds__(256) gen_kernel(BatchArgs b, int proto, uint64_t seed, uint64_t first_idx)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / 64;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64; i < b.n; i += groups) {
+        uint8_t *p = b.base + pkt_off(b, i);
+        const uint32_t len = pkt_len(b, i);
+        const uint64_t idx = first_idx + i;
+        const uint64_t ha = gen_word(seed, idx, 0x1FFF), hb = gen_word(seed, idx, 0x1FFE);
+        const uint32_t src = 0x0A000000u | (uint32_t)(ha & 0xFFFFFF);
+        const uint32_t dst = 0xC0A80000u | (uint32_t)((ha >> 24) & 0xFFFF);
+        const uint32_t hlen = proto == 17 ? 28 : (proto == 6 ? 40 : 20);
+        for (uint32_t w = lane; 8 * w < len; w += 64) {
+            uint64_t x = gen_word(seed, idx, w);
+            if (8 * w < hlen) {
+                uint8_t hb8[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t o = 8 * w + k;
+                    uint32_t v = (uint32_t)(x >> (8 * k)) & 0xFF;
+                    if (o < hlen) {
+                        v = 0;
+                        switch (o) {
+                        case 0: v = 0x45; break;
+                        case 2: v = (len >> 8) & 0xFF; break;
+                        case 3: v = len & 0xFF; break;
+                        case 4: v = (uint32_t)(idx >> 8) & 0xFF; break;
+                        case 5: v = (uint32_t)idx & 0xFF; break;
+                        case 8: v = 64; break;
+                        case 9: v = (uint32_t)proto; break;
+                        case 12: v = src >> 24; break;
+                        case 13: v = (src >> 16) & 0xFF; break;
+                        case 14: v = (src >> 8) & 0xFF; break;
+                        case 15: v = src & 0xFF; break;
+                        case 16: v = dst >> 24; break;
+                        case 17: v = (dst >> 16) & 0xFF; break;
+                        case 18: v = (dst >> 8) & 0xFF; break;
+                        case 19: v = dst & 0xFF; break;
+                        default: {
+                            const uint32_t sport = (uint32_t)(ha >> 40) & 0xFFFF;
+                            if (proto == 17) {
+                                const uint32_t dport = ((uint32_t)(ha >> 56) | 0x400) & 0xFFFF;
+                                const uint32_t ulen = len >= 20 ? len - 20 : 0;
+                                if (o == 20) v = sport >> 8;
+                                else if (o == 21) v = sport & 0xFF;
+                                else if (o == 22) v = dport >> 8;
+                                else if (o == 23) v = dport & 0xFF;
+                                else if (o == 24) v = (ulen >> 8) & 0xFF;
+                                else if (o == 25) v = ulen & 0xFF;
+                            } else if (proto == 6) {
+                                const uint32_t win = (uint32_t)(ha >> 48) & 0xFFFF;
+                                if (o == 20) v = sport >> 8;
+                                else if (o == 21) v = sport & 0xFF;
+                                else if (o == 22) v = 0;
+                                else if (o == 23) v = 80;
+                                else if (o >= 24 && o < 32) v = (uint32_t)(hb >> (8 * (o - 24))) & 0xFF;
+                                else if (o == 32) v = 0x50;
+                                else if (o == 33) v = 0x10;
+                                else if (o == 34) v = win >> 8;
+                                else if (o == 35) v = win & 0xFF;
+                            }
+                        }
+                        }
+                    }
+                    hb8[k] = (uint8_t)v;
+                }
+                x = 0;
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    x |= (uint64_t)hb8[k] << (8 * k);
+            }
+            uint8_t *dstp = p + 8 * w;
+            const uint32_t nb = len - 8 * w < 8 ? len - 8 * w : 8;
+            if (nb == 8 && (((uint64_t)dstp & 7) == 0)) {
+                *(uint64_t *)dstp = x;
+            } else {
+                for (uint32_t k = 0; k < nb; k++)
+                    dstp[k] = (uint8_t)(x >> (8 * k));
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) corrupt_kernel(BatchArgs b, uint64_t seed, uint32_t rate_log2)
+{
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t mask = rate_log2 >= 64 ? ~0ull : ((1ull << rate_log2) - 1);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += nthreads) {
+        const uint64_t h = splitmix64(seed ^ (i * 0xD1B54A32D192ED03ull));
+        if ((h & mask) != 0)
+            continue;
+        const uint32_t len = pkt_len(b, i);
+        const uint32_t lo = len > 40 ? 40 : (len > 20 ? 20 : 0);
+        if (len <= lo)
+            continue;
+        const uint32_t pos = lo + (uint32_t)((h >> 20) % (uint64_t)(len - lo));
+        uint8_t *p = b.base + pkt_off(b, i) + pos;
+        *p ^= (uint8_t)(1u << ((h >> 8) & 7));
+    }
+}
+
+__global__ void __launch_bounds__(256) read_stream_kernel(const u32x4 *p, uint64_t n16, unsigned long long *out)
+{
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t acc = 0;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * nthreads < n16; i += 4 * nthreads) {
+        const u32x4 a0 = p[i], a1 = p[i + nthreads], a2 = p[i + 2 * nthreads], a3 = p[i + 3 * nthreads];
+        acc += (a0[0] ^ a0[1] ^ a0[2] ^ a0[3]) + (a1[0] ^ a1[1] ^ a1[2] ^ a1[3])
+             + (a2[0] ^ a2[1] ^ a2[2] ^ a2[3]) + (a3[0] ^ a3[1] ^ a3[2] ^ a3[3]);
+    }
+    for (; i < n16; i += nthreads) {
+        const u32x4 a0 = p[i];
+        acc += a0[0] ^ a0[1] ^ a0[2] ^ a0[3];
+    }
+    for (int m = 32; m >= 1; m >>= 1)
+        acc += __shfl_xor(acc, m, 64);
+    if ((threadIdx.x & 63) == 0 && acc)
+        atomicAdd(out, (unsigned long long)acc);
+}
+
+} // namespace clk

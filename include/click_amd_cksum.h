@@ -1,0 +1,181 @@
+/*
+ * click_amd_cksum.h -- C ABI of the MI355X (gfx950) Internet-checksum path.
+ *
+ * Drop-in boundary for Click's software checksum path.  The reference has no
+ * FFI for this path: the checksum functions are leaves called from element
+ * simple_action()s (kohler/click 2.1, lib/in_cksum.c, include/clicknet/ip.h,
+ * elements/ip, elements/tcpudp).  Each batched entry point below replaces one
+ * such per-packet call, applied to a whole struct-of-arrays packet batch that
+ * is resident in device memory (HBM); the element glue that would call it
+ * from Click's tree is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - plain C: pointers, sizes, POD structs; no C++ types, no exceptions;
+ *   - every function returns 0 (CLK_SUCCESS) or a negative CLK_E* code, and
+ *     clk_last_error(ctx) describes the last failure on that context;
+ *   - batched calls are ASYNCHRONOUS on the context's HIP stream; results are
+ *     valid after clk_ctx_sync() (or an event recorded on clk_ctx_stream());
+ *   - all buffers are owned by the caller; device pointers must come from
+ *     hipMalloc (or any allocator with page-granular device allocations);
+ *   - one context per host thread (Click RouterThread); a context is not
+ *     re-entrant, distinct contexts are thread-safe.
+ *
+ * Byte order: 16-bit words are summed in little-endian order, like the
+ * reference on x86-64, so results are bit-identical to lib/in_cksum.c and
+ * are stored into the header fields exactly as the reference stores them.
+ */
+#ifndef CLICK_AMD_CKSUM_H
+#define CLICK_AMD_CKSUM_H
+#include <stdint.h>
+#include <stddef.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CLK_ABI_VERSION 1
+
+/* ---- return codes -------------------------------------------------------- */
+#define CLK_SUCCESS 0
+#define CLK_EINVAL (-1)   /* bad argument (null pointer, n too large, ...)    */
+#define CLK_EHIP (-2)     /* HIP runtime error; see clk_last_error()           */
+#define CLK_ENODEV (-3)   /* no such device / device is not gfx950             */
+
+/* ---- per-packet result codes ---------------------------------------------
+ * Check elements: 0 = packet passes (output 0); otherwise 1 + the element's
+ * Reason enum value (the packet is dropped: output 1 if connected, else
+ * killed; drops/drop_details handlers count it).                          */
+enum clk_ip_verdict {                 /* CheckIPHeader::Reason, checkipheader.hh:150-158 */
+    CLK_OK = 0,
+    CLK_IP_MINISCULE_PACKET = 1,
+    CLK_IP_BAD_VERSION = 2,
+    CLK_IP_BAD_HLEN = 3,
+    CLK_IP_BAD_IP_LEN = 4,
+    CLK_IP_BAD_CHECKSUM = 5,
+    CLK_IP_BAD_SADDR = 6
+};
+enum clk_l4_verdict {                 /* Check{UDP,TCP}Header::Reason */
+    CLK_L4_NOT_PROTO = 1,             /* NOT_UDP / NOT_TCP */
+    CLK_L4_BAD_LENGTH = 2,
+    CLK_L4_BAD_CHECKSUM = 3
+};
+enum clk_set_status {                 /* Set*Checksum outcome */
+    CLK_SET_OK = 0,                   /* field written; output 0                    */
+    CLK_SET_OUTPUT1 = 1,              /* SetUDPChecksum: fragment or short -> output 1
+                                         (setudpchecksum.cc:48-61); nothing written */
+    CLK_SET_KILL = 2                  /* SetIPChecksum / SetTCPChecksum bad lengths:
+                                         packet killed; nothing written            */
+};
+
+/* ---- context ------------------------------------------------------------- */
+typedef struct clk_ctx clk_ctx;
+
+/* Create a context on HIP device `device` with its own non-blocking stream. */
+int clk_ctx_create(int device, clk_ctx **out);
+int clk_ctx_destroy(clk_ctx *ctx);
+/* Launch on hipStream_t `hip_stream` from now on (e.g. the stream of the
+ * caller's framework; NULL is HIP's null stream, as in the HIP API).
+ * clk_ctx_own_stream() returns the context's own stream, for switching back. */
+int clk_ctx_set_stream(clk_ctx *ctx, void *hip_stream);
+void *clk_ctx_stream(clk_ctx *ctx);
+void *clk_ctx_own_stream(clk_ctx *ctx);
+int clk_ctx_sync(clk_ctx *ctx);
+int clk_ctx_device(clk_ctx *ctx);
+/* Last error text for `ctx` (or for the calling thread when ctx == NULL). */
+const char *clk_last_error(clk_ctx *ctx);
+int clk_abi_version(void);
+
+/* ---- batch descriptor (struct of arrays, device-resident) ----------------
+ * Packet i's bytes are [base + off_i, base + off_i + len_i) where
+ *   off_i = off ? off[i] : i * stride        (byte offset of the header the
+ *                                             element looks at)
+ *   len_i = len ? len[i] : fixed_len          (bytes available from there to
+ *                                             the packet's end_data())
+ * For the IP/UDP/TCP elements the header is the packet's network (L3)
+ * header; the transport header is taken at L3 + ip_hl*4, as CheckIPHeader /
+ * MarkIPHeader set it.  Offsets may have any alignment (Click requires 2).
+ * Set elements write their checksum field in place into `base`. */
+typedef struct clk_batch {
+    uint8_t *base;
+    const uint64_t *off;
+    uint64_t stride;
+    const uint32_t *len;
+    uint32_t fixed_len;
+    uint32_t max_len;   /* optional upper bound on len_i (0 = unknown); picks
+                           the lanes-per-packet geometry when len != NULL     */
+    uint64_t n;
+} clk_batch;
+
+/* ---- checksum arithmetic ---------------------------------------------------
+ * click_in_cksum(base+off_i, len_i) for every i        (lib/in_cksum.c:20-51)
+ * out_sum[i] is the returned uint16_t.                                      */
+int clk_in_cksum(clk_ctx *ctx, const clk_batch *ranges, uint16_t *out_sum);
+
+/* ---- elements ------------------------------------------------------------- */
+
+/* CheckIPHeader::simple_action (elements/ip/checkipheader.cc:161-226).
+ * The batch points at each packet's data(); `offset` is the OFFSET keyword.
+ * checksum = CHECKSUM keyword (0 gives CheckIPHeader2, checkipheader2.cc:27-31).
+ * badsrc/gooddst: device arrays of raw (network-order) s_addr words for the
+ * BADSRC/GOODDST/INTERFACES keywords (may be NULL with count 0).
+ * out_verdict[i]: enum clk_ip_verdict.                                      */
+typedef struct clk_ip_check_cfg {
+    uint32_t offset;
+    int32_t checksum;
+    const uint32_t *badsrc;
+    uint32_t nbadsrc;
+    uint32_t ngooddst;
+    const uint32_t *gooddst;
+} clk_ip_check_cfg;
+int clk_check_ip_header(clk_ctx *ctx, const clk_batch *batch,
+                        const clk_ip_check_cfg *cfg, uint8_t *out_verdict);
+
+/* SetIPChecksum::simple_action (elements/ip/setipchecksum.cc:74-95).
+ * Writes ip_sum in place; out_status[i]: enum clk_set_status (OK or KILL);
+ * out_sum (nullable): the 16-bit value stored (0 when not OK).              */
+int clk_set_ip_checksum(clk_ctx *ctx, const clk_batch *batch,
+                        uint8_t *out_status, uint16_t *out_sum);
+
+/* CheckUDPHeader::simple_action (elements/tcpudp/checkudpheader.cc:84-107).
+ * out_verdict[i]: 0 or enum clk_l4_verdict.                                 */
+int clk_check_udp_header(clk_ctx *ctx, const clk_batch *batch, uint8_t *out_verdict);
+
+/* SetUDPChecksum::simple_action (elements/tcpudp/setudpchecksum.cc:37-69).
+ * out_status[i]: OK or OUTPUT1.                                              */
+int clk_set_udp_checksum(clk_ctx *ctx, const clk_batch *batch,
+                         uint8_t *out_status, uint16_t *out_sum);
+
+/* CheckTCPHeader::simple_action (elements/tcpudp/checktcpheader.cc:85-107). */
+int clk_check_tcp_header(clk_ctx *ctx, const clk_batch *batch, uint8_t *out_verdict);
+
+/* SetTCPChecksum::simple_action (elements/tcpudp/settcpchecksum.cc:44-75);
+ * fixoff = FIXOFF keyword (settcpchecksum.cc:39-41, 57-63).
+ * out_status[i]: OK or KILL.                                                 */
+int clk_set_tcp_checksum(clk_ctx *ctx, const clk_batch *batch, int fixoff,
+                         uint8_t *out_status, uint16_t *out_sum);
+
+/* ---- batch utilities ------------------------------------------------------- */
+
+/* counts[c] += number of i with codes[i] == c, for c < ncounts (device u64). */
+int clk_count_codes(clk_ctx *ctx, const uint8_t *codes, uint64_t n,
+                    uint64_t *counts, uint32_t ncounts);
+
+/* Synthetic traffic (bench/test source, like InfiniteSource/RandomSource):
+ * writes len_i bytes of packet (first_idx + i): IPv4 header (ihl 5, ttl 64,
+ * protocol `proto`: 17 UDP, 6 TCP), transport header, pseudo-random payload
+ * from splitmix64; every checksum field is 0.  Bytes past len_i in a slot
+ * are not touched.                                                           */
+int clk_gen_packets(clk_ctx *ctx, const clk_batch *batch, int proto,
+                    uint64_t seed, uint64_t first_idx);
+/* Flip one payload bit in every packet whose hash(seed, i) has its low
+ * `rate_log2` bits zero (1 in 2^rate_log2), for Check-mode drop tests.      */
+int clk_gen_corrupt(clk_ctx *ctx, const clk_batch *batch, uint64_t seed,
+                    uint32_t rate_log2);
+
+/* Sum of `bytes` starting at device `base`, read once as 16-byte loads: the
+ * measured HBM read-stream ceiling for the roofline (bench only).          */
+int clk_read_stream(clk_ctx *ctx, const void *base, uint64_t bytes, uint64_t *out_sum);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLICK_AMD_CKSUM_H */

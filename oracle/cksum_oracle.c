@@ -1,0 +1,458 @@
+/*
+ * cksum_oracle.c -- CPU restatement of Click's Internet-checksum path.
+ *
+ * TEST INFRASTRUCTURE ONLY (the parity checker and the CPU baseline); the
+ * product library in click_amd/ never links or calls this file.
+ *
+ * Restated from the reference (kohler/click 2.1):
+ *   lib/in_cksum.c:20-51    click_in_cksum
+ *   lib/in_cksum.c:53-80    click_in_cksum_pseudohdr_raw (portable branch 74-78;
+ *                           the i386 asm branch 58-72 is not on x86-64/gfx950)
+ *   lib/in_cksum.c:83-111   click_in_cksum_pseudohdr_hard
+ *   lib/in_cksum.c:113-121  click_update_zero_in_cksum_hard
+ *   include/clicknet/ip.h:152-160  click_in_cksum_pseudohdr (dispatch)
+ *   include/clicknet/ip.h:177-185  click_update_in_cksum (RFC 1624)
+ *   elements/ip/checkipheader.cc:161-226   CheckIPHeader::simple_action
+ *   elements/ip/setipchecksum.cc:74-95     SetIPChecksum::simple_action
+ *   elements/tcpudp/checkudpheader.cc:84-107  CheckUDPHeader::simple_action
+ *   elements/tcpudp/setudpchecksum.cc:37-69   SetUDPChecksum::simple_action
+ *   elements/tcpudp/checktcpheader.cc:85-107  CheckTCPHeader::simple_action
+ *   elements/tcpudp/settcpchecksum.cc:44-75   SetTCPChecksum::simple_action
+ *
+ * Built with Click's own optimisation flags (-O2 -g, userlevel/Makefile.in:85-86)
+ * by oracle/Makefile.  Parity: see cksum_oracle.h and DESIGN.md.
+ */
+#define _GNU_SOURCE
+#include "cksum_oracle.h"
+#include <string.h>
+#include <pthread.h>
+#include <time.h>
+#include <stdlib.h>
+
+/* Codes shared with include/click_amd_cksum.h (tests assert they agree). */
+#define CLK_OK 0
+#define CLK_IP_MINISCULE_PACKET 1
+#define CLK_IP_BAD_VERSION 2
+#define CLK_IP_BAD_HLEN 3
+#define CLK_IP_BAD_IP_LEN 4
+#define CLK_IP_BAD_CHECKSUM 5
+#define CLK_IP_BAD_SADDR 6
+#define CLK_L4_NOT_PROTO 1
+#define CLK_L4_BAD_LENGTH 2
+#define CLK_L4_BAD_CHECKSUM 3
+#define CLK_SET_OUTPUT1 1
+#define CLK_SET_KILL 2
+
+static inline uint16_t ld16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
+static inline uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
+static inline void st16(uint8_t *p, uint16_t v) { memcpy(p, &v, 2); }
+/* htons/ntohs on a little-endian host; the argument is truncated to 16 bits
+ * exactly as glibc's __bswap_16(uint16_t) does for htons(int). */
+static inline uint16_t bswap16(uint32_t v) { v &= 0xFFFF; return (uint16_t)((v >> 8) | (v << 8)); }
+
+/* lib/in_cksum.c:20-51.  32-bit accumulator with silent wrap (25,34), odd
+ * trailing byte added as the low byte of a zero word (39-42), two-step carry
+ * fold (45-46), complement truncated to 16 bits (49).  `len` is an int: a
+ * negative length sums nothing, exactly as the reference's while loop. */
+uint16_t oracle_in_cksum(const uint8_t *addr, int len)
+{
+    int nleft = len;
+    const uint8_t *w = addr;
+    uint32_t sum = 0;
+    while (nleft > 1) {
+        sum += ld16(w);
+        w += 2;
+        nleft -= 2;
+    }
+    if (nleft == 1)
+        sum += *w;
+    sum = (sum & 0xffff) + (sum >> 16);
+    sum += (sum >> 16);
+    return (uint16_t)~sum;
+}
+
+/* lib/in_cksum.c:53-80, portable branch (74-78). */
+uint16_t oracle_in_cksum_pseudohdr_raw(uint32_t csum, uint32_t src, uint32_t dst,
+                                       int proto, int packet_len)
+{
+    csum = ~csum & 0xFFFF;                                  /* 57 */
+    csum += (src & 0xffff) + (src >> 16);                   /* 74 */
+    csum += (dst & 0xffff) + (dst >> 16);                   /* 75 */
+    csum += bswap16((uint32_t)packet_len) + bswap16((uint32_t)proto); /* 76 */
+    csum = (csum & 0xffff) + (csum >> 16);                  /* 77 */
+    return (uint16_t)(~(csum + (csum >> 16)) & 0xFFFF);     /* 78 */
+}
+
+/* lib/in_cksum.c:83-111: option walk for the source-route final destination. */
+uint16_t oracle_in_cksum_pseudohdr_hard(uint32_t csum, const uint8_t *iph, int packet_len)
+{
+    const uint8_t *opt = iph + 20;                          /* 86 */
+    const uint8_t *end_opt = iph + ((iph[0] & 0xF) << 2);   /* 87 */
+    while (opt < end_opt) {                                 /* 88 */
+        if (*opt == 1) {                                    /* IPOPT_NOP, 90-92 */
+            opt++;
+            continue;
+        } else if (*opt == 0)                               /* IPOPT_EOL, 93-94 */
+            break;
+        if (opt + 1 >= end_opt || opt[1] < 2 || opt + opt[1] > end_opt) /* 97-98 */
+            break;
+        if ((*opt == 137 || *opt == 131) && opt[1] >= 7) {  /* SSRR/LSRR, 101-105 */
+            uint32_t daddr = ld32(opt + opt[1] - 4);
+            return oracle_in_cksum_pseudohdr_raw(csum, ld32(iph + 12), daddr, iph[9], packet_len);
+        }
+        opt += opt[1];                                      /* 107 */
+    }
+    return oracle_in_cksum_pseudohdr_raw(csum, ld32(iph + 12), ld32(iph + 16), iph[9], packet_len); /* 110 */
+}
+
+/* include/clicknet/ip.h:152-160 */
+uint16_t oracle_in_cksum_pseudohdr(uint32_t csum, const uint8_t *iph, int transport_len)
+{
+    if ((iph[0] & 0xF) == 5)
+        return oracle_in_cksum_pseudohdr_raw(csum, ld32(iph + 12), ld32(iph + 16), iph[9], transport_len);
+    return oracle_in_cksum_pseudohdr_hard(csum, iph, transport_len);
+}
+
+/* include/clicknet/ip.h:177-185 (RFC 1624). */
+uint16_t oracle_update_in_cksum(uint16_t csum, uint16_t old_hw, uint16_t new_hw)
+{
+    uint32_t sum = (~(uint32_t)csum & 0xFFFF) + (~(uint32_t)old_hw & 0xFFFF) + new_hw;
+    sum = (sum & 0xFFFF) + (sum >> 16);
+    return (uint16_t)~(sum + (sum >> 16));
+}
+
+/* include/clicknet/ip.h:196-201 + lib/in_cksum.c:113-121. */
+uint16_t oracle_update_zero_in_cksum(uint16_t csum, const uint8_t *x, int len)
+{
+    if (csum != 0)
+        return csum;
+    for (; len > 0; --len, ++x)
+        if (*x)
+            return csum;
+    return (uint16_t)~0;
+}
+
+/* ---- elements ------------------------------------------------------------ */
+
+/* elements/ip/checkipheader.cc:161-226.  `data`/`length` are the packet's
+ * data() and length(); OFFSET is `offset` (checkipheader.cc:163-164). */
+int oracle_check_ip_header(const uint8_t *data, uint32_t length, uint32_t offset,
+                           int checksum, const uint32_t *badsrc, int nbadsrc,
+                           const uint32_t *gooddst, int ngooddst)
+{
+    const uint8_t *ip = data + offset;
+    uint32_t plen = length - offset;
+    if ((int)plen < 20)                                     /* 168-170 */
+        return CLK_IP_MINISCULE_PACKET;
+    if ((ip[0] >> 4) != 4)                                  /* 172-173 */
+        return CLK_IP_BAD_VERSION;
+    uint32_t hlen = (uint32_t)(ip[0] & 0xF) << 2;           /* 175-177 */
+    if (hlen < 20)
+        return CLK_IP_BAD_HLEN;
+    uint32_t len = bswap16(ld16(ip + 2));                   /* 179-181 */
+    if (len > plen || len < hlen)
+        return CLK_IP_BAD_IP_LEN;
+    if (checksum && oracle_in_cksum(ip, (int)hlen) != 0)    /* 183-197, userlevel branch 193 */
+        return CLK_IP_BAD_CHECKSUM;
+    /* 204-206: BADSRC unless GOODDST */
+    uint32_t src = ld32(ip + 12), dst = ld32(ip + 16);
+    int bad = 0, good = 0;
+    for (int i = 0; i < nbadsrc; i++)
+        if (badsrc[i] == src) { bad = 1; break; }
+    if (bad) {
+        for (int i = 0; i < ngooddst; i++)
+            if (gooddst[i] == dst) { good = 1; break; }
+        if (!good)
+            return CLK_IP_BAD_SADDR;
+    }
+    return CLK_OK;
+}
+
+/* elements/ip/setipchecksum.cc:74-95; `plen` = end_data() - nh_data (80). */
+int oracle_set_ip_checksum(uint8_t *iph, uint32_t plen)
+{
+    uint32_t hlen;
+    if (plen >= 20 && (hlen = (uint32_t)(iph[0] & 0xF) << 2) >= 20 && hlen <= plen) { /* 82-84 */
+        st16(iph + 10, 0);                                  /* 85 */
+        st16(iph + 10, oracle_in_cksum(iph, (int)hlen));    /* 86 */
+        return CLK_OK;
+    }
+    return CLK_SET_KILL;                                    /* 90-92 */
+}
+
+
+/* elements/tcpudp/checkudpheader.cc:84-107.  `nh`/`caplen` are the network
+ * header and the bytes from it to end_data(); the transport header is
+ * nh + ip_hl*4, as CheckIPHeader/MarkIPHeader set it.  Domain guards, which
+ * replace only reads the reference would make outside the packet:
+ *   caplen < 20      -> BAD_LENGTH (no full base IP header to read)
+ *   caplen < hl + 8  -> BAD_LENGTH (the reference returns BAD_LENGTH for any
+ *                       uh_ulen it could read there, 94-98). */
+int oracle_check_udp_header(const uint8_t *nh, uint32_t caplen)
+{
+    if (caplen < 20)
+        return CLK_L4_BAD_LENGTH;
+    if (nh[9] != 17)                                        /* 91-92 */
+        return CLK_L4_NOT_PROTO;
+    uint32_t iph_len = (uint32_t)(nh[0] & 0xF) << 2;        /* 94 */
+    if (caplen < iph_len + 8)
+        return CLK_L4_BAD_LENGTH;
+    const uint8_t *udph = nh + iph_len;
+    uint32_t len = bswap16(ld16(udph + 4));                 /* 95 */
+    if (len < 8 || caplen < len + iph_len)                  /* 96-98 */
+        return CLK_L4_BAD_LENGTH;
+    if (ld16(udph + 6) != 0) {                              /* 100 */
+        unsigned csum = oracle_in_cksum(udph, (int)len);    /* 101 */
+        if (oracle_in_cksum_pseudohdr(csum, nh, (int)len) != 0) /* 102-103 */
+            return CLK_L4_BAD_CHECKSUM;
+    }
+    return CLK_OK;
+}
+
+/* elements/tcpudp/setudpchecksum.cc:37-69.  tlen = transport_length().
+ * Domain guard: caplen < 20 -> OUTPUT1 (no full base IP header). */
+int oracle_set_udp_checksum(uint8_t *nh, uint32_t caplen)
+{
+    if (caplen < 20)
+        return CLK_SET_OUTPUT1;
+    uint32_t hl = (uint32_t)(nh[0] & 0xF) << 2;
+    int tlen = (int)caplen - (int)hl;
+    uint8_t *udph = nh + hl;
+    int len;
+    int isfrag = (bswap16(ld16(nh + 6)) & 0x3FFF) != 0;     /* IP_ISFRAG, ip.h:121 */
+    if (isfrag || tlen < 8                                  /* 48-51 */
+        || (len = bswap16(ld16(udph + 4)), tlen < len))
+        return CLK_SET_OUTPUT1;                             /* 52-61 */
+    st16(udph + 6, 0);                                      /* 64 */
+    unsigned csum = oracle_in_cksum(udph, len);             /* 65 */
+    st16(udph + 6, oracle_in_cksum_pseudohdr(csum, nh, len)); /* 66 */
+    return CLK_OK;
+}
+
+/* elements/tcpudp/checktcpheader.cc:85-107.  Unsigned length arithmetic as
+ * in the reference (len = ip_len - hl may wrap; click_in_cksum then takes a
+ * negative int and sums nothing).  Domain guards: caplen < 20 -> BAD_LENGTH;
+ * caplen < hl + 13 (th_off unreadable) -> BAD_LENGTH, which is what the
+ * reference returns for every th_off it could read there unless ip_len < hl. */
+int oracle_check_tcp_header(const uint8_t *nh, uint32_t caplen)
+{
+    if (caplen < 20)
+        return CLK_L4_BAD_LENGTH;
+    if (nh[9] != 6)                                         /* 92-93 */
+        return CLK_L4_NOT_PROTO;
+    uint32_t iph_len = (uint32_t)(nh[0] & 0xF) << 2;        /* 95 */
+    uint32_t len = (uint32_t)bswap16(ld16(nh + 2)) - iph_len; /* 96 */
+    if (caplen < iph_len + 13)
+        return CLK_L4_BAD_LENGTH;
+    const uint8_t *tcph = nh + iph_len;
+    uint32_t tcph_len = (uint32_t)(tcph[12] >> 4) << 2;     /* 97 */
+    if (tcph_len < 20 || len < tcph_len || caplen < len + iph_len) /* 98-100 */
+        return CLK_L4_BAD_LENGTH;
+    unsigned csum = oracle_in_cksum(tcph, (int)len);        /* 102 */
+    if (oracle_in_cksum_pseudohdr(csum, nh, (int)len) != 0) /* 103-104 */
+        return CLK_L4_BAD_CHECKSUM;
+    return CLK_OK;
+}
+
+/* elements/tcpudp/settcpchecksum.cc:44-75.  Domain guard: hl > caplen
+ * (negative transport_length, where the reference would read and write
+ * outside the packet) -> KILL. */
+int oracle_set_tcp_checksum(uint8_t *nh, uint32_t caplen, int fixoff)
+{
+    if (caplen < 20)
+        return CLK_SET_KILL;
+    uint32_t hl = (uint32_t)(nh[0] & 0xF) << 2;
+    if (hl > caplen)
+        return CLK_SET_KILL;
+    uint8_t *tcph = nh + hl;
+    uint32_t plen = (uint32_t)bswap16(ld16(nh + 2)) - hl;   /* 50 */
+    uint32_t tlen = caplen - hl;
+    if (plen < 20 || plen > tlen)                           /* 53-55 */
+        return CLK_SET_KILL;                                /* 71-74 */
+    if (fixoff) {                                           /* 57-63 */
+        uint32_t off = (uint32_t)(tcph[12] >> 4) << 2;
+        int isfrag = (bswap16(ld16(nh + 6)) & 0x3FFF) != 0;
+        if (off < 20)
+            tcph[12] = (uint8_t)((tcph[12] & 0x0F) | (5 << 4));
+        else if (off > plen && !isfrag)
+            tcph[12] = (uint8_t)((tcph[12] & 0x0F) | (((plen >> 2) & 0xF) << 4));
+    }
+    st16(tcph + 16, 0);                                     /* 65 */
+    unsigned csum = oracle_in_cksum(tcph, (int)plen);       /* 66 */
+    st16(tcph + 16, oracle_in_cksum_pseudohdr(csum, nh, (int)plen)); /* 67 */
+    return CLK_OK;
+}
+
+/* ---- batch drivers ------------------------------------------------------- */
+
+static inline uint64_t pkt_off(const uint64_t *off, uint64_t stride, uint64_t i)
+{ return off ? off[i] : i * stride; }
+static inline uint32_t pkt_len(const uint32_t *len, uint32_t fixed_len, uint64_t i)
+{ return len ? len[i] : fixed_len; }
+
+static int run_one(int op, uint8_t *p, uint32_t l, int arg, uint16_t *sum)
+{
+    int r = 0;
+    switch (op) {
+    case ORACLE_OP_IN_CKSUM:
+        *sum = oracle_in_cksum(p, (int)l);
+        return 0;
+    case ORACLE_OP_CHECK_IP:
+        return oracle_check_ip_header(p, l, 0, arg, 0, 0, 0, 0);
+    case ORACLE_OP_SET_IP:
+        r = oracle_set_ip_checksum(p, l);
+        *sum = r == 0 ? ld16(p + 10) : 0;
+        return r;
+    case ORACLE_OP_CHECK_UDP:
+        return oracle_check_udp_header(p, l);
+    case ORACLE_OP_SET_UDP:
+        r = oracle_set_udp_checksum(p, l);
+        *sum = r == 0 ? ld16(p + ((p[0] & 0xF) << 2) + 6) : 0;
+        return r;
+    case ORACLE_OP_CHECK_TCP:
+        return oracle_check_tcp_header(p, l);
+    case ORACLE_OP_SET_TCP:
+        r = oracle_set_tcp_checksum(p, l, arg);
+        *sum = r == 0 ? ld16(p + ((p[0] & 0xF) << 2) + 16) : 0;
+        return r;
+    }
+    return -1;
+}
+
+int oracle_batch(int op, uint8_t *base, const uint64_t *off, uint64_t stride,
+                 const uint32_t *len, uint32_t fixed_len, uint64_t n, int arg,
+                 uint8_t *out8, uint16_t *out16)
+{
+    for (uint64_t i = 0; i < n; i++) {
+        uint16_t s = 0;
+        int r = run_one(op, base + pkt_off(off, stride, i), pkt_len(len, fixed_len, i), arg, &s);
+        if (r < 0)
+            return -1;
+        if (out8)
+            out8[i] = (uint8_t)r;
+        if (out16)
+            out16[i] = s;
+    }
+    return 0;
+}
+
+/* ---- synthetic packets (bench.py / tests) ----------------
+ * Byte 8w..8w+7 of packet idx is splitmix64 of counter (idx << 13 | w), then
+ * the IPv4 + UDP/TCP header fields overwrite the front.  All checksum fields
+ * are left 0; the Set elements fill them.  Identical to clk_gen_packets. */
+uint64_t oracle_splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+static inline uint64_t gen_word(uint64_t seed, uint64_t idx, uint64_t w)
+{ return oracle_splitmix64(seed ^ ((idx << 13) | (w & 0x1FFF))); }
+
+static inline void put_be16(uint8_t *p, uint32_t v) { p[0] = (uint8_t)(v >> 8); p[1] = (uint8_t)v; }
+
+void oracle_gen_packet(uint8_t *pkt, uint32_t length, int proto, uint64_t seed, uint64_t idx)
+{
+    uint8_t hdr[40];
+    for (uint32_t i = 0; i < length; i += 8) {
+        uint64_t h = gen_word(seed, idx, i >> 3);
+        for (uint32_t k = 0; k < 8 && i + k < length; k++)
+            pkt[i + k] = (uint8_t)(h >> (8 * k));
+    }
+    /* header words use counters past the payload's (w = 0x1FFF, 0x1FFE) */
+    uint64_t a = gen_word(seed, idx, 0x1FFF), b = gen_word(seed, idx, 0x1FFE);
+    memset(hdr, 0, sizeof hdr);
+    hdr[0] = 0x45;
+    put_be16(hdr + 2, length);
+    put_be16(hdr + 4, (uint32_t)(idx & 0xFFFF));
+    hdr[8] = 64;
+    hdr[9] = (uint8_t)proto;
+    /* src 10.x.y.z, dst 192.168.x.y -- stored big-endian like s_addr */
+    uint32_t src = 0x0A000000u | (uint32_t)(a & 0xFFFFFF);
+    uint32_t dst = 0xC0A80000u | (uint32_t)((a >> 24) & 0xFFFF);
+    put_be16(hdr + 12, src >> 16); put_be16(hdr + 14, src);
+    put_be16(hdr + 16, dst >> 16); put_be16(hdr + 18, dst);
+    uint32_t hlen = 20;
+    if (proto == 17) {
+        put_be16(hdr + 20, (uint32_t)(a >> 40));
+        put_be16(hdr + 22, (uint32_t)(a >> 56) | 0x400);
+        put_be16(hdr + 24, length >= 20 ? length - 20 : 0);
+        hlen = 28;
+    } else if (proto == 6) {
+        put_be16(hdr + 20, (uint32_t)(a >> 40));
+        put_be16(hdr + 22, 80);
+        memcpy(hdr + 24, &b, 8);                 /* seq, ack */
+        hdr[32] = 0x50;                          /* th_off = 5 */
+        hdr[33] = 0x10;                          /* ACK */
+        put_be16(hdr + 34, (uint32_t)(a >> 48)); /* window */
+        hlen = 40;
+    }
+    for (uint32_t i = 0; i < hlen && i < length; i++)
+        pkt[i] = hdr[i];
+}
+
+void oracle_gen_batch(uint8_t *base, const uint64_t *off, uint64_t stride,
+                      const uint32_t *len, uint32_t fixed_len, uint64_t n,
+                      int proto, uint64_t seed, uint64_t first_idx)
+{
+    for (uint64_t i = 0; i < n; i++)
+        oracle_gen_packet(base + pkt_off(off, stride, i), pkt_len(len, fixed_len, i),
+                          proto, seed, first_idx + i);
+}
+
+/* ---- CPU baseline --------------------------------------------------------- */
+
+struct bench_arg {
+    int op, reps, arg;
+    uint8_t *base;
+    uint64_t stride, lo, hi;
+    uint32_t fixed_len;
+    volatile uint64_t sink;
+};
+
+static void *bench_thread(void *vp)
+{
+    struct bench_arg *a = (struct bench_arg *)vp;
+    uint64_t acc = 0;
+    for (int r = 0; r < a->reps; r++)
+        for (uint64_t i = a->lo; i < a->hi; i++) {
+            uint16_t s = 0;
+            acc += (uint64_t)run_one(a->op, a->base + i * a->stride, a->fixed_len, a->arg, &s) + s;
+        }
+    a->sink = acc;
+    return 0;
+}
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+double oracle_bench(int op, uint8_t *base, uint64_t stride, uint32_t fixed_len,
+                    uint64_t n, int reps, int nthreads)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    struct bench_arg *args = calloc((size_t)nthreads, sizeof *args);
+    pthread_t *th = calloc((size_t)nthreads, sizeof *th);
+    for (int t = 0; t < nthreads; t++) {
+        args[t].op = op; args[t].reps = reps; args[t].arg = 1;
+        args[t].base = base; args[t].stride = stride; args[t].fixed_len = fixed_len;
+        args[t].lo = n * (uint64_t)t / (uint64_t)nthreads;
+        args[t].hi = n * (uint64_t)(t + 1) / (uint64_t)nthreads;
+    }
+    double t0 = now_s();
+    for (int t = 1; t < nthreads; t++)
+        pthread_create(&th[t], 0, bench_thread, &args[t]);
+    bench_thread(&args[0]);
+    for (int t = 1; t < nthreads; t++)
+        pthread_join(th[t], 0);
+    double dt = now_s() - t0;
+    free(args);
+    free(th);
+    return dt;
+}

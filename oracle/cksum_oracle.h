@@ -1,0 +1,79 @@
+/*
+ * cksum_oracle.h -- CPU restatement of Click's Internet-checksum path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the parity checker for the HIP kernels
+ * in click_amd/csrc.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.  The product library never links it.
+ *
+ * Every function restates the reference algorithm and cites the reference
+ * line it follows (paths are relative to the kohler/click tree).  Parity is
+ * pinned by the golden vectors in tests/golden/, which are taken from the
+ * reference's own test files (see tests/golden/make_golden.py); the
+ * reference lib/in_cksum.c itself cannot be compiled here without the
+ * configure-generated <click/config.h> ("Oracle").
+ *
+ * Byte order: like the reference on x86-64, 16-bit words are read in host
+ * (little-endian) order; gfx950 is little-endian too.
+ */
+#ifndef CLICK_AMD_CKSUM_ORACLE_H
+#define CLICK_AMD_CKSUM_ORACLE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- lib/in_cksum.c and include/clicknet/ip.h ---------------------------- */
+uint16_t oracle_in_cksum(const uint8_t *addr, int len);
+uint16_t oracle_in_cksum_pseudohdr_raw(uint32_t csum, uint32_t src, uint32_t dst,
+                                       int proto, int packet_len);
+uint16_t oracle_in_cksum_pseudohdr_hard(uint32_t csum, const uint8_t *iph, int packet_len);
+uint16_t oracle_in_cksum_pseudohdr(uint32_t csum, const uint8_t *iph, int transport_len);
+uint16_t oracle_update_in_cksum(uint16_t csum, uint16_t old_hw, uint16_t new_hw);
+uint16_t oracle_update_zero_in_cksum(uint16_t csum, const uint8_t *x, int len);
+
+/* ---- element simple_action()s, one packet -------------------------------
+ * Codes are the ones include/click_amd_cksum.h exports (CLK_*): 0 = the
+ * packet leaves on output 0; otherwise 1 + the element's Reason enum value
+ * (checks) or a set status (sets).                                          */
+int oracle_check_ip_header(const uint8_t *data, uint32_t length, uint32_t offset,
+                           int checksum, const uint32_t *badsrc, int nbadsrc,
+                           const uint32_t *gooddst, int ngooddst);
+int oracle_set_ip_checksum(uint8_t *nh, uint32_t plen);
+int oracle_check_udp_header(const uint8_t *nh, uint32_t caplen);
+int oracle_set_udp_checksum(uint8_t *nh, uint32_t caplen);
+int oracle_check_tcp_header(const uint8_t *nh, uint32_t caplen);
+int oracle_set_tcp_checksum(uint8_t *nh, uint32_t caplen, int fixoff);
+
+/* ---- batch drivers with the C-ABI's batch semantics ----------------------
+ * Packet i starts at base + (off ? off[i] : i*stride) and has
+ * (len ? len[i] : fixed_len) bytes.                                          */
+enum {
+    ORACLE_OP_IN_CKSUM = 0,   /* out16[i] = click_in_cksum(pkt, len)            */
+    ORACLE_OP_CHECK_IP = 1,   /* out8[i] = verdict; arg = CHECKSUM flag         */
+    ORACLE_OP_SET_IP = 2,     /* out8 status, out16 stored ip_sum               */
+    ORACLE_OP_CHECK_UDP = 3,
+    ORACLE_OP_SET_UDP = 4,    /* out16 stored uh_sum                             */
+    ORACLE_OP_CHECK_TCP = 5,
+    ORACLE_OP_SET_TCP = 6,    /* arg = FIXOFF; out16 stored th_sum               */
+};
+int oracle_batch(int op, uint8_t *base, const uint64_t *off, uint64_t stride,
+                 const uint32_t *len, uint32_t fixed_len, uint64_t n, int arg,
+                 uint8_t *out8, uint16_t *out16);
+
+/* ---- synthetic packet generator (same bytes as clk_gen_packets) ---------- */
+uint64_t oracle_splitmix64(uint64_t x);
+void oracle_gen_packet(uint8_t *pkt, uint32_t length, int proto, uint64_t seed, uint64_t idx);
+void oracle_gen_batch(uint8_t *base, const uint64_t *off, uint64_t stride,
+                      const uint32_t *len, uint32_t fixed_len, uint64_t n,
+                      int proto, uint64_t seed, uint64_t first_idx);
+
+/* ---- CPU baseline timing (bench.py cpu_baseline leg) ---------------------
+ * Runs `op` over the batch `reps` times on `nthreads` threads (disjoint
+ * contiguous shards) and returns the wall seconds of the timed passes.     */
+double oracle_bench(int op, uint8_t *base, uint64_t stride, uint32_t fixed_len,
+                    uint64_t n, int reps, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

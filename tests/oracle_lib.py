@@ -1,0 +1,79 @@
+"""ctypes binding of the CPU oracle (oracle/cksum_oracle.c) -- test infrastructure.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE = os.path.join(ROOT, "oracle", "libcksum_oracle.so")
+
+OP_IN_CKSUM, OP_CHECK_IP, OP_SET_IP, OP_CHECK_UDP, OP_SET_UDP, OP_CHECK_TCP, OP_SET_TCP = range(7)
+OPS = {"in_cksum": OP_IN_CKSUM, "check_ip": OP_CHECK_IP, "set_ip": OP_SET_IP, "check_udp": OP_CHECK_UDP,
+       "set_udp": OP_SET_UDP, "check_tcp": OP_CHECK_TCP, "set_tcp": OP_SET_TCP}
+
+_P = ctypes.c_void_p
+_lib = None
+
+
+def load_oracle():
+    global _lib
+    if _lib is not None:
+        return _lib
+    src = os.path.join(ROOT, "oracle", "cksum_oracle.c")
+    if not os.path.exists(ORACLE) or os.path.getmtime(ORACLE) < os.path.getmtime(src):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    L = ctypes.CDLL(ORACLE)
+    L.oracle_in_cksum.restype = ctypes.c_uint16
+    L.oracle_in_cksum.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    L.oracle_in_cksum_pseudohdr_raw.restype = ctypes.c_uint16
+    L.oracle_in_cksum_pseudohdr_raw.argtypes = [ctypes.c_uint32] * 3 + [ctypes.c_int] * 2
+    L.oracle_in_cksum_pseudohdr_hard.restype = ctypes.c_uint16
+    L.oracle_in_cksum_pseudohdr_hard.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_int]
+    L.oracle_in_cksum_pseudohdr.restype = ctypes.c_uint16
+    L.oracle_in_cksum_pseudohdr.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_int]
+    L.oracle_update_in_cksum.restype = ctypes.c_uint16
+    L.oracle_update_in_cksum.argtypes = [ctypes.c_uint16] * 3
+    L.oracle_update_zero_in_cksum.restype = ctypes.c_uint16
+    L.oracle_update_zero_in_cksum.argtypes = [ctypes.c_uint16, ctypes.c_char_p, ctypes.c_int]
+    L.oracle_batch.restype = ctypes.c_int
+    L.oracle_batch.argtypes = [ctypes.c_int, _P, _P, ctypes.c_uint64, _P, ctypes.c_uint32, ctypes.c_uint64,
+                               ctypes.c_int, _P, _P]
+    L.oracle_gen_batch.restype = None
+    L.oracle_gen_batch.argtypes = [_P, _P, ctypes.c_uint64, _P, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int,
+                                   ctypes.c_uint64, ctypes.c_uint64]
+    L.oracle_bench.restype = ctypes.c_double
+    L.oracle_bench.argtypes = [ctypes.c_int, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                               ctypes.c_int, ctypes.c_int]
+    L.oracle_splitmix64.restype = ctypes.c_uint64
+    L.oracle_splitmix64.argtypes = [ctypes.c_uint64]
+    _lib = L
+    return L
+
+
+def _np_ptr(a):
+    return None if a is None else a.ctypes.data_as(_P)
+
+
+def batch(op, arena, n, stride=0, fixed_len=0, off=None, length=None, arg=1):
+    """Run an element over a numpy byte arena (modified in place for sets).
+    Returns (codes uint8[n], sums uint16[n])."""
+    L = load_oracle()
+    codes = np.zeros(max(n, 1), np.uint8)
+    sums = np.zeros(max(n, 1), np.uint16)
+    off = None if off is None else np.ascontiguousarray(off, np.uint64)
+    length = None if length is None else np.ascontiguousarray(length, np.uint32)
+    rc = L.oracle_batch(OPS[op] if isinstance(op, str) else op, _np_ptr(arena), _np_ptr(off), stride,
+                        _np_ptr(length), fixed_len, n, arg, _np_ptr(codes), _np_ptr(sums))
+    assert rc == 0
+    return codes[:n], sums[:n]
+
+
+def gen(arena, n, stride=0, fixed_len=0, off=None, length=None, proto=17, seed=0x5EED, first_idx=0):
+    L = load_oracle()
+    off = None if off is None else np.ascontiguousarray(off, np.uint64)
+    length = None if length is None else np.ascontiguousarray(length, np.uint32)
+    L.oracle_gen_batch(_np_ptr(arena), _np_ptr(off), stride, _np_ptr(length), fixed_len, n, proto, seed, first_idx)

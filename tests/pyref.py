@@ -1,0 +1,190 @@
+"""A second, independent restatement of the checksum path in pure Python.
+
+Test infrastructure: used only to cross-check the C oracle on small inputs
+(two restatements written separately must agree before either is trusted
+as the checker for the HIP kernels).  Follows the same reference lines as
+oracle/cksum_oracle.c, but is written from RFC 1071 / RFC 791 terms:
+big-endian one's-complement arithmetic is NOT used here either, because the
+reference's u32-wrap behaviour differs from it past 131,074 bytes.
+"""
+import struct
+
+M32 = 0xFFFFFFFF
+
+
+def in_cksum(b, length=None):
+    """lib/in_cksum.c:20-51 on bytes `b` (length may be negative/int)."""
+    n = len(b) if length is None else length
+    s = 0
+    i = 0
+    while n > 1:
+        s = (s + (b[i] | (b[i + 1] << 8))) & M32
+        i += 2
+        n -= 2
+    if n == 1:
+        s = (s + b[i]) & M32
+    s = (s & 0xFFFF) + (s >> 16)
+    s += s >> 16
+    return (~s) & 0xFFFF
+
+
+def bswap16(v):
+    v &= 0xFFFF
+    return ((v >> 8) | (v << 8)) & 0xFFFF
+
+
+def pseudohdr_raw(csum, src, dst, proto, plen):
+    """lib/in_cksum.c:74-78."""
+    c = (~csum) & 0xFFFF
+    c += (src & 0xFFFF) + (src >> 16)
+    c += (dst & 0xFFFF) + (dst >> 16)
+    c += bswap16(plen) + bswap16(proto)
+    c = (c & 0xFFFF) + (c >> 16)
+    return (~(c + (c >> 16))) & 0xFFFF
+
+
+def u32le(b, o):
+    return struct.unpack_from("<I", b, o)[0]
+
+
+def final_dst(iph):
+    """lib/in_cksum.c:86-110 option walk."""
+    hl = (iph[0] & 0xF) * 4
+    o = 20
+    while o < hl:
+        t = iph[o]
+        if t == 1:
+            o += 1
+            continue
+        if t == 0:
+            break
+        if o + 1 >= hl or iph[o + 1] < 2 or o + iph[o + 1] > hl:
+            break
+        ln = iph[o + 1]
+        if t in (137, 131) and ln >= 7:
+            return u32le(iph, o + ln - 4)
+        o += ln
+    return u32le(iph, 16)
+
+
+def pseudohdr(csum, iph, plen):
+    """include/clicknet/ip.h:152-160."""
+    dst = u32le(iph, 16) if (iph[0] & 0xF) == 5 else final_dst(iph)
+    return pseudohdr_raw(csum, u32le(iph, 12), dst, iph[9], plen)
+
+
+def be16(b, o):
+    return (b[o] << 8) | b[o + 1]
+
+
+def check_ip(data, length, offset=0, checksum=True, badsrc=(), gooddst=()):
+    ip = data[offset:]
+    plen = (length - offset) & M32
+    if plen >= 0x80000000 or plen < 20:
+        return 1
+    if ip[0] >> 4 != 4:
+        return 2
+    hl = (ip[0] & 0xF) * 4
+    if hl < 20:
+        return 3
+    ln = be16(ip, 2)
+    if ln > plen or ln < hl:
+        return 4
+    if checksum and in_cksum(ip[:hl]) != 0:
+        return 5
+    if u32le(ip, 12) in badsrc and u32le(ip, 16) not in gooddst:
+        return 6
+    return 0
+
+
+def set_ip(b, plen):
+    """Returns (status, new bytes)."""
+    b = bytearray(b)
+    if plen >= 20:
+        hl = (b[0] & 0xF) * 4
+        if 20 <= hl <= plen:
+            b[10:12] = b"\0\0"
+            struct.pack_into("<H", b, 10, in_cksum(b[:hl]))
+            return 0, bytes(b)
+    return 2, bytes(b)
+
+
+def check_udp(b, caplen):
+    if caplen < 20:
+        return 2
+    if b[9] != 17:
+        return 1
+    hl = (b[0] & 0xF) * 4
+    if caplen < hl + 8:
+        return 2
+    ln = be16(b, hl + 4)
+    if ln < 8 or caplen < ln + hl:
+        return 2
+    if b[hl + 6] | b[hl + 7]:
+        if pseudohdr(in_cksum(b[hl:hl + ln]), b, ln) != 0:
+            return 3
+    return 0
+
+
+def set_udp(b, caplen):
+    b = bytearray(b)
+    if caplen < 20:
+        return 1, bytes(b)
+    hl = (b[0] & 0xF) * 4
+    tlen = caplen - hl
+    frag = be16(b, 6) & 0x3FFF
+    if frag or tlen < 8:
+        return 1, bytes(b)
+    ln = be16(b, hl + 4)
+    if tlen < ln:
+        return 1, bytes(b)
+    b[hl + 6:hl + 8] = b"\0\0"
+    struct.pack_into("<H", b, hl + 6, pseudohdr(in_cksum(b[hl:hl + ln]), b, ln))
+    return 0, bytes(b)
+
+
+def _as_int(u):
+    u &= M32
+    return u - (1 << 32) if u & 0x80000000 else u
+
+
+def check_tcp(b, caplen):
+    if caplen < 20:
+        return 2
+    if b[9] != 6:
+        return 1
+    hl = (b[0] & 0xF) * 4
+    ln = (be16(b, 2) - hl) & M32
+    if caplen < hl + 13:
+        return 2
+    thl = (b[hl + 12] >> 4) * 4
+    if thl < 20 or ln < thl or caplen < ((ln + hl) & M32):
+        return 2
+    n = _as_int(ln)
+    seg = b[hl:hl + max(n, 0)]
+    if pseudohdr(in_cksum(seg, n), b, n) != 0:
+        return 3
+    return 0
+
+
+def set_tcp(b, caplen, fixoff=False):
+    b = bytearray(b)
+    if caplen < 20:
+        return 2, bytes(b)
+    hl = (b[0] & 0xF) * 4
+    if hl > caplen:
+        return 2, bytes(b)
+    plen = (be16(b, 2) - hl) & M32
+    tlen = caplen - hl
+    if plen < 20 or plen > tlen:
+        return 2, bytes(b)
+    if fixoff:
+        off = (b[hl + 12] >> 4) * 4
+        frag = be16(b, 6) & 0x3FFF
+        if off < 20:
+            b[hl + 12] = (b[hl + 12] & 0xF) | 0x50
+        elif off > plen and not frag:
+            b[hl + 12] = (b[hl + 12] & 0xF) | (((plen >> 2) & 0xF) << 4)
+    b[hl + 16:hl + 18] = b"\0\0"
+    struct.pack_into("<H", b, hl + 16, pseudohdr(in_cksum(b[hl:hl + plen]), b, plen))
+    return 0, bytes(b)

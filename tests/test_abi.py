@@ -1,0 +1,98 @@
+"""CPU tests of the drop-in boundary: the library builds, loads, exports every
+symbol include/click_amd_cksum.h declares, and the Python ctypes mirror has
+the C struct layouts.  No compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from click_amd import _abi, build
+
+ROOT = build.ROOT
+HEADER = os.path.join(ROOT, "include", "click_amd_cksum.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(clk_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_builds_for_gfx950():
+    lib = build.build_library()
+    assert os.path.exists(lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib],
+                         capture_output=True, text=True)
+    blob = open(lib, "rb").read()
+    assert b"gfx950" in blob, out.stdout[-400:]
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _abi.load()
+    names = declared_functions()
+    assert len(names) >= 18
+    for name in names:
+        assert hasattr(lib, name), name
+        assert name in _abi.SIGNATURES, "ctypes binding lacks " + name
+    assert lib.clk_abi_version() == 1
+
+
+def test_codes_agree_with_header_and_oracle():
+    text = open(HEADER).read()
+    for name in ("CLK_IP_MINISCULE_PACKET", "CLK_IP_BAD_VERSION", "CLK_IP_BAD_HLEN", "CLK_IP_BAD_IP_LEN",
+                 "CLK_IP_BAD_CHECKSUM", "CLK_IP_BAD_SADDR", "CLK_L4_NOT_PROTO", "CLK_L4_BAD_LENGTH",
+                 "CLK_L4_BAD_CHECKSUM", "CLK_SET_OUTPUT1", "CLK_SET_KILL"):
+        m = re.search(r"\b%s\s*=\s*(\d+)" % name, text)
+        assert m and int(m.group(1)) == getattr(_abi, name), name
+        src = open(os.path.join(ROOT, "oracle", "cksum_oracle.c")).read()
+        alias = name.replace("CLK_L4_NOT_PROTO", "CLK_L4_NOT_PROTO")
+        m2 = re.search(r"#define %s (\d+)" % alias, src)
+        assert m2 and int(m2.group(1)) == getattr(_abi, name), name
+
+
+def test_struct_layouts_match_c():
+    prog = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "click_amd_cksum.h"
+int main(void) {
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(clk_batch), offsetof(clk_batch, off),
+         offsetof(clk_batch, stride), offsetof(clk_batch, len), offsetof(clk_batch, fixed_len),
+         offsetof(clk_batch, max_len), offsetof(clk_batch, n));
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(clk_ip_check_cfg), offsetof(clk_ip_check_cfg, checksum),
+         offsetof(clk_ip_check_cfg, badsrc), offsetof(clk_ip_check_cfg, nbadsrc),
+         offsetof(clk_ip_check_cfg, ngooddst), offsetof(clk_ip_check_cfg, gooddst));
+  return 0; }
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "l.c")
+        open(c, "w").write(prog)
+        subprocess.run(["gcc", "-I", os.path.dirname(HEADER), "-o", os.path.join(d, "l"), c], check=True)
+        out = subprocess.run([os.path.join(d, "l")], capture_output=True, text=True, check=True).stdout.split("\n")
+    b = [int(x) for x in out[0].split()]
+    cfg = [int(x) for x in out[1].split()]
+    B = _abi.clk_batch
+    assert b == [ctypes.sizeof(B), B.off.offset, B.stride.offset, B.len.offset, B.fixed_len.offset,
+                 B.max_len.offset, B.n.offset]
+    C = _abi.clk_ip_check_cfg
+    assert cfg == [ctypes.sizeof(C), C.checksum.offset, C.badsrc.offset, C.nbadsrc.offset,
+                   C.ngooddst.offset, C.gooddst.offset]
+
+
+def test_header_is_plain_c():
+    """The boundary header compiles as C99 with no C++ or torch types."""
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "h.c")
+        open(c, "w").write('#include "click_amd_cksum.h"\nint main(void){return 0;}\n')
+        subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-pedantic", "-I", os.path.dirname(HEADER),
+                        "-c", "-o", os.path.join(d, "h.o"), c], check=True)
+    text = open(HEADER).read()
+    assert "torch" not in re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    with pytest.raises(OSError):
+        _abi.load(str(tmp_path / "nope.so"))

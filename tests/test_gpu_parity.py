@@ -1,0 +1,257 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the CPU oracle.
+
+Bit-exact on every output: per-packet verdict/status codes, returned 16-bit
+checksums, and every byte of the arena after a Set element (no stray
+writes).  Inputs: the golden vectors from the reference's files, seeded
+fuzzed batches covering every branch and alignment, and full-size batches
+checked through size-independent properties.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests import oracle_lib, fuzz
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "golden_vectors.json")
+OPS_L4 = {17: ("check_udp", "set_udp"), 6: ("check_tcp", "set_tcp")}
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+@pytest.fixture(scope="module")
+def ctx(torch):
+    import click_amd
+    c = click_amd.Context(0)
+    yield c
+    c.close()
+
+
+def dev_batch(torch, arena, n, off=None, length=None, stride=0, fixed_len=0, max_len=0):
+    import click_amd
+    base = torch.from_numpy(arena).to("cuda:0")
+    o = torch.from_numpy(off.astype(np.uint64).view(np.int64)).to("cuda:0") if off is not None else None
+    ln = torch.from_numpy(length.astype(np.uint32).view(np.int32)).to("cuda:0") if length is not None else None
+    return click_amd.Batch(base, n, stride=stride, fixed_len=fixed_len, off=o, length=ln, max_len=max_len)
+
+
+def run_gpu(ctx, op, b, arg=1):
+    if op == "in_cksum":
+        return None, ctx.in_cksum(b)
+    if op == "check_ip":
+        return ctx.check_ip_header(b, checksum=bool(arg)), None
+    if op == "set_ip":
+        return ctx.set_ip_checksum(b)
+    if op == "check_udp":
+        return ctx.check_udp_header(b), None
+    if op == "set_udp":
+        return ctx.set_udp_checksum(b)
+    if op == "check_tcp":
+        return ctx.check_tcp_header(b), None
+    if op == "set_tcp":
+        return ctx.set_tcp_checksum(b, fixoff=bool(arg))
+    raise ValueError(op)
+
+
+def compare(torch, ctx, op, arena, n, off=None, length=None, stride=0, fixed_len=0, max_len=0, arg=1):
+    """Run op on GPU and oracle over identical inputs; assert bit-exactness."""
+    b = dev_batch(torch, arena, n, off, length, stride, fixed_len, max_len)
+    codes, sums = run_gpu(ctx, op, b, arg)
+    ctx.sync()
+    ref = arena.copy()
+    rc, rs = oracle_lib.batch(op, ref, n, stride=stride, fixed_len=fixed_len, off=off, length=length, arg=arg)
+    if codes is not None:
+        g = codes.cpu().numpy()
+        bad = np.nonzero(g != rc)[0]
+        assert bad.size == 0, (op, bad[:10], g[bad[:10]], rc[bad[:10]])
+    if sums is not None:
+        g = sums.cpu().numpy()
+        bad = np.nonzero(g != rs)[0]
+        assert bad.size == 0, (op, bad[:10], g[bad[:10]], rs[bad[:10]])
+    after = b.base.cpu().numpy()
+    diff = np.nonzero(after != ref)[0]
+    assert diff.size == 0, (op, "arena differs at", diff[:10])
+    return rc, rs
+
+
+# ---------------------------------------------------------------------------
+def test_golden_vectors_on_gpu(torch, ctx):
+    vecs = json.load(open(GOLDEN))["vectors"]
+    for v in vecs:
+        data = bytes([v["fill"]]) * v["caplen"] if "fill" in v else bytes.fromhex(v["l3"])
+        op = "set_tcp" if v["op"] == "set_tcp_then_rfc1071" else v["op"]
+        for shift in (0, 1, 2, 3, 14):          # the vector at several alignments
+            arena = np.zeros(shift + len(data) + 32, np.uint8)
+            arena[shift:shift + len(data)] = np.frombuffer(data, np.uint8)
+            off = np.array([shift], np.uint64)
+            ln = np.array([v["caplen"]], np.uint32)
+            b = dev_batch(torch, arena, 1, off, ln, max_len=v["caplen"])
+            codes, sums = run_gpu(ctx, op, b, v.get("arg", 1 if op != "set_tcp" else 0))
+            ctx.sync()
+            if v["op"] == "set_tcp_then_rfc1071":
+                assert int(codes.cpu()[0]) == 0, v["name"]
+                from tests.test_oracle import rfc1071_tcp_ok
+                out = b.base.cpu().numpy()[shift:shift + len(data)].tobytes()
+                assert rfc1071_tcp_ok(out, v["final_dst"]), v["name"]
+                continue
+            got = int(sums.cpu()[0]) if (op == "in_cksum" or op.startswith("set_")) else int(codes.cpu()[0])
+            assert got == v["expect"], (v["name"], shift, got)
+
+
+@pytest.mark.parametrize("proto", [17, 6])
+@pytest.mark.parametrize("max_total,align", [(96, "any"), (400, "any"), (1600, "even"), (1600, "any"),
+                                             (5000, "any"), (20000, "even")])
+def test_fuzz_parity(torch, ctx, proto, max_total, align):
+    rng = np.random.default_rng(proto * 1000 + max_total + (align == "any"))
+    n = 3000 if max_total <= 1600 else 400
+    arena, off, caplen, ml = fuzz.make_batch(rng, n, proto, max_total=max_total, align=align)
+    for op in ("check_ip", "set_ip") + OPS_L4[proto]:
+        compare(torch, ctx, op, arena, n, off=off, length=caplen, max_len=ml, arg=1)
+    compare(torch, ctx, "set_tcp" if proto == 6 else "set_udp", arena, n, off=off, length=caplen, max_len=ml, arg=0)
+    compare(torch, ctx, "check_ip", arena, n, off=off, length=caplen, max_len=ml, arg=0)   # CheckIPHeader2
+
+
+@pytest.mark.parametrize("max_len_hint", [0, 64, 500, 2000, 100000])
+def test_geometry_hint_does_not_change_results(torch, ctx, max_len_hint):
+    """Lanes per packet (1/4/16/64, multi-pass) is a speed choice only; a
+    hint smaller than the real maximum must stay exact (multi-pass)."""
+    rng = np.random.default_rng(77)
+    arena, off, caplen, _ = fuzz.make_batch(rng, 800, 17, max_total=3000)
+    for op in ("check_udp", "set_udp", "in_cksum"):
+        compare(torch, ctx, op, arena, 800, off=off, length=caplen, max_len=max_len_hint)
+
+
+def test_in_cksum_ranges(torch, ctx):
+    rng = np.random.default_rng(5)
+    n = 1500
+    lens = np.concatenate([np.arange(0, 300), rng.integers(0, 70000, n - 310),
+                           np.array([131072, 131074, 131076, 200000, 262147, 0, 1, 2, 3, 5])]).astype(np.uint32)
+    off = np.zeros(n, np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(rng.integers(0, 16))
+        off[i] = pos
+        pos += int(lens[i])
+    arena = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    for i in range(n - 10, n - 5):              # the wrap cases are all 0xFF
+        arena[int(off[i]):int(off[i]) + int(lens[i])] = 0xFF
+    compare(torch, ctx, "in_cksum", arena, n, off=off, length=lens, max_len=int(lens.max()))
+    compare(torch, ctx, "in_cksum", arena, n, off=off, length=lens, max_len=0)
+    # negative int lengths sum nothing (click_in_cksum's `int len`)
+    neg = np.array([0xFFFFFFF0, 0x80000000], np.uint32)
+    compare(torch, ctx, "in_cksum", arena, 2, off=off[:2], length=neg, max_len=64)
+
+
+def test_fixed_stride_and_generator(torch, ctx):
+    import click_amd
+    for proto, L, stride in ((17, 1500, 1536), (6, 9000, 9024), (17, 46, 64), (6, 64, 64), (17, 577, 640)):
+        n = 1000
+        arena = np.zeros(n * stride, np.uint8)
+        oracle_lib.gen(arena, n, stride=stride, fixed_len=L, proto=proto, seed=0x5EED, first_idx=7)
+        dev = torch.zeros(n * stride, dtype=torch.uint8, device="cuda:0")
+        b = click_amd.Batch(dev, n, stride=stride, fixed_len=L)
+        ctx.gen_packets(b, proto=proto, seed=0x5EED, first_idx=7)
+        ctx.sync()
+        g = dev.cpu().numpy()
+        assert np.array_equal(g, arena), (proto, L, np.nonzero(g != arena)[0][:8])
+        for op in ("set_ip", "check_ip") + OPS_L4[proto]:
+            compare(torch, ctx, op, arena, n, stride=stride, fixed_len=L)
+            oracle_lib.batch(op, arena, n, stride=stride, fixed_len=L)
+
+
+def test_check_ip_offset_badsrc(torch, ctx):
+    rng = np.random.default_rng(9)
+    n, L, stride = 2000, 60, 80
+    arena = np.zeros(n * stride + 64, np.uint8)
+    oracle_lib.gen(arena[14:], n, stride=stride, fixed_len=L, proto=17)
+    oracle_lib.batch("set_ip", arena[14:], n, stride=stride, fixed_len=L)
+    # BADSRC: a handful of the packets' own sources; GOODDST: some dsts
+    words = arena[14:].view(np.uint8)
+    src_words = np.array([int.from_bytes(words[i * stride + 12:i * stride + 16].tobytes(), "little")
+                          for i in range(n)], np.uint32)
+    dst_words = np.array([int.from_bytes(words[i * stride + 16:i * stride + 20].tobytes(), "little")
+                          for i in range(n)], np.uint32)
+    bad = src_words[rng.choice(n, 50, replace=False)]
+    good = dst_words[rng.choice(n, 700, replace=False)]
+    b = dev_batch(torch, arena, n, stride=stride, fixed_len=L + 14)
+    bt = torch.from_numpy(bad.view(np.int32)).to("cuda:0")
+    gt = torch.from_numpy(good.view(np.int32)).to("cuda:0")
+    codes = ctx.check_ip_header(b, offset=14, checksum=True, badsrc=bt, gooddst=gt).cpu().numpy()
+    L_ = oracle_lib.load_oracle()
+    exp = np.array([L_.oracle_check_ip_header(arena[i * stride:].ctypes.data, L + 14, 14, 1,
+                                              bad.ctypes.data, len(bad), good.ctypes.data, len(good))
+                    for i in range(n)], np.uint8)
+    assert np.array_equal(codes, exp)
+    assert (exp == 6).sum() > 0 and (exp == 0).sum() > 0
+
+
+def test_count_codes(torch, ctx):
+    rng = np.random.default_rng(11)
+    c = rng.integers(0, 7, 1_000_003, dtype=np.uint8)
+    counts = ctx.count_codes(torch.from_numpy(c).to("cuda:0"), ncounts=8).cpu().numpy()
+    assert np.array_equal(counts, np.bincount(c, minlength=8))
+
+
+# ---------------------------------------------------------------------------
+# Full-size properties (BASELINE configs 2 and 3 shapes).
+# ---------------------------------------------------------------------------
+def splitmix64_np(x):
+    x = (x + np.uint64(0x9E3779B97F4A7C15))
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+@pytest.mark.parametrize("proto,L,stride,n", [(17, 1500, 1536, 16 << 20), (17, 46, 64, 16 << 20),
+                                              (6, 9000, 9024, 1 << 20)])
+def test_full_size_properties(torch, ctx, proto, L, stride, n):
+    """Set then Check passes everywhere; one flipped bit in 1/1024 packets is
+    caught exactly on those packets; a random sample of packets matches the
+    oracle byte for byte."""
+    import click_amd
+    with np.errstate(over="ignore"):
+        arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda:0")
+        b = click_amd.Batch(arena, n, stride=stride, fixed_len=L)
+        ctx.gen_packets(b, proto=proto)
+        st, sums = ctx.set_ip_checksum(b)
+        assert int(ctx.count_codes(st)[0]) == n
+        if L >= 28:
+            st, sums = (ctx.set_udp_checksum(b) if proto == 17 else ctx.set_tcp_checksum(b))
+            assert int(ctx.count_codes(st)[0]) == n
+            v = ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)
+            assert int(ctx.count_codes(v)[0]) == n
+        v = ctx.check_ip_header(b)
+        assert int(ctx.count_codes(v)[0]) == n
+        # sample vs oracle
+        rng = np.random.default_rng(12)
+        idx = np.sort(rng.choice(n, 512, replace=False))
+        host = arena.view(n, stride)[torch.from_numpy(idx).to("cuda:0")].cpu().numpy().reshape(-1)
+        ref = np.zeros_like(host)
+        for k, i in enumerate(idx):
+            oracle_lib.gen(ref[k * stride:], 1, stride=stride, fixed_len=L, proto=proto, first_idx=int(i))
+        oracle_lib.batch("set_ip", ref, len(idx), stride=stride, fixed_len=L)
+        if L >= 28:
+            oracle_lib.batch("set_udp" if proto == 17 else "set_tcp", ref, len(idx), stride=stride,
+                             fixed_len=L, arg=0)
+        assert np.array_equal(host, ref)
+        # corruption is caught exactly where it was injected
+        if L >= 28:
+            ctx.gen_corrupt(b, seed=0xBAD, rate_log2=10)
+            v = (ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)).cpu().numpy()
+            i64 = np.arange(n, dtype=np.uint64)
+            h = splitmix64_np(np.uint64(0xBAD) ^ (i64 * np.uint64(0xD1B54A32D192ED03)))
+            sel = (h & np.uint64(1023)) == 0
+            assert sel.sum() > 0
+            assert np.array_equal(v == 3, sel)
+            assert np.array_equal(v == 0, ~sel)
+        del arena
+        torch.cuda.empty_cache()

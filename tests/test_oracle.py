@@ -1,0 +1,220 @@
+"""CPU tests: pin the oracle (oracle/cksum_oracle.c) before it checks the GPU.
+
+1. every golden vector extracted from the reference's own files
+   (tests/golden/golden_vectors.json, made by tests/golden/make_golden.py);
+2. agreement with a second, independently written restatement (tests/pyref.py)
+   on randomized and fuzzed inputs, including the u32-wrap overflow case;
+3. the synthetic-traffic generator's invariants.
+"""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+from tests import oracle_lib, pyref, fuzz
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "golden_vectors.json")
+
+
+def golden_vectors():
+    with open(GOLDEN) as f:
+        return json.load(f)["vectors"]
+
+
+def run_vector_oracle(v):
+    """Returns (result, bytes after) for one golden vector on the oracle."""
+    if "fill" in v:
+        data = bytes([v["fill"]]) * v["caplen"]
+    else:
+        data = bytes.fromhex(v["l3"])
+    arena = np.frombuffer(data + b"\0" * 8, np.uint8).copy()
+    op = v["op"]
+    if op == "set_tcp_then_rfc1071":
+        codes, sums = oracle_lib.batch("set_tcp", arena, 1, stride=0, fixed_len=v["caplen"], arg=0)
+        return int(codes[0]), arena[:v["caplen"]].tobytes()
+    codes, sums = oracle_lib.batch(op, arena, 1, stride=0, fixed_len=v["caplen"], arg=v.get("arg", 1))
+    if op == "in_cksum" or op.startswith("set_"):
+        res = int(sums[0])
+    else:
+        res = int(codes[0])
+    return res, arena[:v["caplen"]].tobytes()
+
+
+def rfc1071_tcp_ok(pkt, final_dst):
+    """Independent verification in RFC 793/1071 terms (big-endian one's
+    complement sum over pseudo-header + segment), as tcpdump does."""
+    hl = (pkt[0] & 0xF) * 4
+    seg = pkt[hl:]
+    dst = bytes(int(x) for x in final_dst.split("."))
+    ph = pkt[12:16] + dst + bytes([0, pkt[9]]) + len(seg).to_bytes(2, "big")
+    data = ph + seg + (b"\0" if len(seg) % 2 else b"")
+    s = 0
+    for i in range(0, len(data), 2):
+        s += (data[i] << 8) | data[i + 1]
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    return s == 0xFFFF
+
+
+@pytest.mark.parametrize("v", golden_vectors(), ids=lambda v: v["name"])
+def test_golden_vector(v):
+    res, after = run_vector_oracle(v)
+    if v["op"] == "set_tcp_then_rfc1071":
+        assert res == 0
+        assert rfc1071_tcp_ok(after, v["final_dst"]), v["source"]
+    else:
+        assert res == v["expect"], v["source"]
+
+
+def test_golden_covers_every_op():
+    ops = {v["op"] for v in golden_vectors()}
+    assert {"in_cksum", "check_ip", "set_ip", "check_udp", "set_udp", "check_tcp", "set_tcp"} <= ops
+    pins = {v["pin"] for v in golden_vectors()}
+    assert {"reference-output", "reference-accepts", "captured", "survey-ref-run", "tcpdump-ok"} <= pins
+
+
+def test_in_cksum_matches_pyref_random():
+    L = oracle_lib.load_oracle()
+    rng = np.random.default_rng(1)
+    for _ in range(400):
+        n = int(rng.integers(0, 3000))
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        elif kind == 1:
+            b = b"\0" * n
+        elif kind == 2:
+            b = b"\xff" * n
+        else:
+            b = bytes(rng.integers(250, 256, n, dtype=np.uint8))
+        assert L.oracle_in_cksum(b, n) == pyref.in_cksum(b)
+
+
+@pytest.mark.parametrize("n", [131072, 131074, 131076, 200000, 262147])
+def test_in_cksum_u32_wrap(n):
+    """The reference's u32 accumulator wraps past 131,074 bytes of 0xFF."""
+    L = oracle_lib.load_oracle()
+    b = b"\xff" * n
+    assert L.oracle_in_cksum(b, n) == pyref.in_cksum(b)
+
+
+def test_in_cksum_edge_lengths():
+    L = oracle_lib.load_oracle()
+    assert L.oracle_in_cksum(b"", 0) == 0xFFFF
+    assert L.oracle_in_cksum(b"\x12", 1) == (~0x12) & 0xFFFF
+    assert L.oracle_in_cksum(b"\x12\x34", 2) == (~0x3412) & 0xFFFF
+    assert L.oracle_in_cksum(b"\x12\x34\x56", 3) == (~(0x3412 + 0x56)) & 0xFFFF
+    assert L.oracle_in_cksum(b"abcd", -4) == 0xFFFF         # negative int len sums nothing
+    # a nonzero input whose folded sum is 0xFFFF yields 0x0000
+    assert L.oracle_in_cksum(b"\xff\xff", 2) == 0
+
+
+def test_pseudohdr_matches_pyref_random():
+    L = oracle_lib.load_oracle()
+    rng = np.random.default_rng(2)
+    for _ in range(3000):
+        csum = int(rng.integers(0, 65536))
+        src, dst = (int(x) for x in rng.integers(0, 2 ** 32, 2, dtype=np.uint64))
+        proto = int(rng.integers(0, 256))
+        plen = int(rng.integers(-70000, 70000))
+        assert L.oracle_in_cksum_pseudohdr_raw(csum, src, dst, proto, plen) == \
+            pyref.pseudohdr_raw(csum, src, dst, proto, plen & 0xFFFFFFFF)
+
+
+def test_pseudohdr_hard_matches_pyref_options():
+    L = oracle_lib.load_oracle()
+    rng = np.random.default_rng(3)
+    for _ in range(3000):
+        words = int(rng.integers(0, 11))
+        hdr = bytearray(rng.integers(0, 256, 20, dtype=np.uint8).tobytes()) + fuzz._options(rng, words)
+        hdr[0] = 0x40 | (5 + words)
+        csum = int(rng.integers(0, 65536))
+        plen = int(rng.integers(0, 65536))
+        assert L.oracle_in_cksum_pseudohdr(csum, bytes(hdr), plen) == pyref.pseudohdr(csum, bytes(hdr), plen)
+
+
+def test_update_in_cksum_rfc1624():
+    """ip.h:177-185: an incremental update equals a recomputation (except the
+    0x0000/0xFFFF representation, ip.h:166-176)."""
+    L = oracle_lib.load_oracle()
+    rng = np.random.default_rng(4)
+    for _ in range(500):
+        hdr = bytearray(rng.integers(0, 256, 20, dtype=np.uint8).tobytes())
+        hdr[10:12] = b"\0\0"
+        s = L.oracle_in_cksum(bytes(hdr), 20)
+        struct.pack_into("<H", hdr, 10, s)
+        k = 2 * int(rng.integers(0, 10))
+        if k == 10:
+            continue
+        old = struct.unpack_from("<H", hdr, k)[0]
+        new = int(rng.integers(0, 65536))
+        struct.pack_into("<H", hdr, k, new)
+        upd = L.oracle_update_in_cksum(s, old, new)
+        hdr2 = bytearray(hdr)
+        hdr2[10:12] = b"\0\0"
+        full = L.oracle_in_cksum(bytes(hdr2), 20)
+        assert upd == full or {upd, full} == {0, 0xFFFF}
+    assert L.oracle_update_zero_in_cksum(0, b"\0\0\0\0", 4) == 0xFFFF
+    assert L.oracle_update_zero_in_cksum(0, b"\0\1\0\0", 4) == 0
+
+
+@pytest.mark.parametrize("proto", [17, 6])
+def test_elements_match_pyref_fuzz(proto):
+    rng = np.random.default_rng(10 + proto)
+    arena, off, caplen, _ = fuzz.make_batch(rng, 600, proto, max_total=400)
+    n = len(off)
+    ops = ["check_ip", "set_ip"] + (["check_udp", "set_udp"] if proto == 17 else ["check_tcp", "set_tcp"])
+    for op in ops:
+        a = arena.copy()
+        codes, sums = oracle_lib.batch(op, a, n, off=off, length=caplen, arg=1 if op != "set_tcp" else 1)
+        for i in range(n):
+            o, c = int(off[i]), int(caplen[i])
+            pkt = arena[o:o + c].tobytes()
+            # pyref works on the caplen bytes it may read (domain guards keep
+            # the oracle inside them)
+            padded = pkt + b"\0" * 64
+            if op == "check_ip":
+                exp = pyref.check_ip(padded, c)
+            elif op == "check_udp":
+                exp = pyref.check_udp(padded, c)
+            elif op == "check_tcp":
+                exp = pyref.check_tcp(padded, c)
+            else:
+                fn = {"set_ip": pyref.set_ip, "set_udp": pyref.set_udp,
+                      "set_tcp": lambda b, cl: pyref.set_tcp(b, cl, True)}[op]
+                exp, newb = fn(padded, c)
+                assert a[o:o + c].tobytes() == newb[:c], (op, i)
+            assert codes[i] == exp, (op, i, pkt.hex())
+
+
+def test_generator_packets_are_valid():
+    """Synthetic traffic: header fields as documented; Set then Check passes."""
+    for proto, L in ((17, 1500), (6, 9000), (17, 46)):
+        n = 64
+        stride = (L + 63) // 64 * 64
+        arena = np.zeros(n * stride, np.uint8)
+        oracle_lib.gen(arena, n, stride=stride, fixed_len=L, proto=proto)
+        p0 = arena[:L].tobytes()
+        assert p0[0] == 0x45 and p0[9] == proto and int.from_bytes(p0[2:4], "big") == L
+        assert p0[10:12] == b"\0\0"
+        oracle_lib.batch("set_ip", arena, n, stride=stride, fixed_len=L)
+        c, _ = oracle_lib.batch("check_ip", arena, n, stride=stride, fixed_len=L)
+        assert not c.any()
+        if L >= 28:
+            s = "set_udp" if proto == 17 else "set_tcp"
+            k = "check_udp" if proto == 17 else "check_tcp"
+            c, _ = oracle_lib.batch(s, arena, n, stride=stride, fixed_len=L, arg=0)
+            assert not c.any()
+            c, _ = oracle_lib.batch(k, arena, n, stride=stride, fixed_len=L)
+            assert not c.any()
+
+
+def test_oracle_bench_runs():
+    L = oracle_lib.load_oracle()
+    n, stride = 256, 1536
+    arena = np.zeros(n * stride, np.uint8)
+    oracle_lib.gen(arena, n, stride=stride, fixed_len=1500)
+    dt = L.oracle_bench(oracle_lib.OP_SET_UDP, arena.ctypes.data, stride, 1500, n, 2, 2)
+    assert dt > 0
