@@ -351,7 +351,27 @@ __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_
                     sum += fix_delta;
             }
             const uint32_t csum = in_cksum_fold(sum);
-            const uint32_t r = pseudohdr(csum, nh, b0, src, dst, proto, plen_ph);
+            uint32_t r;
+            if (SET && hl < 20) {
+                // ip_hl < 5: the transport header overlaps the IP header.  The
+                // reference zeroes the field (and FIXOFF rewrites th_off)
+                // BEFORE the pseudo-header reads ip_src/ip_dst, and the option
+                // walk is empty (in_cksum.c:86-88), so patch those bytes in.
+                uint32_t s2 = src, d2 = dst;
+                auto patch = [&](uint32_t pos, uint32_t val) {
+                    if (pos >= 12 && pos < 16)
+                        s2 = (s2 & ~(0xFFu << (8 * (pos - 12)))) | (val << (8 * (pos - 12)));
+                    else if (pos >= 16 && pos < 20)
+                        d2 = (d2 & ~(0xFFu << (8 * (pos - 16)))) | (val << (8 * (pos - 16)));
+                };
+                if (fix)
+                    patch(hl + 12, new_b12);
+                patch(hl + FIELD, 0);
+                patch(hl + FIELD + 1, 0);
+                r = pseudohdr_raw(csum, s2, d2, proto, plen_ph);
+            } else {
+                r = pseudohdr(csum, nh, b0, src, dst, proto, plen_ph);
+            }
             if (SET) {
                 if (fix)
                     nh[hl + 12] = (uint8_t)new_b12;

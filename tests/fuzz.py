@@ -86,7 +86,7 @@ def _mutate(rng, b, proto):
         b[0] = (b[0] & 0xF0) | int(rng.integers(0, 16))                 # ip_hl
     elif r < 0.18:
         b[2:4] = int(rng.integers(0, 65536)).to_bytes(2, "big")         # ip_len
-    elif r < 0.24 and len(b) > hl + 6:
+    elif r < 0.24 and len(b) > hl + 13:
         if proto == 17:
             b[hl + 4:hl + 6] = int(rng.choice([0, 7, 8, len(b) - hl + 1, int(rng.integers(0, 65536))])).to_bytes(2, "big")
         else:

@@ -39,6 +39,9 @@ def load_oracle():
     L.oracle_update_in_cksum.argtypes = [ctypes.c_uint16] * 3
     L.oracle_update_zero_in_cksum.restype = ctypes.c_uint16
     L.oracle_update_zero_in_cksum.argtypes = [ctypes.c_uint16, ctypes.c_char_p, ctypes.c_int]
+    L.oracle_check_ip_header.restype = ctypes.c_int
+    L.oracle_check_ip_header.argtypes = [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, _P, ctypes.c_int,
+                                         _P, ctypes.c_int]
     L.oracle_batch.restype = ctypes.c_int
     L.oracle_batch.argtypes = [ctypes.c_int, _P, _P, ctypes.c_uint64, _P, ctypes.c_uint32, ctypes.c_uint64,
                                ctypes.c_int, _P, _P]

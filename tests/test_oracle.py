@@ -218,3 +218,14 @@ def test_oracle_bench_runs():
     oracle_lib.gen(arena, n, stride=stride, fixed_len=1500)
     dt = L.oracle_bench(oracle_lib.OP_SET_UDP, arena.ctypes.data, stride, 1500, n, 2, 2)
     assert dt > 0
+
+
+@pytest.mark.parametrize("proto", [17, 6])
+def test_fuzz_batches_build(proto):
+    """The GPU parity tests' fuzzed batches build (same seeds as there)."""
+    for max_total, align in [(96, "any"), (400, "any"), (1600, "even"), (1600, "any"), (5000, "any"),
+                             (20000, "even")]:
+        rng = np.random.default_rng(proto * 1000 + max_total + (align == "any"))
+        n = 3000 if max_total <= 1600 else 400
+        arena, off, caplen, ml = fuzz.make_batch(rng, n, proto, max_total=max_total, align=align)
+        assert len(off) == n and ml <= max(max_total, 60)
