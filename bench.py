@@ -3,11 +3,14 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5]
 
-One step = one pass of the element over one device-resident batch
-(inputs generated in HBM before timing).  Default workload C3: SetUDPChecksum
-over 16M x 1500 B UDP/IPv4 packets in 1536 B slots per GPU; the 64 B
-min-size batch (C2: SetIPChecksum over 16M packets in 64 B slots) is measured
-in the same run and reported under "c2_64b" because the metric names both.
+One step = one pass of one element over one device-resident batch (inputs
+generated in HBM before timing).  Default workload C3: 16M x 1500 B
+UDP/IPv4 packets in 1536 B slots per GPU; the headline element is
+CheckUDPHeader (full-payload checksum + verdict, read-bound), and
+SetUDPChecksum (checksum written in place) is timed beside it under
+"elements".  The 64 B min-size batch (C2: CheckIPHeader and SetIPChecksum
+over 16M packets in 64 B slots) is measured in the same run under "c2_64b"
+because the metric names both sizes.
 Multi-GPU (torchrun, one process per GPU): every rank generates and
 processes its own shard of global packet indices -- packets are independent,
 so there is no collective in the data path (weak scaling); one RCCL
@@ -33,18 +36,28 @@ METRIC = "GiB/s checksummed (device-resident) + Mpps, 64B and 1500B packet batch
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 GIB = float(1 << 30)
 
-# workload: (proto, element, packet bytes L, slot stride, packets per GPU,
-#            bytes "checksummed" per packet (metric), algorithmic HBM bytes per packet)
+# workload: protocol, packet bytes L, slot stride, packets per GPU, bytes
+# "checksummed" per packet (the metric's numerator), and the elements timed:
+# the first is the headline, the others are reported beside it.  Algorithmic
+# HBM bytes per packet per element: Check = L read + 1 verdict byte;
+# Set = L read + 2 field bytes + 1 status byte (CheckIPHeader/SetIPChecksum
+# read the 20 B header, not the slot).
 WORKLOADS = {
-    "c3": dict(proto=17, element="SetUDPChecksum", L=1500, stride=1536, n=16 << 20, ck=1500, alg=1500 + 2 + 1,
-               desc="C3: SetUDPChecksum, 1500 B UDP/IPv4 packets, 16M-packet batch per GPU, 1536 B slots"),
-    "c2": dict(proto=17, element="SetIPChecksum", L=46, stride=64, n=16 << 20, ck=20, alg=20 + 2 + 1,
-               desc="C2: SetIPChecksum, 64 B min-size slots (IP length 46), 16M-packet batch per GPU"),
-    "c5": dict(proto=6, element="SetTCPChecksum", L=9000, stride=9024, n=16 << 20, ck=9000, alg=9000 + 2 + 1,
-               desc="C5: SetTCPChecksum, 9000 B jumbo TCP/IPv4, 16M packets per GPU (128M over 8 GPUs)"),
-    "c4": dict(proto=17, element="SetUDPChecksum", L=0, stride=0, n=64 << 20, ck=None, alg=None,
-               desc="C4: SetUDPChecksum, IMIX 64/576/1500 (7:4:1), 64M packets, 64 B-aligned packing"),
+    "c3": dict(proto=17, L=1500, stride=1536, n=16 << 20, ck=1500,
+               elements=("CheckUDPHeader", "SetUDPChecksum"),
+               desc="C3: 1500 B UDP/IPv4 full-payload checksum, 16M-packet batch per GPU, 1536 B slots"),
+    "c2": dict(proto=17, L=46, stride=64, n=16 << 20, ck=20,
+               elements=("CheckIPHeader", "SetIPChecksum"),
+               desc="C2: 64 B min-size packets (IP length 46, 64 B slots), IP-header checksum, 16M-packet batch per GPU"),
+    "c5": dict(proto=6, L=9000, stride=9024, n=16 << 20, ck=9000,
+               elements=("CheckTCPHeader", "SetTCPChecksum"),
+               desc="C5: 9000 B jumbo TCP/IPv4 checksum, 16M packets per GPU (128M over 8 GPUs)"),
+    "c4": dict(proto=17, L=0, stride=0, n=64 << 20, ck=None,
+               elements=("CheckUDPHeader", "SetUDPChecksum"),
+               desc="C4: IMIX 64/576/1500 (7:4:1) UDP/IPv4 checksum, 64M packets, 64 B-aligned packing"),
 }
+ALG = {"CheckUDPHeader": lambda L: L + 1, "CheckTCPHeader": lambda L: L + 1, "CheckIPHeader": lambda L: 20 + 1,
+       "SetUDPChecksum": lambda L: L + 3, "SetTCPChecksum": lambda L: L + 3, "SetIPChecksum": lambda L: 20 + 3}
 
 
 def log(*a):
@@ -70,19 +83,28 @@ def imix_layout(torch, n, seed, first_idx):
     return (torch.from_numpy(off).cuda(), torch.from_numpy(L.astype(np.int32)).cuda(), total, int(L.sum()))
 
 
-def run_element(ctx, w, b, status):
-    if w["element"] == "SetUDPChecksum":
+def run_element(ctx, name, b, status):
+    if name == "SetUDPChecksum":
         ctx.set_udp_checksum(b, status=status, want_sums=False)
-    elif w["element"] == "SetTCPChecksum":
+    elif name == "SetTCPChecksum":
         ctx.set_tcp_checksum(b, status=status, want_sums=False)
-    elif w["element"] == "SetIPChecksum":
+    elif name == "SetIPChecksum":
         ctx.set_ip_checksum(b, status=status, want_sums=False)
+    elif name == "CheckUDPHeader":
+        ctx.check_udp_header(b, out=status)
+    elif name == "CheckTCPHeader":
+        ctx.check_tcp_header(b, out=status)
+    elif name == "CheckIPHeader":
+        ctx.check_ip_header(b, out=status)
     else:
-        raise ValueError(w["element"])
+        raise ValueError(name)
 
 
 def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
-    """Generate the shard, run warmup + timed steps; returns a dict."""
+    """Generate the shard in HBM, make every checksum valid (untimed), then
+    time each of the workload's elements: warmup + `steps` launches between
+    barriers + synchronize; HIP events on the launch stream give the kernel
+    time.  Returns {element: result}."""
     import click_amd
     w = dict(WORKLOADS[wname])
     n = w["n"]
@@ -92,49 +114,54 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
         arena = torch.empty(total, dtype=torch.uint8, device="cuda")
         b = click_amd.Batch(arena, n, off=off, length=ln, max_len=1500)
         ck_bytes = sum_l
-        alg_bytes = sum_l + 3 * n + 12 * n      # + field write + status + descriptor (off u64, len u32)
+        alg = {e: (sum_l + (ALG[e](0)) * n + 12 * n) for e in w["elements"]}   # + descriptor (off u64, len u32)
     else:
         arena = torch.empty(n * w["stride"], dtype=torch.uint8, device="cuda")
         b = click_amd.Batch(arena, n, stride=w["stride"], fixed_len=w["L"])
         ck_bytes = w["ck"] * n
-        alg_bytes = w["alg"] * n
+        alg = {e: ALG[e](w["L"]) * n for e in w["elements"]}
     status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ctx.reserve(n)
     ctx.gen_packets(b, proto=w["proto"], seed=seed, first_idx=first)
     ctx.set_ip_checksum(b, status=status, want_sums=False)
+    run_element(ctx, "SetTCPChecksum" if w["proto"] == 6 else "SetUDPChecksum", b, status)
     stream = torch.cuda.current_stream()
-    for _ in range(warmup):
-        run_element(ctx, w, b, status)
-    torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(steps):
-        ev[k][0].record(stream)
-        run_element(ctx, w, b, status)
-        ev[k][1].record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    if dist:
-        dist.barrier()
-    kms = [a.elapsed_time(z) for a, z in ev]
-    kernel_ms = sum(kms) / len(kms)
-    ok = int(ctx.count_codes(status)[0])
-    res = dict(wall=wall, kernel_ms=kernel_ms, kernel_ms_min=min(kms), n=n, ck_bytes=ck_bytes,
-               alg_bytes=alg_bytes, ok=ok, w=w)
-    if dist:
-        t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        d = torch.tensor([ok, n], dtype=torch.int64, device="cuda")
-        dist.all_reduce(d, op=dist.ReduceOp.SUM)
-        res["wall"], res["kernel_ms"] = float(t[0]), float(t[1])
-        res["ok_total"], res["n_total"] = int(d[0]), int(d[1])
-    else:
-        res["ok_total"], res["n_total"] = ok, n
+    out = {}
+    for e in w["elements"]:
+        for _ in range(warmup):
+            run_element(ctx, e, b, status)
+        torch.cuda.synchronize()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            ev[k][0].record(stream)
+            run_element(ctx, e, b, status)
+            ev[k][1].record(stream)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        if dist:
+            dist.barrier()
+        kms = [a.elapsed_time(z) for a, z in ev]
+        kernel_ms = sum(kms) / len(kms)
+        ok = int(ctx.count_codes(status)[0])
+        res = dict(wall=wall, kernel_ms=kernel_ms, kernel_ms_min=min(kms), n=n, ck_bytes=ck_bytes,
+                   alg_bytes=alg[e], ok=ok, w=w, element=e)
+        if dist:
+            t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            d = torch.tensor([ok, n], dtype=torch.int64, device="cuda")
+            dist.all_reduce(d, op=dist.ReduceOp.SUM)
+            res["wall"], res["kernel_ms"] = float(t[0]), float(t[1])
+            res["ok_total"], res["n_total"] = int(d[0]), int(d[1])
+        else:
+            res["ok_total"], res["n_total"] = ok, n
+        out[e] = res
     del arena, status, b
     torch.cuda.empty_cache()
-    return res
+    return out
 
 
 def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5):
@@ -157,20 +184,24 @@ def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5):
     return nbytes / (best * 1e-3) / 1e9
 
 
-def cpu_baseline(wname, seconds=8.0):
-    """Oracle (restated lib/in_cksum.c + element, -O2 -g) over a bounded
-    sample of the same workload, on the host cores; single thread and
-    `threads` threads on disjoint shards."""
+def cpu_baseline(wname, element, seconds=8.0):
+    """Oracle (restated lib/in_cksum.c + the element, -O2 -g) over a bounded
+    sample of the same workload in host DRAM, on the host cores: one thread
+    and `threads` threads on disjoint contiguous shards."""
     import numpy as np
     from tests import oracle_lib
     w = WORKLOADS[wname]
     L_ = oracle_lib.load_oracle()
     op = {"SetUDPChecksum": oracle_lib.OP_SET_UDP, "SetTCPChecksum": oracle_lib.OP_SET_TCP,
-          "SetIPChecksum": oracle_lib.OP_SET_IP}[w["element"]]
+          "SetIPChecksum": oracle_lib.OP_SET_IP, "CheckUDPHeader": oracle_lib.OP_CHECK_UDP,
+          "CheckTCPHeader": oracle_lib.OP_CHECK_TCP, "CheckIPHeader": oracle_lib.OP_CHECK_IP}[element]
     n = max(1, min(w["n"], (256 << 20) // w["stride"]))      # <= 256 MB sample
     arena = np.zeros(n * w["stride"], np.uint8)
     oracle_lib.gen(arena, n, stride=w["stride"], fixed_len=w["L"], proto=w["proto"])
     oracle_lib.batch("set_ip", arena, n, stride=w["stride"], fixed_len=w["L"])
+    if w["L"] >= 28:
+        oracle_lib.batch("set_tcp" if w["proto"] == 6 else "set_udp", arena, n, stride=w["stride"],
+                         fixed_len=w["L"], arg=0)
     ptr = arena.ctypes.data
     L_.oracle_bench(op, ptr, w["stride"], w["L"], n, 1, 1)                 # warm
     one = L_.oracle_bench(op, ptr, w["stride"], w["L"], n, 1, 1)
@@ -194,20 +225,41 @@ def cpu_baseline(wname, seconds=8.0):
         "value": round(pkn * w["ck"] / GIB, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
         "mpps": round(pkn / 1e6, 3),
         "single_thread": {"value": round(pk1 * w["ck"] / GIB, 3), "mpps": round(pk1 / 1e6, 3), "cores": 1},
-        "sample": "%d x %d B packets (%s, %d B slots) in host DRAM, %d+%d passes; oracle/cksum_oracle.c -O2 -g"
-                  % (n, w["L"], w["element"], w["stride"], reps1, repsn),
+        "sample": "%s over %d x %d B packets (%d B slots) in host DRAM, %d + %d passes; oracle/cksum_oracle.c -O2 -g"
+                  % (element, n, w["L"], w["stride"], reps1, repsn),
         "cpu": model,
     }
 
 
-def load_traffic(wname):
+def load_traffic(wname, element):
+    """HBM bytes per launch of `element` from the committed PMC summary."""
     p = os.path.join(ROOT, "profiles", "pmc_%s.json" % wname)
     try:
         with open(p) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+        e = d.get("elements", {}).get(element, {})
+        return e.get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
     except (OSError, ValueError):
         return None, None
+
+
+def summarize(r, steps, wname):
+    """Per-element numbers: rate from the wall clock over the timed steps,
+    roofline from the HIP-event kernel time."""
+    step_s = r["wall"] / steps
+    pps = r["n_total"] / step_s
+    achieved = r["alg_bytes"] / (r["kernel_ms"] * 1e-3) / 1e9
+    traffic, tsrc = load_traffic(wname, r["element"])
+    return {
+        "element": r["element"],
+        "value": round(pps * (r["ck_bytes"] / r["n"]) / GIB, 2), "unit": "GiB/s",
+        "mpps": round(pps / 1e6, 1), "ms_per_step": round(step_s * 1e3, 4),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel_ms": round(r["kernel_ms"], 4), "kernel_ms_min": round(r["kernel_ms_min"], 4),
+                     "alg_bytes_per_launch": r["alg_bytes"], "traffic_source": tsrc},
+        "verify": {"ok": r["ok_total"], "packets": r["n_total"]},
+    }
 
 
 def main():
@@ -242,46 +294,31 @@ def main():
     peak_meas = None if args.no_peak else read_stream_peak(torch, ctx)
 
     if rank == 0:
-        r = main_res
-        w = r["w"]
-        n_total = r["n_total"]
-        step_s = r["wall"] / args.steps
-        pps = n_total / step_s
-        value = pps * (r["ck_bytes"] / r["n"]) / GIB
-        achieved = r["alg_bytes"] / (r["kernel_ms"] * 1e-3) / 1e9
-        traffic, traffic_src = load_traffic(args.workload)
+        w = WORKLOADS[args.workload]
+        head = main_res[w["elements"][0]]
+        hs = summarize(head, args.steps, args.workload)
+        hs["roofline"]["read_stream_measured_GBs"] = round(peak_meas, 1) if peak_meas else None
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s",
-            "mpps": round(pps / 1e6, 1),
+            "metric": METRIC, "value": hs["value"], "unit": "GiB/s", "mpps": hs["mpps"],
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "u32", "data": "synthetic (splitmix64 packets generated in HBM)",
-            "config": {"workload": w["desc"], "element": w["element"], "packets_per_gpu": r["n"],
+            "ms_per_step": hs["ms_per_step"], "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u32", "data": "synthetic (splitmix64 IPv4 packets generated in HBM)",
+            "config": {"workload": w["desc"], "element": head["element"], "packets_per_gpu": head["n"],
                        "packet_bytes": w["L"] or "imix", "slot_bytes": w["stride"] or "64B-aligned",
                        "parallelism": "dp%d (disjoint packet shards, no data-path collective)" % world},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel_ms": round(r["kernel_ms"], 4), "kernel_ms_min": round(r["kernel_ms_min"], 4),
-                         "alg_bytes_per_launch": r["alg_bytes"], "traffic_source": traffic_src,
-                         "read_stream_measured_GBs": round(peak_meas, 1) if peak_meas else None},
-            "verify": {"ok": r["ok_total"], "packets": n_total},
+            "roofline": hs["roofline"],
+            "verify": hs["verify"],
+            "elements": {e: summarize(r, args.steps, args.workload) for e, r in main_res.items()},
         }
         if c2:
-            s2 = c2["wall"] / args.steps
-            pps2 = c2["n_total"] / s2
-            a2 = c2["alg_bytes"] / (c2["kernel_ms"] * 1e-3) / 1e9
-            t2, t2src = load_traffic("c2")
-            line["c2_64b"] = {"workload": c2["w"]["desc"], "mpps": round(pps2 / 1e6, 1),
-                              "value": round(pps2 * 20 / GIB, 2), "unit": "GiB/s (20 B IP header per packet)",
-                              "ms_per_step": round(s2 * 1e3, 4), "kernel_ms": round(c2["kernel_ms"], 4),
-                              "roofline": {"bound": "hbm", "achieved": round(a2, 1), "peak": HBM_PEAK_GBS,
-                                           "unit": "GB/s", "frac": round(a2 / HBM_PEAK_GBS, 4),
-                                           "slot_GBs": round((64 + 3) * c2["n"] / (c2["kernel_ms"] * 1e-3) / 1e9, 1),
-                                           "traffic": t2, "traffic_source": t2src},
-                              "verify": {"ok": c2["ok_total"], "packets": c2["n_total"]}}
+            line["c2_64b"] = {"workload": WORKLOADS["c2"]["desc"],
+                              "elements": {e: summarize(r, args.steps, "c2") for e, r in c2.items()}}
+            for e, r in c2.items():
+                line["c2_64b"]["elements"][e]["slot_GBs"] = round(
+                    (64 + ALG[e](46) - 20) * r["n"] / (r["kernel_ms"] * 1e-3) / 1e9, 1)
         if world == 1 and not args.no_cpu and args.workload != "c4":
             try:
-                line["cpu_baseline"] = cpu_baseline(args.workload, args.cpu_seconds)
+                line["cpu_baseline"] = cpu_baseline(args.workload, head["element"], args.cpu_seconds)
             except Exception as e:        # reported, not fatal
                 line["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(line), flush=True)

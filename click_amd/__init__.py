@@ -67,10 +67,10 @@ class Context:
     the tensors; "own" uses the context's own non-blocking stream; or any
     torch stream / raw hipStream_t handle."""
 
-    def __init__(self, device=0, stream="torch"):
+    def __init__(self, device=0, stream="torch", lib_path=None):
         import torch
         self._torch = torch
-        self.lib = lib()
+        self.lib = lib() if lib_path is None else _abi.load(lib_path)
         self.device = device
         h = ctypes.c_void_p()
         self._check(self.lib.clk_ctx_create(device, ctypes.byref(h)), None)
@@ -114,6 +114,9 @@ class Context:
 
     def sync(self):
         self._check(self.lib.clk_ctx_sync(self.h))
+
+    def reserve(self, max_packets):
+        self._check(self.lib.clk_ctx_reserve(self.h, int(max_packets)))
 
     # -- helpers ---------------------------------------------------------------
     def _out(self, n, dtype):

@@ -67,6 +67,7 @@ SIGNATURES = {
     "clk_ctx_own_stream": (_P, [_P]),
     "clk_ctx_sync": (ctypes.c_int, [_P]),
     "clk_ctx_device": (ctypes.c_int, [_P]),
+    "clk_ctx_reserve": (ctypes.c_int, [_P, ctypes.c_uint64]),
     "clk_last_error": (ctypes.c_char_p, [_P]),
     "clk_in_cksum": (ctypes.c_int, [_P, _BP, _P]),
     "clk_check_ip_header": (ctypes.c_int, [_P, _BP, ctypes.POINTER(clk_ip_check_cfg), _P]),
@@ -82,6 +83,7 @@ SIGNATURES = {
 }
 
 _lib = None
+_variants = {}
 
 
 def load(path=LIB_PATH):
@@ -89,6 +91,8 @@ def load(path=LIB_PATH):
     global _lib
     if _lib is not None and path == LIB_PATH:
         return _lib
+    if path in _variants:
+        return _variants[path]
     if not os.path.exists(path):
         raise OSError("click_amd: %s is missing; run `python -m click_amd.build` "
                       "(there is no CPU fallback)" % path)
@@ -99,4 +103,6 @@ def load(path=LIB_PATH):
         fn.argtypes = args
     if path == LIB_PATH:
         _lib = lib
+    else:
+        _variants[path] = lib
     return lib

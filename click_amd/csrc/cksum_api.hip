@@ -14,7 +14,11 @@ struct clk_ctx {
     int device;
     hipStream_t own;
     hipStream_t cur;
-    int max_blocks;
+    int max_blocks;    // grid cap (tuning: CLK_MAX_BLOCKS)
+    int force_group;   // lanes per packet override (tuning: CLK_FORCE_GROUP)
+    int set_mode;      // -1 auto; 0: Set kernels store the field; 1: two-phase (CLK_SET_MODE)
+    void *scratch;     // two-phase work array (grown on demand)
+    size_t scratch_bytes;
     char err[512];
 };
 
@@ -55,6 +59,28 @@ int check_launch(clk_ctx *ctx, const char *what)
     return CLK_SUCCESS;
 }
 
+// Device scratch for the two-phase Set (one u32 per packet).  Grown with a
+// synchronous hipMalloc the first time a larger batch arrives; steady-state
+// calls allocate nothing.
+int ensure_scratch(clk_ctx *ctx, size_t bytes)
+{
+    if (ctx->scratch_bytes >= bytes)
+        return CLK_SUCCESS;
+    if (ctx->scratch) {
+        hipError_t e = hipStreamSynchronize(ctx->cur);
+        if (e != hipSuccess)
+            return hip_fail(ctx, e, "hipStreamSynchronize");
+        (void)hipFree(ctx->scratch);
+        ctx->scratch = nullptr;
+        ctx->scratch_bytes = 0;
+    }
+    hipError_t e = hipMalloc(&ctx->scratch, bytes);
+    if (e != hipSuccess)
+        return hip_fail(ctx, e, "hipMalloc(scratch)");
+    ctx->scratch_bytes = bytes;
+    return CLK_SUCCESS;
+}
+
 int check_batch(clk_ctx *ctx, const clk_batch *b, const char *fn)
 {
     if (!b)
@@ -79,12 +105,17 @@ clk::BatchArgs args_of(const clk_batch *b)
 }
 
 constexpr int BLOCK = 256;
-constexpr int K = 8;   // 16-byte chunk loads in flight per lane per pass
+#ifndef CLK_K
+#define CLK_K 8
+#endif
+constexpr int K = CLK_K;   // 16-byte chunk loads in flight per lane per pass
 
 // Lanes per packet: the fewest (of 1, 4, 16, 64) whose K-deep pass covers
 // the largest packet in one pass; 64 beyond that (multi-pass).
-int pick_group(const clk_batch *b)
+int pick_group(const clk_ctx *ctx, const clk_batch *b)
 {
+    if (ctx->force_group)
+        return ctx->force_group;
     uint32_t ml = b->len ? b->max_len : b->fixed_len;
     if (b->len && ml == 0)
         return 16;
@@ -111,10 +142,30 @@ void launch_range(clk_ctx *ctx, const clk_batch *b, uint16_t *out)
 }
 
 template <int PROTO, bool SET, int G>
-void launch_l4_g(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint16_t *sum)
+void launch_l4_g(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint16_t *sum, uint32_t *work)
 {
-    hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K>), dim3(grid_for(ctx, b->n * G)), dim3(BLOCK), 0,
-                       ctx->cur, args_of(b), fixoff, code, sum);
+    if (SET && work)
+        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, true>), dim3(grid_for(ctx, b->n * G)), dim3(BLOCK),
+                           0, ctx->cur, args_of(b), fixoff, code, sum, work);
+    else
+        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, false>), dim3(grid_for(ctx, b->n * G)), dim3(BLOCK),
+                           0, ctx->cur, args_of(b), fixoff, code, sum, work);
+}
+
+template <int PROTO, bool SET>
+int launch_l4_dispatch(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint16_t *sum,
+                       uint32_t *work, int g)
+{
+    switch (g) {
+    case 1: launch_l4_g<PROTO, SET, 1>(ctx, b, fixoff, code, sum, work); break;
+    case 2: launch_l4_g<PROTO, SET, 2>(ctx, b, fixoff, code, sum, work); break;
+    case 4: launch_l4_g<PROTO, SET, 4>(ctx, b, fixoff, code, sum, work); break;
+    case 8: launch_l4_g<PROTO, SET, 8>(ctx, b, fixoff, code, sum, work); break;
+    case 16: launch_l4_g<PROTO, SET, 16>(ctx, b, fixoff, code, sum, work); break;
+    case 32: launch_l4_g<PROTO, SET, 32>(ctx, b, fixoff, code, sum, work); break;
+    default: launch_l4_g<PROTO, SET, 64>(ctx, b, fixoff, code, sum, work); break;
+    }
+    return 0;
 }
 
 template <int PROTO, bool SET>
@@ -125,11 +176,17 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
     if ((r = check_batch(ctx, b, fn))) return r;
     if (b->n == 0) return CLK_SUCCESS;
     if (!code) return fail(ctx, CLK_EINVAL, "%s: null output", fn);
-    switch (pick_group(b)) {
-    case 1: launch_l4_g<PROTO, SET, 1>(ctx, b, fixoff, code, sum); break;
-    case 4: launch_l4_g<PROTO, SET, 4>(ctx, b, fixoff, code, sum); break;
-    case 16: launch_l4_g<PROTO, SET, 16>(ctx, b, fixoff, code, sum); break;
-    default: launch_l4_g<PROTO, SET, 64>(ctx, b, fixoff, code, sum); break;
+    uint32_t *work = nullptr;
+    if (SET && ctx->set_mode != 0) {         // auto: two-phase for UDP/TCP Set
+        if ((r = ensure_scratch(ctx, b->n * sizeof(uint32_t)))) return r;
+        work = (uint32_t *)ctx->scratch;
+    }
+    launch_l4_dispatch<PROTO, SET>(ctx, b, fixoff, code, sum, work, pick_group(ctx, b));
+    if (work) {
+        constexpr int FIELD = PROTO == clk::UDP ? 6 : 16;
+        hipLaunchKernelGGL((clk::field_scatter_kernel<FIELD, true>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
+                           ctx->cur, args_of(b), (const uint32_t *)work, (const uint8_t *)nullptr,
+                           (const uint16_t *)nullptr);
     }
     return check_launch(ctx, fn);
 }
@@ -169,11 +226,22 @@ int clk_ctx_create(int device, clk_ctx **out)
         return fail(nullptr, CLK_EINVAL, "clk_ctx_create: out of memory");
     c->device = device;
     c->err[0] = 0;
-    c->max_blocks = 8192;
+    c->max_blocks = 262144;
     if (const char *mb = std::getenv("CLK_MAX_BLOCKS")) {
         int v = std::atoi(mb);
         if (v > 0)
             c->max_blocks = v;
+    }
+    c->scratch = nullptr;
+    c->scratch_bytes = 0;
+    c->set_mode = -1;
+    if (const char *sm = std::getenv("CLK_SET_MODE"))
+        c->set_mode = std::atoi(sm) == 1 ? 1 : 0;
+    c->force_group = 0;
+    if (const char *fg = std::getenv("CLK_FORCE_GROUP")) {
+        int v = std::atoi(fg);
+        if (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 || v == 64)
+            c->force_group = v;
     }
     e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -192,6 +260,8 @@ int clk_ctx_destroy(clk_ctx *ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->cur);
     (void)hipStreamDestroy(ctx->own);
+    if (ctx->scratch)
+        (void)hipFree(ctx->scratch);
     delete ctx;
     return CLK_SUCCESS;
 }
@@ -207,6 +277,13 @@ int clk_ctx_set_stream(clk_ctx *ctx, void *hip_stream)
 void *clk_ctx_stream(clk_ctx *ctx) { return ctx ? (void *)ctx->cur : nullptr; }
 void *clk_ctx_own_stream(clk_ctx *ctx) { return ctx ? (void *)ctx->own : nullptr; }
 int clk_ctx_device(clk_ctx *ctx) { return ctx ? ctx->device : -1; }
+
+int clk_ctx_reserve(clk_ctx *ctx, uint64_t max_packets)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    return ensure_scratch(ctx, max_packets * sizeof(uint32_t));
+}
 
 int clk_ctx_sync(clk_ctx *ctx)
 {
@@ -227,10 +304,13 @@ int clk_in_cksum(clk_ctx *ctx, const clk_batch *b, uint16_t *out_sum)
     if ((r = check_batch(ctx, b, "clk_in_cksum"))) return r;
     if (b->n == 0) return CLK_SUCCESS;
     if (!out_sum) return fail(ctx, CLK_EINVAL, "clk_in_cksum: null output");
-    switch (pick_group(b)) {
+    switch (pick_group(ctx, b)) {
     case 1: launch_range<1>(ctx, b, out_sum); break;
+    case 2: launch_range<2>(ctx, b, out_sum); break;
     case 4: launch_range<4>(ctx, b, out_sum); break;
+    case 8: launch_range<8>(ctx, b, out_sum); break;
     case 16: launch_range<16>(ctx, b, out_sum); break;
+    case 32: launch_range<32>(ctx, b, out_sum); break;
     default: launch_range<64>(ctx, b, out_sum); break;
     }
     return check_launch(ctx, "clk_in_cksum");
@@ -248,11 +328,11 @@ int clk_check_ip_header(clk_ctx *ctx, const clk_batch *b, const clk_ip_check_cfg
     if (!out_verdict) return fail(ctx, CLK_EINVAL, "clk_check_ip_header: null output");
     const unsigned grid = grid_for(ctx, b->n);
     if (cfg->checksum)
-        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
+        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
                            args_of(b), cfg->offset, cfg->badsrc, cfg->nbadsrc, cfg->gooddst, cfg->ngooddst,
                            out_verdict, (uint16_t *)nullptr);
     else
-        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK_NOCKSUM>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
+        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK_NOCKSUM, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
                            args_of(b), cfg->offset, cfg->badsrc, cfg->nbadsrc, cfg->gooddst, cfg->ngooddst,
                            out_verdict, (uint16_t *)nullptr);
     return check_launch(ctx, "clk_check_ip_header");
@@ -265,9 +345,23 @@ int clk_set_ip_checksum(clk_ctx *ctx, const clk_batch *b, uint8_t *out_status, u
     if ((r = check_batch(ctx, b, "clk_set_ip_checksum"))) return r;
     if (b->n == 0) return CLK_SUCCESS;
     if (!out_status) return fail(ctx, CLK_EINVAL, "clk_set_ip_checksum: null output");
-    hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_SET>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0, ctx->cur,
-                       args_of(b), 0u, (const uint32_t *)nullptr, 0u, (const uint32_t *)nullptr, 0u,
-                       out_status, out_sum);
+    if (ctx->set_mode == 1) {                // auto: fused for SetIPChecksum
+        uint16_t *sums = out_sum;
+        if (!sums) {
+            if ((r = ensure_scratch(ctx, b->n * sizeof(uint16_t)))) return r;
+            sums = (uint16_t *)ctx->scratch;
+        }
+        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_SET, true>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
+                           ctx->cur, args_of(b), 0u, (const uint32_t *)nullptr, 0u, (const uint32_t *)nullptr, 0u,
+                           out_status, sums);
+        hipLaunchKernelGGL((clk::field_scatter_kernel<10, false>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
+                           ctx->cur, args_of(b), (const uint32_t *)nullptr, (const uint8_t *)out_status,
+                           (const uint16_t *)sums);
+    } else {
+        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_SET, false>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
+                           ctx->cur, args_of(b), 0u, (const uint32_t *)nullptr, 0u, (const uint32_t *)nullptr, 0u,
+                           out_status, out_sum);
+    }
     return check_launch(ctx, "clk_set_ip_checksum");
 }
 

@@ -9,8 +9,9 @@
 //     S = A + 256*B   when s is even   (word k = b[s+2k] | b[s+2k+1] << 8)
 //     S = B + 256*A   when s is odd,
 // and an odd trailing byte lands in the low half as in_cksum.c:39-42 adds it.
-// Lanes therefore load 16-byte-aligned chunks, mask the bytes outside the
-// range, and accumulate A/B; any alignment of s is exact.
+// Lanes therefore load 16-byte-aligned chunks and accumulate S directly
+// with v_dot2_u32_u16 (even s), or A and B with v_dot4_u32_u8 (odd s); only
+// the bytes of the two boundary chunks are masked.  Any alignment is exact.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -53,37 +54,68 @@ __device__ __forceinline__ uint32_t lowmask(int k)
     return k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
 }
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// v_dot2_u32_u16: acc + lo16(d) + hi16(d), wrapping mod 2^32 (no clamp) --
+// one instruction per dword of an even-start range (the word sum A + 256 B).
+__device__ __forceinline__ uint32_t dot_words(uint32_t d, uint32_t acc)
+{
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, d), u16x2{1, 1}, acc, false);
+}
+// v_dot4_u32_u8 with byte weights: acc + sum of the selected bytes.
+__device__ __forceinline__ uint32_t dot_even_bytes(uint32_t d, uint32_t acc)
+{
+    return __builtin_amdgcn_udot4(d, 0x00010001u, acc, false);
+}
+__device__ __forceinline__ uint32_t dot_odd_bytes(uint32_t d, uint32_t acc)
+{
+    return __builtin_amdgcn_udot4(d, 0x01000100u, acc, false);
+}
+
+// Per-lane accumulators of a range sum.  Even start: s0 = the word sum.
+// Odd start: s0 = A (even-address bytes), s1 = B (odd-address bytes).
+struct RangeAcc {
+    uint32_t s0, s1;
+};
+
 // Accumulate one 16-byte chunk whose first byte is at relative position rel
 // (chunk address - range start, may be negative) against a range of length
-// len.  A gets the even-address bytes, B the odd-address bytes (the chunk is
-// 16-aligned, so byte j of the chunk has the parity of j).
-__device__ __forceinline__ void chunk_accumulate(const u32x4 v, int rel, int len,
-                                                 uint32_t &A, uint32_t &B)
+// len.  Interior chunks take 4 (even) or 8 (odd start) dot instructions;
+// only the two boundary chunks of a range pay for byte masks.
+__device__ __forceinline__ void chunk_accumulate(const u32x4 v, int rel, int len, bool odd, RangeAcc &acc)
 {
-    uint32_t xe = 0, xo = 0;
+    if (rel >= 0 && rel + 16 <= len) {
+        if (!odd) {
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int lo = -rel - 4 * j;
-        const int hi = len - rel - 4 * j;
-        const uint32_t m = lowmask(hi) & ~lowmask(lo);
-        const uint32_t d = v[j] & m;
-        xe += d & 0x00FF00FFu;
-        xo += (d >> 8) & 0x00FF00FFu;
+            for (int j = 0; j < 4; j++)
+                acc.s0 = dot_words(v[j], acc.s0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                acc.s0 = dot_even_bytes(v[j], acc.s0);
+                acc.s1 = dot_odd_bytes(v[j], acc.s1);
+            }
+        }
+    } else if (rel < len && rel + 16 > 0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int lo = -rel - 4 * j;
+            const int hi = len - rel - 4 * j;
+            const uint32_t d = v[j] & lowmask(hi) & ~lowmask(lo);
+            if (!odd) {
+                acc.s0 = dot_words(d, acc.s0);
+            } else {
+                acc.s0 = dot_even_bytes(d, acc.s0);
+                acc.s1 = dot_odd_bytes(d, acc.s1);
+            }
+        }
     }
-    A += (xe & 0xFFFFu) + (xe >> 16);
-    B += (xo & 0xFFFFu) + (xo >> 16);
 }
 
-// Word sum of a range from its A/B byte sums and start parity.
-__device__ __forceinline__ uint32_t word_sum(uint32_t A, uint32_t B, uint64_t start)
+// Word sum of a range from its accumulators and start parity.
+__device__ __forceinline__ uint32_t word_sum(const RangeAcc &acc, bool odd)
 {
-    return (start & 1) ? (B + (A << 8)) : (A + (B << 8));
-}
-
-// Contribution of byte value b at relative offset r to the word sum.
-__device__ __forceinline__ uint32_t byte_term(uint32_t b, int r)
-{
-    return (r & 1) ? (b << 8) : b;
+    return odd ? (acc.s1 + (acc.s0 << 8)) : acc.s0;
 }
 
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t *p) { return *p; }

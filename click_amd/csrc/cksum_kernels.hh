@@ -15,6 +15,19 @@
 #pragma once
 #include "cksum_device.hh"
 
+#ifndef CLK_NT_LOADS
+#define CLK_NT_LOADS 0     // tuning knob: nontemporal chunk loads
+#endif
+#ifndef CLK_NT_STORES
+#define CLK_NT_STORES 0    // tuning knob: nontemporal checksum-field stores
+#endif
+#ifndef CLK_DIAG_NO_FIELD_STORE
+#define CLK_DIAG_NO_FIELD_STORE 0   // diagnostic builds only (results wrong)
+#endif
+#ifndef CLK_DIAG_NO_STATUS_STORE
+#define CLK_DIAG_NO_STATUS_STORE 0  // diagnostic builds only (results wrong)
+#endif
+
 namespace clk {
 
 struct BatchArgs {
@@ -50,7 +63,7 @@ constexpr uint32_t SET_OUTPUT1 = 1, SET_KILL = 2;
 // ---------------------------------------------------------------------------
 enum IpMode { IP_CHECK = 0, IP_CHECK_NOCKSUM = 1, IP_SET = 2 };
 
-template <int MODE>
+template <int MODE, bool DEFER>
 __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t offset,
                                                         const uint32_t *badsrc, uint32_t nbadsrc,
                                                         const uint32_t *gooddst, uint32_t ngooddst,
@@ -73,8 +86,9 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
             const uint32_t sh = (uint32_t)(a & 3);
             const uint8_t *q = (const uint8_t *)(a & ~3ull);
             const u32x4 d0 = *(const u32x4_a4 *)q;
-            uint32_t d4 = *(const uint32_t *)(q + 16);
-            uint32_t d5 = sh ? *(const uint32_t *)(q + 20) : 0u;
+            uint32_t d4, d5;
+            d4 = *(const uint32_t *)(q + 16);
+            d5 = sh ? *(const uint32_t *)(q + 20) : 0u;
             uint32_t h[5];
             h[0] = __builtin_amdgcn_alignbyte(d0[1], d0[0], sh);
             h[1] = __builtin_amdgcn_alignbyte(d0[2], d0[1], sh);
@@ -86,7 +100,7 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
             uint32_t sum = 0;
 #pragma unroll
             for (int k = 0; k < 5; k++)
-                sum += (h[k] & 0xFFFF) + (h[k] >> 16);
+                sum = dot_words(h[k], sum);
             if (MODE == IP_SET) {
                 if (hlen < 20 || hlen > plen) {
                     code = SET_KILL;
@@ -97,7 +111,10 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
                     }
                     sum -= h[2] >> 16;                 // ip_sum = 0 (setipchecksum.cc:85)
                     stored = in_cksum_fold(sum);       // setipchecksum.cc:86
-                    st_u16(ip + 10, stored);
+#if !CLK_DIAG_NO_FIELD_STORE
+                    if (!DEFER)                        // else field_scatter_kernel writes it
+                        st_u16(ip + 10, stored);
+#endif
                 }
             } else {
                 const uint32_t len = bswap16(h[0] >> 16);
@@ -149,22 +166,25 @@ __device__ __forceinline__ void load_pass(const uint8_t *c0, uint32_t nch, uint3
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const uint32_t idx = pass * (G * K) + (uint32_t)k * G + gl;
+#if CLK_NT_LOADS
+        v[k] = idx < nch ? __builtin_nontemporal_load((const u32x4 *)(c0 + 16ull * idx)) : u32x4{0, 0, 0, 0};
+#else
         v[k] = idx < nch ? *(const u32x4 *)(c0 + 16ull * idx) : u32x4{0, 0, 0, 0};
+#endif
     }
 }
 
 template <int G, int K>
-__device__ __forceinline__ void group_range_ab(const uint8_t *c0, uint32_t nch, uint32_t gl,
-                                               const u32x4 (&first)[K], uint64_t s, int len,
-                                               uint32_t &A, uint32_t &B)
+__device__ __forceinline__ uint32_t group_range_sum(const uint8_t *c0, uint32_t nch, uint32_t gl,
+                                                    const u32x4 (&first)[K], uint64_t s, int len)
 {
-    A = 0;
-    B = 0;
+    RangeAcc acc{0, 0};
+    const bool odd = (s & 1) != 0;
     const int rel0 = (int)((uint64_t)c0 - s);       // chunk 0 relative to s (<= 0)
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const uint32_t idx = (uint32_t)k * G + gl;
-        chunk_accumulate(first[k], rel0 + 16 * (int)idx, len, A, B);
+        chunk_accumulate(first[k], rel0 + 16 * (int)idx, len, odd, acc);
     }
     const uint32_t npass = (nch + G * K - 1) / (G * K);
     for (uint32_t p = 1; p < npass; p++) {
@@ -173,14 +193,16 @@ __device__ __forceinline__ void group_range_ab(const uint8_t *c0, uint32_t nch, 
 #pragma unroll
         for (int k = 0; k < K; k++) {
             const uint32_t idx = p * (G * K) + (uint32_t)k * G + gl;
-            chunk_accumulate(v[k], rel0 + 16 * (int)idx, len, A, B);
+            chunk_accumulate(v[k], rel0 + 16 * (int)idx, len, odd, acc);
         }
     }
 #pragma unroll
     for (int m = 1; m < G; m <<= 1) {
-        A += __shfl_xor(A, m, 64);
-        B += __shfl_xor(B, m, 64);
+        acc.s0 += __shfl_xor(acc.s0, m, 64);
+        if (odd)
+            acc.s1 += __shfl_xor(acc.s1, m, 64);
     }
+    return word_sum(acc, odd);
 }
 
 // clk_in_cksum: click_in_cksum(base+off_i, len_i) (lib/in_cksum.c:20-51).
@@ -197,10 +219,9 @@ __global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_s
         const uint32_t nch = len > 0 ? (uint32_t)(((s + (uint64_t)len + 15) & ~15ull) - (uint64_t)c0) / 16 : 0;
         u32x4 v[K];
         load_pass<G, K>(c0, nch, 0, gl, v);
-        uint32_t A, B;
-        group_range_ab<G, K>(c0, nch, gl, v, s, len, A, B);
+        const uint32_t sum = group_range_sum<G, K>(c0, nch, gl, v, s, len);
         if (gl == 0)
-            out_sum[i] = (uint16_t)in_cksum_fold(word_sum(A, B, s));
+            out_sum[i] = (uint16_t)in_cksum_fold(sum);
     }
 }
 
@@ -212,9 +233,9 @@ __global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_s
 // instruction), so one memory round trip serves the parse and the sum.
 // Header parse is speculative on ip_hl = 5; options are re-read.
 // ---------------------------------------------------------------------------
-template <int PROTO, bool SET, int G, int K>
+template <int PROTO, bool SET, int G, int K, bool DEFER>
 __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
-                                                 uint16_t *out_sum)
+                                                 uint16_t *out_sum, uint32_t *work)
 {
     constexpr int HDR_DW = PROTO == TCP ? 11 : 8;   // aligned dwords covering bytes [0, 40) / [0, 28)
     constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16; // uh_sum / th_sum offset in the transport header
@@ -335,11 +356,10 @@ __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_
         }
         const bool summing = (code == OK) && (rlen != 0 || plen_ph != 0 || SET);
         const uint64_t s = a + hl;
-        uint32_t A, B;
         // a lane whose packet needs no sum masks everything (len 0)
-        group_range_ab<G, K>(c0, nch, gl, v, s, summing ? rlen : 0, A, B);
-        if (gl == 0 && code == OK && summing) {
-            uint32_t sum = word_sum(A, B, s);
+        uint32_t sum = group_range_sum<G, K>(c0, nch, gl, v, s, summing ? rlen : 0);
+        // every lane holds the group's total; all lanes finish the packet
+        if (code == OK && summing) {
             if (SET) {
                 // the field was zeroed before summing (setudpchecksum.cc:64,
                 // settcpchecksum.cc:65): remove its bytes that lie in range
@@ -373,18 +393,56 @@ __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_
                 r = pseudohdr(csum, nh, b0, src, dst, proto, plen_ph);
             }
             if (SET) {
-                if (fix)
-                    nh[hl + 12] = (uint8_t)new_b12;
-                st_u16(nh + hl + FIELD, r);
                 stored = r;
+#if !CLK_DIAG_NO_FIELD_STORE
+                if (gl == 0) {
+                    if (fix)
+                        nh[hl + 12] = (uint8_t)new_b12;
+                    if (DEFER)       // the field is written by field_scatter_kernel
+                        work[i] = 0x80000000u | (hl << 16) | r;
+                    else
+                        st_u16(nh + hl + FIELD, r);
+                }
+#endif
             } else if (r != 0) {
                 code = L4_BAD_CHECKSUM;
             }
         }
         if (gl == 0) {
+#if !CLK_DIAG_NO_STATUS_STORE
             out_code[i] = (uint8_t)code;
+#else
+            if (code == 0xFF) out_code[i] = 0;
+#endif
+            if (SET && DEFER && code != OK)
+                work[i] = 0;
             if (SET && out_sum)
                 out_sum[i] = (uint16_t)stored;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Deferred Set stores.  Writing the 2-byte checksum field into the packet
+// while the same kernel streams packet bytes in costs far more than its
+// bytes (DESIGN.md "Set stores"); the two-phase Set computes in a read-only
+// pass (field value + transport offset into work[]) and this pass scatters
+// the fields: base + off_i + field_at(work) <- value for work bit 31.
+// FIELD_BASE: 10 for ip_sum (work = 0x80000000 | value), or the transport
+// field offset (6 / 16) added to the hl packed in work bits 16..23.
+// ---------------------------------------------------------------------------
+template <int FIELD_BASE, bool L4>
+__global__ void __launch_bounds__(256) field_scatter_kernel(BatchArgs b, const uint32_t *work,
+                                                            const uint8_t *status, const uint16_t *sums)
+{
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += nthreads) {
+        if (L4) {
+            const uint32_t w = work[i];
+            if (w & 0x80000000u)
+                st_u16(b.base + pkt_off(b, i) + ((w >> 16) & 0xFF) + FIELD_BASE, w & 0xFFFF);
+        } else if (status[i] == 0) {
+            st_u16(b.base + pkt_off(b, i) + FIELD_BASE, sums[i]);
         }
     }
 }

@@ -80,6 +80,11 @@ void *clk_ctx_stream(clk_ctx *ctx);
 void *clk_ctx_own_stream(clk_ctx *ctx);
 int clk_ctx_sync(clk_ctx *ctx);
 int clk_ctx_device(clk_ctx *ctx);
+/* Pre-size the context's device scratch for batches of up to max_packets
+ * (4 bytes per packet, used by the two-phase UDP/TCP Set); without it the
+ * first larger batch allocates synchronously.  After a reserve, batched
+ * calls of that size allocate nothing (safe inside hipGraph capture). */
+int clk_ctx_reserve(clk_ctx *ctx, uint64_t max_packets);
 /* Last error text for `ctx` (or for the calling thread when ctx == NULL). */
 const char *clk_last_error(clk_ctx *ctx);
 int clk_abi_version(void);

@@ -256,3 +256,23 @@ def test_full_size_properties(torch, ctx, proto, L, stride, n):
             assert np.array_equal(v == 0, ~sel)
         del arena
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_set_modes_bit_exact(torch, mode, monkeypatch):
+    """Fused (mode 0) and two-phase (mode 1, compute then scatter) Set
+    kernels give identical results on fuzzed batches."""
+    import click_amd
+    monkeypatch.setenv("CLK_SET_MODE", mode)
+    c = click_amd.Context(0)
+    rng = np.random.default_rng(31)
+    for proto in (17, 6):
+        arena, off, caplen, ml = fuzz.make_batch(rng, 1500, proto, max_total=1600)
+        for op in ("set_ip", OPS_L4[proto][1]):
+            compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=1)
+    n, L, stride = 4096, 1500, 1536
+    arena = np.zeros(n * stride, np.uint8)
+    oracle_lib.gen(arena, n, stride=stride, fixed_len=L)
+    for op in ("set_ip", "set_udp"):
+        compare(torch, c, op, arena, n, stride=stride, fixed_len=L)
+    c.close()

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Profile bench.py on the GPU box (run through gpurun from the repo root):
+#   1. rocprofv3 --kernel-trace --stats         (per-kernel durations)
+#   2. rocprofv3 --pmc FETCH_SIZE   (own pass)  (HBM read bytes)
+#   3. rocprofv3 --pmc WRITE_SIZE   (own pass)  (HBM write bytes)
+# then tools/pmc_summary.py writes profiles/<tag>/ and profiles/pmc_<wl>.json.
+# Usage: tools/profile.sh <tag> <workload> [bench args...]
+set -euo pipefail
+TAG=$1; WL=$2; shift 2
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_${TAG}_${WL}
+mkdir -p "$OUT"
+ARGS="--workload $WL --no-cpu --no-peak --no-c2 $*"
+# summaries land in gpurun_out/profiles/ (merged back); copy them into profiles/
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
+    python3 bench.py --steps 10 --warmup 2 $ARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
+    python3 bench.py --steps 3 --warmup 1 $ARGS > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
+    python3 bench.py --steps 3 --warmup 1 $ARGS > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
+python3 tools/pmc_summary.py "$OUT" "$TAG" "$WL" gpurun_out/profiles

@@ -1,0 +1,129 @@
+#!/usr/bin/env python3
+"""A/B tuning of kernel variants, interleaved in ONE process (guide rule 24).
+
+  python tools/tune.py --build                 # here: compile variant .so files
+  python tools/tune.py --workload c3 ...       # on the GPU box (via gpurun)
+
+Variants are compile-time flags (-DCLK_K, -DCLK_NT_LOADS) and/or the
+runtime tuning knobs read at context creation (CLK_MAX_BLOCKS,
+CLK_FORCE_GROUP).  Every variant runs the same element over the same
+device-resident batch; rounds interleave the variants; the median and min
+kernel time per variant are printed as JSON.
+"""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+VDIR = os.path.join(ROOT, "build", "variants")
+
+# name -> (compile flags, runtime env)
+VARIANTS = {
+    "base": ([], {}),
+    "k8": (["-DCLK_K=8"], {}),
+    "k16": (["-DCLK_K=16"], {}),
+    "nt": (["-DCLK_NT_LOADS=1"], {}),
+    "g16": ([], {"CLK_FORCE_GROUP": "16"}),
+    "g32": ([], {"CLK_FORCE_GROUP": "32"}),
+    "fused": ([], {"CLK_SET_MODE": "0"}),
+    "two": ([], {"CLK_SET_MODE": "1"}),
+    "mb8k": ([], {"CLK_MAX_BLOCKS": "8192"}),
+    "mb64k": ([], {"CLK_MAX_BLOCKS": "65536"}),
+    "mb1m": ([], {"CLK_MAX_BLOCKS": "1048576"}),
+    "diag_nofield": (["-DCLK_DIAG_NO_FIELD_STORE=1"], {}),
+}
+
+
+def lib_for(name):
+    flags, _ = VARIANTS[name]
+    if not flags or os.environ.get("TUNE_NO_VARIANT_LIBS"):
+        return os.path.join(ROOT, "click_amd", "libclick_amd_cksum.so")
+    return os.path.join(VDIR, "lib_%s.so" % name)
+
+
+def build(names):
+    from click_amd import build as b
+    b.build_library()
+    os.makedirs(VDIR, exist_ok=True)
+    for n in names:
+        flags, _ = VARIANTS[n]
+        if not flags:
+            continue
+        out = lib_for(n)
+        cmd = [b._hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-I" + os.path.join(ROOT, "include")] + flags + ["-o", out] + b.SOURCES
+        print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--workload", default="c3")
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--launches", type=int, default=5)
+    args = ap.parse_args()
+    names = args.variants.split(",")
+    if args.build:
+        build(names)
+        return
+    import torch
+    import click_amd
+    import bench
+    w = bench.WORKLOADS[args.workload]
+    n = w["n"]
+    arena = torch.empty(n * w["stride"], dtype=torch.uint8, device="cuda")
+    base_ctx = click_amd.Context(0)
+    b = click_amd.Batch(arena, n, stride=w["stride"], fixed_len=w["L"])
+    base_ctx.gen_packets(b, proto=w["proto"])
+    base_ctx.set_ip_checksum(b, want_sums=False)
+    status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    bench.run_element(base_ctx, "SetTCPChecksum" if w["proto"] == 6 else "SetUDPChecksum", b, status)
+    ctxs = {}
+    for nm in names:
+        _, env = VARIANTS[nm]
+        saved = {k: os.environ.get(k) for k in ("CLK_MAX_BLOCKS", "CLK_FORCE_GROUP", "CLK_SET_MODE")}
+        for k in saved:
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        ctxs[nm] = click_amd.Context(0, lib_path=lib_for(nm))
+        for k, v in saved.items():
+            if v is not None:
+                os.environ[k] = v
+            else:
+                os.environ.pop(k, None)
+    elements = {"SetUDPChecksum": lambda c: c.set_udp_checksum(b, status=status, want_sums=False),
+                "SetTCPChecksum": lambda c: c.set_tcp_checksum(b, status=status, want_sums=False),
+                "SetIPChecksum": lambda c: c.set_ip_checksum(b, status=status, want_sums=False),
+                "CheckUDPHeader": lambda c: c.check_udp_header(b, out=status),
+                "CheckTCPHeader": lambda c: c.check_tcp_header(b, out=status),
+                "CheckIPHeader": lambda c: c.check_ip_header(b, out=status)}
+    element = os.environ.get("TUNE_ELEMENT", w["elements"][-1])
+    run = elements[element]
+    times = {nm: [] for nm in names}
+    for r in range(args.rounds):
+        for nm in names:
+            c = ctxs[nm]
+            run(c)
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(args.launches):
+                run(c)
+            e.record()
+            torch.cuda.synchronize()
+            times[nm].append(s.elapsed_time(e) / args.launches)
+    alg = bench.ALG[element](w["L"]) * n
+    out = {nm: {"median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
+                "GBs": round(alg / (statistics.median(t) * 1e-3) / 1e9, 1)} for nm, t in times.items()}
+    print(json.dumps({"workload": args.workload, "element": element,
+                      "variants": out}))
+
+
+if __name__ == "__main__":
+    main()
