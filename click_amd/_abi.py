@@ -57,7 +57,7 @@ class clk_ip_check_cfg(ctypes.Structure):
 _P = ctypes.c_void_p
 _BP = ctypes.POINTER(clk_batch)
 
-# name -> (restype, argtypes); every symbol include/click_amd_cksum.h declares
+# name -> (restype, argtypes); every symbol include/*.h declares
 SIGNATURES = {
     "clk_abi_version": (ctypes.c_int, []),
     "clk_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
@@ -80,6 +80,15 @@ SIGNATURES = {
     "clk_gen_packets": (ctypes.c_int, [_P, _BP, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
     "clk_gen_corrupt": (ctypes.c_int, [_P, _BP, ctypes.c_uint64, ctypes.c_uint32]),
     "clk_read_stream": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P]),
+    # include/click_amd_elements.h
+    "clk_element_create": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                          ctypes.POINTER(_P)]),
+    "clk_element_destroy": (ctypes.c_int, [_P]),
+    "clk_element_push": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64]),
+    "clk_element_flush": (ctypes.c_int, [_P]),
+    "clk_element_results": (ctypes.c_uint64, [_P, _P, _P, _P, ctypes.c_uint64]),
+    "clk_element_read_handler": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
+    "clk_element_take_messages": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
 }
 
 _lib = None

@@ -3,6 +3,7 @@
 // selection (lanes per packet), launches on the context's stream.
 #include "cksum_kernels.hh"
 #include "../../include/click_amd_cksum.h"
+#include "internal.hh"
 
 #include <cstdarg>
 #include <cstdio>
@@ -296,6 +297,11 @@ int clk_ctx_sync(clk_ctx *ctx)
 }
 
 const char *clk_last_error(clk_ctx *ctx) { return ctx ? ctx->err : tls_err; }
+
+int clk_ctx_set_error_internal(clk_ctx *ctx, const char *msg)
+{
+    return fail(ctx, CLK_EINVAL, "%s", msg);
+}
 
 int clk_in_cksum(clk_ctx *ctx, const clk_batch *b, uint16_t *out_sum)
 {

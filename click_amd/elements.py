@@ -1,0 +1,92 @@
+"""Python handle on the batched GPU checksum elements (include/click_amd_elements.h).
+
+The element logic is C++ (click_amd/host/elements.cc); this is the binding
+a Python host (tests, bench) uses, as the Click adapter in INTEGRATION.md is
+the binding Click's tree uses.
+
+    ctx = click_amd.Context(0)
+    e = Element(ctx, "CheckIPHeader", "OFFSET 14, DETAILS true", noutputs=2)
+    e.push(frame_bytes_ndarray, nh_offset=14, token=7)
+    e.flush()
+    for token, port, length in e.results(): ...
+    e.read_handler("drop_details")
+"""
+import ctypes
+
+import numpy as np
+
+from . import _abi, ClickAmdError
+
+PORT_OUT0, PORT_OUT1, PORT_KILL = 0, 1, -1
+
+
+class Element:
+    def __init__(self, ctx, class_name, config="", name=None, noutputs=1):
+        self.ctx = ctx
+        self.lib = ctx.lib
+        h = ctypes.c_void_p()
+        rc = self.lib.clk_element_create(ctx.h, class_name.encode(), config.encode(),
+                                         name.encode() if name else None, noutputs, ctypes.byref(h))
+        if rc != 0:
+            raise ClickAmdError("%s(%s): %s" % (class_name, config, (self.lib.clk_last_error(ctx.h) or b"").decode()))
+        self.h = h
+        self._keep = []          # host buffers that must outlive flush()
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.clk_element_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def push(self, buf, length=None, nh_offset=-1, token=0):
+        """buf: a writable uint8 numpy array (or view) holding the packet."""
+        length = buf.size if length is None else length
+        self._keep.append(buf)
+        rc = self.lib.clk_element_push(self.h, buf.ctypes.data_as(ctypes.c_void_p), length, nh_offset, token)
+        if rc < 0:
+            raise ClickAmdError("push failed: %d" % rc)
+        return rc == 1
+
+    def push_ptr(self, ptr, length, nh_offset=-1, token=0):
+        rc = self.lib.clk_element_push(self.h, ctypes.c_void_p(ptr), length, nh_offset, token)
+        if rc < 0:
+            raise ClickAmdError("push failed: %d" % rc)
+        return rc == 1
+
+    def flush(self):
+        rc = self.lib.clk_element_flush(self.h)
+        if rc != 0:
+            raise ClickAmdError("flush failed: %d" % rc)
+        self._keep = []
+
+    def results(self, cap=1 << 20):
+        out = []
+        while True:
+            t = np.zeros(cap, np.uint64)
+            p = np.zeros(cap, np.int32)
+            ln = np.zeros(cap, np.uint32)
+            n = self.lib.clk_element_results(self.h, t.ctypes.data_as(ctypes.c_void_p),
+                                             p.ctypes.data_as(ctypes.c_void_p), ln.ctypes.data_as(ctypes.c_void_p),
+                                             cap)
+            out.append((t[:n], p[:n], ln[:n]))
+            if n < cap:
+                break
+        return (np.concatenate([o[0] for o in out]), np.concatenate([o[1] for o in out]),
+                np.concatenate([o[2] for o in out]))
+
+    def read_handler(self, name):
+        buf = ctypes.create_string_buffer(1 << 16)
+        n = self.lib.clk_element_read_handler(self.h, name.encode(), buf, len(buf))
+        if n < 0:
+            raise ClickAmdError("no handler %s" % name)
+        return buf.value.decode()
+
+    def messages(self):
+        buf = ctypes.create_string_buffer(1 << 20)
+        self.lib.clk_element_take_messages(self.h, buf, len(buf))
+        return [m for m in buf.value.decode().split("\n") if m]

@@ -1,0 +1,199 @@
+// elements.hh -- host-side C++ element glue for the GPU checksum path.
+//
+// Each class keeps the reference element's configuration keywords, routing
+// (output 0 / output 1 / kill), counters, handlers and click_chatter text,
+// and runs the checksum work as one GPU batch per flush() through the C ABI
+// (include/click_amd_cksum.h).  See include/click_amd_elements.h.
+#pragma once
+#include <cstdint>
+#include <deque>
+#include <string>
+#include <vector>
+
+#include "../../include/click_amd_cksum.h"
+
+namespace clk {
+namespace host {
+
+struct Result {
+    uint64_t token;
+    int32_t port;        // 0, 1, or -1 (kill)
+    uint32_t length;     // packet length after the element
+};
+
+// Click-style configuration: comma-separated arguments, "KEYWORD value".
+struct ConfArgs {
+    std::vector<std::pair<std::string, std::string>> kw;   // keyword arguments
+    std::vector<std::string> pos;                          // positional arguments
+    static bool split(const std::string &conf, ConfArgs *out, std::string *err);
+    bool take(const char *key, std::string *value);        // removes it
+};
+bool parse_bool(const std::string &s, bool *v);
+bool parse_int(const std::string &s, long *v);
+bool parse_ip(const std::string &s, uint32_t *saddr);       // raw network-order s_addr
+bool parse_prefix(const std::string &s, uint32_t *saddr, uint32_t *mask);
+
+class BatchElement {
+  public:
+    BatchElement(clk_ctx *ctx, const std::string &name, int noutputs);
+    virtual ~BatchElement();
+    virtual const char *class_name() const = 0;
+    virtual int configure(ConfArgs &args, std::string *err);
+    int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token);
+    int flush();
+    uint64_t pop_results(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint64_t cap);
+    virtual std::string read_handler(const std::string &h) const;
+    std::string take_messages();
+    const std::string &name() const { return name_; }
+    std::string declaration() const { return name_ + " :: " + class_name(); }
+    const std::string &last_error() const { return err_; }
+    size_t pending() const { return pend_.size(); }
+
+  protected:
+    struct Pending {
+        uint8_t *data;
+        uint32_t length;
+        int32_t nh_off;
+        uint64_t token;
+        int32_t host_code;   // >= 0: decided on the host (not staged)
+        uint64_t slot;       // staging offset of the span
+        uint32_t span_off;   // span start relative to data
+        uint32_t span_len;
+    };
+    // Bytes the kernel needs, relative to data; return false to decide on the
+    // host with *code (routed like a kernel result).
+    virtual bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const = 0;
+    virtual int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) = 0;
+    virtual void route(Pending &p, int code, uint16_t sum, Result *r) = 0;
+    virtual bool wants_sums() const { return false; }
+    void chatter(const std::string &s) { msgs_.push_back(s); }
+    static uint32_t be16(const uint8_t *p) { return (uint32_t(p[0]) << 8) | p[1]; }
+
+    clk_ctx *ctx_;
+    std::string name_;
+    int noutputs_;
+    uint32_t batch_cap_ = 65536;
+    std::string err_;
+    uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0;
+
+  private:
+    int grow_host(size_t bytes, size_t n);
+    int grow_dev(size_t bytes, size_t n);
+    std::vector<Pending> pend_;
+    std::deque<Result> results_;
+    std::vector<std::string> msgs_;
+    uint8_t *h_arena_ = nullptr;
+    size_t h_arena_cap_ = 0, h_used_ = 0;
+    uint64_t *h_off_ = nullptr;
+    uint32_t *h_len_ = nullptr;
+    uint8_t *h_codes_ = nullptr;
+    uint16_t *h_sums_ = nullptr;
+    size_t h_n_cap_ = 0;
+    uint8_t *d_arena_ = nullptr;
+    size_t d_arena_cap_ = 0;
+    uint64_t *d_off_ = nullptr;
+    uint32_t *d_len_ = nullptr;
+    uint8_t *d_codes_ = nullptr;
+    uint16_t *d_sums_ = nullptr;
+    size_t d_n_cap_ = 0;
+    void *ev_[2] = {nullptr, nullptr};
+};
+
+// Check elements share drop(): elements/ip/checkipheader.cc:143-159 and the
+// CheckUDPHeader/CheckTCPHeader copies of it.
+class CheckElement : public BatchElement {
+  public:
+    using BatchElement::BatchElement;
+    std::string read_handler(const std::string &h) const override;
+
+  protected:
+    virtual const char *const *reason_texts() const = 0;
+    virtual int nreasons() const = 0;
+    virtual std::string drop_message(const char *reason) const = 0;
+    int drop(int reason);   // returns the port
+    int conf_verbose_details(ConfArgs &args, std::string *err);
+    bool verbose_ = false;
+    bool details_ = false;
+    uint32_t drops_ = 0;
+    std::vector<uint32_t> reason_drops_;
+};
+
+class CheckIPHeader : public CheckElement {
+  public:
+    CheckIPHeader(clk_ctx *ctx, const std::string &name, int noutputs, bool checksum_default = true);
+    ~CheckIPHeader() override;
+    const char *class_name() const override { return checksum_default_ ? "CheckIPHeader" : "CheckIPHeader2"; }
+    int configure(ConfArgs &args, std::string *err) override;
+
+  protected:
+    bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
+    int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
+    void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    const char *const *reason_texts() const override;
+    int nreasons() const override { return 6; }
+    std::string drop_message(const char *reason) const override;
+
+  private:
+    bool checksum_default_;
+    bool checksum_ = true;
+    uint32_t offset_ = 0;
+    std::vector<uint32_t> bad_src_, good_dst_;
+    uint32_t *d_lists_ = nullptr;
+};
+
+class SetIPChecksum : public BatchElement {
+  public:
+    using BatchElement::BatchElement;
+    const char *class_name() const override { return "SetIPChecksum"; }
+    std::string read_handler(const std::string &h) const override;
+
+  protected:
+    bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
+    int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
+    void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    bool wants_sums() const override { return true; }
+
+  private:
+    uint32_t drops_ = 0;
+};
+
+class CheckL4Header : public CheckElement {
+  public:
+    CheckL4Header(clk_ctx *ctx, const std::string &name, int noutputs, int proto);
+    const char *class_name() const override { return proto_ == 17 ? "CheckUDPHeader" : "CheckTCPHeader"; }
+    int configure(ConfArgs &args, std::string *err) override;
+
+  protected:
+    bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
+    int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
+    void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    const char *const *reason_texts() const override;
+    int nreasons() const override { return 3; }
+    std::string drop_message(const char *reason) const override;
+
+  private:
+    int proto_;
+};
+
+class SetL4Checksum : public BatchElement {
+  public:
+    SetL4Checksum(clk_ctx *ctx, const std::string &name, int noutputs, int proto);
+    const char *class_name() const override { return proto_ == 17 ? "SetUDPChecksum" : "SetTCPChecksum"; }
+    int configure(ConfArgs &args, std::string *err) override;
+
+  protected:
+    bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
+    int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
+    void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    bool wants_sums() const override { return true; }
+
+  private:
+    int proto_;
+    bool fixoff_ = false;
+    bool warned_ = false;   // router()->force_attachment("SetUDPChecksum_message")
+};
+
+BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::string &name, int noutputs);
+
+} // namespace host
+} // namespace clk

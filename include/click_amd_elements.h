@@ -1,0 +1,87 @@
+/*
+ * click_amd_elements.h -- C ABI of the batched, GPU-backed checksum elements.
+ *
+ * The host-side element glue (click_amd/host/elements.{hh,cc}, C++) keeps
+ * the semantics of Click's element classes -- configuration keywords,
+ * output-0/output-1/kill routing, `drops`/`drop_details` handlers and the
+ * click_chatter messages -- while the checksum work runs on the GPU through
+ * include/click_amd_cksum.h.  Packets are HOST packets (Click's Packet
+ * data(), as a DPDK/pcap source hands them over): push() gathers their
+ * bytes into a pinned struct-of-arrays staging batch, flush() copies the
+ * batch to HBM, runs the element kernel, copies verdicts/checksums back,
+ * writes Set results into the host packets and routes every packet.
+ *
+ * Click's Element API is one packet at a time (element.cc:2891-2972); the
+ * Click-side adapter that turns push(port, Packet*) into these calls --
+ * holding packets until flush, flushing on batch-full, timer and
+ * router stop -- is in INTEGRATION.md.
+ *
+ * Classes (same names and keywords as the reference):
+ *   CheckIPHeader   INTERFACES, BADSRC, GOODDST, OFFSET, VERBOSE, DETAILS,
+ *                   CHECKSUM; legacy positional [BADSRC,] OFFSET
+ *                                      (elements/ip/checkipheader.cc:87-141)
+ *   CheckIPHeader2  as CheckIPHeader, never checksums (checkipheader2.cc)
+ *   SetIPChecksum   (no keywords)      (elements/ip/setipchecksum.cc)
+ *   CheckUDPHeader  VERBOSE, DETAILS   (elements/tcpudp/checkudpheader.cc:50-64)
+ *   SetUDPChecksum  (no keywords)      (elements/tcpudp/setudpchecksum.cc)
+ *   CheckTCPHeader  VERBOSE, DETAILS   (elements/tcpudp/checktcpheader.cc:50-64)
+ *   SetTCPChecksum  [FIXOFF]           (elements/tcpudp/settcpchecksum.cc:36-42)
+ * plus glue keywords BATCH (packets per GPU batch, default 65536).
+ */
+#ifndef CLICK_AMD_ELEMENTS_H
+#define CLICK_AMD_ELEMENTS_H
+#include <stdint.h>
+#include <stddef.h>
+#include "click_amd_cksum.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct clk_element clk_element;
+
+/* Where a flushed packet goes (the reference's routing). */
+enum clk_port {
+    CLK_PORT_OUT0 = 0,        /* output(0).push(p)                          */
+    CLK_PORT_OUT1 = 1,        /* output(1).push(p) (drop port / SetUDP short) */
+    CLK_PORT_KILL = -1        /* p->kill()                                   */
+};
+
+/* name: the element's name in messages (Click's name(); NULL = class name);
+ * noutputs: 1 or 2 (whether output 1 is connected).
+ * Returns CLK_EINVAL with clk_last_error(ctx) set on a configure error,
+ * worded like the reference's ErrorHandler messages.                      */
+int clk_element_create(clk_ctx *ctx, const char *class_name, const char *config,
+                       const char *name, int noutputs, clk_element **out);
+int clk_element_destroy(clk_element *e);
+
+/* Stage one host packet.  data/length = Packet::data()/length();
+ * nh_offset = network_header_offset() (-1 = no network header: the IP
+ * elements then use data(), as SetIPChecksum does, setipchecksum.cc:78).
+ * Set elements write their result into `data` at flush(), so the packet
+ * memory must stay valid until then.  Returns 1 when the batch is full and
+ * should be flushed, 0 otherwise, < 0 on error.                            */
+int clk_element_push(clk_element *e, uint8_t *data, uint32_t length, int32_t nh_offset,
+                     uint64_t token);
+
+/* Run the staged batch on the GPU and route it (synchronous).  Results are
+ * appended to the element's result queue in push order.                  */
+int clk_element_flush(clk_element *e);
+
+/* Pop up to `cap` results: token, port (enum clk_port) and the packet's
+ * new length (CheckIPHeader trims to ip_len, checkipheader.cc:216-217;
+ * otherwise unchanged).  Returns the number popped.                        */
+uint64_t clk_element_results(clk_element *e, uint64_t *tokens, int32_t *ports,
+                             uint32_t *lengths, uint64_t cap);
+
+/* Handler text, as Click's read handlers print it ("drops",
+ * "drop_details", plus the glue's "batches", "packets", "gpu_ns").
+ * Returns the full length (may exceed cap-1; output is NUL-terminated).   */
+int clk_element_read_handler(clk_element *e, const char *handler, char *buf, size_t cap);
+
+/* Pop the click_chatter lines the element produced, '\n'-separated. */
+int clk_element_take_messages(clk_element *e, char *buf, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CLICK_AMD_ELEMENTS_H */

@@ -13,12 +13,16 @@ from click_amd import _abi, build
 
 ROOT = build.ROOT
 HEADER = os.path.join(ROOT, "include", "click_amd_cksum.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "click_amd_elements.h")]
 
 
 def declared_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(clk_[a-z0-9_]+)\s*\(", text)))
+    names = set()
+    for h in HEADERS:
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names |= set(re.findall(r"\b(clk_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
 
 
 def test_library_builds_for_gfx950():
@@ -33,7 +37,7 @@ def test_library_builds_for_gfx950():
 def test_library_exports_every_declared_symbol():
     lib = _abi.load()
     names = declared_functions()
-    assert len(names) >= 18
+    assert len(names) >= 26
     for name in names:
         assert hasattr(lib, name), name
         assert name in _abi.SIGNATURES, "ctypes binding lacks " + name
@@ -86,7 +90,7 @@ def test_header_is_plain_c():
     """The boundary header compiles as C99 with no C++ or torch types."""
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "h.c")
-        open(c, "w").write('#include "click_amd_cksum.h"\nint main(void){return 0;}\n')
+        open(c, "w").write('#include "click_amd_cksum.h"\n#include "click_amd_elements.h"\nint main(void){return 0;}\n')
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-pedantic", "-I", os.path.dirname(HEADER),
                         "-c", "-o", os.path.join(d, "h.o"), c], check=True)
     text = open(HEADER).read()

@@ -1,0 +1,202 @@
+"""GPU tests of the host element glue (click_amd/host/elements.cc): the
+batched elements route, count, trim, write back and chatter exactly as the
+reference elements would, packet by packet (the oracle decides each packet;
+the routing rules are the reference's: checkipheader.cc:143-159,
+setipchecksum.cc:88-93, setudpchecksum.cc:48-61, settcpchecksum.cc:71-74)."""
+import numpy as np
+import pytest
+
+from tests import oracle_lib, fuzz
+
+pytestmark = pytest.mark.gpu
+
+IP_REASONS = ["tiny packet", "bad IP version", "bad IP header length", "bad IP length", "bad IP checksum",
+              "bad source address"]
+UDP_REASONS = ["not UDP", "bad packet length", "bad UDP checksum"]
+TCP_REASONS = ["not TCP", "bad packet length", "bad TCP checksum"]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import click_amd
+    c = click_amd.Context(0)
+    yield c
+    c.close()
+
+
+def frames(rng, n, proto, max_total=1600, eth=14):
+    """Ethernet-framed fuzzed packets in one arena: frame i at foff[i],
+    flen[i] bytes, L3 at foff[i] + eth."""
+    arena3, off3, cap3, _ = fuzz.make_batch(rng, n, proto, max_total=max_total)
+    flen = (cap3 + eth).astype(np.uint32)
+    foff = np.zeros(n, np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(rng.integers(0, 8)) * 2
+        foff[i] = pos
+        pos += int(flen[i]) + 4
+    arena = np.zeros(pos + 64, np.uint8)
+    for i in range(n):
+        o = int(foff[i])
+        arena[o:o + eth] = rng.integers(0, 256, eth, dtype=np.uint8)
+        arena[o + eth:o + flen[i]] = arena3[int(off3[i]):int(off3[i]) + int(cap3[i])]
+    return arena, foff, flen
+
+
+def run_element(ctx, cls, config, arena, foff, flen, nh, noutputs, batch=None):
+    from click_amd.elements import Element
+    e = Element(ctx, cls, config + ((", BATCH %d" % batch) if batch else ""), name="e0", noutputs=noutputs)
+    base = arena.ctypes.data
+    for i in range(len(foff)):
+        full = e.push_ptr(base + int(foff[i]), int(flen[i]), nh, token=i)
+        if full:
+            e.flush()
+    e.flush()
+    tok, port, ln = e.results()
+    assert np.array_equal(tok, np.arange(len(foff))), "results out of push order"
+    return e, port, ln
+
+
+def expected_drop_messages(name_prefix, codes, reasons, verbose):
+    msgs = []
+    drops = 0
+    for c in codes:
+        if c:
+            if drops == 0 or verbose:
+                msgs.append(name_prefix + reasons[c - 1])
+            drops += 1
+    return msgs
+
+
+@pytest.mark.parametrize("noutputs,verbose", [(2, False), (1, True)])
+def test_check_ip_header_element(ctx, noutputs, verbose):
+    rng = np.random.default_rng(100 + noutputs)
+    arena, foff, flen = frames(rng, 2500, 17)
+    e, port, ln = run_element(ctx, "CheckIPHeader", "OFFSET 14, DETAILS true, VERBOSE %s" % str(verbose).lower(),
+                              arena, foff, flen, -1, noutputs, batch=700)
+    L = oracle_lib.load_oracle()
+    codes = np.array([L.oracle_check_ip_header(arena.ctypes.data + int(foff[i]), int(flen[i]), 14, 1,
+                                               None, 0, None, 0) for i in range(len(foff))])
+    exp_port = np.where(codes == 0, 0, 1 if noutputs == 2 else -1)
+    assert np.array_equal(port, exp_port)
+    for i in np.nonzero(codes == 0)[0]:
+        o = int(foff[i])
+        ip_len = (int(arena[o + 16]) << 8) | int(arena[o + 17])
+        assert ln[i] == min(int(flen[i]), 14 + ip_len)
+    assert e.read_handler("drops") == str(int((codes != 0).sum()))
+    det = e.read_handler("drop_details").splitlines()
+    assert det == ["%d\t%s" % (int((codes == k + 1).sum()), IP_REASONS[k]) for k in range(6)]
+    assert e.messages() == expected_drop_messages("e0: IP header check failed: ", codes, IP_REASONS, verbose)
+    assert int(e.read_handler("packets")) == len(foff) and int(e.read_handler("batches")) >= 4
+
+
+def test_check_ip_header_interfaces(ctx):
+    """INTERFACES 18.26.4.1/24 (checkipheader.cc:51-74): broadcast and 0/255
+    sources are bad unless the destination is one of the interfaces."""
+    from click_amd.elements import Element
+    rng = np.random.default_rng(5)
+    n = 400
+    arena = np.zeros(n * 64, np.uint8)
+    oracle_lib.gen(arena, n, stride=64, fixed_len=40, proto=17)
+    srcs = [b"\x12\x1a\x04\xff", b"\x00\x00\x00\x00", b"\xff\xff\xff\xff", b"\x0a\x00\x00\x01"]
+    dsts = [b"\x12\x1a\x04\x01", b"\x12\x1a\x07\x01", b"\x0a\x00\x00\x02"]
+    for i in range(n):
+        arena[i * 64 + 12:i * 64 + 16] = np.frombuffer(srcs[rng.integers(0, 4)], np.uint8)
+        arena[i * 64 + 16:i * 64 + 20] = np.frombuffer(dsts[rng.integers(0, 3)], np.uint8)
+    oracle_lib.batch("set_ip", arena, n, stride=64, fixed_len=40)
+    e = Element(ctx, "CheckIPHeader", "INTERFACES 18.26.4.1/24 18.26.7.1/24", noutputs=2)
+    for i in range(n):
+        e.push_ptr(arena.ctypes.data + i * 64, 40, -1, i)
+    e.flush()
+    _, port, _ = e.results()
+    bad = [bytes(arena[i * 64 + 12:i * 64 + 16]) in srcs[:3] and
+           bytes(arena[i * 64 + 16:i * 64 + 20]) not in dsts[:2] for i in range(n)]
+    assert np.array_equal(port, np.where(bad, 1, 0))
+    assert sum(bad) > 0
+
+
+def test_set_ip_checksum_element(ctx):
+    rng = np.random.default_rng(7)
+    arena, foff, flen = frames(rng, 2000, 6)
+    ref = arena.copy()
+    e, port, ln = run_element(ctx, "SetIPChecksum", "", arena, foff, flen, 14, 1)
+    codes, _ = oracle_lib.batch("set_ip", ref, len(foff), off=foff + 14, length=flen - 14)
+    assert np.array_equal(port, np.where(codes == 0, 0, -1))
+    assert np.array_equal(arena, ref)
+    assert e.read_handler("drops") == str(int((codes != 0).sum()))
+    assert e.messages() == (["SetIPChecksum: bad input packet"] if (codes != 0).any() else [])
+
+
+@pytest.mark.parametrize("proto", [17, 6])
+@pytest.mark.parametrize("noutputs", [1, 2])
+def test_check_l4_element(ctx, proto, noutputs):
+    rng = np.random.default_rng(proto + 10 * noutputs)
+    arena, foff, flen = frames(rng, 2500, proto)
+    cls = "CheckUDPHeader" if proto == 17 else "CheckTCPHeader"
+    e, port, ln = run_element(ctx, cls, "DETAILS true", arena, foff, flen, 14, noutputs, batch=1000)
+    codes, _ = oracle_lib.batch("check_udp" if proto == 17 else "check_tcp", arena.copy(), len(foff),
+                                off=foff + 14, length=flen - 14)
+    assert np.array_equal(port, np.where(codes == 0, 0, 1 if noutputs == 2 else -1))
+    assert np.array_equal(ln, flen)
+    reasons = UDP_REASONS if proto == 17 else TCP_REASONS
+    det = e.read_handler("drop_details").splitlines()
+    assert det == ["%d\t%s" % (int((codes == k + 1).sum()), reasons[k]) for k in range(3)]
+    prefix = "UDP header check failed: " if proto == 17 else "e0 :: CheckTCPHeader: TCP header check failed: "
+    assert e.messages() == expected_drop_messages(prefix, codes, reasons, False)
+
+
+@pytest.mark.parametrize("proto,config,noutputs", [(17, "", 1), (17, "", 2), (6, "", 1), (6, "FIXOFF true", 1),
+                                                   (6, "true", 1)])
+def test_set_l4_element(ctx, proto, config, noutputs):
+    rng = np.random.default_rng(proto * 3 + noutputs + len(config))
+    arena, foff, flen = frames(rng, 2500, proto)
+    ref = arena.copy()
+    cls = "SetUDPChecksum" if proto == 17 else "SetTCPChecksum"
+    e, port, ln = run_element(ctx, cls, config, arena, foff, flen, 14, noutputs)
+    fix = 1 if "true" in config else 0
+    codes, _ = oracle_lib.batch("set_udp" if proto == 17 else "set_tcp", ref, len(foff), off=foff + 14,
+                                length=flen - 14, arg=fix)
+    if proto == 17:
+        exp = np.where(codes == 0, 0, 1 if noutputs == 2 else -1)
+    else:
+        exp = np.where(codes == 0, 0, -1)
+    assert np.array_equal(port, exp)
+    assert np.array_equal(arena, ref)
+    m = e.messages()
+    if proto == 17:
+        assert m == (["e0 :: SetUDPChecksum: fragment or short packet"] if noutputs == 1 and (codes != 0).any()
+                     else [])
+    else:
+        assert m == ["SetTCPChecksum: bad lengths"] * int((codes != 0).sum())
+
+
+def test_no_network_header(ctx):
+    """Without a network header CheckUDPHeader drops NOT_UDP
+    (checkudpheader.cc:91-92) and SetTCPChecksum kills (settcpchecksum.cc:53)."""
+    from click_amd.elements import Element
+    buf = np.zeros(100, np.uint8)
+    e = Element(ctx, "CheckUDPHeader", "DETAILS true", noutputs=2)
+    e.push(buf, nh_offset=-1, token=3)
+    e.flush()
+    t, p, _ = e.results()
+    assert list(t) == [3] and list(p) == [1]
+    assert e.read_handler("drop_details").splitlines()[0] == "1\tnot UDP"
+    e2 = Element(ctx, "SetTCPChecksum", "", noutputs=1)
+    e2.push(buf, nh_offset=-1, token=4)
+    e2.flush()
+    assert list(e2.results()[1]) == [-1]
+
+
+def test_configure_errors(ctx):
+    from click_amd import ClickAmdError
+    from click_amd.elements import Element
+    for cls, conf in [("CheckIPHeader", "OFFSET x"), ("CheckIPHeader", "BOGUS 1"), ("CheckUDPHeader", "5"),
+                      ("SetTCPChecksum", "FIXOFF maybe"), ("NoSuchElement", ""),
+                      ("CheckIPHeader", "INTERFACES 1.2.3.4"), ("CheckUDPHeader", "VERBOSE True")]:
+        with pytest.raises(ClickAmdError):
+            Element(ctx, cls, conf)
+    Element(ctx, "CheckIPHeader2", "14")
+    Element(ctx, "CheckIPHeader", "CHECKSUM false, OFFSET 14, VERBOSE true")
