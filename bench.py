@@ -262,6 +262,95 @@ def summarize(r, steps, wname):
     }
 
 
+def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24, glue_pkts=1 << 18):
+    """End-to-end rates with the packets in HOST memory (DESIGN.md "E2E").
+
+    (a) device C ABI over pinned SoA chunks: per chunk, hipMemcpyAsync H2D of
+        the packet slots, the element kernel, D2H of the 1 B verdicts (and
+        2 B checksums for Set), double-buffered on two streams so chunk k+1's
+        H2D overlaps chunk k's kernel and D2H;
+    (b) the host element glue (click_amd/host/elements.cc) fed one packet
+        at a time, as a Click element would be: gather into pinned staging,
+        H2D, kernel, D2H, route -- single host thread."""
+    import click_amd
+    from click_amd.elements import Element
+    w = WORKLOADS[wname]
+    L, stride = w["L"], w["stride"]
+    host = torch.empty(chunk_pkts * stride * 2, dtype=torch.uint8, pin_memory=True)
+    dev = [torch.empty(chunk_pkts * stride, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    status = [torch.empty(chunk_pkts, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    sums = [torch.empty(chunk_pkts, dtype=torch.uint16, device="cuda") for _ in range(2)]
+    # host packets: generate on the GPU, copy down once
+    g = click_amd.Batch(dev[0], chunk_pkts, stride=stride, fixed_len=L)
+    ctx.gen_packets(g, proto=w["proto"])
+    ctx.set_ip_checksum(g, want_sums=False)
+    run_element(ctx, "SetTCPChecksum" if w["proto"] == 6 else "SetUDPChecksum", g, status[0])
+    torch.cuda.synchronize()
+    host[:chunk_pkts * stride].copy_(dev[0])
+    host[chunk_pkts * stride:].copy_(dev[0])
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    # one context per stream: a context's scratch is not shared across streams
+    ctxs = [click_amd.Context(ctx.device, stream=st) for st in streams]
+    for c in ctxs:
+        c.reserve(chunk_pkts)
+    is_set = element.startswith("Set")
+
+    def chunk(k):
+        j = k % 2
+        st = streams[j]
+        c = ctxs[j]
+        with torch.cuda.stream(st):
+            src = host[(k % 2) * chunk_pkts * stride:(k % 2 + 1) * chunk_pkts * stride]
+            dev[j].copy_(src, non_blocking=True)
+            b = click_amd.Batch(dev[j], chunk_pkts, stride=stride, fixed_len=L)
+            if is_set:
+                {"SetUDPChecksum": c.set_udp_checksum, "SetTCPChecksum": c.set_tcp_checksum,
+                 "SetIPChecksum": c.set_ip_checksum}[element](b, status=status[j], sums=sums[j])
+                out_h[j * chunk_pkts * 3:(j * 3 + 2) * chunk_pkts].view(torch.uint16).copy_(sums[j], non_blocking=True)
+            else:
+                run_element(c, element, b, status[j])
+            out_h[(j * 3 + 2) * chunk_pkts:(j * 3 + 3) * chunk_pkts].copy_(status[j], non_blocking=True)
+
+    out_h = torch.empty(chunk_pkts * 6, dtype=torch.uint8, pin_memory=True)
+    chunk(0)
+    chunk(1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(nchunks):
+        chunk(k)
+    torch.cuda.synchronize()
+    dt_a = time.perf_counter() - t0
+    for c in ctxs:
+        c.close()
+    pk_a = chunk_pkts * nchunks
+    ok_a = int((out_h[2 * chunk_pkts:3 * chunk_pkts] == 0).sum())
+    # (b) element glue, one packet at a time
+    e = Element(ctx, element, "BATCH %d" % glue_pkts, noutputs=2)
+    base = host.data_ptr()
+    nh = 0 if element in ("CheckIPHeader", "SetIPChecksum") else 0
+    t0 = time.perf_counter()
+    for i in range(glue_pkts):
+        e.push_ptr(base + i * stride, L, nh, i)
+    e.flush()
+    dt_b = time.perf_counter() - t0
+    _, ports, _ = e.results()
+    ok_b = int((ports == 0).sum())
+    gpu_ns = int(e.read_handler("gpu_ns"))
+    e.close()
+    return {
+        "metric": "end-to-end (host-resident packets) GiB/s checksummed", "element": element,
+        "workload": w["desc"],
+        "pinned_soa": {"value": round(pk_a * L / dt_a / GIB, 2), "unit": "GiB/s", "mpps": round(pk_a / dt_a / 1e6, 1),
+                       "pcie_GBs": round(pk_a * (stride + (3 if is_set else 1)) / dt_a / 1e9, 1),
+                       "packets": pk_a, "chunk_packets": chunk_pkts, "ok": ok_a,
+                       "note": "H2D of slots + kernel + D2H of verdicts/checksums, 2 streams"},
+        "element_glue": {"value": round(glue_pkts * L / dt_b / GIB, 3), "unit": "GiB/s",
+                         "mpps": round(glue_pkts / dt_b / 1e6, 3), "packets": glue_pkts, "ok": ok_b,
+                         "gpu_ms": round(gpu_ns / 1e6, 3), "wall_ms": round(dt_b * 1e3, 3),
+                         "note": "per-packet push (gather memcpy into pinned staging), 1 host thread"},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -272,6 +361,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-peak", action="store_true", help="skip the read-stream ceiling")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--e2e", action="store_true", help="measure the host-resident end-to-end rates instead")
     args = ap.parse_args()
 
     import torch
@@ -286,6 +376,13 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     ctx = click_amd.Context(local)
+    if args.e2e:
+        w = WORKLOADS[args.workload]
+        res = [e2e(torch, ctx, args.workload, el) for el in w["elements"]]
+        if rank == 0:
+            print(json.dumps({"e2e": res}), flush=True)
+        ctx.close()
+        return
 
     main_res = measure(torch, ctx, dist, rank, world, args.workload, args.steps, args.warmup)
     c2 = None
