@@ -58,6 +58,19 @@ class Element:
             raise ClickAmdError("push failed: %d" % rc)
         return rc == 1
 
+    def push_burst(self, ptrs, lengths, nh_offsets=None, first_token=0):
+        """ptrs: uint64 array of packet addresses; lengths: uint32 array;
+        nh_offsets: int32 array or None.  Flushes whenever the batch fills."""
+        ptrs = np.ascontiguousarray(ptrs, np.uint64)
+        lengths = np.ascontiguousarray(lengths, np.uint32)
+        nh = None if nh_offsets is None else np.ascontiguousarray(nh_offsets, np.int32)
+        rc = self.lib.clk_element_push_burst(self.h, ptrs.ctypes.data_as(ctypes.c_void_p),
+                                             lengths.ctypes.data_as(ctypes.c_void_p),
+                                             None if nh is None else nh.ctypes.data_as(ctypes.c_void_p),
+                                             first_token, len(ptrs))
+        if rc != 0:
+            raise ClickAmdError("push_burst failed: %d" % rc)
+
     def flush(self):
         rc = self.lib.clk_element_flush(self.h)
         if rc != 0:

@@ -813,6 +813,21 @@ int clk_element_push(clk_element *w, uint8_t *data, uint32_t length, int32_t nh_
     return w->e->push(data, length, nh_offset, token);
 }
 
+int clk_element_push_burst(clk_element *w, uint8_t *const *datas, const uint32_t *lengths,
+                           const int32_t *nh_offsets, uint64_t first_token, uint32_t n)
+{
+    if (!w || (n && (!datas || !lengths)))
+        return CLK_EINVAL;
+    for (uint32_t k = 0; k < n; k++) {
+        int r = w->e->push(datas[k], lengths[k], nh_offsets ? nh_offsets[k] : -1, first_token + k);
+        if (r < 0)
+            return r;
+        if (r == 1 && (r = w->e->flush()) != 0)
+            return r;
+    }
+    return CLK_SUCCESS;
+}
+
 int clk_element_flush(clk_element *w)
 {
     if (!w)

@@ -63,6 +63,13 @@ int clk_element_destroy(clk_element *e);
 int clk_element_push(clk_element *e, uint8_t *data, uint32_t length, int32_t nh_offset,
                      uint64_t token);
 
+/* Stage a burst of n host packets (an rte_eth_rx_burst-style array of
+ * packet pointers; fromdpdkdevice.cc:98-115); token of packet k is
+ * first_token + k.  nh_offsets may be NULL (= -1 for all).  Flushes by
+ * itself whenever the batch fills.  Returns 0 or < 0 on error.           */
+int clk_element_push_burst(clk_element *e, uint8_t *const *datas, const uint32_t *lengths,
+                           const int32_t *nh_offsets, uint64_t first_token, uint32_t n);
+
 /* Run the staged batch on the GPU and route it (synchronous).  Results are
  * appended to the element's result queue in push order.                  */
 int clk_element_flush(clk_element *e);
