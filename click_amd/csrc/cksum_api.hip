@@ -18,6 +18,8 @@ struct clk_ctx {
     int max_blocks;    // grid cap (tuning: CLK_MAX_BLOCKS)
     int force_group;   // lanes per packet override (tuning: CLK_FORCE_GROUP)
     int set_mode;      // -1 auto; 0: Set kernels store the field; 1: two-phase (CLK_SET_MODE)
+    uint64_t bin_min;  // variable-length batches of >= bin_min packets run by size class (CLK_BIN_MIN)
+    int bin_grid;      // grid cap of a size-class pass (CLK_BIN_GRID)
     void *scratch;     // two-phase work array (grown on demand)
     size_t scratch_bytes;
     char err[512];
@@ -102,6 +104,8 @@ clk::BatchArgs args_of(const clk_batch *b)
     a.len = b->len;
     a.fixed_len = b->fixed_len;
     a.n = b->n;
+    a.perm = nullptr;
+    a.range = nullptr;
     return a;
 }
 
@@ -135,36 +139,102 @@ unsigned grid_for(const clk_ctx *ctx, uint64_t threads)
     return g ? (unsigned)g : 1u;
 }
 
-template <int G>
-void launch_range(clk_ctx *ctx, const clk_batch *b, uint16_t *out)
+// Scratch layout for n packets: [work u32 x n][perm u32 x n][counts u32 x
+// NCLASS x nblocks][range u64 x 2 x NCLASS].
+struct ScratchLayout {
+    size_t work, perm, counts, range, bytes;
+    uint32_t nblocks;
+};
+ScratchLayout scratch_layout(uint64_t n)
 {
-    hipLaunchKernelGGL((clk::range_kernel<G, K>), dim3(grid_for(ctx, b->n * G)), dim3(BLOCK), 0,
-                       ctx->cur, args_of(b), out);
+    ScratchLayout L;
+    L.nblocks = (uint32_t)((n + clk::BIN_TILE - 1) / clk::BIN_TILE);
+    L.work = 0;
+    L.perm = (n * 4 + 255) & ~size_t(255);
+    L.counts = L.perm + ((n * 4 + 255) & ~size_t(255));
+    L.range = L.counts + (((size_t)clk::NCLASS * L.nblocks * 4 + 255) & ~size_t(255));
+    L.bytes = L.range + 2 * clk::NCLASS * 8;
+    return L;
+}
+
+// Host mirror of clk::size_class (lanes per packet G = 1 << class).
+int size_class_host(uint32_t len)
+{
+    const uint64_t nch = (uint64_t)len / 16 + 2;
+    int c = 0;
+    while (c < clk::NCLASS - 1 && nch > ((uint64_t)K << c))
+        c++;
+    return c;
+}
+
+bool use_bins(const clk_ctx *ctx, const clk_batch *b)
+{
+    return b->len && !ctx->force_group && b->n >= ctx->bin_min && b->n < (1ull << 32);
+}
+
+// Partition the batch by size class into the scratch (count, scan, scatter).
+int bin_batch(clk_ctx *ctx, const clk_batch *b, const ScratchLayout &L)
+{
+    uint8_t *sc = (uint8_t *)ctx->scratch;
+    uint32_t *counts = (uint32_t *)(sc + L.counts);
+    hipLaunchKernelGGL((clk::bin_count_kernel<K>), dim3(L.nblocks), dim3(BLOCK), 0, ctx->cur, b->len, b->n, counts,
+                       L.nblocks);
+    hipLaunchKernelGGL(clk::bin_scan_kernel, dim3(1), dim3(1024), 0, ctx->cur, counts, L.nblocks,
+                       (uint64_t *)(sc + L.range), b->n);
+    hipLaunchKernelGGL((clk::bin_scatter_kernel<K>), dim3(L.nblocks), dim3(BLOCK), 0, ctx->cur, b->len, b->n,
+                       (const uint32_t *)counts, L.nblocks, (uint32_t *)(sc + L.perm));
+    return CLK_SUCCESS;
+}
+
+// Classes that can be non-empty: 0 .. class of max_len (all when unknown).
+int max_class(const clk_batch *b)
+{
+    return b->max_len ? size_class_host(b->max_len) : clk::NCLASS - 1;
+}
+
+template <int G>
+void launch_range(clk_ctx *ctx, const clk::BatchArgs &a, unsigned grid, uint16_t *out)
+{
+    hipLaunchKernelGGL((clk::range_kernel<G, K>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a, out);
+}
+
+void launch_range_dispatch(clk_ctx *ctx, const clk::BatchArgs &a, unsigned grid, uint16_t *out, int g)
+{
+    switch (g) {
+    case 1: launch_range<1>(ctx, a, grid, out); break;
+    case 2: launch_range<2>(ctx, a, grid, out); break;
+    case 4: launch_range<4>(ctx, a, grid, out); break;
+    case 8: launch_range<8>(ctx, a, grid, out); break;
+    case 16: launch_range<16>(ctx, a, grid, out); break;
+    case 32: launch_range<32>(ctx, a, grid, out); break;
+    default: launch_range<64>(ctx, a, grid, out); break;
+    }
 }
 
 template <int PROTO, bool SET, int G>
-void launch_l4_g(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint16_t *sum, uint32_t *work)
+void launch_l4_g(clk_ctx *ctx, const clk::BatchArgs &a, unsigned grid, int fixoff, uint8_t *code, uint16_t *sum,
+                 uint32_t *work)
 {
     if (SET && work)
-        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, true>), dim3(grid_for(ctx, b->n * G)), dim3(BLOCK),
-                           0, ctx->cur, args_of(b), fixoff, code, sum, work);
+        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, true>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a, fixoff,
+                           code, sum, work);
     else
-        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, false>), dim3(grid_for(ctx, b->n * G)), dim3(BLOCK),
-                           0, ctx->cur, args_of(b), fixoff, code, sum, work);
+        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a, fixoff,
+                           code, sum, work);
 }
 
 template <int PROTO, bool SET>
-int launch_l4_dispatch(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint16_t *sum,
-                       uint32_t *work, int g)
+int launch_l4_dispatch(clk_ctx *ctx, const clk::BatchArgs &a, unsigned grid, int fixoff, uint8_t *code,
+                       uint16_t *sum, uint32_t *work, int g)
 {
     switch (g) {
-    case 1: launch_l4_g<PROTO, SET, 1>(ctx, b, fixoff, code, sum, work); break;
-    case 2: launch_l4_g<PROTO, SET, 2>(ctx, b, fixoff, code, sum, work); break;
-    case 4: launch_l4_g<PROTO, SET, 4>(ctx, b, fixoff, code, sum, work); break;
-    case 8: launch_l4_g<PROTO, SET, 8>(ctx, b, fixoff, code, sum, work); break;
-    case 16: launch_l4_g<PROTO, SET, 16>(ctx, b, fixoff, code, sum, work); break;
-    case 32: launch_l4_g<PROTO, SET, 32>(ctx, b, fixoff, code, sum, work); break;
-    default: launch_l4_g<PROTO, SET, 64>(ctx, b, fixoff, code, sum, work); break;
+    case 1: launch_l4_g<PROTO, SET, 1>(ctx, a, grid, fixoff, code, sum, work); break;
+    case 2: launch_l4_g<PROTO, SET, 2>(ctx, a, grid, fixoff, code, sum, work); break;
+    case 4: launch_l4_g<PROTO, SET, 4>(ctx, a, grid, fixoff, code, sum, work); break;
+    case 8: launch_l4_g<PROTO, SET, 8>(ctx, a, grid, fixoff, code, sum, work); break;
+    case 16: launch_l4_g<PROTO, SET, 16>(ctx, a, grid, fixoff, code, sum, work); break;
+    case 32: launch_l4_g<PROTO, SET, 32>(ctx, a, grid, fixoff, code, sum, work); break;
+    default: launch_l4_g<PROTO, SET, 64>(ctx, a, grid, fixoff, code, sum, work); break;
     }
     return 0;
 }
@@ -178,11 +248,30 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
     if (b->n == 0) return CLK_SUCCESS;
     if (!code) return fail(ctx, CLK_EINVAL, "%s: null output", fn);
     uint32_t *work = nullptr;
-    if (SET && ctx->set_mode != 0) {         // auto: two-phase for UDP/TCP Set
-        if ((r = ensure_scratch(ctx, b->n * sizeof(uint32_t)))) return r;
-        work = (uint32_t *)ctx->scratch;
+    const bool bins = use_bins(ctx, b);
+    const bool two = SET && ctx->set_mode != 0;            // auto: two-phase for UDP/TCP Set
+    const ScratchLayout L = scratch_layout(b->n);
+    if (two || bins) {
+        if ((r = ensure_scratch(ctx, L.bytes))) return r;
+        if (two)
+            work = (uint32_t *)ctx->scratch;
     }
-    launch_l4_dispatch<PROTO, SET>(ctx, b, fixoff, code, sum, work, pick_group(ctx, b));
+    if (bins) {
+        bin_batch(ctx, b, L);
+        clk::BatchArgs a = args_of(b);
+        a.perm = (const uint32_t *)((uint8_t *)ctx->scratch + L.perm);
+        for (int c = 0; c <= max_class(b); c++) {
+            a.range = (const uint64_t *)((uint8_t *)ctx->scratch + L.range) + 2 * c;
+            const int g = 1 << c;
+            uint64_t blocks = (b->n * (uint64_t)g + BLOCK - 1) / BLOCK;
+            if (blocks > (uint64_t)ctx->bin_grid)
+                blocks = (uint64_t)ctx->bin_grid;
+            launch_l4_dispatch<PROTO, SET>(ctx, a, (unsigned)blocks, fixoff, code, sum, work, g);
+        }
+    } else {
+        const int g = pick_group(ctx, b);
+        launch_l4_dispatch<PROTO, SET>(ctx, args_of(b), grid_for(ctx, b->n * (uint64_t)g), fixoff, code, sum, work, g);
+    }
     if (work) {
         constexpr int FIELD = PROTO == clk::UDP ? 6 : 16;
         hipLaunchKernelGGL((clk::field_scatter_kernel<FIELD, true>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
@@ -238,6 +327,15 @@ int clk_ctx_create(int device, clk_ctx **out)
     c->set_mode = -1;
     if (const char *sm = std::getenv("CLK_SET_MODE"))
         c->set_mode = std::atoi(sm) == 1 ? 1 : 0;
+    c->bin_min = 65536;
+    if (const char *bm = std::getenv("CLK_BIN_MIN"))
+        c->bin_min = (uint64_t)std::strtoull(bm, nullptr, 10);
+    c->bin_grid = 16384;
+    if (const char *bg = std::getenv("CLK_BIN_GRID")) {
+        int v = std::atoi(bg);
+        if (v > 0)
+            c->bin_grid = v;
+    }
     c->force_group = 0;
     if (const char *fg = std::getenv("CLK_FORCE_GROUP")) {
         int v = std::atoi(fg);
@@ -283,7 +381,7 @@ int clk_ctx_reserve(clk_ctx *ctx, uint64_t max_packets)
 {
     int r = enter(ctx);
     if (r) return r;
-    return ensure_scratch(ctx, max_packets * sizeof(uint32_t));
+    return ensure_scratch(ctx, scratch_layout(max_packets).bytes);
 }
 
 int clk_ctx_sync(clk_ctx *ctx)
@@ -310,14 +408,22 @@ int clk_in_cksum(clk_ctx *ctx, const clk_batch *b, uint16_t *out_sum)
     if ((r = check_batch(ctx, b, "clk_in_cksum"))) return r;
     if (b->n == 0) return CLK_SUCCESS;
     if (!out_sum) return fail(ctx, CLK_EINVAL, "clk_in_cksum: null output");
-    switch (pick_group(ctx, b)) {
-    case 1: launch_range<1>(ctx, b, out_sum); break;
-    case 2: launch_range<2>(ctx, b, out_sum); break;
-    case 4: launch_range<4>(ctx, b, out_sum); break;
-    case 8: launch_range<8>(ctx, b, out_sum); break;
-    case 16: launch_range<16>(ctx, b, out_sum); break;
-    case 32: launch_range<32>(ctx, b, out_sum); break;
-    default: launch_range<64>(ctx, b, out_sum); break;
+    if (use_bins(ctx, b)) {
+        const ScratchLayout L = scratch_layout(b->n);
+        if ((r = ensure_scratch(ctx, L.bytes))) return r;
+        bin_batch(ctx, b, L);
+        clk::BatchArgs a = args_of(b);
+        a.perm = (const uint32_t *)((uint8_t *)ctx->scratch + L.perm);
+        for (int c = 0; c <= max_class(b); c++) {
+            a.range = (const uint64_t *)((uint8_t *)ctx->scratch + L.range) + 2 * c;
+            uint64_t blocks = (b->n * (uint64_t)(1 << c) + BLOCK - 1) / BLOCK;
+            if (blocks > (uint64_t)ctx->bin_grid)
+                blocks = (uint64_t)ctx->bin_grid;
+            launch_range_dispatch(ctx, a, (unsigned)blocks, out_sum, 1 << c);
+        }
+    } else {
+        const int g = pick_group(ctx, b);
+        launch_range_dispatch(ctx, args_of(b), grid_for(ctx, b->n * (uint64_t)g), out_sum, g);
     }
     return check_launch(ctx, "clk_in_cksum");
 }

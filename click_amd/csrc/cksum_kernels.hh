@@ -37,6 +37,10 @@ struct BatchArgs {
     const uint32_t *len;
     uint32_t fixed_len;
     uint64_t n;
+    // size-class pass (bin_* kernels below): packets perm[j] for j in
+    // [range[0], range[1]); perm == nullptr: packets 0..n-1
+    const uint32_t *perm;
+    const uint64_t *range;
 };
 
 __device__ __forceinline__ uint64_t pkt_off(const BatchArgs &b, uint64_t i)
@@ -211,7 +215,9 @@ __global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_s
 {
     const uint32_t lane = threadIdx.x & 63, gl = lane & (G - 1);
     const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
-    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; i < b.n; i += groups) {
+    const uint64_t jbeg = b.perm ? b.range[0] : 0, jend = b.perm ? b.range[1] : b.n;
+    for (uint64_t j = jbeg + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; j < jend; j += groups) {
+        const uint64_t i = b.perm ? (uint64_t)b.perm[j] : j;
         const uint8_t *p = b.base + pkt_off(b, i);
         const int len = (int)pkt_len(b, i);
         const uint64_t s = (uint64_t)p;
@@ -241,7 +247,9 @@ __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_
     constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16; // uh_sum / th_sum offset in the transport header
     const uint32_t lane = threadIdx.x & 63, gl = lane & (G - 1);
     const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
-    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; i < b.n; i += groups) {
+    const uint64_t jbeg = b.perm ? b.range[0] : 0, jend = b.perm ? b.range[1] : b.n;
+    for (uint64_t j = jbeg + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; j < jend; j += groups) {
+        const uint64_t i = b.perm ? (uint64_t)b.perm[j] : j;
         uint8_t *nh = b.base + pkt_off(b, i);
         const uint32_t caplen = pkt_len(b, i);
         const uint64_t a = (uint64_t)nh;
@@ -444,6 +452,127 @@ __global__ void __launch_bounds__(256) field_scatter_kernel(BatchArgs b, const u
         } else if (status[i] == 0) {
             st_u16(b.base + pkt_off(b, i) + FIELD_BASE, sums[i]);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Size classes for variable-length batches (IMIX).  One geometry cannot fit
+// 64 B and 1500 B packets at once (a 16-lane group on a 64 B packet idles
+// 12 lanes; a lane per 1500 B packet serialises 12 passes), so a stable
+// partition by size class -- count, scan, scatter of packet indices -- lets
+// each class run with its own lanes-per-packet G = 1 << class.
+// ---------------------------------------------------------------------------
+constexpr int NCLASS = 7;                       // G = 1, 2, 4, ..., 64
+constexpr uint32_t BIN_TILE = 4096;             // packets per block in the bin kernels
+
+template <int K>
+__device__ __forceinline__ uint32_t size_class(uint32_t len)
+{
+    const uint32_t nch = len / 16 + 2;          // chunks of a range at the worst alignment
+    uint32_t c = 0;
+    while (c < NCLASS - 1 && nch > (uint32_t)K << c)
+        c++;
+    return c;
+}
+
+template <int K>
+__global__ void __launch_bounds__(256) bin_count_kernel(const uint32_t *len, uint64_t n, uint32_t *counts,
+                                                        uint32_t nblocks)
+{
+    __shared__ uint32_t h[NCLASS];
+    if (threadIdx.x < NCLASS)
+        h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t lo = (uint64_t)blockIdx.x * BIN_TILE;
+    const uint64_t hi = lo + BIN_TILE < n ? lo + BIN_TILE : n;
+    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
+        atomicAdd(&h[size_class<K>(len[i])], 1u);
+    __syncthreads();
+    if (threadIdx.x < NCLASS)
+        counts[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// One block: exclusive scan of counts in class-major order (in place), and
+// the class ranges range[2c], range[2c+1] = [start, end) into perm.
+__global__ void __launch_bounds__(1024) bin_scan_kernel(uint32_t *counts, uint32_t nblocks, uint64_t *range,
+                                                        uint64_t n)
+{
+    __shared__ uint64_t part[1024];
+    __shared__ uint64_t cstart[NCLASS];
+    const uint64_t total = (uint64_t)NCLASS * nblocks;
+    const uint64_t per = (total + blockDim.x - 1) / blockDim.x;
+    const uint64_t lo = threadIdx.x * per < total ? threadIdx.x * per : total;
+    const uint64_t hi = lo + per < total ? lo + per : total;
+    uint64_t s = 0;
+    for (uint64_t k = lo; k < hi; k++)
+        s += counts[k];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t run = 0;
+        for (uint32_t t = 0; t < blockDim.x; t++) {
+            const uint64_t v = part[t];
+            part[t] = run;
+            run += v;
+        }
+    }
+    __syncthreads();
+    uint64_t run = part[threadIdx.x];
+    for (uint64_t k = lo; k < hi; k++) {
+        const uint32_t v = counts[k];
+        counts[k] = (uint32_t)run;
+        if (k % nblocks == 0)
+            cstart[k / nblocks] = run;                  // first block of class k / nblocks
+        run += v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NCLASS) {
+        const uint32_t c = threadIdx.x;
+        range[2 * c] = cstart[c];
+        range[2 * c + 1] = c + 1 < NCLASS ? cstart[c + 1] : n;
+    }
+}
+
+// Stable scatter: block b writes the indices of its tile, class by class, in
+// packet order, at the offsets bin_scan_kernel produced.
+template <int K>
+__global__ void __launch_bounds__(256) bin_scatter_kernel(const uint32_t *len, uint64_t n, const uint32_t *offsets,
+                                                          uint32_t nblocks, uint32_t *perm)
+{
+    __shared__ uint32_t base[NCLASS];
+    __shared__ uint32_t wave_cnt[4][NCLASS];
+    if (threadIdx.x < NCLASS)
+        base[threadIdx.x] = offsets[threadIdx.x * nblocks + blockIdx.x];
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t lo = (uint64_t)blockIdx.x * BIN_TILE;
+    const uint64_t hi = lo + BIN_TILE < n ? lo + BIN_TILE : n;
+    for (uint64_t s0 = lo; s0 < hi; s0 += blockDim.x) {
+        const uint64_t i = s0 + threadIdx.x;
+        const bool live = i < hi;
+        const uint32_t c = live ? size_class<K>(len[i]) : NCLASS;
+        uint32_t rank = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < NCLASS; k++) {
+            const uint64_t m = __ballot(c == k);
+            if (c == k)
+                rank = __popcll(m & ((1ull << lane) - 1));
+            if (lane == 0)
+                wave_cnt[wv][k] = (uint32_t)__popcll(m);
+        }
+        __syncthreads();
+        if (live) {
+            uint32_t before = 0;
+            for (uint32_t w = 0; w < wv; w++)
+                before += wave_cnt[w][c];
+            perm[base[c] + before + rank] = (uint32_t)i;
+        }
+        __syncthreads();
+        if (threadIdx.x < NCLASS) {
+            const uint32_t k = threadIdx.x;
+            base[k] += wave_cnt[0][k] + wave_cnt[1][k] + wave_cnt[2][k] + wave_cnt[3][k];
+        }
+        __syncthreads();
     }
 }
 

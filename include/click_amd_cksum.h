@@ -81,8 +81,9 @@ void *clk_ctx_own_stream(clk_ctx *ctx);
 int clk_ctx_sync(clk_ctx *ctx);
 int clk_ctx_device(clk_ctx *ctx);
 /* Pre-size the context's device scratch for batches of up to max_packets
- * (4 bytes per packet, used by the two-phase UDP/TCP Set); without it the
- * first larger batch allocates synchronously.  After a reserve, batched
+ * (about 8 bytes per packet: the two-phase UDP/TCP Set's work array and the
+ * size-class partition of variable-length batches); without it the first
+ * larger batch allocates synchronously.  After a reserve, batched
  * calls of that size allocate nothing (safe inside hipGraph capture). */
 int clk_ctx_reserve(clk_ctx *ctx, uint64_t max_packets);
 /* Last error text for `ctx` (or for the calling thread when ctx == NULL). */
@@ -105,8 +106,11 @@ typedef struct clk_batch {
     uint64_t stride;
     const uint32_t *len;
     uint32_t fixed_len;
-    uint32_t max_len;   /* optional upper bound on len_i (0 = unknown); picks
-                           the lanes-per-packet geometry when len != NULL     */
+    uint32_t max_len;   /* optional upper bound on len_i (0 = unknown).  With
+                           len != NULL, large batches are partitioned by
+                           size class on the device and each class runs with
+                           its own lanes-per-packet; smaller ones use one
+                           geometry picked from max_len                      */
     uint64_t n;
 } clk_batch;
 

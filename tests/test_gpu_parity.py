@@ -276,3 +276,33 @@ def test_set_modes_bit_exact(torch, mode, monkeypatch):
     for op in ("set_ip", "set_udp"):
         compare(torch, c, op, arena, n, stride=stride, fixed_len=L)
     c.close()
+
+
+@pytest.mark.parametrize("bin_min", ["1", "100000000"])
+def test_size_class_partition_bit_exact(torch, bin_min, monkeypatch):
+    """Variable-length batches run by size class (count/scan/scatter of
+    packet indices, one lanes-per-packet geometry per class) or in one
+    geometry give identical, oracle-exact results."""
+    import click_amd
+    monkeypatch.setenv("CLK_BIN_MIN", bin_min)
+    c = click_amd.Context(0)
+    rng = np.random.default_rng(41)
+    for proto, mt in ((17, 1600), (6, 9000), (17, 200)):
+        arena, off, caplen, ml = fuzz.make_batch(rng, 2000, proto, max_total=mt)
+        for op in ("in_cksum",) + OPS_L4[proto]:
+            compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=1)
+            compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=0, arg=1)
+    # IMIX-like sizes across many bin tiles (BIN_TILE = 4096 packets)
+    n = 20000
+    L = rng.choice(np.array([64, 576, 1500], np.uint32), n, p=[7 / 12, 4 / 12, 1 / 12]).astype(np.uint32)
+    slot = (L + 63) // 64 * 64
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(slot[:-1])
+    arena = np.zeros(int(off[-1] + slot[-1]), np.uint8)
+    for i in range(n):
+        oracle_lib.gen(arena[int(off[i]):], 1, stride=0, fixed_len=int(L[i]), proto=17, first_idx=i)
+    oracle_lib.batch("set_ip", arena, n, off=off, length=L)
+    for op in ("set_udp", "check_udp", "in_cksum"):
+        compare(torch, c, op, arena, n, off=off, length=L, max_len=1500)
+        oracle_lib.batch(op, arena, n, off=off, length=L)
+    c.close()
