@@ -106,9 +106,10 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
     barriers + synchronize; HIP events on the launch stream give the kernel
     time.  Returns {element: result}."""
     import click_amd
+    from click_amd import shard
     w = dict(WORKLOADS[wname])
     n = w["n"]
-    first = rank * n
+    first, _ = shard.shard_range(rank, world, n * world)   # this rank's global packet indices
     if wname == "c4":
         off, ln, total, sum_l = imix_layout(torch, n, seed, first)
         arena = torch.empty(total, dtype=torch.uint8, device="cuda")
@@ -146,19 +147,19 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
             dist.barrier()
         kms = [a.elapsed_time(z) for a, z in ev]
         kernel_ms = sum(kms) / len(kms)
-        ok = int(ctx.count_codes(status)[0])
-        res = dict(wall=wall, kernel_ms=kernel_ms, kernel_ms_min=min(kms), n=n, ck_bytes=ck_bytes,
-                   alg_bytes=alg[e], ok=ok, w=w, element=e)
-        if dist:
-            t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            d = torch.tensor([ok, n], dtype=torch.int64, device="cuda")
-            dist.all_reduce(d, op=dist.ReduceOp.SUM)
-            res["wall"], res["kernel_ms"] = float(t[0]), float(t[1])
-            res["ok_total"], res["n_total"] = int(d[0]), int(d[1])
-        else:
-            res["ok_total"], res["n_total"] = ok, n
-        out[e] = res
+        # untimed: the result digest (Set: with the checksums it wrote)
+        sums = None
+        if e.startswith("Set"):
+            sums = torch.empty(n, dtype=torch.uint16, device="cuda")
+            {"SetUDPChecksum": ctx.set_udp_checksum, "SetTCPChecksum": ctx.set_tcp_checksum,
+             "SetIPChecksum": ctx.set_ip_checksum}[e](b, status=status, sums=sums)
+        torch.cuda.synchronize()
+        dig = shard.digest(torch, status, sums)
+        wall, kernel_ms, dig = shard.reduce_results(torch, dist, "cuda", wall, kernel_ms, dig)
+        out[e] = dict(wall=wall, kernel_ms=kernel_ms, kernel_ms_min=min(kms), n=n, ck_bytes=ck_bytes,
+                      alg_bytes=alg[e], w=w, element=e, ok_total=dig[0], n_total=dig[1],
+                      digest={"ok": dig[0], "packets": dig[1], "sum16": dig[2], "xor16": dig[3]})
+        del sums
     del arena, status, b
     torch.cuda.empty_cache()
     return out
@@ -258,7 +259,7 @@ def summarize(r, steps, wname):
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel_ms": round(r["kernel_ms"], 4), "kernel_ms_min": round(r["kernel_ms_min"], 4),
                      "alg_bytes_per_launch": r["alg_bytes"], "traffic_source": tsrc},
-        "verify": {"ok": r["ok_total"], "packets": r["n_total"]},
+        "verify": r["digest"],
     }
 
 
@@ -373,12 +374,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # CLK_BENCH_SAME_DEVICE=1 + CLK_BENCH_BACKEND=gloo rehearse the
+    # multi-rank code path with every rank on GPU 0 (RCCL refuses duplicate
+    # GPUs); the driver's N>1 runs use RCCL, one rank per GPU.
+    dev = 0 if os.environ.get("CLK_BENCH_SAME_DEVICE") == "1" else local
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    ctx = click_amd.Context(local)
+        backend = os.environ.get("CLK_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+    ctx = click_amd.Context(dev)
     if args.e2e:
         w = WORKLOADS[args.workload]
         res = [e2e(torch, ctx, args.workload, el) for el in w["elements"]]
