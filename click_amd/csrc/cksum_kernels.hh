@@ -233,18 +233,217 @@ __global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_s
 
 // ---------------------------------------------------------------------------
 // UDP / TCP check and set (checkudpheader.cc:84-107, setudpchecksum.cc:37-69,
-// checktcpheader.cc:85-107, settcpchecksum.cc:44-75).  Every lane of a group
-// issues the packet's chunk loads for [nh, nh+caplen) AND loads the first 40
-// header bytes (same addresses across the group: one request per wave
-// instruction), so one memory round trip serves the parse and the sum.
-// Header parse is speculative on ip_hl = 5; options are re-read.
+// checktcpheader.cc:85-107, settcpchecksum.cc:44-75), split in three steps
+// shared by the fixed-geometry kernel (l4_kernel) and the variable-length
+// kernel (l4_varlen_kernel):
+//   l4_parse  -- header checks; the summed range [nh+hl, nh+hl+rlen)
+//   (range sum by the caller)
+//   l4_finish -- Set field correction, fold, pseudo-header, verdict / store
+// The header parse reads the first 28 (UDP) / 40 (TCP) bytes as aligned
+// dwords and is speculative on ip_hl = 5; other header lengths re-read.
 // ---------------------------------------------------------------------------
+struct L4State {
+    uint32_t code;
+    int rlen;            // summed range length (int, as click_in_cksum's)
+    uint32_t plen_ph;    // packet_len for the pseudo-header
+    uint32_t hl, b0, proto, src, dst;
+    uint32_t fb0, fb1;   // Set: the stored field's two bytes
+    uint32_t new_b12, fix_delta;
+    bool fix, summing;
+};
+
+template <int PROTO, bool SET>
+__device__ __forceinline__ void l4_parse(uint8_t *nh, uint32_t caplen, int fixoff, L4State &st)
+{
+    constexpr int HDR_DW = PROTO == TCP ? 11 : 8;   // aligned dwords covering bytes [0, 40) / [0, 28)
+    constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
+    const uint64_t a = (uint64_t)nh;
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint8_t *q = (const uint8_t *)(a & ~3ull);
+    const uint64_t end = a + caplen;
+    uint32_t d[HDR_DW];
+#pragma unroll
+    for (int k = 0; k < HDR_DW; k++)
+        d[k] = (uint64_t)(q + 4 * k) < end ? *(const uint32_t *)(q + 4 * k) : 0u;
+    uint32_t h[HDR_DW - 1];                 // h[k] = bytes [4k, 4k+4) of the header, LE
+#pragma unroll
+    for (int k = 0; k < HDR_DW - 1; k++)
+        h[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+
+    const uint32_t b0 = h[0] & 0xFF;
+    const uint32_t hl = (b0 & 0xF) << 2;
+    const uint32_t ip_len = bswap16(h[0] >> 16);
+    const uint32_t proto = (h[2] >> 8) & 0xFF;
+    const bool isfrag = (bswap16(h[1] >> 16) & 0x3FFF) != 0;   // IP_ISFRAG, ip.h:121
+    auto tbyte = [&](uint32_t r) -> uint32_t {    // byte hl + r (speculated hl = 20)
+        if (hl == 20) {
+            const uint32_t o = 20 + r;
+            return (h[o >> 2] >> (8 * (o & 3))) & 0xFF;
+        }
+        return ld_u8(nh + hl + r);
+    };
+    st.code = OK;
+    st.rlen = 0;
+    st.plen_ph = 0;
+    st.hl = hl;
+    st.b0 = b0;
+    st.proto = proto;
+    st.src = h[3];
+    st.dst = h[4];
+    st.fb0 = st.fb1 = 0;
+    st.new_b12 = st.fix_delta = 0;
+    st.fix = false;
+    if (caplen < 20) {
+        st.code = PROTO == UDP ? (SET ? SET_OUTPUT1 : L4_BAD_LENGTH) : (SET ? SET_KILL : L4_BAD_LENGTH);
+    } else if (PROTO == UDP && !SET) {
+        if (proto != 17)
+            st.code = L4_NOT_PROTO;
+        else if (caplen < hl + 8)
+            st.code = L4_BAD_LENGTH;
+        else {
+            const uint32_t ulen = (tbyte(4) << 8) | tbyte(5);
+            if (ulen < 8 || caplen < ulen + hl)
+                st.code = L4_BAD_LENGTH;
+            else if ((tbyte(6) | tbyte(7)) != 0) {      // uh_sum == 0: not checked (checkudpheader.cc:100)
+                st.rlen = (int)ulen;
+                st.plen_ph = ulen;
+            }
+        }
+    } else if (PROTO == UDP && SET) {
+        const int tlen = (int)caplen - (int)hl;
+        if (isfrag || tlen < 8)
+            st.code = SET_OUTPUT1;
+        else {
+            const uint32_t ulen = (tbyte(4) << 8) | tbyte(5);
+            if (tlen < (int)ulen)
+                st.code = SET_OUTPUT1;
+            else {
+                st.rlen = (int)ulen;
+                st.plen_ph = ulen;
+            }
+        }
+    } else if (PROTO == TCP && !SET) {
+        if (proto != 6)
+            st.code = L4_NOT_PROTO;
+        else if (caplen < hl + 13)
+            st.code = L4_BAD_LENGTH;
+        else {
+            const uint32_t len = ip_len - hl;
+            const uint32_t thl = (tbyte(12) >> 4) << 2;
+            if (thl < 20 || len < thl || caplen < len + hl)
+                st.code = L4_BAD_LENGTH;
+            else {
+                st.rlen = (int)len;
+                st.plen_ph = len;
+            }
+        }
+    } else {   // TCP set
+        if (hl > caplen)
+            st.code = SET_KILL;
+        else {
+            const uint32_t plen = ip_len - hl, tlen = caplen - hl;
+            if (plen < 20 || plen > tlen)
+                st.code = SET_KILL;
+            else {
+                st.rlen = (int)plen;
+                st.plen_ph = plen;
+                if (fixoff) {                   // settcpchecksum.cc:57-63
+                    const uint32_t ob = tbyte(12);
+                    const uint32_t off = (ob >> 4) << 2;
+                    if (off < 20) {
+                        st.new_b12 = (ob & 0x0F) | (5u << 4);
+                        st.fix = true;
+                    } else if (off > plen && !isfrag) {
+                        st.new_b12 = (ob & 0x0F) | (((plen >> 2) & 0xF) << 4);
+                        st.fix = true;
+                    }
+                    if (st.fix)
+                        st.fix_delta = st.new_b12 - ob;
+                }
+            }
+        }
+    }
+    st.summing = (st.code == OK) && (st.rlen != 0 || st.plen_ph != 0 || SET);
+    if (SET && st.summing) {
+        st.fb0 = (int)FIELD < st.rlen ? tbyte(FIELD) : 0;
+        st.fb1 = (int)FIELD + 1 < st.rlen ? tbyte(FIELD + 1) : 0;
+    }
+}
+
+// Finish one packet from its range sum.  `writer` lanes store.
+template <int PROTO, bool SET, bool DEFER>
+__device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum, L4State &st, bool writer,
+                                          uint8_t *out_code, uint16_t *out_sum, uint32_t *work)
+{
+    constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
+    uint32_t stored = 0;
+    if (st.code == OK && st.summing) {
+        if (SET) {
+            // the field was zeroed before summing (setudpchecksum.cc:64,
+            // settcpchecksum.cc:65): remove its bytes that lie in range
+            sum -= st.fb0 + (st.fb1 << 8);
+            if (st.fix && 12 < st.rlen)
+                sum += st.fix_delta;
+        }
+        const uint32_t csum = in_cksum_fold(sum);
+        uint32_t r;
+        if (SET && st.hl < 20) {
+            // ip_hl < 5: the transport header overlaps the IP header.  The
+            // reference zeroes the field (and FIXOFF rewrites th_off)
+            // BEFORE the pseudo-header reads ip_src/ip_dst, and the option
+            // walk is empty (in_cksum.c:86-88), so patch those bytes in.
+            uint32_t s2 = st.src, d2 = st.dst;
+            auto patch = [&](uint32_t pos, uint32_t val) {
+                if (pos >= 12 && pos < 16)
+                    s2 = (s2 & ~(0xFFu << (8 * (pos - 12)))) | (val << (8 * (pos - 12)));
+                else if (pos >= 16 && pos < 20)
+                    d2 = (d2 & ~(0xFFu << (8 * (pos - 16)))) | (val << (8 * (pos - 16)));
+            };
+            if (st.fix)
+                patch(st.hl + 12, st.new_b12);
+            patch(st.hl + FIELD, 0);
+            patch(st.hl + FIELD + 1, 0);
+            r = pseudohdr_raw(csum, s2, d2, st.proto, st.plen_ph);
+        } else {
+            r = pseudohdr(csum, nh, st.b0, st.src, st.dst, st.proto, st.plen_ph);
+        }
+        if (SET) {
+            stored = r;
+#if !CLK_DIAG_NO_FIELD_STORE
+            if (writer) {
+                if (st.fix)
+                    nh[st.hl + 12] = (uint8_t)st.new_b12;
+                if (DEFER)       // the field is written by field_scatter_kernel
+                    work[i] = 0x80000000u | (st.hl << 16) | r;
+                else
+                    st_u16(nh + st.hl + FIELD, r);
+            }
+#endif
+        } else if (r != 0) {
+            st.code = L4_BAD_CHECKSUM;
+        }
+    }
+    if (writer) {
+#if !CLK_DIAG_NO_STATUS_STORE
+        out_code[i] = (uint8_t)st.code;
+#else
+        if (st.code == 0xFF) out_code[i] = 0;
+#endif
+        if (SET && DEFER && st.code != OK)
+            work[i] = 0;
+        if (SET && out_sum)
+            out_sum[i] = (uint16_t)stored;
+    }
+}
+
+// Fixed geometry: G lanes per packet.  Every lane of a group issues the
+// packet's pass-0 chunk loads for [nh, nh+caplen) AND the header dwords
+// (same addresses across the group: one request per wave instruction), so
+// one memory round trip serves the parse and the sum.
 template <int PROTO, bool SET, int G, int K, bool DEFER>
 __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                  uint16_t *out_sum, uint32_t *work)
 {
-    constexpr int HDR_DW = PROTO == TCP ? 11 : 8;   // aligned dwords covering bytes [0, 40) / [0, 28)
-    constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16; // uh_sum / th_sum offset in the transport header
     const uint32_t lane = threadIdx.x & 63, gl = lane & (G - 1);
     const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
     const uint64_t jbeg = b.perm ? b.range[0] : 0, jend = b.perm ? b.range[1] : b.n;
@@ -255,178 +454,156 @@ __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_
         const uint64_t a = (uint64_t)nh;
         const uint8_t *c0 = (const uint8_t *)(a & ~15ull);
         const uint32_t nch = (uint32_t)((((a + caplen + 15) & ~15ull) - (uint64_t)c0) / 16);
-        // issue: chunk loads for pass 0, then the header dwords
         u32x4 v[K];
-        load_pass<G, K>(c0, nch, 0, gl, v);
-        const uint32_t sh = (uint32_t)(a & 3);
-        const uint8_t *q = (const uint8_t *)(a & ~3ull);
-        const uint64_t end = a + caplen;
-        uint32_t d[HDR_DW];
-#pragma unroll
-        for (int k = 0; k < HDR_DW; k++)
-            d[k] = (uint64_t)(q + 4 * k) < end ? *(const uint32_t *)(q + 4 * k) : 0u;
-        uint32_t h[HDR_DW - 1];                 // h[k] = bytes [4k, 4k+4) of the header, LE
-#pragma unroll
-        for (int k = 0; k < HDR_DW - 1; k++)
-            h[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        load_pass<G, K>(c0, nch, 0, gl, v);      // issued before the header loads
+        L4State st;
+        l4_parse<PROTO, SET>(nh, caplen, fixoff, st);
+        // a lane whose packet needs no sum masks everything (len 0)
+        const uint32_t sum = group_range_sum<G, K>(c0, nch, gl, v, a + st.hl, st.summing ? st.rlen : 0);
+        l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, gl == 0, out_code, out_sum, work);
+    }
+}
 
-        const uint32_t b0 = h[0] & 0xFF;
-        const uint32_t hl = (b0 & 0xF) << 2;
-        const uint32_t ip_len = bswap16(h[0] >> 16);
-        const uint32_t proto = (h[2] >> 8) & 0xFF;
-        const uint32_t src = h[3], dst = h[4];
-        const bool isfrag = (bswap16(h[1] >> 16) & 0x3FFF) != 0;   // IP_ISFRAG, ip.h:121
-        // transport fields at nh + hl (speculated hl = 20)
-        auto tbyte = [&](uint32_t r) -> uint32_t {    // byte hl + r
-            if (hl == 20) {
-                const uint32_t o = 20 + r;
-                return (h[o >> 2] >> (8 * (o & 3))) & 0xFF;
-            }
-            return ld_u8(nh + hl + r);
-        };
-        uint32_t code = OK, stored = 0;
-        int rlen = 0;             // summed range length (int, as click_in_cksum's)
-        uint32_t plen_ph = 0;     // packet_len passed to the pseudo-header
-        uint32_t fix_delta = 0;   // set TCP FIXOFF: new byte 12 - old byte 12 (mod 2^32)
-        uint32_t new_b12 = 0;
-        bool fix = false;
-        if (caplen < 20) {
-            code = PROTO == UDP ? (SET ? SET_OUTPUT1 : L4_BAD_LENGTH) : (SET ? SET_KILL : L4_BAD_LENGTH);
-        } else if (PROTO == UDP && !SET) {
-            if (proto != 17)
-                code = L4_NOT_PROTO;
-            else if (caplen < hl + 8)
-                code = L4_BAD_LENGTH;
-            else {
-                const uint32_t ulen = (tbyte(4) << 8) | tbyte(5);
-                if (ulen < 8 || caplen < ulen + hl)
-                    code = L4_BAD_LENGTH;
-                else if ((tbyte(6) | tbyte(7)) == 0)
-                    code = OK;                      // uh_sum == 0: not checked (checkudpheader.cc:100)
-                else {
-                    rlen = (int)ulen;
-                    plen_ph = ulen;
+// Variable lengths (IMIX): a wave takes 64 consecutive packets.
+//   Phase A: one lane per packet parses its header and publishes, in LDS,
+//            its summed range as 16-byte chunks: first chunk address, chunk
+//            offset in the wave's concatenated chunk list (exclusive scan),
+//            range start within the first chunk, range length.
+//   Phase B: the wave walks the concatenated chunk list, KV chunks per
+//            lane per pass, each lane a contiguous run (lane l of pass p owns
+//            chunks p*64*KV + l*KV + [0, KV)): the lane finds its first
+//            chunk's packet by binary search, steps forward at packet
+//            boundaries, sums in registers and adds the partial into the
+//            packet's LDS accumulator only when the packet changes (u32
+//            adds, exact mod 2^32).  A pass reads 64*KV*16 contiguous bytes
+//            of a packed arena.
+//   Phase C: each lane finishes its packet from its accumulator.
+// No workgroup barriers: every LDS word is private to one wave.
+#ifndef CLK_VL_INTERLEAVE
+#define CLK_VL_INTERLEAVE 0   // tuning: 1 = lane owns chunks cb + k*64 + lane (coalesced per instruction)
+#endif
+template <int PROTO, bool SET, bool DEFER, int KV>
+__global__ void __launch_bounds__(256) l4_varlen_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
+                                                        uint16_t *out_sum, uint32_t *work)
+{
+    __shared__ u32x4 pk[4][64];       // {cfirst lo, cfirst hi, chunk start, rlen | (s & 15) << 24}
+    __shared__ uint32_t cst[4][68];   // chunk starts; cst[64] = total, padded
+    __shared__ uint32_t acc[4][64];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t nruns = (b.n + 63) / 64;
+    const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t run = (uint64_t)blockIdx.x * (blockDim.x / 64) + wv; run < nruns; run += wstride) {
+        const uint64_t i = run * 64 + lane;
+        const bool live = i < b.n;
+        uint8_t *nh = b.base;
+        L4State st;
+        st.summing = false;
+        st.code = OK;
+        st.rlen = 0;
+        st.hl = 0;
+        if (live) {
+            nh = b.base + pkt_off(b, i);
+            l4_parse<PROTO, SET>(nh, pkt_len(b, i), fixoff, st);
+        }
+        const int rlen = st.summing ? st.rlen : 0;
+        const uint64_t s = (uint64_t)nh + st.hl;
+        const uint64_t cfirst = s & ~15ull;
+        const uint32_t nchunks = rlen > 0 ? (uint32_t)((((s + (uint64_t)rlen + 15) & ~15ull) - cfirst) >> 4) : 0u;
+        uint32_t incl = nchunks;                             // wave-inclusive scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(incl, d, 64);
+            if ((int)lane >= d)
+                incl += t;
+        }
+        const uint32_t total = __shfl(incl, 63, 64);
+        const uint32_t rl = rlen > 0 ? (uint32_t)rlen : 0u;   // L4 ranges are < 2^16 bytes
+        pk[wv][lane] = u32x4{(uint32_t)cfirst, (uint32_t)(cfirst >> 32), incl - nchunks,
+                             rl | ((uint32_t)(s & 15) << 24)};
+        cst[wv][lane] = incl - nchunks;
+        if (lane == 63)
+            cst[wv][64] = total;
+        acc[wv][lane] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t cb = 0; cb < total; cb += 64 * KV) {          // wave-uniform
+            const uint32_t c0 = CLK_VL_INTERLEAVE ? cb + lane : cb + lane * KV;
+            auto chunk_of = [&](int k) -> uint32_t { return CLK_VL_INTERLEAVE ? c0 + 64 * k : c0 + k; };
+            // last packet whose chunk start <= c0
+            uint32_t j = 0;
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (j + step < 64 && cst[wv][j + step] <= c0)
+                    j += step;
+            uint32_t nxt = cst[wv][j + 1];
+            u32x4 P = pk[wv][j];
+            u32x4 v[KV];
+            u32x4 Pk[KV];
+            uint32_t jk[KV];
+#pragma unroll
+            for (int k = 0; k < KV; k++) {
+                const uint32_t c = chunk_of(k);
+                if (CLK_VL_INTERLEAVE && k > 0 && c < total) {     // fresh search from the last packet
+                    uint32_t lo = j;
+#pragma unroll
+                    for (int step = 32; step >= 1; step >>= 1)
+                        if (lo + step < 64 && cst[wv][lo + step] <= c)
+                            lo += step;
+                    if (lo != j) {
+                        j = lo;
+                        P = pk[wv][j];
+                    }
+                } else if (c < total && c >= nxt) {
+                    do {                                           // skip to the chunk's packet
+                        j++;
+                        nxt = cst[wv][j + 1];
+                    } while (c >= nxt);
+                    P = pk[wv][j];
                 }
+                jk[k] = j;
+                Pk[k] = P;
+                const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
+                v[k] = c < total ? *(const u32x4 *)(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
             }
-        } else if (PROTO == UDP && SET) {
-            const int tlen = (int)caplen - (int)hl;
-            if (isfrag || tlen < 8)
-                code = SET_OUTPUT1;
-            else {
-                const uint32_t ulen = (tbyte(4) << 8) | tbyte(5);
-                if (tlen < (int)ulen)
-                    code = SET_OUTPUT1;
-                else {
-                    rlen = (int)ulen;
-                    plen_ph = ulen;
+            uint32_t cur = jk[0], part = 0;
+#pragma unroll
+            for (int k = 0; k < KV; k++) {
+                const uint32_t c = chunk_of(k);
+                if (c >= total)
+                    break;
+                if (jk[k] != cur) {
+                    atomicAdd(&acc[wv][cur], part);
+                    part = 0;
+                    cur = jk[k];
                 }
-            }
-        } else if (PROTO == TCP && !SET) {
-            if (proto != 6)
-                code = L4_NOT_PROTO;
-            else if (caplen < hl + 13)
-                code = L4_BAD_LENGTH;
-            else {
-                const uint32_t len = ip_len - hl;
-                const uint32_t thl = (tbyte(12) >> 4) << 2;
-                if (thl < 20 || len < thl || caplen < len + hl)
-                    code = L4_BAD_LENGTH;
-                else {
-                    rlen = (int)len;
-                    plen_ph = len;
-                }
-            }
-        } else {   // TCP set
-            if (hl > caplen)
-                code = SET_KILL;
-            else {
-                const uint32_t plen = ip_len - hl, tlen = caplen - hl;
-                if (plen < 20 || plen > tlen)
-                    code = SET_KILL;
-                else {
-                    rlen = (int)plen;
-                    plen_ph = plen;
-                    if (fixoff) {                   // settcpchecksum.cc:57-63
-                        const uint32_t ob = tbyte(12);
-                        const uint32_t off = (ob >> 4) << 2;
-                        if (off < 20) {
-                            new_b12 = (ob & 0x0F) | (5u << 4);
-                            fix = true;
-                        } else if (off > plen && !isfrag) {
-                            new_b12 = (ob & 0x0F) | (((plen >> 2) & 0xF) << 4);
-                            fix = true;
-                        }
-                        if (fix)
-                            fix_delta = new_b12 - ob;
+                const u32x4 Q = Pk[k];
+                const int rlj = (int)(Q[3] & 0xFFFFFF);
+                const uint32_t s15 = Q[3] >> 24;
+                const uint32_t sel = (s15 & 1) ? 0x02030001u : 0x03020100u;   // odd start: swap bytes
+                const int rel = (int)(16 * (c - Q[2])) - (int)s15;          // chunk start - range start
+                if (rel >= 0 && rel + 16 <= rlj) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        part = dot_words(__builtin_amdgcn_perm(v[k][q], v[k][q], sel), part);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t dm = v[k][q] & lowmask(rlj - rel - 4 * q) & ~lowmask(-rel - 4 * q);
+                        part = dot_words(__builtin_amdgcn_perm(dm, dm, sel), part);
                     }
                 }
             }
+            if (c0 < total)
+                atomicAdd(&acc[wv][cur], part);
         }
-        const bool summing = (code == OK) && (rlen != 0 || plen_ph != 0 || SET);
-        const uint64_t s = a + hl;
-        // a lane whose packet needs no sum masks everything (len 0)
-        uint32_t sum = group_range_sum<G, K>(c0, nch, gl, v, s, summing ? rlen : 0);
-        // every lane holds the group's total; all lanes finish the packet
-        if (code == OK && summing) {
-            if (SET) {
-                // the field was zeroed before summing (setudpchecksum.cc:64,
-                // settcpchecksum.cc:65): remove its bytes that lie in range
-                if ((int)FIELD < rlen)
-                    sum -= tbyte(FIELD);
-                if ((int)FIELD + 1 < rlen)
-                    sum -= tbyte(FIELD + 1) << 8;
-                if (fix && 12 < rlen)
-                    sum += fix_delta;
-            }
-            const uint32_t csum = in_cksum_fold(sum);
-            uint32_t r;
-            if (SET && hl < 20) {
-                // ip_hl < 5: the transport header overlaps the IP header.  The
-                // reference zeroes the field (and FIXOFF rewrites th_off)
-                // BEFORE the pseudo-header reads ip_src/ip_dst, and the option
-                // walk is empty (in_cksum.c:86-88), so patch those bytes in.
-                uint32_t s2 = src, d2 = dst;
-                auto patch = [&](uint32_t pos, uint32_t val) {
-                    if (pos >= 12 && pos < 16)
-                        s2 = (s2 & ~(0xFFu << (8 * (pos - 12)))) | (val << (8 * (pos - 12)));
-                    else if (pos >= 16 && pos < 20)
-                        d2 = (d2 & ~(0xFFu << (8 * (pos - 16)))) | (val << (8 * (pos - 16)));
-                };
-                if (fix)
-                    patch(hl + 12, new_b12);
-                patch(hl + FIELD, 0);
-                patch(hl + FIELD + 1, 0);
-                r = pseudohdr_raw(csum, s2, d2, proto, plen_ph);
-            } else {
-                r = pseudohdr(csum, nh, b0, src, dst, proto, plen_ph);
-            }
-            if (SET) {
-                stored = r;
-#if !CLK_DIAG_NO_FIELD_STORE
-                if (gl == 0) {
-                    if (fix)
-                        nh[hl + 12] = (uint8_t)new_b12;
-                    if (DEFER)       // the field is written by field_scatter_kernel
-                        work[i] = 0x80000000u | (hl << 16) | r;
-                    else
-                        st_u16(nh + hl + FIELD, r);
-                }
-#endif
-            } else if (r != 0) {
-                code = L4_BAD_CHECKSUM;
-            }
-        }
-        if (gl == 0) {
-#if !CLK_DIAG_NO_STATUS_STORE
-            out_code[i] = (uint8_t)code;
-#else
-            if (code == 0xFF) out_code[i] = 0;
-#endif
-            if (SET && DEFER && code != OK)
-                work[i] = 0;
-            if (SET && out_sum)
-                out_sum[i] = (uint16_t)stored;
-        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t sum = acc[wv][lane];
+        if (live)
+            l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work);
+        __builtin_amdgcn_wave_barrier();
     }
 }
 

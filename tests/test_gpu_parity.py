@@ -278,13 +278,15 @@ def test_set_modes_bit_exact(torch, mode, monkeypatch):
     c.close()
 
 
-@pytest.mark.parametrize("bin_min", ["1", "100000000"])
-def test_size_class_partition_bit_exact(torch, bin_min, monkeypatch):
-    """Variable-length batches run by size class (count/scan/scatter of
-    packet indices, one lanes-per-packet geometry per class) or in one
-    geometry give identical, oracle-exact results."""
+@pytest.mark.parametrize("bin_min,varlen", [("1", "1"), ("1", "0"), ("100000000", "1")])
+def test_size_class_partition_bit_exact(torch, bin_min, varlen, monkeypatch):
+    """Variable-length batches run by the wave-cooperative kernel (varlen
+    1), by size class (count/scan/scatter of packet indices, one
+    lanes-per-packet geometry per class; varlen 0), or in one geometry: all
+    identical and oracle-exact."""
     import click_amd
     monkeypatch.setenv("CLK_BIN_MIN", bin_min)
+    monkeypatch.setenv("CLK_VARLEN", varlen)
     c = click_amd.Context(0)
     rng = np.random.default_rng(41)
     for proto, mt in ((17, 1600), (6, 9000), (17, 200)):

@@ -35,6 +35,13 @@ VARIANTS = {
     "mb64k": ([], {"CLK_MAX_BLOCKS": "65536"}),
     "mb1m": ([], {"CLK_MAX_BLOCKS": "1048576"}),
     "diag_nofield": (["-DCLK_DIAG_NO_FIELD_STORE=1"], {}),
+    "kv1": (["-DCLK_KV=1"], {}),
+    "kv2": (["-DCLK_KV=2"], {}),
+    "il2": (["-DCLK_KV=2", "-DCLK_VL_INTERLEAVE=1"], {}),
+    "il4": (["-DCLK_KV=4", "-DCLK_VL_INTERLEAVE=1"], {}),
+    "il8": (["-DCLK_KV=8", "-DCLK_VL_INTERLEAVE=1"], {}),
+    "kv8": (["-DCLK_KV=8"], {}),
+    "bins": ([], {"CLK_VARLEN": "0"}),
 }
 
 
@@ -77,9 +84,14 @@ def main():
     import bench
     w = bench.WORKLOADS[args.workload]
     n = w["n"]
-    arena = torch.empty(n * w["stride"], dtype=torch.uint8, device="cuda")
     base_ctx = click_amd.Context(0)
-    b = click_amd.Batch(arena, n, stride=w["stride"], fixed_len=w["L"])
+    if args.workload == "c4":
+        off, ln, total, sum_l = bench.imix_layout(torch, n, 0x5EED, 0)
+        arena = torch.empty(total, dtype=torch.uint8, device="cuda")
+        b = click_amd.Batch(arena, n, off=off, length=ln, max_len=1500)
+    else:
+        arena = torch.empty(n * w["stride"], dtype=torch.uint8, device="cuda")
+        b = click_amd.Batch(arena, n, stride=w["stride"], fixed_len=w["L"])
     base_ctx.gen_packets(b, proto=w["proto"])
     base_ctx.set_ip_checksum(b, want_sums=False)
     status = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -87,7 +99,7 @@ def main():
     ctxs = {}
     for nm in names:
         _, env = VARIANTS[nm]
-        saved = {k: os.environ.get(k) for k in ("CLK_MAX_BLOCKS", "CLK_FORCE_GROUP", "CLK_SET_MODE")}
+        saved = {k: os.environ.get(k) for k in ("CLK_MAX_BLOCKS", "CLK_FORCE_GROUP", "CLK_SET_MODE", "CLK_VARLEN")}
         for k in saved:
             os.environ.pop(k, None)
         os.environ.update(env)
@@ -118,7 +130,7 @@ def main():
             e.record()
             torch.cuda.synchronize()
             times[nm].append(s.elapsed_time(e) / args.launches)
-    alg = bench.ALG[element](w["L"]) * n
+    alg = bench.ALG[element](w["L"]) * n if args.workload != "c4" else sum_l + (bench.ALG[element](0) + 12) * n
     out = {nm: {"median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
                 "GBs": round(alg / (statistics.median(t) * 1e-3) / 1e9, 1)} for nm, t in times.items()}
     print(json.dumps({"workload": args.workload, "element": element,
