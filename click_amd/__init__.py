@@ -176,6 +176,21 @@ class Context:
                                                   _ptr(status), _ptr(sums)))
         return status[:b.n], (sums[:b.n] if sums is not None else None)
 
+    def check_icmp_header(self, b, out=None):
+        out = self._out(b.n, self._torch.uint8) if out is None else out
+        cb = b.c()
+        self._check(self.lib.clk_check_icmp_header(self.h, ctypes.byref(cb), _ptr(out)))
+        return out[:b.n]
+
+    def dec_ip_ttl(self, b, multicast=True, status=None, sums=None, want_sums=True):
+        status = self._out(b.n, self._torch.uint8) if status is None else status
+        if sums is None and want_sums:
+            sums = self._out(b.n, self._torch.uint16)
+        cb = b.c()
+        self._check(self.lib.clk_dec_ip_ttl(self.h, ctypes.byref(cb), 1 if multicast else 0,
+                                            _ptr(status), _ptr(sums)))
+        return status[:b.n], (sums[:b.n] if sums is not None else None)
+
     # -- utilities ---------------------------------------------------------------
     def count_codes(self, codes, ncounts=8, counts=None):
         if counts is None:

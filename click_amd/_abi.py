@@ -29,6 +29,9 @@ CLK_L4_BAD_CHECKSUM = 3
 CLK_SET_OK = 0
 CLK_SET_OUTPUT1 = 1
 CLK_SET_KILL = 2
+CLK_TTL_OK = 0
+CLK_TTL_EXPIRED = 1
+CLK_TTL_UNCHANGED = 2
 
 
 class clk_batch(ctypes.Structure):
@@ -76,6 +79,8 @@ SIGNATURES = {
     "clk_set_udp_checksum": (ctypes.c_int, [_P, _BP, _P, _P]),
     "clk_check_tcp_header": (ctypes.c_int, [_P, _BP, _P]),
     "clk_set_tcp_checksum": (ctypes.c_int, [_P, _BP, ctypes.c_int, _P, _P]),
+    "clk_check_icmp_header": (ctypes.c_int, [_P, _BP, _P]),
+    "clk_dec_ip_ttl": (ctypes.c_int, [_P, _BP, ctypes.c_int, _P, _P]),
     "clk_count_codes": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P, ctypes.c_uint32]),
     "clk_gen_packets": (ctypes.c_int, [_P, _BP, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
     "clk_gen_corrupt": (ctypes.c_int, [_P, _BP, ctypes.c_uint64, ctypes.c_uint32]),

@@ -117,7 +117,10 @@ constexpr int BLOCK = 256;
 #endif
 constexpr int K = CLK_K;   // 16-byte chunk loads in flight per lane per pass
 #ifndef CLK_KV
-#define CLK_KV 2           // chunks per lane per pass of the variable-length kernel
+#define CLK_KV 2           // chunks per lane per sub-pass of the variable-length kernel
+#endif
+#ifndef CLK_VU
+#define CLK_VU 1           // sub-passes whose loads are issued together
 #endif
 
 // Lanes per packet: the fewest (of 1, 4, 16, 64) whose K-deep pass covers
@@ -262,15 +265,15 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
             work = (uint32_t *)ctx->scratch;
     }
     if (bins && ctx->varlen) {
-        constexpr int KV = CLK_KV;
+        constexpr int KV = CLK_KV, VU = CLK_VU;
         uint64_t blocks = (b->n + 255) / 256;            // 4 waves x 64 packets per block
         if (blocks > (uint64_t)ctx->max_blocks)
             blocks = (uint64_t)ctx->max_blocks;
         if (work)
-            hipLaunchKernelGGL((clk::l4_varlen_kernel<PROTO, SET, true, KV>), dim3((unsigned)blocks), dim3(BLOCK), 0,
+            hipLaunchKernelGGL((clk::l4_varlen_kernel<PROTO, SET, true, KV, VU>), dim3((unsigned)blocks), dim3(BLOCK), 0,
                                ctx->cur, args_of(b), fixoff, code, sum, work);
         else
-            hipLaunchKernelGGL((clk::l4_varlen_kernel<PROTO, SET, false, KV>), dim3((unsigned)blocks), dim3(BLOCK),
+            hipLaunchKernelGGL((clk::l4_varlen_kernel<PROTO, SET, false, KV, VU>), dim3((unsigned)blocks), dim3(BLOCK),
                                0, ctx->cur, args_of(b), fixoff, code, sum, work);
     } else if (bins) {
         bin_batch(ctx, b, L);
@@ -514,6 +517,23 @@ int clk_check_tcp_header(clk_ctx *ctx, const clk_batch *b, uint8_t *out_verdict)
 int clk_set_tcp_checksum(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *out_status, uint16_t *out_sum)
 {
     return launch_l4<clk::TCP, true>(ctx, b, fixoff ? 1 : 0, out_status, out_sum, "clk_set_tcp_checksum");
+}
+
+int clk_check_icmp_header(clk_ctx *ctx, const clk_batch *b, uint8_t *out_verdict)
+{
+    return launch_l4<clk::ICMP, false>(ctx, b, 0, out_verdict, nullptr, "clk_check_icmp_header");
+}
+
+int clk_dec_ip_ttl(clk_ctx *ctx, const clk_batch *b, int multicast, uint8_t *out_status, uint16_t *out_sum)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, "clk_dec_ip_ttl"))) return r;
+    if (b->n == 0) return CLK_SUCCESS;
+    if (!out_status) return fail(ctx, CLK_EINVAL, "clk_dec_ip_ttl: null output");
+    hipLaunchKernelGGL(clk::dec_ttl_kernel, dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0, ctx->cur, args_of(b),
+                       multicast ? 1 : 0, out_status, out_sum);
+    return check_launch(ctx, "clk_dec_ip_ttl");
 }
 
 int clk_count_codes(clk_ctx *ctx, const uint8_t *codes, uint64_t n, uint64_t *counts, uint32_t ncounts)

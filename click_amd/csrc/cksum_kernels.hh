@@ -52,7 +52,7 @@ __device__ __forceinline__ uint32_t pkt_len(const BatchArgs &b, uint64_t i)
     return b.len ? b.len[i] : b.fixed_len;
 }
 
-enum Proto { UDP = 17, TCP = 6 };
+enum Proto { ICMP = 1, UDP = 17, TCP = 6 };
 
 // codes (include/click_amd_cksum.h)
 constexpr uint32_t OK = 0;
@@ -60,6 +60,7 @@ constexpr uint32_t IP_MINISCULE = 1, IP_BAD_VERSION = 2, IP_BAD_HLEN = 3, IP_BAD
                    IP_BAD_CHECKSUM = 5, IP_BAD_SADDR = 6;
 constexpr uint32_t L4_NOT_PROTO = 1, L4_BAD_LENGTH = 2, L4_BAD_CHECKSUM = 3;
 constexpr uint32_t SET_OUTPUT1 = 1, SET_KILL = 2;
+constexpr uint32_t TTL_EXPIRED = 1, TTL_UNCHANGED = 2;
 
 // ---------------------------------------------------------------------------
 // IP header: CheckIPHeader (checkipheader.cc:161-226) and SetIPChecksum
@@ -322,6 +323,27 @@ __device__ __forceinline__ void l4_parse(uint8_t *nh, uint32_t caplen, int fixof
                 st.plen_ph = ulen;
             }
         }
+    } else if (PROTO == ICMP) {          // checkicmpheader.cc:83-141 (check only)
+        if (proto != 1)
+            st.code = L4_NOT_PROTO;
+        else if (caplen < hl || caplen - hl < 8)   // guard (icmp_len would wrap) / 93-94
+            st.code = L4_BAD_LENGTH;
+        else {
+            const uint32_t ilen = caplen - hl, type = tbyte(0);
+            bool bad = false;                    // 96-134
+            if (type == 3 || type == 4 || type == 5 || type == 11 || type == 12)
+                bad = ilen < 8 + 28;
+            else if (type == 13 || type == 14)
+                bad = ilen != 20;
+            else if (type == 15 || type == 16)
+                bad = ilen != 8;
+            if (bad)
+                st.code = L4_BAD_LENGTH;
+            else {
+                st.rlen = (int)ilen;
+                st.plen_ph = ilen;
+            }
+        }
     } else if (PROTO == TCP && !SET) {
         if (proto != 6)
             st.code = L4_NOT_PROTO;
@@ -387,7 +409,9 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
         }
         const uint32_t csum = in_cksum_fold(sum);
         uint32_t r;
-        if (SET && st.hl < 20) {
+        if (PROTO == ICMP) {
+            r = csum;                           // click_in_cksum(icmph, icmp_len) != 0, 136-138
+        } else if (SET && st.hl < 20) {
             // ip_hl < 5: the transport header overlaps the IP header.  The
             // reference zeroes the field (and FIXOFF rewrites th_off)
             // BEFORE the pseudo-header reads ip_src/ip_dst, and the option
@@ -469,9 +493,10 @@ __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_
 //            its summed range as 16-byte chunks: first chunk address, chunk
 //            offset in the wave's concatenated chunk list (exclusive scan),
 //            range start within the first chunk, range length.
-//   Phase B: the wave walks the concatenated chunk list, KV chunks per
-//            lane per pass, each lane a contiguous run (lane l of pass p owns
-//            chunks p*64*KV + l*KV + [0, KV)): the lane finds its first
+//   Phase B: the wave walks the concatenated chunk list in passes of VU
+//            sub-passes of KV chunks per lane, each lane a contiguous run
+//            (lane l of sub-pass u owns chunks u*64*KV + l*KV + [0, KV));
+//            all VU*KV loads are issued before any is summed.  The lane finds its first
 //            chunk's packet by binary search, steps forward at packet
 //            boundaries, sums in registers and adds the partial into the
 //            packet's LDS accumulator only when the packet changes (u32
@@ -479,10 +504,7 @@ __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_
 //            of a packed arena.
 //   Phase C: each lane finishes its packet from its accumulator.
 // No workgroup barriers: every LDS word is private to one wave.
-#ifndef CLK_VL_INTERLEAVE
-#define CLK_VL_INTERLEAVE 0   // tuning: 1 = lane owns chunks cb + k*64 + lane (coalesced per instruction)
-#endif
-template <int PROTO, bool SET, bool DEFER, int KV>
+template <int PROTO, bool SET, bool DEFER, int KV, int VU>
 __global__ void __launch_bounds__(256) l4_varlen_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                         uint16_t *out_sum, uint32_t *work)
 {
@@ -527,75 +549,72 @@ __global__ void __launch_bounds__(256) l4_varlen_kernel(BatchArgs b, int fixoff,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t cb = 0; cb < total; cb += 64 * KV) {          // wave-uniform
-            const uint32_t c0 = CLK_VL_INTERLEAVE ? cb + lane : cb + lane * KV;
-            auto chunk_of = [&](int k) -> uint32_t { return CLK_VL_INTERLEAVE ? c0 + 64 * k : c0 + k; };
-            // last packet whose chunk start <= c0
-            uint32_t j = 0;
+        for (uint32_t cb = 0; cb < total; cb += 64 * KV * VU) {     // wave-uniform
+            u32x4 v[VU * KV];
+            u32x4 Pk[VU * KV];
+            uint32_t jk[VU * KV];
 #pragma unroll
-            for (int step = 32; step >= 1; step >>= 1)
-                if (j + step < 64 && cst[wv][j + step] <= c0)
-                    j += step;
-            uint32_t nxt = cst[wv][j + 1];
-            u32x4 P = pk[wv][j];
-            u32x4 v[KV];
-            u32x4 Pk[KV];
-            uint32_t jk[KV];
+            for (int u = 0; u < VU; u++) {
+                const uint32_t c0 = cb + 64 * KV * u + lane * KV;
+                // last packet whose chunk start <= c0
+                uint32_t j = 0;
 #pragma unroll
-            for (int k = 0; k < KV; k++) {
-                const uint32_t c = chunk_of(k);
-                if (CLK_VL_INTERLEAVE && k > 0 && c < total) {     // fresh search from the last packet
-                    uint32_t lo = j;
+                for (int step = 32; step >= 1; step >>= 1)
+                    if (j + step < 64 && cst[wv][j + step] <= c0)
+                        j += step;
+                uint32_t nxt = cst[wv][j + 1];
+                u32x4 P = pk[wv][j];
 #pragma unroll
-                    for (int step = 32; step >= 1; step >>= 1)
-                        if (lo + step < 64 && cst[wv][lo + step] <= c)
-                            lo += step;
-                    if (lo != j) {
-                        j = lo;
+                for (int k = 0; k < KV; k++) {
+                    const uint32_t c = c0 + k;
+                    if (c < total && c >= nxt) {
+                        do {                                       // skip to the chunk's packet
+                            j++;
+                            nxt = cst[wv][j + 1];
+                        } while (c >= nxt);
                         P = pk[wv][j];
                     }
-                } else if (c < total && c >= nxt) {
-                    do {                                           // skip to the chunk's packet
-                        j++;
-                        nxt = cst[wv][j + 1];
-                    } while (c >= nxt);
-                    P = pk[wv][j];
+                    jk[u * KV + k] = j;
+                    Pk[u * KV + k] = P;
+                    const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
+                    v[u * KV + k] = c < total ? *(const u32x4 *)(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
                 }
-                jk[k] = j;
-                Pk[k] = P;
-                const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
-                v[k] = c < total ? *(const u32x4 *)(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
             }
-            uint32_t cur = jk[0], part = 0;
 #pragma unroll
-            for (int k = 0; k < KV; k++) {
-                const uint32_t c = chunk_of(k);
-                if (c >= total)
-                    break;
-                if (jk[k] != cur) {
-                    atomicAdd(&acc[wv][cur], part);
-                    part = 0;
-                    cur = jk[k];
-                }
-                const u32x4 Q = Pk[k];
-                const int rlj = (int)(Q[3] & 0xFFFFFF);
-                const uint32_t s15 = Q[3] >> 24;
-                const uint32_t sel = (s15 & 1) ? 0x02030001u : 0x03020100u;   // odd start: swap bytes
-                const int rel = (int)(16 * (c - Q[2])) - (int)s15;          // chunk start - range start
-                if (rel >= 0 && rel + 16 <= rlj) {
+            for (int u = 0; u < VU; u++) {
+                const uint32_t c0 = cb + 64 * KV * u + lane * KV;
+                uint32_t cur = jk[u * KV], part = 0;
 #pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        part = dot_words(__builtin_amdgcn_perm(v[k][q], v[k][q], sel), part);
-                } else {
+                for (int k = 0; k < KV; k++) {
+                    const uint32_t c = c0 + k;
+                    if (c >= total)
+                        break;
+                    if (jk[u * KV + k] != cur) {
+                        atomicAdd(&acc[wv][cur], part);
+                        part = 0;
+                        cur = jk[u * KV + k];
+                    }
+                    const u32x4 Q = Pk[u * KV + k];
+                    const u32x4 V = v[u * KV + k];
+                    const int rlj = (int)(Q[3] & 0xFFFFFF);
+                    const uint32_t s15 = Q[3] >> 24;
+                    const uint32_t sel = (s15 & 1) ? 0x02030001u : 0x03020100u;   // odd start: swap bytes
+                    const int rel = (int)(16 * (c - Q[2])) - (int)s15;          // chunk start - range start
+                    if (rel >= 0 && rel + 16 <= rlj) {
 #pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const uint32_t dm = v[k][q] & lowmask(rlj - rel - 4 * q) & ~lowmask(-rel - 4 * q);
-                        part = dot_words(__builtin_amdgcn_perm(dm, dm, sel), part);
+                        for (int q = 0; q < 4; q++)
+                            part = dot_words(__builtin_amdgcn_perm(V[q], V[q], sel), part);
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            const uint32_t dm = V[q] & lowmask(rlj - rel - 4 * q) & ~lowmask(-rel - 4 * q);
+                            part = dot_words(__builtin_amdgcn_perm(dm, dm, sel), part);
+                        }
                     }
                 }
+                if (c0 < total)
+                    atomicAdd(&acc[wv][cur], part);
             }
-            if (c0 < total)
-                atomicAdd(&acc[wv][cur], part);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -604,6 +623,44 @@ __global__ void __launch_bounds__(256) l4_varlen_kernel(BatchArgs b, int fixoff,
         if (live)
             l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work);
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// DecIPTTL (decipttl.cc:45-77) with ACTIVE true: one lane per packet reads
+// ip_ttl..ip_sum and the first byte of ip_dst, and rewrites ip_ttl and
+// ip_sum by the reference's RFC 1624 shortcut ~(~sum + 0xFEFF) (72-73).
+// Codes: OK (decremented), TTL_EXPIRED (ttl <= 1: output 1), TTL_UNCHANGED.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) dec_ttl_kernel(BatchArgs b, int multicast, uint8_t *out_code,
+                                                      uint16_t *out_sum)
+{
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += nthreads) {
+        uint8_t *ip = b.base + pkt_off(b, i);
+        uint32_t code = TTL_UNCHANGED, stored = 0;
+        if (pkt_len(b, i) >= 20) {               // guard: no length check in the reference
+            const uint32_t w = ld_u32_unaligned(ip + 8);        // ttl, proto, sum (LE)
+            if (multicast || (ld_u8(ip + 16) & 0xF0) != 0xE0) { // 51-52, is_multicast
+                const uint32_t ttl = w & 0xFF;
+                if (ttl <= 1) {
+                    code = TTL_EXPIRED;                          // 54-57
+                } else {
+                    const uint32_t s = (~(uint32_t)bswap16(w >> 16) & 0xFFFF) + 0xFEFF;
+                    stored = ~(uint32_t)bswap16((s + (s >> 16)) & 0xFFFF) & 0xFFFF;
+                    if (((uint64_t)ip & 3) == 0) {
+                        *(uint32_t *)(ip + 8) = (ttl - 1) | (w & 0xFF00) | (stored << 16);
+                    } else {
+                        ip[8] = (uint8_t)(ttl - 1);
+                        st_u16(ip + 10, stored);
+                    }
+                    code = OK;
+                }
+            }
+        }
+        out_code[i] = (uint8_t)code;
+        if (out_sum)
+            out_sum[i] = (uint16_t)stored;
     }
 }
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CLK_ABI_VERSION 1
+#define CLK_ABI_VERSION 2
 
 /* ---- return codes -------------------------------------------------------- */
 #define CLK_SUCCESS 0
@@ -53,8 +53,8 @@ enum clk_ip_verdict {                 /* CheckIPHeader::Reason, checkipheader.hh
     CLK_IP_BAD_CHECKSUM = 5,
     CLK_IP_BAD_SADDR = 6
 };
-enum clk_l4_verdict {                 /* Check{UDP,TCP}Header::Reason */
-    CLK_L4_NOT_PROTO = 1,             /* NOT_UDP / NOT_TCP */
+enum clk_l4_verdict {                 /* Check{UDP,TCP,ICMP}Header::Reason */
+    CLK_L4_NOT_PROTO = 1,             /* NOT_UDP / NOT_TCP / NOT_ICMP */
     CLK_L4_BAD_LENGTH = 2,
     CLK_L4_BAD_CHECKSUM = 3
 };
@@ -64,6 +64,12 @@ enum clk_set_status {                 /* Set*Checksum outcome */
                                          (setudpchecksum.cc:48-61); nothing written */
     CLK_SET_KILL = 2                  /* SetIPChecksum / SetTCPChecksum bad lengths:
                                          packet killed; nothing written            */
+};
+enum clk_ttl_status {                 /* DecIPTTL outcome (decipttl.cc:45-77) */
+    CLK_TTL_OK = 0,                   /* ip_ttl decremented, ip_sum updated; output 0 */
+    CLK_TTL_EXPIRED = 1,              /* ip_ttl <= 1: drops++, output 1 (or killed)   */
+    CLK_TTL_UNCHANGED = 2             /* MULTICAST false and a multicast ip_dst, or
+                                         caplen < 20: output 0, nothing written     */
 };
 
 /* ---- context ------------------------------------------------------------- */
@@ -161,6 +167,21 @@ int clk_check_tcp_header(clk_ctx *ctx, const clk_batch *batch, uint8_t *out_verd
  * out_status[i]: OK or KILL.                                                 */
 int clk_set_tcp_checksum(clk_ctx *ctx, const clk_batch *batch, int fixoff,
                          uint8_t *out_status, uint16_t *out_sum);
+
+/* CheckICMPHeader::simple_action (elements/icmp/checkicmpheader.cc:83-141).
+ * The ICMP header is at L3 + ip_hl*4 (the transport header CheckIPHeader
+ * sets); icmp_len = len_i - ip_hl*4.  out_verdict[i]: 0 or enum
+ * clk_l4_verdict (NOT_ICMP, BAD_LENGTH incl. the per-type length rules,
+ * BAD_CHECKSUM).                                                            */
+int clk_check_icmp_header(clk_ctx *ctx, const clk_batch *batch, uint8_t *out_verdict);
+
+/* DecIPTTL::simple_action (elements/ip/decipttl.cc:45-77) with ACTIVE true
+ * (ACTIVE false passes packets without reading them: do not call).
+ * multicast = MULTICAST keyword.  Decrements ip_ttl and updates ip_sum in
+ * place by RFC 1624 (72-73); out_status[i]: enum clk_ttl_status; out_sum
+ * (nullable): the ip_sum stored (0 when not OK).                          */
+int clk_dec_ip_ttl(clk_ctx *ctx, const clk_batch *batch, int multicast,
+                   uint8_t *out_status, uint16_t *out_sum);
 
 /* ---- batch utilities ------------------------------------------------------- */
 

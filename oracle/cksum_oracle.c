@@ -42,6 +42,8 @@
 #define CLK_L4_BAD_CHECKSUM 3
 #define CLK_SET_OUTPUT1 1
 #define CLK_SET_KILL 2
+#define CLK_TTL_EXPIRED 1
+#define CLK_TTL_UNCHANGED 2
 
 static inline uint16_t ld16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
 static inline uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
@@ -283,6 +285,66 @@ int oracle_set_tcp_checksum(uint8_t *nh, uint32_t caplen, int fixoff)
     return CLK_OK;
 }
 
+/* elements/icmp/checkicmpheader.cc:83-141.  The transport header is the
+ * one CheckIPHeader / MarkIPHeader set: nh + ip_hl*4 (set_ip_header).
+ * Domain guards: caplen < 20 -> BAD_LENGTH (no full base IP header);
+ * caplen < hl -> BAD_LENGTH (icmp_len would wrap and the reference would
+ * read the type byte outside the packet). */
+int oracle_check_icmp_header(const uint8_t *nh, uint32_t caplen)
+{
+    if (caplen < 20)
+        return CLK_L4_BAD_LENGTH;
+    if (nh[9] != 1)                                         /* 89-90, IP_PROTO_ICMP */
+        return CLK_L4_NOT_PROTO;
+    uint32_t hl = (uint32_t)(nh[0] & 0xF) << 2;
+    if (caplen < hl)
+        return CLK_L4_BAD_LENGTH;
+    uint32_t icmp_len = caplen - hl;                        /* 92 */
+    if (icmp_len < 8)                                       /* 93-94, sizeof(click_icmp) */
+        return CLK_L4_BAD_LENGTH;
+    const uint8_t *icmph = nh + hl;
+    switch (icmph[0]) {                                     /* 96-134 */
+    case 3: case 11: case 12: case 4: case 5:   /* UNREACH TIMXCEED PARAMPROB SOURCEQUENCH REDIRECT */
+        if (icmp_len < 8 + 28)
+            return CLK_L4_BAD_LENGTH;
+        break;
+    case 13: case 14:                           /* TSTAMP TSTAMPREPLY: sizeof(click_icmp_tstamp) */
+        if (icmp_len != 20)
+            return CLK_L4_BAD_LENGTH;
+        break;
+    case 15: case 16:                           /* IREQ IREQREPLY */
+        if (icmp_len != 8)
+            return CLK_L4_BAD_LENGTH;
+        break;
+    default:
+        break;
+    }
+    if ((oracle_in_cksum(icmph, (int)icmp_len) & 0xFFFF) != 0)  /* 136-138 */
+        return CLK_L4_BAD_CHECKSUM;
+    return CLK_OK;
+}
+
+/* elements/ip/decipttl.cc:45-77 with ACTIVE true (ACTIVE false returns the
+ * packet before reading it; the caller does not launch).  multicast =
+ * the MULTICAST keyword.  Returns CLK_OK (TTL decremented, ip_sum updated
+ * by RFC 1624, output 0), CLK_TTL_EXPIRED (ip_ttl <= 1: output 1) or
+ * CLK_TTL_UNCHANGED (output 0 untouched).  Domain guard: caplen < 20 ->
+ * UNCHANGED (the reference asserts a network header and reads ip_ttl,
+ * ip_sum and ip_dst without a length check). */
+int oracle_dec_ip_ttl(uint8_t *nh, uint32_t caplen, int multicast)
+{
+    if (caplen < 20)
+        return CLK_TTL_UNCHANGED;
+    if (!multicast && (nh[16] & 0xF0) == 0xE0)             /* 51-52, is_multicast */
+        return CLK_TTL_UNCHANGED;
+    if (nh[8] <= 1)                                         /* 54-57 */
+        return CLK_TTL_EXPIRED;
+    nh[8]--;                                                /* 63 */
+    uint32_t sum = (~(uint32_t)bswap16(ld16(nh + 10)) & 0xFFFF) + 0xFEFF;  /* 72 */
+    st16(nh + 10, (uint16_t)~bswap16((sum + (sum >> 16)) & 0xFFFF));     /* 73 */
+    return CLK_OK;
+}
+
 /* ---- batch drivers ------------------------------------------------------- */
 
 static inline uint64_t pkt_off(const uint64_t *off, uint64_t stride, uint64_t i)
@@ -314,6 +376,12 @@ static int run_one(int op, uint8_t *p, uint32_t l, int arg, uint16_t *sum)
     case ORACLE_OP_SET_TCP:
         r = oracle_set_tcp_checksum(p, l, arg);
         *sum = r == 0 ? ld16(p + ((p[0] & 0xF) << 2) + 16) : 0;
+        return r;
+    case ORACLE_OP_CHECK_ICMP:
+        return oracle_check_icmp_header(p, l);
+    case ORACLE_OP_DEC_TTL:
+        r = oracle_dec_ip_ttl(p, l, arg);
+        *sum = r == 0 ? ld16(p + 10) : 0;
         return r;
     }
     return -1;

@@ -43,6 +43,8 @@ int oracle_check_udp_header(const uint8_t *nh, uint32_t caplen);
 int oracle_set_udp_checksum(uint8_t *nh, uint32_t caplen);
 int oracle_check_tcp_header(const uint8_t *nh, uint32_t caplen);
 int oracle_set_tcp_checksum(uint8_t *nh, uint32_t caplen, int fixoff);
+int oracle_check_icmp_header(const uint8_t *nh, uint32_t caplen);
+int oracle_dec_ip_ttl(uint8_t *nh, uint32_t caplen, int multicast);
 
 /* ---- batch drivers with the C-ABI's batch semantics ----------------------
  * Packet i starts at base + (off ? off[i] : i*stride) and has
@@ -55,6 +57,8 @@ enum {
     ORACLE_OP_SET_UDP = 4,    /* out16 stored uh_sum                             */
     ORACLE_OP_CHECK_TCP = 5,
     ORACLE_OP_SET_TCP = 6,    /* arg = FIXOFF; out16 stored th_sum               */
+    ORACLE_OP_CHECK_ICMP = 7,
+    ORACLE_OP_DEC_TTL = 8,    /* arg = MULTICAST; out16 stored ip_sum            */
 };
 int oracle_batch(int op, uint8_t *base, const uint64_t *off, uint64_t stride,
                  const uint32_t *len, uint32_t fixed_len, uint64_t n, int arg,

@@ -54,10 +54,21 @@ def _options(rng, words):
     return bytes(out)
 
 
+ICMP_TYPES = [0, 3, 4, 5, 8, 9, 11, 12, 13, 14, 15, 16, 17, 18, 42]
+
+
 def build(rng, proto, total, opt_words=0):
     """One well-formed IPv4 packet of `total` bytes (checksums zero)."""
     hl = 20 + 4 * opt_words
-    tl = max(total, hl + (8 if proto == 17 else 20))
+    tl = max(total, hl + (8 if proto in (1, 17) else 20))
+    if proto == 1:
+        itype = int(rng.choice(ICMP_TYPES))
+        if itype in (13, 14) and rng.random() < 0.7:      # exact-size types (checkicmpheader.cc:96-134)
+            tl = hl + 20
+        elif itype in (15, 16) and rng.random() < 0.7:
+            tl = hl + 8
+        elif itype in (3, 4, 5, 11, 12) and rng.random() < 0.3:
+            tl = hl + int(rng.integers(8, 44))
     b = bytearray(rng.integers(0, 256, tl, dtype=np.uint8).tobytes())
     b[0] = 0x40 | (hl // 4)
     b[1] = 0
@@ -70,6 +81,9 @@ def build(rng, proto, total, opt_words=0):
     if proto == 17:
         b[hl + 4:hl + 6] = (tl - hl).to_bytes(2, "big")
         b[hl + 6:hl + 8] = b"\0\0"
+    elif proto == 1:
+        b[hl] = itype
+        b[hl + 2:hl + 4] = b"\0\0"
     else:
         b[hl + 12] = (5 + int(rng.integers(0, 3))) << 4 | (b[hl + 12] & 0xF)
         b[hl + 16:hl + 18] = b"\0\0"
@@ -89,6 +103,8 @@ def _mutate(rng, b, proto):
     elif r < 0.24 and len(b) > hl + 13:
         if proto == 17:
             b[hl + 4:hl + 6] = int(rng.choice([0, 7, 8, len(b) - hl + 1, int(rng.integers(0, 65536))])).to_bytes(2, "big")
+        elif proto == 1:
+            b[hl] = int(rng.choice(ICMP_TYPES))
         else:
             b[hl + 12] = (int(rng.integers(0, 16)) << 4) | (b[hl + 12] & 0xF)
     elif r < 0.30:
@@ -135,7 +151,10 @@ def make_batch(rng, n, proto, max_total=1600, opt_frac=0.2, mutate_frac=0.5, tin
         arena[int(off[i]):int(off[i]) + len(p)] = np.frombuffer(p, np.uint8)
     if set_checksums:
         oracle_lib.batch("set_ip", arena, n, off=off, length=caplen)
-        oracle_lib.batch("set_udp" if proto == 17 else "set_tcp", arena, n, off=off, length=caplen, arg=0)
+        if proto == 1:
+            set_icmp_checksums(arena, off, caplen)
+        else:
+            oracle_lib.batch("set_udp" if proto == 17 else "set_tcp", arena, n, off=off, length=caplen, arg=0)
     for i in range(n):
         if rng.random() < mutate_frac and caplen[i] >= 20:
             o = int(off[i])
@@ -144,3 +163,37 @@ def make_batch(rng, n, proto, max_total=1600, opt_frac=0.2, mutate_frac=0.5, tin
         if rng.random() < trunc_frac and caplen[i] > 0:
             caplen[i] = int(rng.integers(0, caplen[i]))
     return arena, off, caplen, int(caplen.max()) if n else 0
+
+
+def set_icmp_checksums(arena, off, caplen):
+    """icmp_cksum over [th, end) as ICMPPingEncap does (icmppingencap.cc:85,99);
+    Click has no SetICMPChecksum element, so fixtures set it here."""
+    L = oracle_lib.load_oracle()
+    for i in range(len(off)):
+        o, c = int(off[i]), int(caplen[i])
+        if c < 20:
+            continue
+        hl = (int(arena[o]) & 0xF) * 4
+        if hl < 20 or c < hl + 4:
+            continue
+        arena[o + hl + 2:o + hl + 4] = 0
+        seg = arena[o + hl:o + c].tobytes()
+        v = L.oracle_in_cksum(seg, len(seg))
+        arena[o + hl + 2] = v & 0xFF
+        arena[o + hl + 3] = v >> 8
+
+
+def vary_ttl(rng, arena, off, caplen, frac=0.4):
+    """DecIPTTL inputs: TTLs at the 0/1/2/255 edges and multicast
+    destinations (decipttl.cc:51-57) in a fraction of the packets."""
+    for i in range(len(off)):
+        o = int(off[i])
+        if caplen[i] < 20 or rng.random() >= frac:
+            continue
+        r = rng.random()
+        if r < 0.5:
+            arena[o + 8] = int(rng.choice([0, 1, 2, 255]))
+        elif r < 0.8:
+            arena[o + 16] = 0xE0 | int(rng.integers(0, 16))
+        else:
+            arena[o + 10] = int(rng.integers(0, 256))          # stale ip_sum: updated all the same

@@ -11,9 +11,11 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE = os.path.join(ROOT, "oracle", "libcksum_oracle.so")
 
-OP_IN_CKSUM, OP_CHECK_IP, OP_SET_IP, OP_CHECK_UDP, OP_SET_UDP, OP_CHECK_TCP, OP_SET_TCP = range(7)
+(OP_IN_CKSUM, OP_CHECK_IP, OP_SET_IP, OP_CHECK_UDP, OP_SET_UDP, OP_CHECK_TCP, OP_SET_TCP, OP_CHECK_ICMP,
+ OP_DEC_TTL) = range(9)
 OPS = {"in_cksum": OP_IN_CKSUM, "check_ip": OP_CHECK_IP, "set_ip": OP_SET_IP, "check_udp": OP_CHECK_UDP,
-       "set_udp": OP_SET_UDP, "check_tcp": OP_CHECK_TCP, "set_tcp": OP_SET_TCP}
+       "set_udp": OP_SET_UDP, "check_tcp": OP_CHECK_TCP, "set_tcp": OP_SET_TCP, "check_icmp": OP_CHECK_ICMP,
+       "dec_ttl": OP_DEC_TTL}
 
 _P = ctypes.c_void_p
 _lib = None

@@ -188,3 +188,41 @@ def set_tcp(b, caplen, fixoff=False):
     b[hl + 16:hl + 18] = b"\0\0"
     struct.pack_into("<H", b, hl + 16, pseudohdr(in_cksum(b[hl:hl + plen]), b, plen))
     return 0, bytes(b)
+
+
+def check_icmp(b, caplen):
+    """CheckICMPHeader (checkicmpheader.cc:83-141) with the oracle's guards."""
+    if caplen < 20:
+        return 2
+    if b[9] != 1:
+        return 1
+    hl = (b[0] & 0xF) * 4
+    if caplen < hl or caplen - hl < 8:
+        return 2
+    ilen = caplen - hl
+    t = b[hl]
+    need = {3: (">=", 36), 4: (">=", 36), 5: (">=", 36), 11: (">=", 36), 12: (">=", 36),
+            13: ("==", 20), 14: ("==", 20), 15: ("==", 8), 16: ("==", 8)}.get(t)
+    if need and ((need[0] == ">=" and ilen < need[1]) or (need[0] == "==" and ilen != need[1])):
+        return 2
+    return 3 if in_cksum(b[hl:hl + ilen]) != 0 else 0
+
+
+def dec_ttl(b, caplen, multicast=True):
+    """DecIPTTL (decipttl.cc:45-77): returns (status, new bytes).  The
+    checksum is updated with the general RFC 1624 form (ip.h:177-185) for
+    the 16-bit word {ttl, proto}, not the reference's 0xFEFF shortcut."""
+    b = bytearray(b)
+    if caplen < 20 or (not multicast and (b[16] & 0xF0) == 0xE0):
+        return 2, bytes(b)
+    if b[8] <= 1:
+        return 1, bytes(b)
+    old_hw = be16(b, 8)
+    b[8] -= 1
+    new_hw = be16(b, 8)
+    hc = be16(b, 10)
+    s = ((~hc) & 0xFFFF) + ((~old_hw) & 0xFFFF) + new_hw
+    while s >> 16:
+        s = (s & 0xFFFF) + (s >> 16)
+    struct.pack_into(">H", b, 10, (~s) & 0xFFFF)
+    return 0, bytes(b)

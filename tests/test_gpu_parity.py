@@ -17,7 +17,7 @@ from tests import oracle_lib, fuzz
 pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "golden_vectors.json")
-OPS_L4 = {17: ("check_udp", "set_udp"), 6: ("check_tcp", "set_tcp")}
+OPS_L4 = {17: ("check_udp", "set_udp"), 6: ("check_tcp", "set_tcp"), 1: ("check_icmp",)}
 
 
 @pytest.fixture(scope="module")
@@ -59,6 +59,10 @@ def run_gpu(ctx, op, b, arg=1):
         return ctx.check_tcp_header(b), None
     if op == "set_tcp":
         return ctx.set_tcp_checksum(b, fixoff=bool(arg))
+    if op == "check_icmp":
+        return ctx.check_icmp_header(b), None
+    if op == "dec_ttl":
+        return ctx.dec_ip_ttl(b, multicast=bool(arg))
     raise ValueError(op)
 
 
@@ -107,7 +111,7 @@ def test_golden_vectors_on_gpu(torch, ctx):
             assert got == v["expect"], (v["name"], shift, got)
 
 
-@pytest.mark.parametrize("proto", [17, 6])
+@pytest.mark.parametrize("proto", [17, 6, 1])
 @pytest.mark.parametrize("max_total,align", [(96, "any"), (400, "any"), (1600, "even"), (1600, "any"),
                                              (5000, "any"), (20000, "even")])
 def test_fuzz_parity(torch, ctx, proto, max_total, align):
@@ -116,8 +120,12 @@ def test_fuzz_parity(torch, ctx, proto, max_total, align):
     arena, off, caplen, ml = fuzz.make_batch(rng, n, proto, max_total=max_total, align=align)
     for op in ("check_ip", "set_ip") + OPS_L4[proto]:
         compare(torch, ctx, op, arena, n, off=off, length=caplen, max_len=ml, arg=1)
-    compare(torch, ctx, "set_tcp" if proto == 6 else "set_udp", arena, n, off=off, length=caplen, max_len=ml, arg=0)
+    if proto != 1:
+        compare(torch, ctx, OPS_L4[proto][1], arena, n, off=off, length=caplen, max_len=ml, arg=0)
     compare(torch, ctx, "check_ip", arena, n, off=off, length=caplen, max_len=ml, arg=0)   # CheckIPHeader2
+    fuzz.vary_ttl(rng, arena, off, caplen)
+    for multicast in (1, 0):                                                            # DecIPTTL
+        compare(torch, ctx, "dec_ttl", arena, n, off=off, length=caplen, max_len=ml, arg=multicast)
 
 
 @pytest.mark.parametrize("max_len_hint", [0, 64, 500, 2000, 100000])
@@ -258,6 +266,27 @@ def test_full_size_properties(torch, ctx, proto, L, stride, n):
         torch.cuda.empty_cache()
 
 
+def test_dec_ttl_full_size(torch, ctx):
+    """DecIPTTL over a C2-sized batch (16M x 64 B slots): every TTL drops by
+    one and the RFC 1624 update equals a full recomputation (CheckIPHeader
+    passes; SetIPChecksum rewrites the same values)."""
+    import click_amd
+    n, L, stride = 16 << 20, 46, 64
+    arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda:0")
+    b = click_amd.Batch(arena, n, stride=stride, fixed_len=L)
+    ctx.gen_packets(b, proto=17)
+    ctx.set_ip_checksum(b, want_sums=False)
+    st, sums = ctx.dec_ip_ttl(b)
+    assert int((st != 0).sum()) == 0
+    assert int(ctx.check_ip_header(b).ne(0).sum()) == 0
+    ttl = arena.view(n, stride)[:, 8]
+    assert int((ttl != 63).sum()) == 0
+    st2, sums2 = ctx.set_ip_checksum(b)
+    assert torch.equal(sums, sums2)
+    del arena
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("mode", ["0", "1"])
 def test_set_modes_bit_exact(torch, mode, monkeypatch):
     """Fused (mode 0) and two-phase (mode 1, compute then scatter) Set
@@ -289,7 +318,7 @@ def test_size_class_partition_bit_exact(torch, bin_min, varlen, monkeypatch):
     monkeypatch.setenv("CLK_VARLEN", varlen)
     c = click_amd.Context(0)
     rng = np.random.default_rng(41)
-    for proto, mt in ((17, 1600), (6, 9000), (17, 200)):
+    for proto, mt in ((17, 1600), (6, 9000), (17, 200), (1, 1600)):
         arena, off, caplen, ml = fuzz.make_batch(rng, 2000, proto, max_total=mt)
         for op in ("in_cksum",) + OPS_L4[proto]:
             compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=1)

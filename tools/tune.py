@@ -37,9 +37,13 @@ VARIANTS = {
     "diag_nofield": (["-DCLK_DIAG_NO_FIELD_STORE=1"], {}),
     "kv1": (["-DCLK_KV=1"], {}),
     "kv2": (["-DCLK_KV=2"], {}),
-    "il2": (["-DCLK_KV=2", "-DCLK_VL_INTERLEAVE=1"], {}),
-    "il4": (["-DCLK_KV=4", "-DCLK_VL_INTERLEAVE=1"], {}),
-    "il8": (["-DCLK_KV=8", "-DCLK_VL_INTERLEAVE=1"], {}),
+    "k1u2": (["-DCLK_KV=1", "-DCLK_VU=2"], {}),
+    "kv4": (["-DCLK_KV=4"], {}),
+    "u2": (["-DCLK_VU=2"], {}),
+    "u3": (["-DCLK_VU=3"], {}),
+    "u4": (["-DCLK_VU=4"], {}),
+    "k1u4": (["-DCLK_KV=1", "-DCLK_VU=4"], {}),
+    "k1u8": (["-DCLK_KV=1", "-DCLK_VU=8"], {}),
     "kv8": (["-DCLK_KV=8"], {}),
     "bins": ([], {"CLK_VARLEN": "0"}),
 }
@@ -118,11 +122,17 @@ def main():
     element = os.environ.get("TUNE_ELEMENT", w["elements"][-1])
     run = elements[element]
     times = {nm: [] for nm in names}
+    ref_status, mismatch = None, []
     for r in range(args.rounds):
         for nm in names:
             c = ctxs[nm]
+            status.fill_(0xEE)
             run(c)
             torch.cuda.synchronize()
+            if ref_status is None:
+                ref_status = status.clone()
+            elif not torch.equal(status, ref_status) and nm not in mismatch and not nm.startswith("d"):
+                mismatch.append(nm)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(args.launches):
@@ -134,7 +144,7 @@ def main():
     out = {nm: {"median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
                 "GBs": round(alg / (statistics.median(t) * 1e-3) / 1e9, 1)} for nm, t in times.items()}
     print(json.dumps({"workload": args.workload, "element": element,
-                      "variants": out}))
+                      "variants": out, "status_mismatch": mismatch}))
 
 
 if __name__ == "__main__":
