@@ -464,7 +464,7 @@ std::string CheckIPHeader::drop_message(const char *reason) const
     return name_ + ": IP header check failed: " + reason;     // checkipheader.cc:146-147
 }
 
-int CheckIPHeader::configure(ConfArgs &args, std::string *err)
+int CheckIPHeader::conf_addresses(ConfArgs &args, std::string *err)
 {
     std::string v;
     if (args.take("INTERFACES", &v)) {           // InterfacesArg, checkipheader.cc:51-74
@@ -500,6 +500,32 @@ int CheckIPHeader::configure(ConfArgs &args, std::string *err)
             good_dst_.push_back(ip);
         }
     }
+    return 0;
+}
+
+int CheckIPHeader::upload_addresses(std::string *err)
+{
+    if (!bad_src_.empty() || !good_dst_.empty()) {
+        const size_t nb = bad_src_.size() + good_dst_.size();
+        if (hipMalloc(&d_lists_, nb * 4) != hipSuccess) {
+            *err = "out of device memory";
+            return -1;
+        }
+        std::vector<uint32_t> all(bad_src_);
+        all.insert(all.end(), good_dst_.begin(), good_dst_.end());
+        if (hipMemcpy(d_lists_, all.data(), nb * 4, hipMemcpyHostToDevice) != hipSuccess) {
+            *err = "hipMemcpy failed";
+            return -1;
+        }
+    }
+    return 0;
+}
+
+int CheckIPHeader::configure(ConfArgs &args, std::string *err)
+{
+    std::string v;
+    if (conf_addresses(args, err))
+        return -1;
     long off;
     if (args.take("OFFSET", &v)) {
         if (!parse_int(v, &off) || off < 0) {
@@ -522,21 +548,8 @@ int CheckIPHeader::configure(ConfArgs &args, std::string *err)
         *err = "too many arguments";
         return -1;
     }
-    if (BatchElement::configure(args, err))
+    if (BatchElement::configure(args, err) || upload_addresses(err))
         return -1;
-    if (!bad_src_.empty() || !good_dst_.empty()) {
-        const size_t nb = bad_src_.size() + good_dst_.size();
-        if (hipMalloc(&d_lists_, nb * 4) != hipSuccess) {
-            *err = "out of device memory";
-            return -1;
-        }
-        std::vector<uint32_t> all(bad_src_);
-        all.insert(all.end(), good_dst_.begin(), good_dst_.end());
-        if (hipMemcpy(d_lists_, all.data(), nb * 4, hipMemcpyHostToDevice) != hipSuccess) {
-            *err = "hipMemcpy failed";
-            return -1;
-        }
-    }
     reason_drops_.resize(details_ ? 6 : 0, 0);
     return 0;
 }
@@ -572,6 +585,81 @@ void CheckIPHeader::route(Pending &p, int code, uint16_t, Result *r)
     if (plen > len)
         r->length = p.length - (plen - len);
     r->port = 0;
+}
+
+// ---- IPInputCombo (elements/ip/ipinputcombo.cc) -----------------------------
+
+IPInputCombo::IPInputCombo(clk_ctx *ctx, const std::string &name, int noutputs)
+    : CheckIPHeader(ctx, name, noutputs, true)
+{
+    offset_ = 14;                                            // Strip(14), 79-80
+}
+
+int IPInputCombo::configure(ConfArgs &args, std::string *err)
+{
+    // read_mp("COLOR"), read_p("BADSRC*", OldBadSrcArg), INTERFACES, BADSRC,
+    // GOODDST (ipinputcombo.cc:41-47)
+    std::string v;
+    const bool kw_color = args.take("COLOR", &v);
+    if (!kw_color) {
+        if (args.pos.empty()) {
+            *err = "missing mandatory COLOR argument";
+            return -1;
+        }
+        v = args.pos[0];
+        args.pos.erase(args.pos.begin());
+    }
+    if (!parse_int(v, &color_)) {
+        *err = "COLOR: expected integer";
+        return -1;
+    }
+    if (!args.pos.empty()) {                                 // old-style BADSRC list
+        for (const std::string &w : words(args.pos[0])) {
+            uint32_t ip;
+            if (!parse_ip(w, &ip)) {
+                *err = "BADSRC: expected list of IP addresses";
+                return -1;
+            }
+            bad_src_.push_back(ip);
+        }
+        bad_src_.push_back(0);                               // OldBadSrcArg, checkipheader.cc:40-47
+        bad_src_.push_back(0xFFFFFFFFu);
+        args.pos.erase(args.pos.begin());
+    }
+    if (conf_addresses(args, err))
+        return -1;
+    if (!args.pos.empty()) {
+        *err = "too many arguments";
+        return -1;
+    }
+    if (BatchElement::configure(args, err) || upload_addresses(err))
+        return -1;
+    return 0;
+}
+
+void IPInputCombo::route(Pending &p, int code, uint16_t, Result *r)
+{
+    if (code != CLK_OK) {                                    // bad: 135-139
+        if (drops_ == 0)
+            chatter("IP checksum failed");
+        drops_++;
+        r->port = -1;
+        return;
+    }
+    // after Strip(14): set_ip_header, shorten to ip_len (125-130)
+    const uint32_t plen = p.length - 14;
+    const uint32_t len = be16(p.data + 14 + 2);
+    r->length = plen > len ? len : plen;
+    r->port = 0;
+}
+
+std::string IPInputCombo::read_handler(const std::string &h) const
+{
+    if (h == "drops")
+        return std::to_string(drops_);
+    if (h == "color")
+        return std::to_string(color_);
+    return BatchElement::read_handler(h);
 }
 
 // ---- SetIPChecksum (elements/ip/setipchecksum.cc:74-95) ---------------------
@@ -613,19 +701,25 @@ std::string SetIPChecksum::read_handler(const std::string &h) const
 
 static const char *const udp_reasons[] = {"not UDP", "bad packet length", "bad UDP checksum"};
 static const char *const tcp_reasons[] = {"not TCP", "bad packet length", "bad TCP checksum"};
+static const char *const icmp_reasons[] = {"not ICMP", "bad packet length", "bad ICMP checksum"};  // checkicmpheader.cc:30-32
 
 CheckL4Header::CheckL4Header(clk_ctx *ctx, const std::string &name, int noutputs, int proto)
     : CheckElement(ctx, name, noutputs), proto_(proto)
 {
 }
 
-const char *const *CheckL4Header::reason_texts() const { return proto_ == 17 ? udp_reasons : tcp_reasons; }
+const char *const *CheckL4Header::reason_texts() const
+{
+    return proto_ == 17 ? udp_reasons : proto_ == 6 ? tcp_reasons : icmp_reasons;
+}
 
 std::string CheckL4Header::drop_message(const char *reason) const
 {
     if (proto_ == 17)
         return std::string("UDP header check failed: ") + reason;             // checkudpheader.cc:70
-    return declaration() + ": TCP header check failed: " + reason;           // checktcpheader.cc:70
+    if (proto_ == 6)
+        return declaration() + ": TCP header check failed: " + reason;       // checktcpheader.cc:70
+    return declaration() + ": ICMP header check failed: " + reason;          // checkicmpheader.cc:67
 }
 
 int CheckL4Header::configure(ConfArgs &args, std::string *err)
@@ -652,7 +746,9 @@ bool CheckL4Header::span(const Pending &p, uint32_t *off, uint32_t *len, int32_t
 
 int CheckL4Header::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
 {
-    return proto_ == 17 ? clk_check_udp_header(ctx_, b, d_codes) : clk_check_tcp_header(ctx_, b, d_codes);
+    if (proto_ == 17)
+        return clk_check_udp_header(ctx_, b, d_codes);
+    return proto_ == 6 ? clk_check_tcp_header(ctx_, b, d_codes) : clk_check_icmp_header(ctx_, b, d_codes);
 }
 
 void CheckL4Header::route(Pending &, int code, uint16_t, Result *r)
@@ -739,8 +835,76 @@ void SetL4Checksum::route(Pending &p, int code, uint16_t sum, Result *r)
     }
 }
 
+// ---- DecIPTTL (elements/ip/decipttl.cc) -------------------------------------
+
+int DecIPTTL::configure(ConfArgs &args, std::string *err)
+{
+    std::string v;                                           // 36-41
+    if (args.take("ACTIVE", &v) && !parse_bool(v, &active_)) {
+        *err = "ACTIVE: expected boolean";
+        return -1;
+    }
+    if (args.take("MULTICAST", &v) && !parse_bool(v, &multicast_)) {
+        *err = "MULTICAST: expected boolean";
+        return -1;
+    }
+    if (!args.pos.empty()) {
+        *err = "too many arguments";
+        return -1;
+    }
+    return BatchElement::configure(args, err);
+}
+
+bool DecIPTTL::span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const
+{
+    // ACTIVE false returns the packet untouched (48-49); so does a packet
+    // without a network header, where the reference asserts (47)
+    if (!active_ || p.nh_off < 0 || (uint32_t)p.nh_off > p.length) {
+        *code = CLK_TTL_UNCHANGED;
+        return false;
+    }
+    *off = (uint32_t)p.nh_off;
+    *len = p.length - *off;
+    return true;
+}
+
+int DecIPTTL::run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums)
+{
+    return clk_dec_ip_ttl(ctx_, b, multicast_ ? 1 : 0, d_codes, d_sums);
+}
+
+void DecIPTTL::route(Pending &p, int code, uint16_t sum, Result *r)
+{
+    if (code == CLK_TTL_EXPIRED) {                           // 54-57: checked_output_push(1, p)
+        drops_++;
+        r->port = noutputs_ == 2 ? 1 : -1;
+        return;
+    }
+    if (code == CLK_TTL_OK) {                                // 63, 72-73
+        uint8_t *iph = p.data + p.nh_off;
+        iph[8]--;
+        std::memcpy(iph + 10, &sum, 2);
+    }
+    r->port = 0;
+}
+
+std::string DecIPTTL::read_handler(const std::string &h) const
+{
+    if (h == "drops")
+        return std::to_string(drops_);
+    if (h == "active")
+        return active_ ? "true" : "false";
+    return BatchElement::read_handler(h);
+}
+
 BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::string &name, int noutputs)
 {
+    if (cls == "CheckICMPHeader")
+        return new (std::nothrow) CheckL4Header(ctx, name, noutputs, 1);
+    if (cls == "DecIPTTL")
+        return new (std::nothrow) DecIPTTL(ctx, name, noutputs);
+    if (cls == "IPInputCombo")
+        return new (std::nothrow) IPInputCombo(ctx, name, noutputs);
     if (cls == "CheckIPHeader")
         return new (std::nothrow) CheckIPHeader(ctx, name, noutputs, true);
     if (cls == "CheckIPHeader2")

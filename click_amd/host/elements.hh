@@ -133,12 +133,34 @@ class CheckIPHeader : public CheckElement {
     int nreasons() const override { return 6; }
     std::string drop_message(const char *reason) const override;
 
-  private:
+  protected:
+    int conf_addresses(ConfArgs &args, std::string *err);   // INTERFACES, BADSRC, GOODDST
+    int upload_addresses(std::string *err);
     bool checksum_default_;
     bool checksum_ = true;
     uint32_t offset_ = 0;
     std::vector<uint32_t> bad_src_, good_dst_;
     uint32_t *d_lists_ = nullptr;
+};
+
+// IPInputCombo (elements/ip/ipinputcombo.cc:66-140): Paint(COLOR) +
+// Strip(14) + CheckIPHeader in one element.  The GPU work is CheckIPHeader's
+// kernel at OFFSET 14; every bad packet is killed and the first one chatters
+// "IP checksum failed".  The result length is the length after Strip(14)
+// and the ip_len trim; painting and pulling the 14 bytes are Packet
+// operations the Click-side adapter performs.
+class IPInputCombo : public CheckIPHeader {
+  public:
+    IPInputCombo(clk_ctx *ctx, const std::string &name, int noutputs);
+    const char *class_name() const override { return "IPInputCombo"; }
+    int configure(ConfArgs &args, std::string *err) override;
+    std::string read_handler(const std::string &h) const override;
+
+  protected:
+    void route(Pending &p, int code, uint16_t sum, Result *r) override;
+
+  private:
+    long color_ = 0;
 };
 
 class SetIPChecksum : public BatchElement {
@@ -157,10 +179,14 @@ class SetIPChecksum : public BatchElement {
     uint32_t drops_ = 0;
 };
 
+// CheckUDPHeader / CheckTCPHeader / CheckICMPHeader (proto 17 / 6 / 1).
 class CheckL4Header : public CheckElement {
   public:
     CheckL4Header(clk_ctx *ctx, const std::string &name, int noutputs, int proto);
-    const char *class_name() const override { return proto_ == 17 ? "CheckUDPHeader" : "CheckTCPHeader"; }
+    const char *class_name() const override
+    {
+        return proto_ == 17 ? "CheckUDPHeader" : proto_ == 6 ? "CheckTCPHeader" : "CheckICMPHeader";
+    }
     int configure(ConfArgs &args, std::string *err) override;
 
   protected:
@@ -191,6 +217,26 @@ class SetL4Checksum : public BatchElement {
     int proto_;
     bool fixoff_ = false;
     bool warned_ = false;   // router()->force_attachment("SetUDPChecksum_message")
+};
+
+// DecIPTTL (elements/ip/decipttl.cc): ACTIVE, MULTICAST; handlers drops,
+// active.  Expired packets (ip_ttl <= 1) go to output 1 or are killed.
+class DecIPTTL : public BatchElement {
+  public:
+    using BatchElement::BatchElement;
+    const char *class_name() const override { return "DecIPTTL"; }
+    int configure(ConfArgs &args, std::string *err) override;
+    std::string read_handler(const std::string &h) const override;
+
+  protected:
+    bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
+    int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
+    void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    bool wants_sums() const override { return true; }
+
+  private:
+    bool active_ = true, multicast_ = true;
+    uint32_t drops_ = 0;
 };
 
 BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::string &name, int noutputs);

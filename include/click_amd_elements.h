@@ -26,6 +26,14 @@
  *   SetUDPChecksum  (no keywords)      (elements/tcpudp/setudpchecksum.cc)
  *   CheckTCPHeader  VERBOSE, DETAILS   (elements/tcpudp/checktcpheader.cc:50-64)
  *   SetTCPChecksum  [FIXOFF]           (elements/tcpudp/settcpchecksum.cc:36-42)
+ *   CheckICMPHeader VERBOSE, DETAILS   (elements/icmp/checkicmpheader.cc:49-60)
+ *   DecIPTTL        ACTIVE, MULTICAST  (elements/ip/decipttl.cc:36-41); handlers
+ *                   drops, active; expired packets to output 1 or killed
+ *   IPInputCombo    COLOR, [BADSRC,] INTERFACES, BADSRC, GOODDST
+ *                   (elements/ip/ipinputcombo.cc:38-64): CheckIPHeader at
+ *                   OFFSET 14, bad packets killed; the result length is the
+ *                   length after Strip(14) and the ip_len trim, and the
+ *                   adapter paints COLOR ("color" handler) and pulls 14 bytes
  * plus glue keywords BATCH (packets per GPU batch, default 65536).
  */
 #ifndef CLICK_AMD_ELEMENTS_H

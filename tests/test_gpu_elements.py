@@ -48,7 +48,8 @@ def frames(rng, n, proto, max_total=1600, eth=14):
 
 def run_element(ctx, cls, config, arena, foff, flen, nh, noutputs, batch=None):
     from click_amd.elements import Element
-    e = Element(ctx, cls, config + ((", BATCH %d" % batch) if batch else ""), name="e0", noutputs=noutputs)
+    conf = ", ".join(c for c in (config, ("BATCH %d" % batch) if batch else "") if c)
+    e = Element(ctx, cls, conf, name="e0", noutputs=noutputs)
     base = arena.ctypes.data
     for i in range(len(foff)):
         full = e.push_ptr(base + int(foff[i]), int(flen[i]), nh, token=i)
@@ -200,3 +201,77 @@ def test_configure_errors(ctx):
             Element(ctx, cls, conf)
     Element(ctx, "CheckIPHeader2", "14")
     Element(ctx, "CheckIPHeader", "CHECKSUM false, OFFSET 14, VERBOSE true")
+
+
+ICMP_REASONS = ["not ICMP", "bad packet length", "bad ICMP checksum"]
+
+
+@pytest.mark.parametrize("noutputs", [1, 2])
+def test_check_icmp_element(ctx, noutputs):
+    rng = np.random.default_rng(200 + noutputs)
+    arena, foff, flen = frames(rng, 2500, 1, max_total=600)
+    e, port, ln = run_element(ctx, "CheckICMPHeader", "DETAILS true", arena, foff, flen, 14, noutputs, batch=900)
+    codes, _ = oracle_lib.batch("check_icmp", arena.copy(), len(foff), off=foff + 14, length=flen - 14)
+    assert np.array_equal(port, np.where(codes == 0, 0, 1 if noutputs == 2 else -1))
+    det = e.read_handler("drop_details").splitlines()
+    assert det == ["%d\t%s" % (int((codes == k + 1).sum()), ICMP_REASONS[k]) for k in range(3)]
+    assert e.messages() == expected_drop_messages("e0 :: CheckICMPHeader: ICMP header check failed: ", codes,
+                                                  ICMP_REASONS, False)
+    assert (codes == 0).any() and (codes == 3).any()
+
+
+@pytest.mark.parametrize("config,noutputs", [("", 2), ("", 1), ("MULTICAST false", 2), ("ACTIVE false", 2)])
+def test_dec_ip_ttl_element(ctx, config, noutputs):
+    """DecIPTTL (decipttl.cc:45-77): TTL and ip_sum rewritten in the host
+    packets exactly as the oracle does; expired packets to output 1 (or
+    killed); ACTIVE false passes everything untouched."""
+    rng = np.random.default_rng(300 + noutputs + len(config))
+    arena, foff, flen = frames(rng, 2000, 17, max_total=300)
+    fuzz.vary_ttl(rng, arena, foff + 14, flen - 14, frac=0.5)
+    ref = arena.copy()
+    e, port, ln = run_element(ctx, "DecIPTTL", config, arena, foff, flen, 14, noutputs, batch=700)
+    if "ACTIVE false" in config:
+        assert np.array_equal(arena, ref) and (port == 0).all()
+        assert e.read_handler("active") == "false"
+        return
+    mc = 0 if "MULTICAST false" in config else 1
+    codes, _ = oracle_lib.batch("dec_ttl", ref, len(foff), off=foff + 14, length=flen - 14, arg=mc)
+    assert np.array_equal(arena, ref)
+    assert np.array_equal(port, np.where(codes == 1, 1 if noutputs == 2 else -1, 0))
+    assert e.read_handler("drops") == str(int((codes == 1).sum()))
+    assert (codes == 0).any() and (codes == 1).any() and (codes == 2).any()
+
+
+def test_ip_input_combo_element(ctx):
+    """IPInputCombo (ipinputcombo.cc:66-140) = Paint + Strip(14) +
+    CheckIPHeader: bad packets are killed, the first chatters once; good
+    ones leave with their length after the strip and the ip_len trim."""
+    rng = np.random.default_rng(400)
+    arena, foff, flen = frames(rng, 2500, 17)
+    e, port, ln = run_element(ctx, "IPInputCombo", "3, INTERFACES 10.0.0.1/8", arena, foff, flen, -1, 1, batch=800)
+    L = oracle_lib.load_oracle()
+    bad = np.array([0xFFFFFFFF, 0, 0x0AFFFFFF], np.uint32)    # INTERFACES 10.0.0.1/8 (checkipheader.cc:51-74)
+    bad_be = bad.byteswap()
+    good = np.array([0x0A000001], np.uint32).byteswap()
+    codes = np.array([L.oracle_check_ip_header(arena.ctypes.data + int(foff[i]), int(flen[i]), 14, 1,
+                                               bad_be.ctypes.data, 3, good.ctypes.data, 1)
+                      for i in range(len(foff))])
+    assert np.array_equal(port, np.where(codes == 0, 0, -1))
+    for i in np.nonzero(codes == 0)[0]:
+        o = int(foff[i])
+        ip_len = (int(arena[o + 16]) << 8) | int(arena[o + 17])
+        assert ln[i] == min(int(flen[i]) - 14, ip_len)
+    assert e.read_handler("drops") == str(int((codes != 0).sum()))
+    assert e.read_handler("color") == "3"
+    assert e.messages() == (["IP checksum failed"] if (codes != 0).any() else [])
+
+
+def test_new_element_configure_errors(ctx):
+    from click_amd import ClickAmdError
+    from click_amd.elements import Element
+    for cls, conf in [("IPInputCombo", ""), ("IPInputCombo", "x"), ("DecIPTTL", "ACTIVE maybe"),
+                      ("DecIPTTL", "3"), ("CheckICMPHeader", "VERBOSE 2")]:
+        with pytest.raises(ClickAmdError):
+            Element(ctx, cls, conf)
+    Element(ctx, "IPInputCombo", "COLOR 1, 18.26.4.255 18.26.7.255")
+    Element(ctx, "DecIPTTL", "MULTICAST false, ACTIVE true")
