@@ -47,7 +47,7 @@ WORKLOADS = {
                elements=("CheckUDPHeader", "SetUDPChecksum"),
                desc="C3: 1500 B UDP/IPv4 full-payload checksum, 16M-packet batch per GPU, 1536 B slots"),
     "c2": dict(proto=17, L=46, stride=64, n=16 << 20, ck=20,
-               elements=("CheckIPHeader", "SetIPChecksum"),
+               elements=("CheckIPHeader", "SetIPChecksum", "DecIPTTL"),
                desc="C2: 64 B min-size packets (IP length 46, 64 B slots), IP-header checksum, 16M-packet batch per GPU"),
     "c5": dict(proto=6, L=9000, stride=9024, n=16 << 20, ck=9000,
                elements=("CheckTCPHeader", "SetTCPChecksum"),
@@ -57,7 +57,10 @@ WORKLOADS = {
                desc="C4: IMIX 64/576/1500 (7:4:1) UDP/IPv4 checksum, 64M packets, 64 B-aligned packing"),
 }
 ALG = {"CheckUDPHeader": lambda L: L + 1, "CheckTCPHeader": lambda L: L + 1, "CheckIPHeader": lambda L: 20 + 1,
-       "SetUDPChecksum": lambda L: L + 3, "SetTCPChecksum": lambda L: L + 3, "SetIPChecksum": lambda L: 20 + 3}
+       "SetUDPChecksum": lambda L: L + 3, "SetTCPChecksum": lambda L: L + 3, "SetIPChecksum": lambda L: 20 + 3,
+       "DecIPTTL": lambda L: 3 + 3 + 1}   # ip_ttl + ip_sum read and written, status (MULTICAST true)
+# C2 slot traffic per packet beyond the 64 B slot read: status + written field bytes
+SLOT_EXTRA = {"CheckIPHeader": 1, "SetIPChecksum": 3, "DecIPTTL": 4}
 
 
 def log(*a):
@@ -96,6 +99,8 @@ def run_element(ctx, name, b, status):
         ctx.check_tcp_header(b, out=status)
     elif name == "CheckIPHeader":
         ctx.check_ip_header(b, out=status)
+    elif name == "DecIPTTL":
+        ctx.dec_ip_ttl(b, status=status, want_sums=False)
     else:
         raise ValueError(name)
 
@@ -129,6 +134,10 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
     stream = torch.cuda.current_stream()
     out = {}
     for e in w["elements"]:
+        if e == "DecIPTTL":
+            # untimed: TTL 255 so that every timed pass decrements (<= 254 passes)
+            arena.view(n, w["stride"])[:, 8] = 255
+            ctx.set_ip_checksum(b, status=status, want_sums=False)
         for _ in range(warmup):
             run_element(ctx, e, b, status)
         torch.cuda.synchronize()
@@ -424,7 +433,7 @@ def main():
                               "elements": {e: summarize(r, args.steps, "c2") for e, r in c2.items()}}
             for e, r in c2.items():
                 line["c2_64b"]["elements"][e]["slot_GBs"] = round(
-                    (64 + ALG[e](46) - 20) * r["n"] / (r["kernel_ms"] * 1e-3) / 1e9, 1)
+                    (64 + SLOT_EXTRA[e]) * r["n"] / (r["kernel_ms"] * 1e-3) / 1e9, 1)
         if world == 1 and not args.no_cpu and args.workload != "c4":
             try:
                 line["cpu_baseline"] = cpu_baseline(args.workload, head["element"], args.cpu_seconds)

@@ -22,13 +22,16 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # element -> kernels one call launches (two-phase Set = compute + scatter)
+# (fixed-geometry l4_kernel or the variable-length l4_varlen_kernel)
 ELEMENT_KERNELS = {
-    "CheckUDPHeader": ["l4_kernel<17, false"],
-    "SetUDPChecksum": ["l4_kernel<17, true", "field_scatter_kernel<6, true"],
-    "CheckTCPHeader": ["l4_kernel<6, false"],
-    "SetTCPChecksum": ["l4_kernel<6, true", "field_scatter_kernel<16, true"],
+    "CheckUDPHeader": ["l4_kernel<17, false", "l4_varlen_kernel<17, false"],
+    "SetUDPChecksum": ["l4_kernel<17, true", "l4_varlen_kernel<17, true", "field_scatter_kernel<6, true"],
+    "CheckTCPHeader": ["l4_kernel<6, false", "l4_varlen_kernel<6, false"],
+    "SetTCPChecksum": ["l4_kernel<6, true", "l4_varlen_kernel<6, true", "field_scatter_kernel<16, true"],
+    "CheckICMPHeader": ["l4_kernel<1, false", "l4_varlen_kernel<1, false"],
     "CheckIPHeader": ["ip_header_kernel<0"],
     "SetIPChecksum": ["ip_header_kernel<2", "field_scatter_kernel<10"],
+    "DecIPTTL": ["dec_ttl_kernel"],
 }
 
 
