@@ -90,10 +90,10 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
             const uint64_t a = (uint64_t)ip;
             const uint32_t sh = (uint32_t)(a & 3);
             const uint8_t *q = (const uint8_t *)(a & ~3ull);
-            const u32x4 d0 = *(const u32x4_a4 *)q;
+            const u32x4 d0 = gload16_a4((uint64_t)q);
             uint32_t d4, d5;
-            d4 = *(const uint32_t *)(q + 16);
-            d5 = sh ? *(const uint32_t *)(q + 20) : 0u;
+            d4 = gload4((uint64_t)(q + 16));
+            d5 = sh ? gload4((uint64_t)(q + 20)) : 0u;
             uint32_t h[5];
             h[0] = __builtin_amdgcn_alignbyte(d0[1], d0[0], sh);
             h[1] = __builtin_amdgcn_alignbyte(d0[2], d0[1], sh);
@@ -174,7 +174,7 @@ __device__ __forceinline__ void load_pass(const uint8_t *c0, uint32_t nch, uint3
 #if CLK_NT_LOADS
         v[k] = idx < nch ? __builtin_nontemporal_load((const u32x4 *)(c0 + 16ull * idx)) : u32x4{0, 0, 0, 0};
 #else
-        v[k] = idx < nch ? *(const u32x4 *)(c0 + 16ull * idx) : u32x4{0, 0, 0, 0};
+        v[k] = idx < nch ? gload16((uint64_t)(c0 + 16ull * idx)) : u32x4{0, 0, 0, 0};
 #endif
     }
 }
@@ -265,7 +265,7 @@ __device__ __forceinline__ void l4_parse(uint8_t *nh, uint32_t caplen, int fixof
     uint32_t d[HDR_DW];
 #pragma unroll
     for (int k = 0; k < HDR_DW; k++)
-        d[k] = (uint64_t)(q + 4 * k) < end ? *(const uint32_t *)(q + 4 * k) : 0u;
+        d[k] = (uint64_t)(q + 4 * k) < end ? gload4((uint64_t)(q + 4 * k)) : 0u;
     uint32_t h[HDR_DW - 1];                 // h[k] = bytes [4k, 4k+4) of the header, LE
 #pragma unroll
     for (int k = 0; k < HDR_DW - 1; k++)
@@ -577,7 +577,7 @@ __global__ void __launch_bounds__(256) l4_varlen_kernel(BatchArgs b, int fixoff,
                     jk[u * KV + k] = j;
                     Pk[u * KV + k] = P;
                     const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
-                    v[u * KV + k] = c < total ? *(const u32x4 *)(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
+                    v[u * KV + k] = c < total ? gload16(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
                 }
             }
 #pragma unroll
