@@ -20,8 +20,8 @@ struct clk_ctx {
     int set_mode;      // -1 auto; 0: Set kernels store the field; 1: two-phase (CLK_SET_MODE)
     uint64_t bin_min;  // variable-length batches of >= bin_min packets run by size class (CLK_BIN_MIN)
     int bin_grid;      // grid cap of a size-class pass (CLK_BIN_GRID)
-    int varlen;        // 1: variable-length batches use the wave-cooperative kernel,
-                       // 0: the size-class partition (CLK_VARLEN)
+    int varlen;        // variable-length batches: 2 the packet-stream kernel, 1 the
+                       // wave-cooperative range kernel, 0 the size-class partition (CLK_VARLEN)
     void *scratch;     // two-phase work array (grown on demand)
     size_t scratch_bytes;
     char err[512];
@@ -121,6 +121,9 @@ constexpr int K = CLK_K;   // 16-byte chunk loads in flight per lane per pass
 #endif
 #ifndef CLK_VU
 #define CLK_VU 1           // sub-passes whose loads are issued together
+#endif
+#ifndef CLK_SKV
+#define CLK_SKV 2          // chunks per lane per pass of the packet-stream kernel
 #endif
 
 // Lanes per packet: the fewest (of 1, 4, 16, 64) whose K-deep pass covers
@@ -264,7 +267,18 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
         if (two)
             work = (uint32_t *)ctx->scratch;
     }
-    if (bins && ctx->varlen) {
+    if (bins && ctx->varlen == 2) {
+        constexpr int KV = CLK_SKV;
+        uint64_t blocks = (b->n + 255) / 256;            // 4 waves x 64 packets per block
+        if (blocks > (uint64_t)ctx->max_blocks)
+            blocks = (uint64_t)ctx->max_blocks;
+        if (work)
+            hipLaunchKernelGGL((clk::l4_stream_kernel<PROTO, SET, true, KV>), dim3((unsigned)blocks), dim3(BLOCK), 0,
+                               ctx->cur, args_of(b), fixoff, code, sum, work);
+        else
+            hipLaunchKernelGGL((clk::l4_stream_kernel<PROTO, SET, false, KV>), dim3((unsigned)blocks), dim3(BLOCK),
+                               0, ctx->cur, args_of(b), fixoff, code, sum, work);
+    } else if (bins && ctx->varlen) {
         constexpr int KV = CLK_KV, VU = CLK_VU;
         uint64_t blocks = (b->n + 255) / 256;            // 4 waves x 64 packets per block
         if (blocks > (uint64_t)ctx->max_blocks)
@@ -355,9 +369,11 @@ int clk_ctx_create(int device, clk_ctx **out)
         if (v > 0)
             c->bin_grid = v;
     }
-    c->varlen = 1;
-    if (const char *vl = std::getenv("CLK_VARLEN"))
-        c->varlen = std::atoi(vl) ? 1 : 0;
+    c->varlen = 2;
+    if (const char *vl = std::getenv("CLK_VARLEN")) {
+        const int v = std::atoi(vl);
+        c->varlen = v >= 0 && v <= 2 ? v : 2;
+    }
     c->force_group = 0;
     if (const char *fg = std::getenv("CLK_FORCE_GROUP")) {
         int v = std::atoi(fg);

@@ -253,19 +253,20 @@ struct L4State {
     bool fix, summing;
 };
 
+template <int PROTO>
+struct L4Hdr {
+    static constexpr int DW = PROTO == TCP ? 11 : 8;   // aligned dwords covering bytes [0, 40) / [0, 28)
+};
+
+// Parse from the header dwords d[k] = the aligned dword at (nh & ~3) + 4k
+// (0 at and beyond nh + caplen).
 template <int PROTO, bool SET>
-__device__ __forceinline__ void l4_parse(uint8_t *nh, uint32_t caplen, int fixoff, L4State &st)
+__device__ __forceinline__ void l4_parse_words(uint8_t *nh, uint32_t caplen, int fixoff,
+                                               const uint32_t (&d)[L4Hdr<PROTO>::DW], L4State &st)
 {
-    constexpr int HDR_DW = PROTO == TCP ? 11 : 8;   // aligned dwords covering bytes [0, 40) / [0, 28)
+    constexpr int HDR_DW = L4Hdr<PROTO>::DW;
     constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
-    const uint64_t a = (uint64_t)nh;
-    const uint32_t sh = (uint32_t)(a & 3);
-    const uint8_t *q = (const uint8_t *)(a & ~3ull);
-    const uint64_t end = a + caplen;
-    uint32_t d[HDR_DW];
-#pragma unroll
-    for (int k = 0; k < HDR_DW; k++)
-        d[k] = (uint64_t)(q + 4 * k) < end ? gload4((uint64_t)(q + 4 * k)) : 0u;
+    const uint32_t sh = (uint32_t)((uint64_t)nh & 3);
     uint32_t h[HDR_DW - 1];                 // h[k] = bytes [4k, 4k+4) of the header, LE
 #pragma unroll
     for (int k = 0; k < HDR_DW - 1; k++)
@@ -390,6 +391,20 @@ __device__ __forceinline__ void l4_parse(uint8_t *nh, uint32_t caplen, int fixof
         st.fb0 = (int)FIELD < st.rlen ? tbyte(FIELD) : 0;
         st.fb1 = (int)FIELD + 1 < st.rlen ? tbyte(FIELD + 1) : 0;
     }
+}
+
+template <int PROTO, bool SET>
+__device__ __forceinline__ void l4_parse(uint8_t *nh, uint32_t caplen, int fixoff, L4State &st)
+{
+    constexpr int HDR_DW = L4Hdr<PROTO>::DW;
+    const uint64_t a = (uint64_t)nh;
+    const uint8_t *q = (const uint8_t *)(a & ~3ull);
+    const uint64_t end = a + caplen;
+    uint32_t d[HDR_DW];
+#pragma unroll
+    for (int k = 0; k < HDR_DW; k++)
+        d[k] = (uint64_t)(q + 4 * k) < end ? gload4((uint64_t)(q + 4 * k)) : 0u;
+    l4_parse_words<PROTO, SET>(nh, caplen, fixoff, d, st);
 }
 
 // Finish one packet from its range sum.  `writer` lanes store.
@@ -622,6 +637,193 @@ __global__ void __launch_bounds__(256) l4_varlen_kernel(BatchArgs b, int fixoff,
         const uint32_t sum = acc[wv][lane];
         if (live)
             l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work);
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Sum of a byte range read straight from global memory by one lane (the
+// stream kernel's fallback for ranges its stash cannot correct).
+__device__ __noinline__ uint32_t lane_range_sum(uint64_t s, int len)
+{
+    if (len <= 0)
+        return 0;
+    RangeAcc acc{0, 0};
+    const bool odd = (s & 1) != 0;
+    const uint64_t c = s & ~15ull;
+    const uint32_t nch = (uint32_t)((((s + (uint64_t)len + 15) & ~15ull) - c) >> 4);
+    for (uint32_t k = 0; k < nch; k++)
+        chunk_accumulate(gload16(c + 16ull * k), (int)(c + 16ull * k - s), len, odd, acc);
+    return word_sum(acc, odd);
+}
+
+// Word sum (relative to a range start of parity `odd`) of the bytes of one
+// 16-byte chunk at absolute address ca that lie OUTSIDE [s, s + len).
+__device__ __forceinline__ uint32_t chunk_outside(const u32x4 V, uint64_t ca, uint64_t s, int len, uint32_t sel,
+                                                  uint32_t acc)
+{
+    const int rel = (int)(int64_t)(ca - s);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t in = lowmask(len - rel - 4 * q) & ~lowmask(-rel - 4 * q);
+        const uint32_t dm = V[q] & ~in;
+        acc = dot_words(__builtin_amdgcn_perm(dm, dm, sel), acc);
+    }
+    return acc;
+}
+
+// Variable lengths, packet-stream form (default for IMIX).  A wave takes 64
+// consecutive packets and streams, unmasked, the 16-byte chunks covering
+// each packet's captured bytes [nh, nh + caplen) -- known from the batch
+// descriptors alone, so the header is not fetched ahead of the stream:
+//   Phase A: lane per packet: chunk span from off/len, wave scan into LDS.
+//   Phase B: lane l owns KV consecutive chunks of the wave's concatenated
+//            chunk list per pass (binary search for its first packet, step
+//            at boundaries); whole-chunk word sums (v_dot2; byte-swapped
+//            when the wave holds an odd-address packet) go to the packet's
+//            LDS accumulator at packet changes.  The lane holding a
+//            packet's chunk 0..HC-1 or its last chunk stashes it in LDS.
+//   Phase C: lane per packet: parse the header from the stash (l4_parse_words),
+//            subtract the stashed chunks' bytes outside the summed range
+//            [nh+hl, nh+hl+rlen), finish.  A range whose unstashed middle
+//            chunks are not all inside it (options past the stash, trailing
+//            bytes) is re-summed from global memory by its lane.
+// The sum mod 2^32 is order-free (cksum_device.hh), so whole-chunk sums
+// minus the excluded bytes equal the reference's word sum exactly.
+template <int PROTO, bool SET, bool DEFER, int KV>
+__global__ void __launch_bounds__(256) l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
+                                                        uint16_t *out_sum, uint32_t *work)
+{
+    constexpr int HDR_DW = L4Hdr<PROTO>::DW;
+    constexpr int HC = PROTO == TCP ? 4 : 3;        // stashed head chunks: (nh&~3) - c0 + 4*HDR_DW <= 16*HC
+    __shared__ u32x4 head[4][64][HC];
+    __shared__ u32x4 tail[4][64];
+    __shared__ u32x4 pk[4][64];       // {c0 lo, c0 hi, chunk start, nch | odd << 31}
+    __shared__ uint32_t cst[4][68];   // chunk starts; cst[64] = total
+    __shared__ uint32_t acc[4][64];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t nruns = (b.n + 63) / 64;
+    const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t run = (uint64_t)blockIdx.x * (blockDim.x / 64) + wv; run < nruns; run += wstride) {
+        const uint64_t i = run * 64 + lane;
+        const bool live = i < b.n;
+        uint8_t *nh = b.base;
+        uint32_t caplen = 0;
+        if (live) {
+            nh = b.base + pkt_off(b, i);
+            caplen = pkt_len(b, i);
+        }
+        const uint64_t a = (uint64_t)nh;
+        const uint64_t c0 = a & ~15ull;
+        const uint32_t nch = caplen ? (uint32_t)((((a + caplen + 15) & ~15ull) - c0) >> 4) : 0u;
+        uint32_t incl = nch;                                   // wave-inclusive scan
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = __shfl_up(incl, d, 64);
+            if ((int)lane >= d)
+                incl += t;
+        }
+        const uint32_t total = __shfl(incl, 63, 64);
+        const bool anyodd = __ballot(live && (a & 1)) != 0;  // wave-uniform
+        pk[wv][lane] = u32x4{(uint32_t)c0, (uint32_t)(c0 >> 32), incl - nch, nch | ((uint32_t)(a & 1) << 31)};
+        cst[wv][lane] = incl - nch;
+        if (lane == 63)
+            cst[wv][64] = total;
+        acc[wv][lane] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
+            const uint32_t cl = cb + lane * KV;
+            uint32_t j = 0;                                    // last packet whose chunk start <= cl
+#pragma unroll
+            for (int step = 32; step >= 1; step >>= 1)
+                if (cst[wv][j + step] <= cl)
+                    j += step;
+            uint32_t nxt = cst[wv][j + 1];
+            u32x4 P = pk[wv][j];
+            u32x4 v[KV];
+            uint32_t jk[KV];
+            u32x4 Pk[KV];
+#pragma unroll
+            for (int k = 0; k < KV; k++) {
+                const uint32_t c = cl + k;
+                if (c < total && c >= nxt) {
+                    do {
+                        j++;
+                        nxt = cst[wv][j + 1];
+                    } while (c >= nxt);
+                    P = pk[wv][j];
+                }
+                jk[k] = j;
+                Pk[k] = P;
+                const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
+                v[k] = c < total ? gload16(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
+            }
+            uint32_t cur = jk[0], part = 0;
+#pragma unroll
+            for (int k = 0; k < KV; k++) {
+                const uint32_t c = cl + k;
+                if (c >= total)
+                    break;
+                if (jk[k] != cur) {
+                    atomicAdd(&acc[wv][cur], part);
+                    part = 0;
+                    cur = jk[k];
+                }
+                const u32x4 V = v[k];
+                const uint32_t r = c - Pk[k][2];               // chunk index within the packet
+                if (r < (uint32_t)HC)
+                    head[wv][jk[k]][r] = V;
+                if (r == (Pk[k][3] & 0x7FFFFFFFu) - 1)
+                    tail[wv][jk[k]] = V;
+                if (anyodd) {
+                    const uint32_t sel = (Pk[k][3] >> 31) ? 0x02030001u : 0x03020100u;
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        part = dot_words(__builtin_amdgcn_perm(V[q], V[q], sel), part);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+                        part = dot_words(V[q], part);
+                }
+            }
+            if (cl < total)
+                atomicAdd(&acc[wv][cur], part);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (live) {
+            const uint32_t *hw = (const uint32_t *)&head[wv][lane][0];
+            const uint32_t q0 = (uint32_t)((a & ~3ull) - c0) >> 2;   // first header dword in the stash
+            const uint64_t end = a + caplen;
+            uint32_t d[HDR_DW];
+#pragma unroll
+            for (int k = 0; k < HDR_DW; k++)
+                d[k] = (a & ~3ull) + 4 * k < end ? hw[q0 + k] : 0u;
+            L4State st;
+            l4_parse_words<PROTO, SET>(nh, caplen, fixoff, d, st);
+            uint32_t sum = 0;
+            const int rlen = st.summing ? st.rlen : 0;
+            if (rlen > 0) {
+                const uint64_t s = a + st.hl, e = s + (uint64_t)rlen;
+                const uint32_t sel = (a & 1) ? 0x02030001u : 0x03020100u;
+                const bool stashed = nch <= (uint32_t)HC + 1 ||
+                                     (s <= c0 + 16 * HC && e >= c0 + 16ull * (nch - 1));
+                if (stashed) {
+                    uint32_t out = 0;
+                    const uint32_t nh_ = nch < (uint32_t)HC ? nch : (uint32_t)HC;
+                    for (uint32_t k = 0; k < nh_; k++)
+                        out = chunk_outside(head[wv][lane][k], c0 + 16ull * k, s, rlen, sel, out);
+                    if (nch > (uint32_t)HC)
+                        out = chunk_outside(tail[wv][lane], c0 + 16ull * (nch - 1), s, rlen, sel, out);
+                    sum = acc[wv][lane] - out;
+                } else {
+                    sum = lane_range_sum(s, rlen);
+                }
+            }
+            l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work);
+        }
         __builtin_amdgcn_wave_barrier();
     }
 }

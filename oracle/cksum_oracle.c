@@ -44,6 +44,7 @@
 #define CLK_SET_KILL 2
 #define CLK_TTL_EXPIRED 1
 #define CLK_TTL_UNCHANGED 2
+#define CLK_GWOPT_ERROR 1
 
 static inline uint16_t ld16(const uint8_t *p) { uint16_t v; memcpy(&v, p, 2); return v; }
 static inline uint32_t ld32(const uint8_t *p) { uint32_t v; memcpy(&v, p, 4); return v; }
@@ -345,6 +346,184 @@ int oracle_dec_ip_ttl(uint8_t *nh, uint32_t caplen, int multicast)
     return CLK_OK;
 }
 
+/* ---- IP output path: IPGWOptions, FixIPSrc, IPOutputCombo ----------------
+ * The option walk shared by IPGWOptions::handle_options
+ * (elements/ip/ipgwoptions.cc:53-160) and IPOutputCombo::push's IPGWOptions
+ * step (elements/ip/ipoutputcombo.cc:59-166).  my_ip = the address RR and
+ * TS flg 1 record (IPGWOptions: the preferred address; IPOutputCombo:
+ * IPADDR); my_addrs = the addresses TS flg 3 matches; ts = the 4 bytes the
+ * reference stores for Timestamp::now() (htonl of ms since midnight), given
+ * by the caller because a parity test cannot share the clock.  `caplen` =
+ * bytes from the IP header to end_data(): an option byte the reference would
+ * read at or past caplen reads as 0 (domain guard; the reference reads
+ * packet tailroom there).  Returns 0 (options done), 1 (error: *problem =
+ * the ICMP parameter-problem offset).  *touched: 1 if any RR/TS option was
+ * reached (IPGWOptions' uniqueify), *changed: 1 if a byte was rewritten
+ * (IPOutputCombo's do_cksum). */
+static inline uint32_t optb(const uint8_t *o, uint32_t i, uint32_t caplen) { return i < caplen ? o[i] : 0; }
+
+int oracle_ip_gw_options(uint8_t *ip, uint32_t caplen, uint32_t my_ip, const uint32_t *my_addrs,
+                         int n_my_addrs, uint32_t ts, int *problem, int *touched, int *changed)
+{
+    int hlen = (ip[0] & 0xF) << 2;                          /* caller: hlen <= caplen */
+    *touched = 0;
+    *changed = 0;
+    int oi;
+    for (oi = 20; oi < hlen;) {
+        unsigned type = ip[oi];
+        if (type == 1) {                                    /* IPOPT_NOP */
+            oi++;
+            continue;
+        } else if (type == 0)                               /* IPOPT_EOL */
+            break;
+        int xlen = (int)optb(ip, (uint32_t)oi + 1, caplen);
+        if (xlen < 2 || oi + xlen > hlen) {                 /* bad length */
+            *problem = oi + 1;
+            return 1;
+        } else if (type != 7 && type != 68) {               /* not IPOPT_RR / IPOPT_TS */
+            oi += xlen;
+            continue;
+        }
+        *touched = 1;
+        if (type == 7) {                                    /* Record Route */
+            int p = (int)optb(ip, (uint32_t)oi + 2, caplen) - 1;
+            if (p >= 3 && p + 4 <= xlen) {
+                memcpy(ip + oi + p, &my_ip, 4);
+                ip[oi + 2] += 4;
+                *changed = 1;
+            } else if (p != xlen) {
+                *problem = oi + 2;
+                return 1;
+            }
+        } else {                                            /* Timestamp */
+            int p = (int)optb(ip, (uint32_t)oi + 2, caplen) - 1;
+            int oflw = (int)optb(ip, (uint32_t)oi + 3, caplen) >> 4;
+            int flg = (int)optb(ip, (uint32_t)oi + 3, caplen) & 0xF;
+            int overflowed = 0;
+            if (p < 4) {
+                *problem = oi + 2;
+                return 1;
+            } else if (flg == 0) {
+                if (p + 4 <= xlen) {
+                    memcpy(ip + oi + p, &ts, 4);
+                    ip[oi + 2] += 4;
+                    *changed = 1;
+                } else
+                    overflowed = 1;
+            } else if (flg == 1) {
+                if (p + 8 <= xlen) {
+                    memcpy(ip + oi + p, &my_ip, 4);
+                    memcpy(ip + oi + p + 4, &ts, 4);
+                    ip[oi + 2] += 8;
+                    *changed = 1;
+                } else
+                    overflowed = 1;
+            } else if (flg == 3 && p + 8 <= xlen) {
+                uint32_t addr = ld32(ip + oi + p);
+                int mine = 0;
+                for (int k = 0; k < n_my_addrs; k++)
+                    if (my_addrs[k] == addr)
+                        mine = 1;
+                if (mine) {
+                    memcpy(ip + oi + p + 4, &ts, 4);
+                    ip[oi + 2] += 8;
+                    *changed = 1;
+                }
+            } else {
+                *problem = oi + 3;
+                return 1;
+            }
+            if (overflowed) {
+                if (oflw < 15) {
+                    ip[oi + 3] = (uint8_t)(((oflw + 1) << 4) | flg);
+                    *changed = 1;
+                } else {
+                    *problem = oi + 3;
+                    return 1;
+                }
+            }
+        }
+        oi += xlen;
+    }
+    return 0;
+}
+
+/* elements/ip/ipgwoptions.cc:164-172 + 53-160.  Returns CLK_OK (output 0;
+ * ip_sum recomputed when an RR/TS option was reached, 155-159) or
+ * CLK_GWOPT_ERROR (output 1, *problem = ICMP_PARAMPROB_ANNO).  Domain guard:
+ * caplen < 20 -> CLK_OK untouched (the reference asserts an IP header). */
+int oracle_ip_gw_options_element(uint8_t *ip, uint32_t caplen, uint32_t my_ip, const uint32_t *my_addrs,
+                                 int n_my_addrs, uint32_t ts, int *problem)
+{
+    int touched, changed;
+    *problem = 0;
+    if (caplen < 20 || ((ip[0] & 0xF) << 2) <= 20)          /* 168 */
+        return CLK_OK;
+    if ((uint32_t)((ip[0] & 0xF) << 2) > caplen)            /* domain guard: options past the packet */
+        return CLK_OK;
+    if (oracle_ip_gw_options(ip, caplen, my_ip, my_addrs, n_my_addrs, ts, problem, &touched, &changed))
+        return CLK_GWOPT_ERROR;                             /* 162-165 */
+    if (touched) {                                          /* 155-159 */
+        int hlen = (ip[0] & 0xF) << 2;
+        st16(ip + 10, 0);
+        st16(ip + 10, oracle_in_cksum(ip, hlen));
+    }
+    return CLK_OK;
+}
+
+/* elements/ip/fixipsrc.cc:52-72: with FIX_IP_SRC_ANNO set, ip_src = IPADDR
+ * and the header checksum is recomputed (hlen from ip_hl, no length check;
+ * domain guard: caplen < 20 or hlen > caplen -> unchanged, CLK_OK). */
+int oracle_fix_ip_src(uint8_t *ip, uint32_t caplen, int anno, uint32_t my_ip)
+{
+    if (!anno || caplen < 20)
+        return CLK_OK;
+    int hlen = (ip[0] & 0xF) << 2;
+    if ((uint32_t)hlen > caplen)
+        return CLK_OK;
+    memcpy(ip + 12, &my_ip, 4);
+    st16(ip + 10, 0);
+    st16(ip + 10, oracle_in_cksum(ip, hlen));
+    return CLK_OK;
+}
+
+/* elements/ip/ipoutputcombo.cc:44-205 after DropBroadcasts and PaintTee
+ * (annotation-only steps the host takes): IPGWOptions (59-166, TS flg 3
+ * matches IPADDR only), FixIPSrc (168-173), the header re-checksum when
+ * either changed a byte (176-179, summed from data() = the IP header),
+ * DecIPTTL (181-191), the MTU test (194-197; `length` = p->length()).
+ * flags bit 0 = FIX_IP_SRC_ANNO.  Returns the output port: 0, 2 (*problem
+ * set), 3 (TTL expired) or 4 (length > MTU).  Domain guard: caplen < 20 ->
+ * port 0 untouched. */
+int oracle_ip_output_combo(uint8_t *ip, uint32_t caplen, uint32_t length, int flags, uint32_t my_ip,
+                           uint32_t mtu, uint32_t ts, int *problem)
+{
+    int touched = 0, changed = 0;
+    *problem = 0;
+    if (caplen < 20)
+        return 0;
+    int hlen = (ip[0] & 0xF) << 2;
+    if (hlen > 20 && (uint32_t)hlen <= caplen &&           /* domain guard: options past the packet */
+        oracle_ip_gw_options(ip, caplen, my_ip, &my_ip, 1, ts, problem, &touched, &changed))
+        return 2;                                           /* 202-204 */
+    if (flags & 1) {                                        /* 169-173 */
+        memcpy(ip + 12, &my_ip, 4);
+        changed = 1;
+    }
+    if (changed && (uint32_t)hlen <= caplen) {              /* 176-179 */
+        st16(ip + 10, 0);
+        st16(ip + 10, oracle_in_cksum(ip, hlen));
+    }
+    if (ip[8] <= 1)                                         /* 182-184 */
+        return 3;
+    ip[8]--;                                                /* 186 */
+    uint32_t sum = (~(uint32_t)bswap16(ld16(ip + 10)) & 0xFFFF) + 0xFEFF;   /* 189 */
+    st16(ip + 10, (uint16_t)~bswap16((sum + (sum >> 16)) & 0xFFFF));       /* 190 */
+    if (length > mtu)                                       /* 194-197 */
+        return 4;
+    return 0;
+}
+
 /* ---- batch drivers ------------------------------------------------------- */
 
 static inline uint64_t pkt_off(const uint64_t *off, uint64_t stride, uint64_t i)
@@ -400,6 +579,33 @@ int oracle_batch(int op, uint8_t *base, const uint64_t *off, uint64_t stride,
             out8[i] = (uint8_t)r;
         if (out16)
             out16[i] = s;
+    }
+    return 0;
+}
+
+int oracle_ip_out_batch(int op, uint8_t *base, const uint64_t *off, uint64_t stride,
+                        const uint32_t *len, uint32_t fixed_len, uint64_t n,
+                        const uint8_t *flags, uint32_t my_ip, const uint32_t *my_addrs, int n_my_addrs,
+                        uint32_t ts, uint32_t mtu, uint8_t *out8, uint8_t *out_prob, uint16_t *out16)
+{
+    for (uint64_t i = 0; i < n; i++) {
+        uint8_t *p = base + pkt_off(off, stride, i);
+        uint32_t l = pkt_len(len, fixed_len, i);
+        int f = flags ? flags[i] : 0, prob = 0, r;
+        if (op == 0)
+            r = oracle_ip_gw_options_element(p, l, my_ip, my_addrs, n_my_addrs, ts, &prob);
+        else if (op == 1)
+            r = oracle_fix_ip_src(p, l, f & 1, my_ip);
+        else if (op == 2)
+            r = oracle_ip_output_combo(p, l, l, f, my_ip, mtu, ts, &prob);
+        else
+            return -1;
+        if (out8)
+            out8[i] = (uint8_t)r;
+        if (out_prob)
+            out_prob[i] = (uint8_t)prob;
+        if (out16)
+            out16[i] = l >= 20 ? ld16(p + 10) : 0;
     }
     return 0;
 }

@@ -46,6 +46,24 @@ int oracle_set_tcp_checksum(uint8_t *nh, uint32_t caplen, int fixoff);
 int oracle_check_icmp_header(const uint8_t *nh, uint32_t caplen);
 int oracle_dec_ip_ttl(uint8_t *nh, uint32_t caplen, int multicast);
 
+/* ---- IP output path (ipgwoptions.cc, fixipsrc.cc, ipoutputcombo.cc) ------
+ * ts = the 4 bytes stored for Timestamp::now() (htonl(ms since midnight)). */
+int oracle_ip_gw_options(uint8_t *ip, uint32_t caplen, uint32_t my_ip, const uint32_t *my_addrs,
+                         int n_my_addrs, uint32_t ts, int *problem, int *touched, int *changed);
+int oracle_ip_gw_options_element(uint8_t *ip, uint32_t caplen, uint32_t my_ip, const uint32_t *my_addrs,
+                                 int n_my_addrs, uint32_t ts, int *problem);
+int oracle_fix_ip_src(uint8_t *ip, uint32_t caplen, int anno, uint32_t my_ip);
+int oracle_ip_output_combo(uint8_t *ip, uint32_t caplen, uint32_t length, int flags, uint32_t my_ip,
+                           uint32_t mtu, uint32_t ts, int *problem);
+
+/* Batch form of the three (op: 0 IPGWOptions, 1 FixIPSrc, 2 IPOutputCombo);
+ * flags[i] bit 0 = FIX_IP_SRC_ANNO (NULL: 0); out8 = code / port, out_prob =
+ * parameter-problem offsets; out16 = the stored ip_sum. */
+int oracle_ip_out_batch(int op, uint8_t *base, const uint64_t *off, uint64_t stride,
+                        const uint32_t *len, uint32_t fixed_len, uint64_t n,
+                        const uint8_t *flags, uint32_t my_ip, const uint32_t *my_addrs, int n_my_addrs,
+                        uint32_t ts, uint32_t mtu, uint8_t *out8, uint8_t *out_prob, uint16_t *out16);
+
 /* ---- batch drivers with the C-ABI's batch semantics ----------------------
  * Packet i starts at base + (off ? off[i] : i*stride) and has
  * (len ? len[i] : fixed_len) bytes.                                          */

@@ -307,12 +307,12 @@ def test_set_modes_bit_exact(torch, mode, monkeypatch):
     c.close()
 
 
-@pytest.mark.parametrize("bin_min,varlen", [("1", "1"), ("1", "0"), ("100000000", "1")])
+@pytest.mark.parametrize("bin_min,varlen", [("1", "2"), ("1", "1"), ("1", "0"), ("100000000", "1")])
 def test_size_class_partition_bit_exact(torch, bin_min, varlen, monkeypatch):
-    """Variable-length batches run by the wave-cooperative kernel (varlen
-    1), by size class (count/scan/scatter of packet indices, one
-    lanes-per-packet geometry per class; varlen 0), or in one geometry: all
-    identical and oracle-exact."""
+    """Variable-length batches run by the packet-stream kernel (varlen 2),
+    the wave-cooperative range kernel (varlen 1), by size class
+    (count/scan/scatter of packet indices, one lanes-per-packet geometry per
+    class; varlen 0), or in one geometry: all identical and oracle-exact."""
     import click_amd
     monkeypatch.setenv("CLK_BIN_MIN", bin_min)
     monkeypatch.setenv("CLK_VARLEN", varlen)

@@ -46,6 +46,11 @@ VARIANTS = {
     "k1u8": (["-DCLK_KV=1", "-DCLK_VU=8"], {}),
     "kv8": (["-DCLK_KV=8"], {}),
     "bins": ([], {"CLK_VARLEN": "0"}),
+    "range": ([], {"CLK_VARLEN": "1"}),
+    "stream": ([], {"CLK_VARLEN": "2"}),
+    "skv1": (["-DCLK_SKV=1"], {"CLK_VARLEN": "2"}),
+    "skv4": (["-DCLK_SKV=4"], {"CLK_VARLEN": "2"}),
+    "skv8": (["-DCLK_SKV=8"], {"CLK_VARLEN": "2"}),
 }
 
 
