@@ -47,7 +47,7 @@ WORKLOADS = {
                elements=("CheckUDPHeader", "SetUDPChecksum"),
                desc="C3: 1500 B UDP/IPv4 full-payload checksum, 16M-packet batch per GPU, 1536 B slots"),
     "c2": dict(proto=17, L=46, stride=64, n=16 << 20, ck=20,
-               elements=("CheckIPHeader", "SetIPChecksum", "DecIPTTL"),
+               elements=("CheckIPHeader", "SetIPChecksum", "DecIPTTL", "IPOutputCombo"),
                desc="C2: 64 B min-size packets (IP length 46, 64 B slots), IP-header checksum, 16M-packet batch per GPU"),
     "c5": dict(proto=6, L=9000, stride=9024, n=16 << 20, ck=9000,
                elements=("CheckTCPHeader", "SetTCPChecksum"),
@@ -58,9 +58,10 @@ WORKLOADS = {
 }
 ALG = {"CheckUDPHeader": lambda L: L + 1, "CheckTCPHeader": lambda L: L + 1, "CheckIPHeader": lambda L: 20 + 1,
        "SetUDPChecksum": lambda L: L + 3, "SetTCPChecksum": lambda L: L + 3, "SetIPChecksum": lambda L: 20 + 3,
-       "DecIPTTL": lambda L: 3 + 3 + 1}   # ip_ttl + ip_sum read and written, status (MULTICAST true)
+       "DecIPTTL": lambda L: 3 + 3 + 1,   # ip_ttl + ip_sum read and written, status (MULTICAST true)
+       "IPOutputCombo": lambda L: 1 + 3 + 3 + 1}   # + ip_hl byte; no options, no FIX_IP_SRC
 # C2 slot traffic per packet beyond the 64 B slot read: status + written field bytes
-SLOT_EXTRA = {"CheckIPHeader": 1, "SetIPChecksum": 3, "DecIPTTL": 4}
+SLOT_EXTRA = {"CheckIPHeader": 1, "SetIPChecksum": 3, "DecIPTTL": 4, "IPOutputCombo": 4}
 
 
 def log(*a):
@@ -101,6 +102,8 @@ def run_element(ctx, name, b, status):
         ctx.check_ip_header(b, out=status)
     elif name == "DecIPTTL":
         ctx.dec_ip_ttl(b, status=status, want_sums=False)
+    elif name == "IPOutputCombo":          # IPOutputCombo(1, 18.26.4.24, 1500)
+        ctx.ip_output_combo(b, 0x18041A12, 1500, port=status, want_problem=False, want_sums=False)
     else:
         raise ValueError(name)
 
@@ -134,7 +137,7 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
     stream = torch.cuda.current_stream()
     out = {}
     for e in w["elements"]:
-        if e == "DecIPTTL":
+        if e in ("DecIPTTL", "IPOutputCombo"):
             # untimed: TTL 255 so that every timed pass decrements (<= 254 passes)
             arena.view(n, w["stride"])[:, 8] = 255
             ctx.set_ip_checksum(b, status=status, want_sums=False)

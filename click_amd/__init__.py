@@ -191,6 +191,44 @@ class Context:
                                             _ptr(status), _ptr(sums)))
         return status[:b.n], (sums[:b.n] if sums is not None else None)
 
+    # -- IP output path ----------------------------------------------------------
+    def _out_cfg(self, my_ip=0, ts=0, my_addrs=None, mtu=0xFFFFFFFF):
+        cfg = _abi.clk_ip_out_cfg()
+        cfg.my_ip, cfg.ts, cfg.mtu = my_ip & 0xFFFFFFFF, ts & 0xFFFFFFFF, mtu & 0xFFFFFFFF
+        cfg.my_addrs, cfg.n_my_addrs = (my_addrs.data_ptr(), my_addrs.numel()) if my_addrs is not None else (None, 0)
+        return cfg
+
+    def ip_gw_options(self, b, my_ip, ts=0, my_addrs=None, status=None, problem=None, sums=None, want_sums=True):
+        """IPGWOptions; my_ip / ts / my_addrs as raw (network-order) words."""
+        status = self._out(b.n, self._torch.uint8) if status is None else status
+        problem = self._out(b.n, self._torch.uint8) if problem is None else problem
+        if sums is None and want_sums:
+            sums = self._out(b.n, self._torch.uint16)
+        cfg, cb = self._out_cfg(my_ip, ts, my_addrs), b.c()
+        self._check(self.lib.clk_ip_gw_options(self.h, ctypes.byref(cb), ctypes.byref(cfg), _ptr(status),
+                                               _ptr(problem), _ptr(sums)))
+        return status[:b.n], problem[:b.n], (sums[:b.n] if sums is not None else None)
+
+    def fix_ip_src(self, b, my_ip, anno=None, sums=None, want_sums=True):
+        if sums is None and want_sums:
+            sums = self._out(b.n, self._torch.uint16)
+        cfg, cb = self._out_cfg(my_ip), b.c()
+        self._check(self.lib.clk_fix_ip_src(self.h, ctypes.byref(cb), ctypes.byref(cfg), _ptr(anno), _ptr(sums)))
+        return sums[:b.n] if sums is not None else None
+
+    def ip_output_combo(self, b, my_ip, mtu, ts=0, flags=None, port=None, problem=None, sums=None,
+                        want_sums=True, want_problem=True):
+        port = self._out(b.n, self._torch.uint8) if port is None else port
+        if problem is None and want_problem:
+            problem = self._out(b.n, self._torch.uint8)
+        if sums is None and want_sums:
+            sums = self._out(b.n, self._torch.uint16)
+        cfg, cb = self._out_cfg(my_ip, ts, None, mtu), b.c()
+        self._check(self.lib.clk_ip_output_combo(self.h, ctypes.byref(cb), ctypes.byref(cfg), _ptr(flags),
+                                                 _ptr(port), _ptr(problem), _ptr(sums)))
+        return port[:b.n], (problem[:b.n] if problem is not None else None), \
+            (sums[:b.n] if sums is not None else None)
+
     # -- utilities ---------------------------------------------------------------
     def count_codes(self, codes, ncounts=8, counts=None):
         if counts is None:

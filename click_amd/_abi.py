@@ -32,6 +32,8 @@ CLK_SET_KILL = 2
 CLK_TTL_OK = 0
 CLK_TTL_EXPIRED = 1
 CLK_TTL_UNCHANGED = 2
+CLK_GWOPT_OK = 0
+CLK_GWOPT_ERROR = 1
 
 
 class clk_batch(ctypes.Structure):
@@ -57,8 +59,19 @@ class clk_ip_check_cfg(ctypes.Structure):
     ]
 
 
+class clk_ip_out_cfg(ctypes.Structure):
+    _fields_ = [
+        ("my_ip", ctypes.c_uint32),
+        ("ts", ctypes.c_uint32),
+        ("my_addrs", ctypes.c_void_p),
+        ("n_my_addrs", ctypes.c_uint32),
+        ("mtu", ctypes.c_uint32),
+    ]
+
+
 _P = ctypes.c_void_p
 _BP = ctypes.POINTER(clk_batch)
+_OP = ctypes.POINTER(clk_ip_out_cfg)
 
 # name -> (restype, argtypes); every symbol include/*.h declares
 SIGNATURES = {
@@ -81,6 +94,9 @@ SIGNATURES = {
     "clk_set_tcp_checksum": (ctypes.c_int, [_P, _BP, ctypes.c_int, _P, _P]),
     "clk_check_icmp_header": (ctypes.c_int, [_P, _BP, _P]),
     "clk_dec_ip_ttl": (ctypes.c_int, [_P, _BP, ctypes.c_int, _P, _P]),
+    "clk_ip_gw_options": (ctypes.c_int, [_P, _BP, _OP, _P, _P, _P]),
+    "clk_fix_ip_src": (ctypes.c_int, [_P, _BP, _OP, _P, _P]),
+    "clk_ip_output_combo": (ctypes.c_int, [_P, _BP, _OP, _P, _P, _P, _P]),
     "clk_count_codes": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P, ctypes.c_uint32]),
     "clk_gen_packets": (ctypes.c_int, [_P, _BP, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
     "clk_gen_corrupt": (ctypes.c_int, [_P, _BP, ctypes.c_uint64, ctypes.c_uint32]),

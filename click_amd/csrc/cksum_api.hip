@@ -552,6 +552,63 @@ int clk_dec_ip_ttl(clk_ctx *ctx, const clk_batch *b, int multicast, uint8_t *out
     return check_launch(ctx, "clk_dec_ip_ttl");
 }
 
+}   // extern "C"
+
+namespace {
+template <int MODE>
+int launch_ip_out(clk_ctx *ctx, const clk_batch *b, const clk_ip_out_cfg *cfg, const uint8_t *flags,
+                  uint8_t *code, uint8_t *problem, uint16_t *sum, const char *fn)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, fn))) return r;
+    if (!cfg) return fail(ctx, CLK_EINVAL, "%s: null cfg", fn);
+    if (cfg->n_my_addrs && !cfg->my_addrs) return fail(ctx, CLK_EINVAL, "%s: null address list", fn);
+    if (b->n == 0) return CLK_SUCCESS;
+    uint8_t *c = code;
+    if (!c) {                                   // FixIPSrc has no per-packet outcome
+        if ((r = ensure_scratch(ctx, b->n))) return r;
+        c = (uint8_t *)ctx->scratch;
+    }
+    clk::IpOutArgs a;
+    a.my_ip = cfg->my_ip;
+    a.ts = cfg->ts;
+    a.n_my_addrs = cfg->n_my_addrs;
+    a.mtu = cfg->mtu;
+    a.my_addrs = cfg->my_addrs;
+    a.flags = flags;
+    hipLaunchKernelGGL((clk::ip_out_kernel<MODE>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0, ctx->cur, args_of(b),
+                       a, c, problem, sum);
+    return check_launch(ctx, fn);
+}
+}   // namespace
+
+extern "C" {
+
+int clk_ip_gw_options(clk_ctx *ctx, const clk_batch *b, const clk_ip_out_cfg *cfg, uint8_t *out_status,
+                      uint8_t *out_problem, uint16_t *out_sum)
+{
+    if (b && b->n && !out_status)
+        return fail(ctx, CLK_EINVAL, "clk_ip_gw_options: null output");
+    return launch_ip_out<clk::OUT_GWOPT>(ctx, b, cfg, nullptr, out_status, out_problem, out_sum,
+                                         "clk_ip_gw_options");
+}
+
+int clk_fix_ip_src(clk_ctx *ctx, const clk_batch *b, const clk_ip_out_cfg *cfg, const uint8_t *anno,
+                   uint16_t *out_sum)
+{
+    return launch_ip_out<clk::OUT_FIXSRC>(ctx, b, cfg, anno, nullptr, nullptr, out_sum, "clk_fix_ip_src");
+}
+
+int clk_ip_output_combo(clk_ctx *ctx, const clk_batch *b, const clk_ip_out_cfg *cfg, const uint8_t *flags,
+                        uint8_t *out_port, uint8_t *out_problem, uint16_t *out_sum)
+{
+    if (b && b->n && !out_port)
+        return fail(ctx, CLK_EINVAL, "clk_ip_output_combo: null output");
+    return launch_ip_out<clk::OUT_COMBO>(ctx, b, cfg, flags, out_port, out_problem, out_sum,
+                                         "clk_ip_output_combo");
+}
+
 int clk_count_codes(clk_ctx *ctx, const uint8_t *codes, uint64_t n, uint64_t *counts, uint32_t ncounts)
 {
     int r = enter(ctx);

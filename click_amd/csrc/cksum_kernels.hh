@@ -867,6 +867,183 @@ __global__ void __launch_bounds__(256) dec_ttl_kernel(BatchArgs b, int multicast
 }
 
 // ---------------------------------------------------------------------------
+// IP output path, one lane per packet: IPGWOptions (ipgwoptions.cc:53-172),
+// FixIPSrc (fixipsrc.cc:52-72) and IPOutputCombo after its annotation-only
+// steps (ipoutputcombo.cc:59-199).  Option-free headers (ip_hl = 5, the
+// common case) take the straight path: one dword and one byte read, TTL
+// and ip_sum rewritten as in DecIPTTL; options are walked byte by byte.
+// ---------------------------------------------------------------------------
+enum IpOutMode { OUT_GWOPT = 0, OUT_FIXSRC = 1, OUT_COMBO = 2 };
+
+struct IpOutArgs {
+    uint32_t my_ip, ts, n_my_addrs, mtu;
+    const uint32_t *my_addrs;
+    const uint8_t *flags;      // per packet: bit 0 FIX_IP_SRC_ANNO (nullptr: FixIPSrc all set, combo none)
+};
+
+__device__ __forceinline__ void st_u8(uint8_t *p, uint32_t v)
+{
+    *(__attribute__((address_space(1))) uint8_t *)p = (uint8_t)v;
+}
+__device__ __forceinline__ void st_u32_bytes(uint8_t *p, uint32_t v)
+{
+    for (int k = 0; k < 4; k++)
+        st_u8(p + k, v >> (8 * k));
+}
+
+// The option walk (ipgwoptions.cc:59-153 / ipoutputcombo.cc:65-166) over a
+// header with 20 < hlen <= caplen.  An option byte at or past caplen reads
+// as 0 (oracle/cksum_oracle.c: the same domain guard).  Returns 1 on a
+// parameter problem (offset in *problem).
+__device__ __noinline__ uint32_t ip_gw_options(uint8_t *ip, int hlen, uint32_t caplen, uint32_t my_ip,
+                                               const uint32_t *my_addrs, uint32_t nmy, uint32_t ts,
+                                               uint32_t *problem, bool *touched, bool *changed)
+{
+    auto optb = [&](int i) -> int { return (uint32_t)i < caplen ? (int)ld_u8(ip + i) : 0; };
+    for (int oi = 20; oi < hlen;) {
+        const int type = (int)ld_u8(ip + oi);
+        if (type == 1) {                          // IPOPT_NOP
+            oi++;
+            continue;
+        } else if (type == 0)                     // IPOPT_EOL
+            break;
+        const int xlen = optb(oi + 1);
+        if (xlen < 2 || oi + xlen > hlen) {
+            *problem = oi + 1;
+            return 1;
+        } else if (type != 7 && type != 68) {     // not IPOPT_RR / IPOPT_TS
+            oi += xlen;
+            continue;
+        }
+        *touched = true;
+        const int p = optb(oi + 2) - 1;
+        if (type == 7) {                          // Record Route
+            if (p >= 3 && p + 4 <= xlen) {
+                st_u32_bytes(ip + oi + p, my_ip);
+                st_u8(ip + oi + 2, (uint32_t)(p + 1 + 4));
+                *changed = true;
+            } else if (p != xlen) {
+                *problem = oi + 2;
+                return 1;
+            }
+        } else {                                  // Timestamp
+            const int oflw = optb(oi + 3) >> 4, flg = optb(oi + 3) & 0xF;
+            bool overflowed = false;
+            if (p < 4) {
+                *problem = oi + 2;
+                return 1;
+            } else if (flg == 0) {
+                if (p + 4 <= xlen) {
+                    st_u32_bytes(ip + oi + p, ts);
+                    st_u8(ip + oi + 2, (uint32_t)(p + 1 + 4));
+                    *changed = true;
+                } else
+                    overflowed = true;
+            } else if (flg == 1) {
+                if (p + 8 <= xlen) {
+                    st_u32_bytes(ip + oi + p, my_ip);
+                    st_u32_bytes(ip + oi + p + 4, ts);
+                    st_u8(ip + oi + 2, (uint32_t)(p + 1 + 8));
+                    *changed = true;
+                } else
+                    overflowed = true;
+            } else if (flg == 3 && p + 8 <= xlen) {
+                const uint32_t addr = ld_u32_unaligned(ip + oi + p);
+                bool mine = !my_addrs && addr == my_ip;   // IPOutputCombo: IPADDR only (144)
+                for (uint32_t k = 0; my_addrs && k < nmy; k++)
+                    mine |= my_addrs[k] == addr;
+                if (mine) {
+                    st_u32_bytes(ip + oi + p + 4, ts);
+                    st_u8(ip + oi + 2, (uint32_t)(p + 1 + 8));
+                    *changed = true;
+                }
+            } else {
+                *problem = oi + 3;
+                return 1;
+            }
+            if (overflowed) {
+                if (oflw < 15) {
+                    st_u8(ip + oi + 3, (uint32_t)(((oflw + 1) << 4) | flg));
+                    *changed = true;
+                } else {
+                    *problem = oi + 3;
+                    return 1;
+                }
+            }
+        }
+        oi += xlen;
+    }
+    return 0;
+}
+
+// ip_sum = 0; ip_sum = click_in_cksum(ip, hlen): stores and returns it.
+__device__ __forceinline__ uint32_t ip_resum(uint8_t *ip, uint32_t hlen)
+{
+    uint32_t sum = 0;
+    for (uint32_t o = 0; o < hlen; o += 4) {
+        const uint32_t w = ld_u32_unaligned(ip + o);
+        sum += (w & 0xFFFF) + (w >> 16);
+    }
+    if (hlen >= 12)                                // the stored ip_sum is in range: zero it
+        sum -= ld_u32_unaligned(ip + 8) >> 16;
+    const uint32_t v = in_cksum_fold(sum);
+    st_u16(ip + 10, v);
+    return v;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(256) ip_out_kernel(BatchArgs b, IpOutArgs c, uint8_t *out_code,
+                                                     uint8_t *out_problem, uint16_t *out_sum)
+{
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += nthreads) {
+        uint8_t *ip = b.base + pkt_off(b, i);
+        const uint32_t caplen = pkt_len(b, i);
+        uint32_t code = 0, problem = 0, cur = 0;
+        if (caplen >= 20) {
+            const uint32_t w8 = ld_u32_unaligned(ip + 8);       // ttl, proto, ip_sum
+            cur = w8 >> 16;
+            const uint32_t hlen = (ld_u8(ip) & 0xF) << 2;
+            const uint32_t flag = c.flags ? c.flags[i] : (MODE == OUT_FIXSRC ? 1u : 0u);
+            bool touched = false, changed = false;
+            if (MODE != OUT_FIXSRC && hlen > 20 && hlen <= caplen &&    // hlen > caplen: domain guard
+                ip_gw_options(ip, (int)hlen, caplen, c.my_ip, MODE == OUT_COMBO ? nullptr : c.my_addrs,
+                              c.n_my_addrs, c.ts, &problem, &touched, &changed)) {
+                code = MODE == OUT_GWOPT ? 1u : 2u;                     // output 1 / output 2
+            } else {
+                bool resum = MODE == OUT_GWOPT && touched;              // ipgwoptions.cc:155-159
+                if (MODE != OUT_GWOPT && (flag & 1) && (MODE == OUT_COMBO || hlen <= caplen)) {
+                    st_u32_bytes(ip + 12, c.my_ip);                     // fixipsrc.cc:60-64 / combo 169-173
+                    changed = true;
+                }
+                if (MODE != OUT_GWOPT)
+                    resum = changed && hlen <= caplen;                  // combo 176-179
+                if (resum)
+                    cur = ip_resum(ip, hlen);
+                if (MODE == OUT_COMBO) {                        // DecIPTTL, ipoutputcombo.cc:182-191
+                    const uint32_t ttl = w8 & 0xFF;             // no earlier step writes byte 8
+                    if (ttl <= 1) {
+                        code = 3;
+                    } else {
+                        const uint32_t s = (~(uint32_t)bswap16(cur) & 0xFFFF) + 0xFEFF;
+                        cur = ~(uint32_t)bswap16((s + (s >> 16)) & 0xFFFF) & 0xFFFF;
+                        st_u8(ip + 8, ttl - 1);
+                        st_u16(ip + 10, cur);
+                        if (caplen > c.mtu)                     // 194-197
+                            code = 4;
+                    }
+                }
+            }
+        }
+        out_code[i] = (uint8_t)code;
+        if (out_problem)
+            out_problem[i] = (uint8_t)problem;
+        if (out_sum)
+            out_sum[i] = (uint16_t)cur;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Deferred Set stores.  Writing the 2-byte checksum field into the packet
 // while the same kernel streams packet bytes in costs far more than its
 // bytes (DESIGN.md "Set stores"); the two-phase Set computes in a read-only

@@ -183,6 +183,54 @@ int clk_check_icmp_header(clk_ctx *ctx, const clk_batch *batch, uint8_t *out_ver
 int clk_dec_ip_ttl(clk_ctx *ctx, const clk_batch *batch, int multicast,
                    uint8_t *out_status, uint16_t *out_sum);
 
+/* ---- IP output path ---------------------------------------------------------
+ * The batch points at each packet's IP header (= data() for these elements
+ * in an IP router graph); len_i = bytes from it to end_data().
+ * cfg->my_ip: raw s_addr written by Record Route / Timestamp flg 1 and by
+ *   FixIPSrc (IPGWOptions: its preferred address; IPOutputCombo / FixIPSrc:
+ *   IPADDR).
+ * cfg->ts: the 4 bytes a Timestamp option stores for "now" (the reference
+ *   stores htonl(ms since midnight) from Timestamp::now(); the host takes it
+ *   once per batch).
+ * cfg->my_addrs / n_my_addrs: device array of raw s_addr, IPGWOptions'
+ *   interface addresses for Timestamp flg 3 (IPOutputCombo matches my_ip).
+ * cfg->mtu: IPOutputCombo's MTU.
+ * out_problem (nullable): ICMP_PARAMPROB_ANNO offsets of the parameter
+ *   problems (0 otherwise).  out_sum (nullable): ip_sum after the element.
+ * Domain guards (as the oracle): len_i < 20 passes untouched; options are
+ * not walked when ip_hl*4 > len_i; an option byte read at or past len_i
+ * reads as 0. */
+typedef struct clk_ip_out_cfg {
+    uint32_t my_ip;
+    uint32_t ts;
+    const uint32_t *my_addrs;
+    uint32_t n_my_addrs;
+    uint32_t mtu;
+} clk_ip_out_cfg;
+
+enum clk_gwopt_status {               /* IPGWOptions outcome (ipgwoptions.cc:53-172) */
+    CLK_GWOPT_OK = 0,                 /* output 0; ip_sum recomputed if an RR/TS option was met */
+    CLK_GWOPT_ERROR = 1               /* parameter problem: drops++, output 1            */
+};
+/* IPGWOptions::simple_action (elements/ip/ipgwoptions.cc:164-172, options 53-160). */
+int clk_ip_gw_options(clk_ctx *ctx, const clk_batch *batch, const clk_ip_out_cfg *cfg,
+                      uint8_t *out_status, uint8_t *out_problem, uint16_t *out_sum);
+
+/* FixIPSrc::simple_action (elements/ip/fixipsrc.cc:52-72).  anno[i] bit 0 =
+ * FIX_IP_SRC_ANNO (NULL: set on every packet); the host clears the
+ * annotation.  Every packet leaves on output 0.                            */
+int clk_fix_ip_src(clk_ctx *ctx, const clk_batch *batch, const clk_ip_out_cfg *cfg,
+                   const uint8_t *anno, uint16_t *out_sum);
+
+/* IPOutputCombo::push (elements/ip/ipoutputcombo.cc:44-205) after its two
+ * annotation-only steps, DropBroadcasts and PaintTee (the host kills
+ * broadcasts and clones painted packets to output 1 before the batch):
+ * IPGWOptions, FixIPSrc (flags[i] bit 0 = FIX_IP_SRC_ANNO; NULL: none), the
+ * header re-checksum, DecIPTTL, the MTU test on len_i.  out_port[i]: 0,
+ * 2 (parameter problem), 3 (TTL expired) or 4 (longer than MTU).          */
+int clk_ip_output_combo(clk_ctx *ctx, const clk_batch *batch, const clk_ip_out_cfg *cfg,
+                        const uint8_t *flags, uint8_t *out_port, uint8_t *out_problem, uint16_t *out_sum);
+
 /* ---- batch utilities ------------------------------------------------------- */
 
 /* counts[c] += number of i with codes[i] == c, for c < ncounts (device u64). */

@@ -197,3 +197,84 @@ def vary_ttl(rng, arena, off, caplen, frac=0.4):
             arena[o + 16] = 0xE0 | int(rng.integers(0, 16))
         else:
             arena[o + 10] = int(rng.integers(0, 256))          # stale ip_sum: updated all the same
+
+
+def _gw_options(rng, words, my_ip):
+    """`words` 32-bit words of options built around Record Route (7) and
+    Timestamp (68) at every pointer / flag / overflow edge
+    (ipgwoptions.cc:59-153), mixed with NOP/EOL/other/malformed options."""
+    n = 4 * words
+    out = bytearray(n)
+    o = 0
+    while o < n:
+        room = n - o
+        kind = int(rng.integers(0, 10))
+        if kind <= 3 and room >= 3:                       # Record Route
+            ln = int(rng.integers(3, room + 1))
+            out[o], out[o + 1] = 7, ln
+            out[o + 2] = int(rng.choice([4, 4 + 4 * int(rng.integers(0, 8)), ln + 1, ln - 2, 0, 1, 3,
+                                         int(rng.integers(0, 256))]))
+            out[o + 3:o + ln] = rng.integers(0, 256, ln - 3, dtype=np.uint8).tobytes()
+            o += ln
+        elif kind <= 6 and room >= 4:                     # Timestamp
+            ln = int(rng.integers(4, room + 1))
+            flg = int(rng.choice([0, 1, 3, 2, 4]))
+            of = int(rng.choice([0, 1, 14, 15]))
+            out[o], out[o + 1] = 68, ln
+            out[o + 2] = int(rng.choice([5, 5 + 4 * int(rng.integers(0, 9)), ln + 1, ln - 3, 4, 1,
+                                         int(rng.integers(0, 256))]))
+            out[o + 3] = (of << 4) | flg
+            out[o + 4:o + ln] = rng.integers(0, 256, ln - 4, dtype=np.uint8).tobytes()
+            if flg == 3 and ln >= 12 and rng.random() < 0.6:
+                p = out[o + 2] - 1
+                if 4 <= p and p + 8 <= ln:
+                    out[o + p:o + p + 4] = int(my_ip).to_bytes(4, "little")
+            o += ln
+        elif kind == 7:
+            out[o] = 1
+            o += 1
+        elif kind == 8:
+            out[o] = 0
+            o += 1
+        else:                                             # other / malformed length
+            out[o] = int(rng.choice([130, 148, 7, 68]))
+            if o + 1 < n:
+                out[o + 1] = int(rng.choice([0, 1, room + 1, 2, min(room, 255)]))
+            o = n
+    return bytes(out)
+
+
+def gw_batch(rng, n, my_ip, max_total=200, opt_frac=0.7, tiny_frac=0.03, trunc_frac=0.05):
+    """Batch for IPGWOptions / FixIPSrc / IPOutputCombo: valid IPv4 headers
+    (ip_sum set) with RR/TS options on most packets, TTLs at the 0/1/2
+    edges, a few tiny or truncated packets; arbitrary alignments.  Returns
+    (arena, off, length, flags) with flags bit 0 = FIX_IP_SRC_ANNO."""
+    pkts = []
+    for _ in range(n):
+        if rng.random() < tiny_frac:
+            pkts.append(rng.integers(0, 256, int(rng.integers(0, 24)), dtype=np.uint8).tobytes())
+            continue
+        ow = int(rng.integers(1, 11)) if rng.random() < opt_frac else 0
+        tl = int(rng.integers(20 + 4 * ow + 8, max_total + 1))
+        b = bytearray(build(rng, 17, tl, 0))
+        b[0] = 0x40 | (5 + ow)
+        b[20:20 + 4 * ow] = _gw_options(rng, ow, my_ip)
+        if rng.random() < 0.2:
+            b[8] = int(rng.choice([0, 1, 2]))
+        pkts.append(bytes(b))
+    caplen = np.array([len(p) for p in pkts], np.uint32)
+    off = np.zeros(n, np.uint64)
+    pos = 0
+    for i, p in enumerate(pkts):
+        pos += int(rng.integers(0, 8))
+        off[i] = pos
+        pos += len(p) + int(rng.integers(0, 8))
+    arena = np.zeros(pos + 64, np.uint8)
+    for i, p in enumerate(pkts):
+        arena[int(off[i]):int(off[i]) + len(p)] = np.frombuffer(p, np.uint8)
+    oracle_lib.batch("set_ip", arena, n, off=off, length=caplen)
+    for i in range(n):
+        if rng.random() < trunc_frac and caplen[i] > 0:
+            caplen[i] = int(rng.integers(0, caplen[i]))
+    flags = (rng.random(n) < 0.3).astype(np.uint8)
+    return arena, off, caplen, flags

@@ -55,8 +55,35 @@ def load_oracle():
                                ctypes.c_int, ctypes.c_int]
     L.oracle_splitmix64.restype = ctypes.c_uint64
     L.oracle_splitmix64.argtypes = [ctypes.c_uint64]
+    L.oracle_ip_out_batch.restype = ctypes.c_int
+    L.oracle_ip_out_batch.argtypes = [ctypes.c_int, _P, _P, ctypes.c_uint64, _P, ctypes.c_uint32, ctypes.c_uint64,
+                                      _P, ctypes.c_uint32, _P, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
+                                      _P, _P, _P]
     _lib = L
     return L
+
+
+IP_OUT_OPS = {"ip_gw_options": 0, "fix_ip_src": 1, "ip_output_combo": 2}
+
+
+def ip_out_batch(op, arena, n, stride=0, fixed_len=0, off=None, length=None, flags=None, my_ip=0,
+                 my_addrs=None, ts=0, mtu=0xFFFFFFFF):
+    """IPGWOptions / FixIPSrc / IPOutputCombo over a numpy arena (modified in
+    place).  Returns (codes or ports uint8[n], problem offsets uint8[n],
+    ip_sum uint16[n])."""
+    L = load_oracle()
+    codes = np.zeros(max(n, 1), np.uint8)
+    prob = np.zeros(max(n, 1), np.uint8)
+    sums = np.zeros(max(n, 1), np.uint16)
+    off = None if off is None else np.ascontiguousarray(off, np.uint64)
+    length = None if length is None else np.ascontiguousarray(length, np.uint32)
+    flags = None if flags is None else np.ascontiguousarray(flags, np.uint8)
+    ma = None if my_addrs is None else np.ascontiguousarray(my_addrs, np.uint32)
+    rc = L.oracle_ip_out_batch(IP_OUT_OPS[op], _np_ptr(arena), _np_ptr(off), stride, _np_ptr(length), fixed_len, n,
+                               _np_ptr(flags), my_ip & 0xFFFFFFFF, _np_ptr(ma), 0 if ma is None else len(ma),
+                               ts & 0xFFFFFFFF, mtu & 0xFFFFFFFF, _np_ptr(codes), _np_ptr(prob), _np_ptr(sums))
+    assert rc == 0
+    return codes[:n], prob[:n], sums[:n]
 
 
 def _np_ptr(a):

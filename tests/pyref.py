@@ -226,3 +226,124 @@ def dec_ttl(b, caplen, multicast=True):
         s = (s & 0xFFFF) + (s >> 16)
     struct.pack_into(">H", b, 10, (~s) & 0xFFFF)
     return 0, bytes(b)
+
+
+# ---- IP output path (RFC 791 Record Route / Timestamp processing) ----------
+def _ip_resum(b, hl):
+    """ip_sum = 0, then the header checksum over hl bytes."""
+    b[10:12] = b"\0\0"
+    struct.pack_into("<H", b, 10, in_cksum(bytes(b[:hl])))
+
+
+def gw_walk(b, caplen, my_ip, my_addrs, ts):
+    """Process RR (7) and TS (68) options in place.  Returns (problem or
+    None, touched, changed).  Option bytes at/after caplen read as 0."""
+    hl = (b[0] & 0xF) * 4
+    at = lambda i: b[i] if i < caplen else 0            # noqa: E731
+    mine_b = struct.pack("<I", my_ip)
+    ts_b = struct.pack("<I", ts)
+    touched = changed = False
+    i = 20
+    while i < hl:
+        kind = b[i]
+        if kind == 0:
+            break
+        if kind == 1:
+            i += 1
+            continue
+        olen = at(i + 1)
+        if olen < 2 or i + olen > hl:
+            return i + 1, touched, changed
+        if kind not in (7, 68):
+            i += olen
+            continue
+        touched = True
+        ptr = at(i + 2)               # 1-origin pointer to the next free slot
+        if kind == 7:
+            if ptr >= 4 and ptr - 1 + 4 <= olen:
+                b[i + ptr - 1:i + ptr + 3] = mine_b
+                b[i + 2] = (ptr + 4) & 0xFF
+                changed = True
+            elif ptr - 1 != olen:                          # not simply full
+                return i + 2, touched, changed
+        else:
+            of, flag = at(i + 3) >> 4, at(i + 3) & 0xF
+            slot = ptr - 1
+            full = False
+            if slot < 4:
+                return i + 2, touched, changed
+            if flag == 0:
+                if slot + 4 <= olen:
+                    b[i + slot:i + slot + 4] = ts_b
+                    b[i + 2] = (ptr + 4) & 0xFF
+                    changed = True
+                else:
+                    full = True
+            elif flag == 1:
+                if slot + 8 <= olen:
+                    b[i + slot:i + slot + 4] = mine_b
+                    b[i + slot + 4:i + slot + 8] = ts_b
+                    b[i + 2] = (ptr + 8) & 0xFF
+                    changed = True
+                else:
+                    full = True
+            elif flag == 3 and slot + 8 <= olen:
+                if u32le(bytes(b), i + slot) in my_addrs:
+                    b[i + slot + 4:i + slot + 8] = ts_b
+                    b[i + 2] = (ptr + 8) & 0xFF
+                    changed = True
+            else:
+                return i + 3, touched, changed
+            if full:
+                if of >= 15:
+                    return i + 3, touched, changed
+                b[i + 3] = ((of + 1) << 4) | flag
+                changed = True
+        i += olen
+    return None, touched, changed
+
+
+def ip_gw_options(b, caplen, my_ip, my_addrs, ts):
+    """IPGWOptions: returns (code, problem, new bytes)."""
+    b = bytearray(b)
+    hl = (b[0] & 0xF) * 4 if caplen >= 20 else 0
+    if caplen < 20 or hl <= 20 or hl > caplen:
+        return 0, 0, bytes(b)
+    prob, touched, _ = gw_walk(b, caplen, my_ip, set(my_addrs), ts)
+    if prob is not None:
+        return 1, prob, bytes(b)
+    if touched:
+        _ip_resum(b, hl)
+    return 0, 0, bytes(b)
+
+
+def fix_ip_src(b, caplen, anno, my_ip):
+    b = bytearray(b)
+    if anno and caplen >= 20 and (b[0] & 0xF) * 4 <= caplen:
+        b[12:16] = struct.pack("<I", my_ip)
+        _ip_resum(b, (b[0] & 0xF) * 4)
+    return bytes(b)
+
+
+def ip_output_combo(b, caplen, flags, my_ip, mtu, ts):
+    """IPOutputCombo after DropBroadcasts/PaintTee: (port, problem, bytes).
+    The TTL step uses the general RFC 1624 update (ip.h:177-185)."""
+    b = bytearray(b)
+    if caplen < 20:
+        return 0, 0, bytes(b)
+    hl = (b[0] & 0xF) * 4
+    changed = False
+    if 20 < hl <= caplen:
+        prob, _, changed = gw_walk(b, caplen, my_ip, {my_ip}, ts)
+        if prob is not None:
+            return 2, prob, bytes(b)
+    if flags & 1:
+        b[12:16] = struct.pack("<I", my_ip)
+        changed = True
+    if changed and hl <= caplen:
+        _ip_resum(b, hl)
+    if b[8] <= 1:
+        return 3, 0, bytes(b)
+    st, nb = dec_ttl(bytes(b), caplen)
+    assert st == 0
+    return (4 if caplen > mtu else 0), 0, nb

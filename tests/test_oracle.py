@@ -276,3 +276,65 @@ def test_dec_ttl_on_reference_headers():
         assert L.oracle_in_cksum(pkt[:hl].tobytes(), hl) == 0, v["name"]
         seen += 1
     assert seen >= 3
+
+
+MY_IP = 0x18041A12          # 18.26.4.24 as a raw s_addr word (network order in memory)
+TS = 0x40E20100
+
+
+@pytest.mark.parametrize("op", ["ip_gw_options", "fix_ip_src", "ip_output_combo"])
+def test_ip_output_path_matches_pyref(op):
+    """IPGWOptions / FixIPSrc / IPOutputCombo: the C oracle against the
+    independent Python restatement on option-heavy fuzzed batches; every
+    outcome (ports 0/2/3/4, parameter-problem offsets) is exercised."""
+    rng = np.random.default_rng(321)
+    arena, off, caplen, flags = fuzz.gw_batch(rng, 3000, MY_IP)
+    n = len(off)
+    addrs = np.array([MY_IP, 0x01020304], np.uint32)
+    a = arena.copy()
+    codes, prob, sums = oracle_lib.ip_out_batch(op, a, n, off=off, length=caplen, flags=flags, my_ip=MY_IP,
+                                                my_addrs=addrs, ts=TS, mtu=120)
+    for i in range(n):
+        o, c = int(off[i]), int(caplen[i])
+        pk = arena[o:o + c].tobytes()
+        if op == "ip_gw_options":
+            code, p, nb = pyref.ip_gw_options(pk, c, MY_IP, addrs.tolist(), TS)
+        elif op == "fix_ip_src":
+            code, p, nb = 0, 0, pyref.fix_ip_src(pk, c, flags[i] & 1, MY_IP)
+        else:
+            code, p, nb = pyref.ip_output_combo(pk, c, int(flags[i]), MY_IP, 120, TS)
+        assert (codes[i], prob[i]) == (code, p), (op, i, codes[i], prob[i], code, p)
+        assert a[o:o + c].tobytes() == nb, (op, i)
+    got = set(np.unique(codes).tolist())
+    assert got == {"ip_gw_options": {0, 1}, "fix_ip_src": {0}, "ip_output_combo": {0, 2, 3, 4}}[op], got
+
+
+def test_iprouter_output_equivalence():
+    """iprouter-01.clicktest: the IP output chain IPGWOptions -> FixIPSrc ->
+    DecIPTTL and its click-xform replacement IPOutputCombo give the same
+    bytes (the test expects OUTA == OUTB), on fuzzed headers with and
+    without RR/TS options that pass both without error."""
+    rng = np.random.default_rng(99)
+    arena, off, caplen, flags = fuzz.gw_batch(rng, 2000, MY_IP)
+    n = len(off)
+    a1, a2 = arena.copy(), arena.copy()
+    g, _, _ = oracle_lib.ip_out_batch("ip_gw_options", a1, n, off=off, length=caplen, my_ip=MY_IP,
+                                      my_addrs=np.array([MY_IP], np.uint32), ts=TS)
+    oracle_lib.ip_out_batch("fix_ip_src", a1, n, off=off, length=caplen, flags=flags, my_ip=MY_IP)
+    d, _ = oracle_lib.batch("dec_ttl", a1, n, off=off, length=caplen)
+    port, _, _ = oracle_lib.ip_out_batch("ip_output_combo", a2, n, off=off, length=caplen, flags=flags,
+                                         my_ip=MY_IP, ts=TS, mtu=1 << 20)
+    same = 0
+    for i in range(n):
+        o, c = int(off[i]), int(caplen[i])
+        if c < 20 or g[i] != 0:
+            continue
+        # IPGWOptions re-checksums whenever it meets an RR/TS option, the
+        # combo only when a byte changed: equal for headers that were valid
+        hl = (int(arena[o]) & 0xF) * 4
+        if hl < 20 or hl > c or pyref.in_cksum(arena[o:o + hl].tobytes()) != 0:
+            continue
+        assert port[i] == (3 if d[i] == 1 else 0), i
+        assert a1[o:o + c].tobytes() == a2[o:o + c].tobytes(), i
+        same += 1
+    assert same > 500
