@@ -346,6 +346,12 @@ int oracle_dec_ip_ttl(uint8_t *nh, uint32_t caplen, int multicast)
     return CLK_OK;
 }
 
+/* Packet i of a batch (the C ABI's clk_batch semantics). */
+static inline uint64_t pkt_off(const uint64_t *off, uint64_t stride, uint64_t i)
+{ return off ? off[i] : i * stride; }
+static inline uint32_t pkt_len(const uint32_t *len, uint32_t fixed_len, uint64_t i)
+{ return len ? len[i] : fixed_len; }
+
 /* ---- IP output path: IPGWOptions, FixIPSrc, IPOutputCombo ----------------
  * The option walk shared by IPGWOptions::handle_options
  * (elements/ip/ipgwoptions.cc:53-160) and IPOutputCombo::push's IPGWOptions
@@ -524,12 +530,131 @@ int oracle_ip_output_combo(uint8_t *ip, uint32_t caplen, uint32_t length, int fl
     return 0;
 }
 
+/* ---- IPFragmenter ---------------------------------------------------------
+ * elements/ip/ipfragmenter.cc:53-86 (optcopy): copy the options whose
+ * copied-flag (0x80) is set, skip NOPs, stop at EOL or a malformed option,
+ * pad to a multiple of 4 with EOL.  Returns the bytes written. */
+static int frag_optcopy(const uint8_t *ip, uint8_t *oout)
+{
+    const uint8_t *oin = ip + 20;
+    const uint8_t *oin_end = ip + ((ip[0] & 0xF) << 2);        /* 60 */
+    int outpos = 0;
+    while (oin < oin_end) {                                     /* 64 */
+        if (*oin == 1)                                          /* NOP: not copied, 65-66 */
+            ++oin;
+        else if (*oin == 0 || oin + 1 == oin_end || oin[1] < 2 || oin + oin[1] > oin_end) /* 67-71 */
+            break;
+        else {
+            if (*oin & 0x80) {                                  /* 73-77 */
+                if (oout)
+                    memcpy(oout + outpos, oin, oin[1]);
+                outpos += oin[1];
+            }
+            oin += oin[1];                                      /* 78 */
+        }
+    }
+    for (; (outpos & 3) != 0; outpos++)                         /* 81-83 */
+        if (oout)
+            oout[outpos] = 0;
+    return outpos;
+}
+
+/* elements/ip/ipfragmenter.cc:88-171 (push + fragment) on one packet whose
+ * IP header is at `ip` with `caplen` = network_length() bytes.  Returns the
+ * port: 0 (network_length <= MTU, untouched), 1 (DF with HONOR_DF, or the
+ * first fragment would carry < 8 data bytes: output 1), 2 (fragmented: the
+ * packet becomes the first fragment in place, *first_len bytes from the IP
+ * header; the others are appended at 16 B-aligned offsets of `arena`
+ * starting at *arena_pos, descriptors at frag_off/frag_len[*nfrag ...]).
+ * new_id replaces ip_id when DF is cleared (the reference uses
+ * click_random(), 112-115).  Domain guards: caplen < 20 with caplen > MTU
+ * -> port 1; fragment bytes past caplen (ip_len > network_length, which
+ * CheckIPHeader excludes) are written as 0.  With arena == NULL only the
+ * counts are produced. */
+int oracle_ip_fragment(uint8_t *ip, uint32_t caplen, uint32_t mtu, int honor_df, uint16_t new_id,
+                       uint8_t *arena, uint64_t *arena_pos, uint64_t *frag_off, uint32_t *frag_len,
+                       uint64_t *nfrag, uint32_t *first_len)
+{
+    *first_len = caplen;
+    if (caplen <= mtu)                                          /* 167-168 */
+        return 0;
+    if (caplen < 20)
+        return 1;
+    int hlen = (ip[0] & 0xF) << 2;                              /* 92 */
+    int first_dlen = ((int)mtu - hlen) & ~7;                    /* 93 */
+    int in_dlen = (int)bswap16(ld16(ip + 2)) - hlen;            /* 94 */
+    if (((ip[6] & 0x40) && honor_df) || first_dlen < 8)         /* 96-102: ip_off & htons(IP_DF) */
+        return 1;
+    if (ip[6] & 0x40) {                                         /* 112-115 */
+        st16(ip + 4, new_id);
+        ip[6] &= (uint8_t)~0x40;
+    }
+    int had_mf = (ip[6] & 0x20) != 0;                           /* 116 */
+    st16(ip + 2, bswap16((uint32_t)(hlen + first_dlen)));      /* 117 */
+    ip[6] |= 0x20;                                              /* 118 */
+    st16(ip + 10, 0);                                           /* 119 */
+    st16(ip + 10, oracle_in_cksum(ip, hlen));                   /* 120 */
+    *first_len = (uint32_t)(hlen + first_dlen);                 /* 121-122 */
+    int out_hlen = 20 + frag_optcopy(ip, 0);                    /* 127 */
+    const uint8_t *th = ip + hlen;
+    for (int off = first_dlen; off < in_dlen;) {                /* 129 */
+        int out_dlen = ((int)mtu - out_hlen) & ~7;              /* 131 */
+        if (out_dlen + off > in_dlen)                           /* 132-133 */
+            out_dlen = in_dlen - off;
+        uint32_t qlen = (uint32_t)(out_hlen + out_dlen);
+        if (arena) {
+            uint8_t *q = arena + *arena_pos;
+            memcpy(q, ip, 20);                                  /* 140 */
+            frag_optcopy(ip, q + 20);                           /* 141 */
+            for (int k = 0; k < out_dlen; k++) {                /* 142 */
+                uint32_t s = (uint32_t)(hlen + off + k);
+                q[out_hlen + k] = s < caplen ? th[off + k] : 0;
+            }
+            q[0] = (uint8_t)((q[0] & 0xF0) | ((out_hlen >> 2) & 0xF)); /* 144 */
+            st16(q + 6, bswap16(bswap16(ld16(ip + 6)) + (uint32_t)(off >> 3))); /* 145 */
+            if (out_dlen + off >= in_dlen && !had_mf)           /* 146-147 */
+                q[6] &= (uint8_t)~0x20;
+            st16(q + 2, bswap16(qlen));                         /* 148 */
+            st16(q + 10, 0);                                    /* 149 */
+            st16(q + 10, oracle_in_cksum(q, out_hlen));         /* 150 */
+            frag_off[*nfrag] = *arena_pos;
+            frag_len[*nfrag] = qlen;
+        }
+        *arena_pos += (qlen + 15) & ~15u;
+        ++*nfrag;
+        off += out_dlen;                                        /* 158 */
+    }
+    return 2;
+}
+
+/* Batch form: packets in order; fragments appended in packet order.
+ * out_port[i], out_first_len[i]; out_frag_first[i] = index of packet i's
+ * first appended fragment; totals[0] = fragments, totals[1] = arena bytes.
+ * new_id (nullable) per packet. */
+int oracle_ip_fragment_batch(uint8_t *base, const uint64_t *off, uint64_t stride, const uint32_t *len,
+                             uint32_t fixed_len, uint64_t n, uint32_t mtu, int honor_df, const uint16_t *new_id,
+                             uint8_t *out_port, uint32_t *out_first_len, uint64_t *out_frag_first,
+                             uint8_t *arena, uint64_t *frag_off, uint32_t *frag_len, uint32_t *frag_src,
+                             uint64_t *totals)
+{
+    uint64_t pos = 0, nf = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        uint64_t before = nf;
+        out_frag_first[i] = nf;
+        out_port[i] = (uint8_t)oracle_ip_fragment(base + pkt_off(off, stride, i), pkt_len(len, fixed_len, i),
+                                                  mtu, honor_df, new_id ? new_id[i] : 0, arena, &pos,
+                                                  frag_off, frag_len, &nf, &out_first_len[i]);
+        if (arena && frag_src)
+            for (uint64_t k = before; k < nf; k++)
+                frag_src[k] = (uint32_t)i;
+    }
+    totals[0] = nf;
+    totals[1] = pos;
+    return 0;
+}
+
 /* ---- batch drivers ------------------------------------------------------- */
 
-static inline uint64_t pkt_off(const uint64_t *off, uint64_t stride, uint64_t i)
-{ return off ? off[i] : i * stride; }
-static inline uint32_t pkt_len(const uint32_t *len, uint32_t fixed_len, uint64_t i)
-{ return len ? len[i] : fixed_len; }
 
 static int run_one(int op, uint8_t *p, uint32_t l, int arg, uint16_t *sum)
 {

@@ -278,3 +278,46 @@ def gw_batch(rng, n, my_ip, max_total=200, opt_frac=0.7, tiny_frac=0.03, trunc_f
             caplen[i] = int(rng.integers(0, caplen[i]))
     flags = (rng.random(n) < 0.3).astype(np.uint8)
     return arena, off, caplen, flags
+
+
+def frag_batch(rng, n, max_total=3000):
+    """Batch for IPFragmenter: IPv4 packets with copied / uncopied / NOP /
+    malformed options, DF / MF / nonzero fragment offsets, ip_len below and
+    above the captured length, tiny packets; arbitrary alignments.  Returns
+    (arena, off, length)."""
+    pkts = []
+    for _ in range(n):
+        if rng.random() < 0.03:
+            pkts.append(rng.integers(0, 256, int(rng.integers(0, 30)), dtype=np.uint8).tobytes())
+            continue
+        ow = int(rng.integers(1, 11)) if rng.random() < 0.4 else 0
+        tl = int(rng.integers(20 + 4 * ow + 8, max_total + 1))
+        b = bytearray(build(rng, int(rng.choice([6, 17])), tl, 0))
+        b[0] = 0x40 | (5 + ow)
+        opts = bytearray(_options(rng, ow))
+        for k in range(len(opts)):                      # set the copied flag on some kinds
+            if opts[k] in (137, 131, 7, 68, 130, 148) and rng.random() < 0.5:
+                opts[k] |= 0x80
+        b[20:20 + 4 * ow] = opts
+        r = rng.random()
+        if r < 0.15:
+            b[6] |= 0x40                                # DF
+        elif r < 0.3:
+            b[6] |= 0x20                                # MF
+        elif r < 0.4:
+            b[6:8] = (int(rng.integers(1, 0x1FFF)) | (0x2000 if rng.random() < 0.5 else 0)).to_bytes(2, "big")
+        if rng.random() < 0.08:
+            b[2:4] = int(rng.integers(0, tl + 64)).to_bytes(2, "big")
+        pkts.append(bytes(b))
+    caplen = np.array([len(p) for p in pkts], np.uint32)
+    off = np.zeros(n, np.uint64)
+    pos = 0
+    for i, p in enumerate(pkts):
+        pos += int(rng.integers(0, 16))
+        off[i] = pos
+        pos += len(p)
+    arena = np.zeros(pos + 64, np.uint8)
+    for i, p in enumerate(pkts):
+        arena[int(off[i]):int(off[i]) + len(p)] = np.frombuffer(p, np.uint8)
+    oracle_lib.batch("set_ip", arena, n, off=off, length=caplen)
+    return arena, off, caplen

@@ -73,6 +73,7 @@ def main():
     args = ap.parse_args()
     R = args.reference
     out = []
+    frag_cases = []
 
     # 1. IPFragmenter-01/02: input packets with IP options (ip_hl = 6) whose
     #    IP and TCP checksums the reference accepts, and the fragment headers
@@ -94,6 +95,13 @@ def main():
         out.append(vec(tname + "-in-tcp-set", src, "reference-accepts", "set_tcp", pkt, le16(pkt, hl + 16),
                        arg=0))
         exp = re.search(r"%expect stderr\n(.*?)\n\n", text, re.S).group(1)
+        # the whole case for the fragmenter: input, configuration, every
+        # fragment Click printed (Print(CONTENTS true): length | bytes)
+        fm = re.search(r"IPFragmenter\((\d+), HONOR_DF (true|false)\)", text)
+        frag_cases.append({"name": tname, "source": "%s:%d" % (rel, line_of(text, fm.group(0))),
+                           "pin": "reference-output", "in": pkt.hex(), "mtu": int(fm.group(1)),
+                           "honor_df": fm.group(2) == "true",
+                           "fragments": [hexbytes(ln.split("|")[1]).hex() for ln in exp.strip().splitlines()]})
         for k, line in enumerate(exp.strip().splitlines()):
             n, hx = line.split("|")
             frag = hexbytes(hx)
@@ -204,7 +212,7 @@ def main():
 
     with open(args.out, "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "reference": "kohler/click 2.1",
-                   "vectors": out}, f, indent=1)
+                   "vectors": out, "fragment_cases": frag_cases}, f, indent=1)
     print("wrote %d vectors to %s" % (len(out), args.out))
 
 

@@ -59,8 +59,40 @@ def load_oracle():
     L.oracle_ip_out_batch.argtypes = [ctypes.c_int, _P, _P, ctypes.c_uint64, _P, ctypes.c_uint32, ctypes.c_uint64,
                                       _P, ctypes.c_uint32, _P, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
                                       _P, _P, _P]
+    L.oracle_ip_fragment_batch.restype = ctypes.c_int
+    L.oracle_ip_fragment_batch.argtypes = [_P, _P, ctypes.c_uint64, _P, ctypes.c_uint32, ctypes.c_uint64,
+                                           ctypes.c_uint32, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P]
     _lib = L
     return L
+
+
+def ip_fragment(arena, n, mtu, honor_df=False, stride=0, fixed_len=0, off=None, length=None, new_id=None):
+    """IPFragmenter over a numpy arena (first fragments rewritten in place).
+    Returns dict(port, first_len, frag_first, frags: list of bytes, frag_src,
+    frag_off, frag_len, arena_bytes)."""
+    L = load_oracle()
+    off = None if off is None else np.ascontiguousarray(off, np.uint64)
+    length = None if length is None else np.ascontiguousarray(length, np.uint32)
+    nid = None if new_id is None else np.ascontiguousarray(new_id, np.uint16)
+    port = np.zeros(max(n, 1), np.uint8)
+    first = np.zeros(max(n, 1), np.uint32)
+    ffirst = np.zeros(max(n, 1), np.uint64)
+    totals = np.zeros(2, np.uint64)
+    scratch = arena.copy()                     # sizing pass: the packets are rewritten in place
+    L.oracle_ip_fragment_batch(_np_ptr(scratch), _np_ptr(off), stride, _np_ptr(length), fixed_len, n, mtu,
+                               int(honor_df), _np_ptr(nid), _np_ptr(port), _np_ptr(first), _np_ptr(ffirst),
+                               None, None, None, None, _np_ptr(totals))
+    nf, nb = int(totals[0]), int(totals[1])
+    out = np.zeros(max(nb, 1), np.uint8)
+    foff = np.zeros(max(nf, 1), np.uint64)
+    flen = np.zeros(max(nf, 1), np.uint32)
+    fsrc = np.zeros(max(nf, 1), np.uint32)
+    L.oracle_ip_fragment_batch(_np_ptr(arena), _np_ptr(off), stride, _np_ptr(length), fixed_len, n, mtu,
+                               int(honor_df), _np_ptr(nid), _np_ptr(port), _np_ptr(first), _np_ptr(ffirst),
+                               _np_ptr(out), _np_ptr(foff), _np_ptr(flen), _np_ptr(fsrc), _np_ptr(totals))
+    frags = [out[int(foff[k]):int(foff[k]) + int(flen[k])].tobytes() for k in range(nf)]
+    return dict(port=port[:n], first_len=first[:n], frag_first=ffirst[:n], frags=frags, frag_src=fsrc[:nf],
+                frag_off=foff[:nf], frag_len=flen[:nf], arena=out[:nb], arena_bytes=nb)
 
 
 IP_OUT_OPS = {"ip_gw_options": 0, "fix_ip_src": 1, "ip_output_combo": 2}

@@ -347,3 +347,67 @@ def ip_output_combo(b, caplen, flags, my_ip, mtu, ts):
     st, nb = dec_ttl(bytes(b), caplen)
     assert st == 0
     return (4 if caplen > mtu else 0), 0, nb
+
+
+# ---- IPFragmenter (RFC 791 fragmentation) ----------------------------------
+def _copied_options(h):
+    """Options with the copied flag, NOPs dropped, EOL-padded to 4 bytes."""
+    hl = (h[0] & 0xF) * 4
+    out = bytearray()
+    i = 20
+    while i < hl:
+        k = h[i]
+        if k == 1:
+            i += 1
+            continue
+        if k == 0 or i + 1 == hl or h[i + 1] < 2 or i + h[i + 1] > hl:
+            break
+        if k & 0x80:
+            out += h[i:i + h[i + 1]]
+        i += h[i + 1]
+    while len(out) % 4:
+        out.append(0)
+    return bytes(out)
+
+
+def ip_fragment(pkt, mtu, honor_df=False, new_id=0):
+    """Returns (port, first fragment bytes or None, [other fragments])."""
+    n = len(pkt)
+    if n <= mtu:
+        return 0, None, []
+    if n < 20:
+        return 1, None, []
+    b = bytearray(pkt)
+    hl = (b[0] & 0xF) * 4
+    per = (mtu - hl) // 8 * 8 if mtu >= hl else -1
+    total_data = be16(b, 2) - hl
+    if (b[6] & 0x40 and honor_df) or per < 8:
+        return 1, None, []
+    if b[6] & 0x40:
+        struct.pack_into("<H", b, 4, new_id)
+        b[6] &= 0xBF
+    more = bool(b[6] & 0x20)
+    struct.pack_into(">H", b, 2, hl + per)
+    b[6] |= 0x20
+    struct.pack_into("<H", b, 10, 0)
+    struct.pack_into("<H", b, 10, in_cksum(bytes(b[:hl])))
+    first = bytes(b[:hl + per])
+    opts = _copied_options(b)
+    qhl = 20 + len(opts)
+    frags = []
+    pos = per
+    payload = bytes(b[hl:]) + bytes(max(0, hl + total_data - n))
+    while pos < total_data:
+        size = min((mtu - qhl) // 8 * 8, total_data - pos)
+        q = bytearray(b[:20]) + opts + payload[pos:pos + size]
+        q[0] = (q[0] & 0xF0) | (qhl // 4)
+        fo = (be16(b, 6) + pos // 8) & 0xFFFF
+        if pos + size >= total_data and not more:
+            fo &= ~0x2000
+        struct.pack_into(">H", q, 6, fo)
+        struct.pack_into(">H", q, 2, qhl + size)
+        struct.pack_into("<H", q, 10, 0)
+        struct.pack_into("<H", q, 10, in_cksum(bytes(q[:qhl])))
+        frags.append(bytes(q))
+        pos += size
+    return 2, first, frags
