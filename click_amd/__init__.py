@@ -229,6 +229,37 @@ class Context:
         return port[:b.n], (problem[:b.n] if problem is not None else None), \
             (sums[:b.n] if sums is not None else None)
 
+    # -- IPFragmenter ------------------------------------------------------------
+    def ip_fragment(self, b, mtu, honor_df=True, new_id=None, arena=None, max_frags=0, port=None,
+                    first_len=None, frag_first=None):
+        """IPFragmenter over the batch.  arena: uint8 device tensor for the
+        appended fragments (None: size it with a first call -- the result's
+        `totals` says what the batch needs).  Returns a dict of device
+        tensors: port, first_len, frag_first, frag_off, frag_len, frag_src,
+        totals (int64[2]: fragments, arena bytes)."""
+        t = self._torch
+        dev = "cuda:%d" % self.device
+        port = self._out(b.n, t.uint8) if port is None else port
+        first_len = self._out(b.n, t.int32) if first_len is None else first_len
+        frag_first = self._out(b.n, t.int64) if frag_first is None else frag_first
+        totals = t.zeros(2, dtype=t.int64, device=dev)
+        fo = t.empty(max(max_frags, 1), dtype=t.int64, device=dev)
+        fl = t.empty(max(max_frags, 1), dtype=t.int32, device=dev)
+        fs = t.empty(max(max_frags, 1), dtype=t.int32, device=dev)
+        cfg = _abi.clk_frag_cfg()
+        cfg.mtu, cfg.honor_df = mtu, 1 if honor_df else 0
+        cfg.new_id = new_id.data_ptr() if new_id is not None else None
+        out = _abi.clk_frag_out()
+        out.arena = arena.data_ptr() if arena is not None else None
+        out.arena_bytes = arena.numel() if arena is not None else 0
+        out.frag_off, out.frag_len, out.frag_src = fo.data_ptr(), fl.data_ptr(), fs.data_ptr()
+        out.max_frags = max_frags
+        cb = b.c()
+        self._check(self.lib.clk_ip_fragment(self.h, ctypes.byref(cb), ctypes.byref(cfg), _ptr(port),
+                                             _ptr(first_len), _ptr(frag_first), ctypes.byref(out), _ptr(totals)))
+        return dict(port=port[:b.n], first_len=first_len[:b.n], frag_first=frag_first[:b.n], frag_off=fo,
+                    frag_len=fl, frag_src=fs, totals=totals)
+
     # -- utilities ---------------------------------------------------------------
     def count_codes(self, codes, ncounts=8, counts=None):
         if counts is None:

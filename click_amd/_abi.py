@@ -69,6 +69,25 @@ class clk_ip_out_cfg(ctypes.Structure):
     ]
 
 
+class clk_frag_cfg(ctypes.Structure):
+    _fields_ = [
+        ("mtu", ctypes.c_uint32),
+        ("honor_df", ctypes.c_int32),
+        ("new_id", ctypes.c_void_p),
+    ]
+
+
+class clk_frag_out(ctypes.Structure):
+    _fields_ = [
+        ("arena", ctypes.c_void_p),
+        ("arena_bytes", ctypes.c_uint64),
+        ("frag_off", ctypes.c_void_p),
+        ("frag_len", ctypes.c_void_p),
+        ("frag_src", ctypes.c_void_p),
+        ("max_frags", ctypes.c_uint64),
+    ]
+
+
 _P = ctypes.c_void_p
 _BP = ctypes.POINTER(clk_batch)
 _OP = ctypes.POINTER(clk_ip_out_cfg)
@@ -97,6 +116,8 @@ SIGNATURES = {
     "clk_ip_gw_options": (ctypes.c_int, [_P, _BP, _OP, _P, _P, _P]),
     "clk_fix_ip_src": (ctypes.c_int, [_P, _BP, _OP, _P, _P]),
     "clk_ip_output_combo": (ctypes.c_int, [_P, _BP, _OP, _P, _P, _P, _P]),
+    "clk_ip_fragment": (ctypes.c_int, [_P, _BP, ctypes.POINTER(clk_frag_cfg), _P, _P, _P,
+                                       ctypes.POINTER(clk_frag_out), _P]),
     "clk_count_codes": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P, ctypes.c_uint32]),
     "clk_gen_packets": (ctypes.c_int, [_P, _BP, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
     "clk_gen_corrupt": (ctypes.c_int, [_P, _BP, ctypes.c_uint64, ctypes.c_uint32]),

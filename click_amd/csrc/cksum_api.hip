@@ -2,6 +2,7 @@
 // kernels in cksum_kernels.hh.  Host side: argument checks, geometry
 // selection (lanes per packet), launches on the context's stream.
 #include "cksum_kernels.hh"
+#include "frag_kernels.hh"
 #include "../../include/click_amd_cksum.h"
 #include "internal.hh"
 
@@ -607,6 +608,56 @@ int clk_ip_output_combo(clk_ctx *ctx, const clk_batch *b, const clk_ip_out_cfg *
         return fail(ctx, CLK_EINVAL, "clk_ip_output_combo: null output");
     return launch_ip_out<clk::OUT_COMBO>(ctx, b, cfg, flags, out_port, out_problem, out_sum,
                                          "clk_ip_output_combo");
+}
+
+int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, uint8_t *out_port,
+                    uint32_t *out_first_len, uint64_t *out_frag_first, const clk_frag_out *out, uint64_t *totals)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, "clk_ip_fragment"))) return r;
+    if (!cfg || !out || !totals)
+        return fail(ctx, CLK_EINVAL, "clk_ip_fragment: null cfg, out or totals");
+    if (cfg->mtu < 8)
+        return fail(ctx, CLK_EINVAL, "clk_ip_fragment: MTU must be at least 8");   // ipfragmenter.cc:51-52
+    if ((out->max_frags && (!out->frag_off || !out->frag_len || !out->frag_src)) ||
+        (out->arena_bytes && !out->arena))
+        return fail(ctx, CLK_EINVAL, "clk_ip_fragment: null fragment buffers");
+    if (b->n >= (1ull << 32))
+        return fail(ctx, CLK_EINVAL, "clk_ip_fragment: batch too large");
+    hipError_t e;
+    if (b->n == 0) {
+        e = hipMemsetAsync(totals, 0, 2 * sizeof(uint64_t), ctx->cur);
+        return e == hipSuccess ? CLK_SUCCESS : hip_fail(ctx, e, "hipMemsetAsync");
+    }
+    if (!out_port || !out_first_len)
+        return fail(ctx, CLK_EINVAL, "clk_ip_fragment: null output");
+    const uint32_t ntiles = (uint32_t)((b->n + clk::FRAG_TILE - 1) / clk::FRAG_TILE);
+    // scratch: [nextra u32 x n][bytes u32 x n][tile sums u64 x 2 x ntiles][frag_first u64 x n if not given]
+    const size_t pl = (b->n * 4 + 255) & ~size_t(255);
+    const size_t ts_end = 2 * pl + (((size_t)ntiles * 16 + 255) & ~size_t(255));
+    if ((r = ensure_scratch(ctx, ts_end + (out_frag_first ? 0 : b->n * 8)))) return r;
+    uint8_t *sc = (uint8_t *)ctx->scratch;
+    uint32_t *pl_n = (uint32_t *)sc, *pl_b = (uint32_t *)(sc + pl);
+    uint64_t *tile_sums = (uint64_t *)(sc + 2 * pl);
+    uint64_t *ffirst = out_frag_first ? out_frag_first : (uint64_t *)(sc + ts_end);
+    clk::FragArgs f;
+    f.mtu = cfg->mtu;
+    f.honor_df = cfg->honor_df ? 1 : 0;
+    f.new_id = cfg->new_id;
+    f.arena = out->arena;
+    f.arena_bytes = out->arena ? out->arena_bytes : 0;
+    f.frag_off = out->frag_off;
+    f.frag_len = out->frag_len;
+    f.frag_src = out->frag_src;
+    f.max_frags = out->frag_off ? out->max_frags : 0;
+    hipLaunchKernelGGL(clk::frag_plan_kernel, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f, out_port,
+                       out_first_len, pl_n, pl_b, tile_sums);
+    hipLaunchKernelGGL(clk::frag_scan_kernel, dim3(1), dim3(1024), 0, ctx->cur, tile_sums, ntiles, totals);
+    hipLaunchKernelGGL(clk::frag_write_kernel, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f,
+                       (const uint8_t *)out_port, (const uint32_t *)pl_n, (const uint32_t *)pl_b,
+                       (const uint64_t *)tile_sums, ffirst);
+    return check_launch(ctx, "clk_ip_fragment");
 }
 
 int clk_count_codes(clk_ctx *ctx, const uint8_t *codes, uint64_t n, uint64_t *counts, uint32_t ncounts)

@@ -231,6 +231,46 @@ int clk_fix_ip_src(clk_ctx *ctx, const clk_batch *batch, const clk_ip_out_cfg *c
 int clk_ip_output_combo(clk_ctx *ctx, const clk_batch *batch, const clk_ip_out_cfg *cfg,
                         const uint8_t *flags, uint8_t *out_port, uint8_t *out_problem, uint16_t *out_sum);
 
+/* ---- IPFragmenter ------------------------------------------------------------
+ * IPFragmenter::push / fragment (elements/ip/ipfragmenter.cc:88-171) on a
+ * batch of packets at their IP headers (len_i = network_length()).
+ * cfg->mtu / honor_df: the MTU and HONOR_DF keywords.  cfg->new_id
+ * (nullable device u16 per packet): the ip_id written when HONOR_DF false
+ * clears a DF bit (the reference draws click_random(), 112-115; NULL keeps
+ * ip_id).
+ * out_port[i]: 0 = not longer than the MTU, untouched, output 0;
+ *              1 = DF with HONOR_DF, or the MTU leaves < 8 data bytes:
+ *                  untouched, output 1 (drops++);
+ *              2 = fragmented: packet i is rewritten IN PLACE as the first
+ *                  fragment (ip_len, IP_MF, DF/ip_id, ip_sum) and keeps its
+ *                  first out_first_len[i] bytes; its other fragments are
+ *                  appended to `out`.
+ * out_first_len[i]: packet i's length after the element.
+ * out_frag_first[i] (nullable): index of packet i's first appended fragment.
+ * Appended fragments are packed in packet order at 16 B-aligned offsets of
+ * out->arena; fragment k is out->frag_len[k] bytes at out->frag_off[k],
+ * cut from packet out->frag_src[k].  totals (device u64[2]) receives the
+ * fragments and arena bytes the batch needs; fragments beyond out->max_frags
+ * or out->arena_bytes are not written (compare after clk_ctx_sync).
+ * Domain guards (as the oracle): len_i < 20 with len_i > MTU -> port 1;
+ * fragment bytes past len_i (ip_len > network_length) are written as 0. */
+typedef struct clk_frag_cfg {
+    uint32_t mtu;
+    int32_t honor_df;
+    const uint16_t *new_id;
+} clk_frag_cfg;
+typedef struct clk_frag_out {
+    uint8_t *arena;
+    uint64_t arena_bytes;
+    uint64_t *frag_off;
+    uint32_t *frag_len;
+    uint32_t *frag_src;
+    uint64_t max_frags;
+} clk_frag_out;
+int clk_ip_fragment(clk_ctx *ctx, const clk_batch *batch, const clk_frag_cfg *cfg, uint8_t *out_port,
+                    uint32_t *out_first_len, uint64_t *out_frag_first, const clk_frag_out *out,
+                    uint64_t *totals);
+
 /* ---- batch utilities ------------------------------------------------------- */
 
 /* counts[c] += number of i with codes[i] == c, for c < ncounts (device u64). */

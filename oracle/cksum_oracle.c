@@ -566,12 +566,12 @@ static int frag_optcopy(const uint8_t *ip, uint8_t *oout)
  * packet becomes the first fragment in place, *first_len bytes from the IP
  * header; the others are appended at 16 B-aligned offsets of `arena`
  * starting at *arena_pos, descriptors at frag_off/frag_len[*nfrag ...]).
- * new_id replaces ip_id when DF is cleared (the reference uses
- * click_random(), 112-115).  Domain guards: caplen < 20 with caplen > MTU
+ * new_id (>= 0) replaces ip_id when DF is cleared (the reference uses
+ * click_random(), 112-115; -1 keeps ip_id).  Domain guards: caplen < 20 with caplen > MTU
  * -> port 1; fragment bytes past caplen (ip_len > network_length, which
  * CheckIPHeader excludes) are written as 0.  With arena == NULL only the
  * counts are produced. */
-int oracle_ip_fragment(uint8_t *ip, uint32_t caplen, uint32_t mtu, int honor_df, uint16_t new_id,
+int oracle_ip_fragment(uint8_t *ip, uint32_t caplen, uint32_t mtu, int honor_df, int new_id,
                        uint8_t *arena, uint64_t *arena_pos, uint64_t *frag_off, uint32_t *frag_len,
                        uint64_t *nfrag, uint32_t *first_len)
 {
@@ -586,7 +586,8 @@ int oracle_ip_fragment(uint8_t *ip, uint32_t caplen, uint32_t mtu, int honor_df,
     if (((ip[6] & 0x40) && honor_df) || first_dlen < 8)         /* 96-102: ip_off & htons(IP_DF) */
         return 1;
     if (ip[6] & 0x40) {                                         /* 112-115 */
-        st16(ip + 4, new_id);
+        if (new_id >= 0)
+            st16(ip + 4, (uint16_t)new_id);
         ip[6] &= (uint8_t)~0x40;
     }
     int had_mf = (ip[6] & 0x20) != 0;                           /* 116 */
@@ -630,7 +631,7 @@ int oracle_ip_fragment(uint8_t *ip, uint32_t caplen, uint32_t mtu, int honor_df,
 /* Batch form: packets in order; fragments appended in packet order.
  * out_port[i], out_first_len[i]; out_frag_first[i] = index of packet i's
  * first appended fragment; totals[0] = fragments, totals[1] = arena bytes.
- * new_id (nullable) per packet. */
+ * new_id (nullable: ip_id kept) per packet. */
 int oracle_ip_fragment_batch(uint8_t *base, const uint64_t *off, uint64_t stride, const uint32_t *len,
                              uint32_t fixed_len, uint64_t n, uint32_t mtu, int honor_df, const uint16_t *new_id,
                              uint8_t *out_port, uint32_t *out_first_len, uint64_t *out_frag_first,
@@ -642,7 +643,7 @@ int oracle_ip_fragment_batch(uint8_t *base, const uint64_t *off, uint64_t stride
         uint64_t before = nf;
         out_frag_first[i] = nf;
         out_port[i] = (uint8_t)oracle_ip_fragment(base + pkt_off(off, stride, i), pkt_len(len, fixed_len, i),
-                                                  mtu, honor_df, new_id ? new_id[i] : 0, arena, &pos,
+                                                  mtu, honor_df, new_id ? (int)new_id[i] : -1, arena, &pos,
                                                   frag_off, frag_len, &nf, &out_first_len[i]);
         if (arena && frag_src)
             for (uint64_t k = before; k < nf; k++)

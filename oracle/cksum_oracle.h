@@ -65,7 +65,7 @@ int oracle_ip_out_batch(int op, uint8_t *base, const uint64_t *off, uint64_t str
                         uint32_t ts, uint32_t mtu, uint8_t *out8, uint8_t *out_prob, uint16_t *out16);
 
 /* ---- IPFragmenter (elements/ip/ipfragmenter.cc:53-171) -------------------- */
-int oracle_ip_fragment(uint8_t *ip, uint32_t caplen, uint32_t mtu, int honor_df, uint16_t new_id,
+int oracle_ip_fragment(uint8_t *ip, uint32_t caplen, uint32_t mtu, int honor_df, int new_id,
                        uint8_t *arena, uint64_t *arena_pos, uint64_t *frag_off, uint32_t *frag_len,
                        uint64_t *nfrag, uint32_t *first_len);
 int oracle_ip_fragment_batch(uint8_t *base, const uint64_t *off, uint64_t stride, const uint32_t *len,

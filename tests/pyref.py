@@ -370,7 +370,7 @@ def _copied_options(h):
     return bytes(out)
 
 
-def ip_fragment(pkt, mtu, honor_df=False, new_id=0):
+def ip_fragment(pkt, mtu, honor_df=False, new_id=None):
     """Returns (port, first fragment bytes or None, [other fragments])."""
     n = len(pkt)
     if n <= mtu:
@@ -384,7 +384,8 @@ def ip_fragment(pkt, mtu, honor_df=False, new_id=0):
     if (b[6] & 0x40 and honor_df) or per < 8:
         return 1, None, []
     if b[6] & 0x40:
-        struct.pack_into("<H", b, 4, new_id)
+        if new_id is not None:
+            struct.pack_into("<H", b, 4, new_id)
         b[6] &= 0xBF
     more = bool(b[6] & 0x20)
     struct.pack_into(">H", b, 2, hl + per)
