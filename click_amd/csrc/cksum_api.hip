@@ -654,6 +654,8 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, u
     hipLaunchKernelGGL(clk::frag_plan_kernel, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f, out_port,
                        out_first_len, pl_n, pl_b, tile_sums);
     hipLaunchKernelGGL(clk::frag_scan_kernel, dim3(1), dim3(1024), 0, ctx->cur, tile_sums, ntiles, totals);
+    if (!out->arena)                         // sizing call: nothing is written
+        return check_launch(ctx, "clk_ip_fragment");
     hipLaunchKernelGGL(clk::frag_write_kernel, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f,
                        (const uint8_t *)out_port, (const uint32_t *)pl_n, (const uint32_t *)pl_b,
                        (const uint64_t *)tile_sums, ffirst);

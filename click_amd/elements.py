@@ -18,6 +18,12 @@ import numpy as np
 from . import _abi, ClickAmdError
 
 PORT_OUT0, PORT_OUT1, PORT_KILL = 0, 1, -1
+ANNO_FIX_IP_SRC, ANNO_BCAST = 0x1, 0x2       # CLK_ANNO_* (include/click_amd_elements.h)
+AUX_CLONE = 0x80000000
+
+
+def anno_paint(color):
+    return (color & 0xFF) << 8
 
 
 class Element:
@@ -43,11 +49,13 @@ class Element:
         except Exception:
             pass
 
-    def push(self, buf, length=None, nh_offset=-1, token=0):
-        """buf: a writable uint8 numpy array (or view) holding the packet."""
+    def push(self, buf, length=None, nh_offset=-1, token=0, anno=0):
+        """buf: a writable uint8 numpy array (or view) holding the packet;
+        anno: CLK_ANNO_* bits (FixIPSrc, IPOutputCombo)."""
         length = buf.size if length is None else length
         self._keep.append(buf)
-        rc = self.lib.clk_element_push(self.h, buf.ctypes.data_as(ctypes.c_void_p), length, nh_offset, token)
+        rc = self.lib.clk_element_push_anno(self.h, buf.ctypes.data_as(ctypes.c_void_p), length, nh_offset, anno,
+                                            token)
         if rc < 0:
             raise ClickAmdError("push failed: %d" % rc)
         return rc == 1
@@ -77,20 +85,32 @@ class Element:
             raise ClickAmdError("flush failed: %d" % rc)
         self._keep = []
 
-    def results(self, cap=1 << 20):
+    def results(self, cap=1 << 20, aux=False):
+        """(tokens, ports, lengths[, aux]) of every flushed packet, in order."""
         out = []
         while True:
             t = np.zeros(cap, np.uint64)
             p = np.zeros(cap, np.int32)
             ln = np.zeros(cap, np.uint32)
-            n = self.lib.clk_element_results(self.h, t.ctypes.data_as(ctypes.c_void_p),
-                                             p.ctypes.data_as(ctypes.c_void_p), ln.ctypes.data_as(ctypes.c_void_p),
-                                             cap)
-            out.append((t[:n], p[:n], ln[:n]))
+            ax = np.zeros(cap, np.uint32)
+            n = self.lib.clk_element_results_aux(self.h, t.ctypes.data_as(ctypes.c_void_p),
+                                                 p.ctypes.data_as(ctypes.c_void_p),
+                                                 ln.ctypes.data_as(ctypes.c_void_p),
+                                                 ax.ctypes.data_as(ctypes.c_void_p), cap)
+            out.append((t[:n], p[:n], ln[:n], ax[:n]))
             if n < cap:
                 break
-        return (np.concatenate([o[0] for o in out]), np.concatenate([o[1] for o in out]),
-                np.concatenate([o[2] for o in out]))
+        r = tuple(np.concatenate([o[k] for o in out]) for k in range(4))
+        return r if aux else r[:3]
+
+    def take_packet(self, key):
+        """Bytes of a new packet the element made (IPFragmenter fragments)."""
+        n = self.lib.clk_element_take_packet(self.h, key, None, 0)
+        if n < 0:
+            raise ClickAmdError("no packet %d" % key)
+        buf = ctypes.create_string_buffer(max(int(n), 1))
+        self.lib.clk_element_take_packet(self.h, key, buf, len(buf))     # copies and releases it
+        return buf.raw[:n]
 
     def read_handler(self, name):
         buf = ctypes.create_string_buffer(1 << 16)

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <new>
 
 namespace clk {
@@ -185,6 +186,10 @@ BatchElement::~BatchElement()
     if (d_len_) (void)hipFree(d_len_);
     if (d_codes_) (void)hipFree(d_codes_);
     if (d_sums_) (void)hipFree(d_sums_);
+    if (d_anno_) (void)hipFree(d_anno_);
+    if (d_aux8_) (void)hipFree(d_aux8_);
+    if (h_anno_) (void)hipHostFree(h_anno_);
+    if (h_aux8_) (void)hipHostFree(h_aux8_);
     for (void *e : ev_)
         if (e) (void)hipEventDestroy((hipEvent_t)e);
 }
@@ -230,9 +235,10 @@ int BatchElement::grow_host(size_t bytes, size_t n)
     if (host_grow(&h_arena_, &h_arena_cap_, bytes, h_used_))
         return -1;
     if (h_n_cap_ < n) {
-        size_t c1 = h_n_cap_, c2 = h_n_cap_, c3 = h_n_cap_, c4 = h_n_cap_;
+        size_t c1 = h_n_cap_, c2 = h_n_cap_, c3 = h_n_cap_, c4 = h_n_cap_, c5 = h_n_cap_, c6 = h_n_cap_;
         if (host_grow(&h_off_, &c1, n, 0) || host_grow(&h_len_, &c2, n, 0) ||
-            host_grow(&h_codes_, &c3, n, 0) || host_grow(&h_sums_, &c4, n, 0))
+            host_grow(&h_codes_, &c3, n, 0) || host_grow(&h_sums_, &c4, n, 0) ||
+            host_grow(&h_anno_, &c5, n, 0) || host_grow(&h_aux8_, &c6, n, 0))
             return -1;
         h_n_cap_ = c1;
     }
@@ -256,17 +262,20 @@ int BatchElement::grow_dev(size_t bytes, size_t n)
         if (d_len_) (void)hipFree(d_len_);
         if (d_codes_) (void)hipFree(d_codes_);
         if (d_sums_) (void)hipFree(d_sums_);
+        if (d_anno_) (void)hipFree(d_anno_);
+        if (d_aux8_) (void)hipFree(d_aux8_);
         if (hipMalloc(&d_off_, c * 8) != hipSuccess || hipMalloc(&d_len_, c * 4) != hipSuccess ||
-            hipMalloc(&d_codes_, c) != hipSuccess || hipMalloc(&d_sums_, c * 2) != hipSuccess)
+            hipMalloc(&d_codes_, c) != hipSuccess || hipMalloc(&d_sums_, c * 2) != hipSuccess ||
+            hipMalloc(&d_anno_, c) != hipSuccess || hipMalloc(&d_aux8_, c) != hipSuccess)
             return -1;
         d_n_cap_ = c;
     }
     return 0;
 }
 
-int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token)
+int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
 {
-    Pending p{data, length, nh_offset, token, -1, 0, 0, 0};
+    Pending p{data, length, nh_offset, token, -1, 0, 0, 0, anno, 0};
     uint32_t off = 0, len = 0;
     int32_t code = 0;
     if (!span(p, &off, &len, &code)) {
@@ -296,10 +305,12 @@ int BatchElement::flush()
     uint32_t maxlen = 0;
     if (grow_host(h_used_ + 64, pend_.size()))
         return CLK_EINVAL;
-    for (const Pending &p : pend_)
+    for (Pending &p : pend_)
         if (p.host_code < 0) {
             h_off_[n] = p.slot;
             h_len_[n] = p.span_len;
+            h_anno_[n] = (uint8_t)p.anno;
+            p.index = (uint32_t)n;
             maxlen = std::max(maxlen, p.span_len);
             n++;
         }
@@ -317,6 +328,8 @@ int BatchElement::flush()
         (void)hipMemcpyAsync(d_arena_, h_arena_, h_used_, hipMemcpyHostToDevice, s);
         (void)hipMemcpyAsync(d_off_, h_off_, n * 8, hipMemcpyHostToDevice, s);
         (void)hipMemcpyAsync(d_len_, h_len_, n * 4, hipMemcpyHostToDevice, s);
+        if (wants_anno())
+            (void)hipMemcpyAsync(d_anno_, h_anno_, n, hipMemcpyHostToDevice, s);
         clk_batch b;
         b.base = d_arena_;
         b.off = d_off_;
@@ -335,6 +348,10 @@ int BatchElement::flush()
         (void)hipMemcpyAsync(h_codes_, d_codes_, n, hipMemcpyDeviceToHost, s);
         if (wants_sums())
             (void)hipMemcpyAsync(h_sums_, d_sums_, n * 2, hipMemcpyDeviceToHost, s);
+        if (wants_arena_back()) {
+            (void)hipMemcpyAsync(h_arena_, d_arena_, h_used_, hipMemcpyDeviceToHost, s);
+            (void)hipMemcpyAsync(h_aux8_, d_aux8_, n, hipMemcpyDeviceToHost, s);
+        }
         hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) {
             err_ = hipGetErrorString(e);
@@ -353,9 +370,11 @@ int BatchElement::flush()
             sum = wants_sums() ? h_sums_[k] : 0;
             k++;
         }
-        Result r{p.token, 0, p.length};
+        Result r{p.token, 0, p.length, 0};
+        pre_route(p, results_);
         route(p, code, sum, &r);
         results_.push_back(r);
+        post_route(p, code, results_);
     }
     batches_++;
     packets_ += pend_.size();
@@ -365,7 +384,8 @@ int BatchElement::flush()
     return 0;
 }
 
-uint64_t BatchElement::pop_results(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint64_t cap)
+uint64_t BatchElement::pop_results(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint32_t *aux,
+                                   uint64_t cap)
 {
     uint64_t i = 0;
     while (i < cap && !results_.empty()) {
@@ -373,10 +393,38 @@ uint64_t BatchElement::pop_results(uint64_t *tokens, int32_t *ports, uint32_t *l
         if (tokens) tokens[i] = r.token;
         if (ports) ports[i] = r.port;
         if (lengths) lengths[i] = r.length;
+        if (aux) aux[i] = r.aux;
         results_.pop_front();
         i++;
     }
     return i;
+}
+
+void BatchElement::write_back(const Pending &p, uint32_t nbytes) const
+{
+    std::memcpy(p.data + p.span_off, h_arena_ + p.slot, std::min(nbytes, p.span_len));
+}
+
+uint32_t BatchElement::keep_packet(const uint8_t *bytes, uint32_t len)
+{
+    const uint32_t key = next_key_++;
+    if (next_key_ >= CLK_AUX_CLONE)
+        next_key_ = 1;
+    packets_kept_[key].assign(bytes, bytes + len);
+    return key;
+}
+
+int64_t BatchElement::take_packet(uint32_t key, uint8_t *buf, size_t cap)
+{
+    auto it = packets_kept_.find(key);
+    if (it == packets_kept_.end())
+        return -1;
+    const size_t len = it->second.size();
+    if (!buf)                                    // length query: kept
+        return (int64_t)len;
+    std::memcpy(buf, it->second.data(), std::min(cap, len));
+    packets_kept_.erase(it);
+    return (int64_t)len;
 }
 
 std::string BatchElement::read_handler(const std::string &h) const
@@ -897,6 +945,434 @@ std::string DecIPTTL::read_handler(const std::string &h) const
     return BatchElement::read_handler(h);
 }
 
+// ---- IP output path --------------------------------------------------------
+
+// Timestamp::now() as the TS option stores it: htonl(ms since midnight)
+// (ipgwoptions.cc:118-119, ipoutputcombo.cc:119-120).
+static uint32_t ts_now()
+{
+    timespec t;
+    clock_gettime(CLOCK_REALTIME, &t);
+    const uint32_t ms = (uint32_t)((t.tv_sec % 86400) * 1000 + t.tv_nsec / 1000000);
+    return ((ms & 0xFF) << 24) | ((ms & 0xFF00) << 8) | ((ms >> 8) & 0xFF00) | (ms >> 24);
+}
+
+// The IP header and the bytes an option walk reads past it (<= hlen + 3).
+template <typename P>
+static bool ip_span(const P &p, uint32_t *off, uint32_t *len)
+{
+    if (p.nh_off < 0 || (uint32_t)p.nh_off >= p.length)
+        return false;
+    *off = (uint32_t)p.nh_off;
+    *len = std::min<uint32_t>(p.length - *off, 64);
+    return true;
+}
+
+static std::string ip_text(const uint8_t *a)
+{
+    return std::to_string(a[0]) + "." + std::to_string(a[1]) + "." + std::to_string(a[2]) + "." + std::to_string(a[3]);
+}
+
+IPGWOptions::~IPGWOptions()
+{
+    if (d_addrs_)
+        (void)hipFree(d_addrs_);
+}
+
+int IPGWOptions::configure(ConfArgs &args, std::string *err)
+{
+    std::string v;                                      // read_mp MYADDR, read_p OTHERADDRS (40-44)
+    if (!args.take("MYADDR", &v)) {
+        if (args.pos.empty()) {
+            *err = "missing mandatory MYADDR argument";
+            return -1;
+        }
+        v = args.pos[0];
+        args.pos.erase(args.pos.begin());
+    }
+    if (!parse_ip(v, &my_ip_)) {
+        *err = "MYADDR: expected IP address";
+        return -1;
+    }
+    std::string o;
+    bool have = args.take("OTHERADDRS", &o);
+    if (!have && !args.pos.empty()) {
+        o = args.pos[0];
+        args.pos.erase(args.pos.begin());
+        have = true;
+    }
+    for (const std::string &w : words(have ? o : std::string())) {
+        uint32_t a;
+        if (!parse_ip(w, &a)) {
+            *err = "OTHERADDRS: expected list of IP addresses";
+            return -1;
+        }
+        addrs_.push_back(a);
+    }
+    addrs_.push_back(my_ip_);                           // 46
+    if (!args.pos.empty()) {
+        *err = "too many arguments";
+        return -1;
+    }
+    if (hipMalloc(&d_addrs_, addrs_.size() * 4) != hipSuccess ||
+        hipMemcpy(d_addrs_, addrs_.data(), addrs_.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        *err = "out of device memory";
+        return -1;
+    }
+    return BatchElement::configure(args, err);
+}
+
+bool IPGWOptions::span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const
+{
+    // ip_hl <= 5: returned untouched without a copy (simple_action, 167-169)
+    if (!ip_span(p, off, len) || *len < 20 || (p.data[*off] & 0xF) <= 5) {
+        *code = CLK_GWOPT_OK;
+        return false;
+    }
+    return true;
+}
+
+int IPGWOptions::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
+{
+    clk_ip_out_cfg cfg{my_ip_, ts_now(), d_addrs_, (uint32_t)addrs_.size(), 0xFFFFFFFFu};
+    return clk_ip_gw_options(ctx_, b, &cfg, d_codes, d_aux8_, nullptr);
+}
+
+void IPGWOptions::route(Pending &p, int code, uint16_t, Result *r)
+{
+    if (p.host_code >= 0) {
+        r->port = 0;
+        return;
+    }
+    write_back(p, p.span_len);                           // options / ip_sum rewritten in place
+    if (code == CLK_GWOPT_ERROR) {                       // send_error, 161-165
+        drops_++;
+        r->aux = h_aux8_[p.index];                       // SET_ICMP_PARAMPROB_ANNO
+        r->port = noutputs_ >= 2 ? 1 : -1;
+        return;
+    }
+    r->port = 0;
+}
+
+std::string IPGWOptions::read_handler(const std::string &h) const
+{
+    if (h == "drops")
+        return std::to_string(drops_);
+    return BatchElement::read_handler(h);
+}
+
+int FixIPSrc::configure(ConfArgs &args, std::string *err)
+{
+    std::string v;                                      // read_mp IPADDR (45)
+    if (!args.take("IPADDR", &v)) {
+        if (args.pos.empty()) {
+            *err = "missing mandatory IPADDR argument";
+            return -1;
+        }
+        v = args.pos[0];
+        args.pos.erase(args.pos.begin());
+    }
+    if (!parse_ip(v, &my_ip_)) {
+        *err = "IPADDR: expected IP address";
+        return -1;
+    }
+    if (!args.pos.empty()) {
+        *err = "too many arguments";
+        return -1;
+    }
+    return BatchElement::configure(args, err);
+}
+
+bool FixIPSrc::span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const
+{
+    // only FIX_IP_SRC_ANNO packets with a network header (simple_action, 69-73)
+    if (!(p.anno & CLK_ANNO_FIX_IP_SRC) || !ip_span(p, off, len)) {
+        *code = 0;
+        return false;
+    }
+    return true;
+}
+
+int FixIPSrc::run(const clk_batch *b, uint8_t *, uint16_t *)
+{
+    clk_ip_out_cfg cfg{my_ip_, 0, nullptr, 0, 0xFFFFFFFFu};
+    return clk_fix_ip_src(ctx_, b, &cfg, nullptr, nullptr);     // every staged packet has the annotation
+}
+
+void FixIPSrc::route(Pending &p, int, uint16_t, Result *r)
+{
+    if (p.host_code < 0)
+        write_back(p, p.span_len);
+    r->port = 0;
+}
+
+int IPOutputCombo::configure(ConfArgs &args, std::string *err)
+{
+    // read_mp COLOR, IPADDR, MTU (ipoutputcombo.cc:37-40)
+    const char *keys[3] = {"COLOR", "IPADDR", "MTU"};
+    std::string v[3];
+    for (int k = 0; k < 3; k++) {
+        if (!args.take(keys[k], &v[k])) {
+            if (args.pos.empty()) {
+                *err = std::string("missing mandatory ") + keys[k] + " argument";
+                return -1;
+            }
+            v[k] = args.pos[0];
+            args.pos.erase(args.pos.begin());
+        }
+    }
+    long mtu;
+    if (!parse_int(v[0], &color_)) {
+        *err = "COLOR: expected integer";
+        return -1;
+    }
+    if (!parse_ip(v[1], &my_ip_)) {
+        *err = "IPADDR: expected IP address";
+        return -1;
+    }
+    if (!parse_int(v[2], &mtu) || mtu < 0 || mtu > 0xFFFFFFFFL) {
+        *err = "MTU: expected unsigned integer";
+        return -1;
+    }
+    mtu_ = (uint32_t)mtu;
+    if (!args.pos.empty()) {
+        *err = "too many arguments";
+        return -1;
+    }
+    return BatchElement::configure(args, err);
+}
+
+bool IPOutputCombo::span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const
+{
+    if (p.anno & CLK_ANNO_BCAST) {                      // DropBroadcasts, 50-53
+        *code = 255;
+        return false;
+    }
+    if (!ip_span(p, off, len)) {                        // the reference asserts a network header (61)
+        *code = 0;
+        return false;
+    }
+    return true;
+}
+
+int IPOutputCombo::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
+{
+    // the staged span is the header only: the MTU test is the host's (194)
+    clk_ip_out_cfg cfg{my_ip_, ts_now(), nullptr, 0, 0xFFFFFFFFu};
+    return clk_ip_output_combo(ctx_, b, &cfg, d_anno_, d_codes, d_aux8_, nullptr);
+}
+
+void IPOutputCombo::pre_route(Pending &p, std::deque<Result> &out)
+{
+    // PaintTee: a clone of the packet as it arrived goes to output 1 first (56-57)
+    if (!(p.anno & CLK_ANNO_BCAST) && (long)((p.anno >> 8) & 0xFF) == color_)
+        out.push_back(Result{p.token, noutputs_ >= 2 ? 1 : -1, p.length, CLK_AUX_CLONE});
+}
+
+void IPOutputCombo::route(Pending &p, int code, uint16_t, Result *r)
+{
+    if (code == 255) {
+        r->port = -1;
+        return;
+    }
+    auto out = [&](int port) { return noutputs_ > port ? port : -1; };   // unconnected: killed
+    if (p.host_code >= 0) {
+        r->port = out(p.length > mtu_ ? 4 : 0);
+        return;
+    }
+    write_back(p, p.span_len);
+    if (code == 2)
+        r->aux = h_aux8_[p.index];
+    r->port = out(code == 0 && p.length > mtu_ ? 4 : code);
+}
+
+std::string IPOutputCombo::read_handler(const std::string &h) const
+{
+    if (h == "color")
+        return std::to_string(color_);
+    return BatchElement::read_handler(h);
+}
+
+// ---- IPFragmenter (elements/ip/ipfragmenter.cc) -----------------------------
+
+IPFragmenter::~IPFragmenter()
+{
+    for (void *q : {(void *)d_frag_, (void *)d_foff_, (void *)d_flen_, (void *)d_fsrc_, (void *)d_first_,
+                    (void *)d_ffirst_, (void *)d_totals_, (void *)d_newid_})
+        if (q)
+            (void)hipFree(q);
+}
+
+int IPFragmenter::configure(ConfArgs &args, std::string *err)
+{
+    std::string v;                                      // 44-53
+    if (!args.take("MTU", &v)) {
+        if (args.pos.empty()) {
+            *err = "missing mandatory MTU argument";
+            return -1;
+        }
+        v = args.pos[0];
+        args.pos.erase(args.pos.begin());
+    }
+    long mtu;
+    if (!parse_int(v, &mtu) || mtu < 0 || mtu > 0xFFFFFFFFL) {
+        *err = "MTU: expected unsigned integer";
+        return -1;
+    }
+    mtu_ = (uint32_t)mtu;
+    const char *opt[2] = {"HONOR_DF", "VERBOSE"};
+    bool *dst[2] = {&honor_df_, &verbose_};
+    for (int k = 0; k < 2; k++) {
+        bool have = args.take(opt[k], &v);
+        if (!have && !args.pos.empty()) {
+            v = args.pos[0];
+            args.pos.erase(args.pos.begin());
+            have = true;
+        }
+        if (have && !parse_bool(v, dst[k])) {
+            *err = std::string(opt[k]) + ": expected boolean";
+            return -1;
+        }
+    }
+    if (args.take("HEADROOM", &v) && (!parse_int(v, &mtu) || mtu < 0)) {   // Packet::make headroom: host side
+        *err = "HEADROOM: expected unsigned integer";
+        return -1;
+    }
+    if (!args.pos.empty()) {
+        *err = "too many arguments";
+        return -1;
+    }
+    if (mtu_ < 8) {                                     // 51-52
+        *err = "MTU must be at least 8";
+        return -1;
+    }
+    return BatchElement::configure(args, err);
+}
+
+bool IPFragmenter::span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const
+{
+    // push(): network_length() <= MTU goes out untouched (165-171)
+    const uint32_t nh = p.nh_off >= 0 ? (uint32_t)p.nh_off : 0u;
+    if (nh > p.length || (int)(p.length - nh) <= (int)mtu_) {
+        *code = 0;
+        return false;
+    }
+    *off = nh;
+    *len = p.length - nh;
+    return true;
+}
+
+template <typename T>
+static int dev_grow(T **p, uint64_t *cap, uint64_t need)
+{
+    if (*cap >= need)
+        return 0;
+    if (*p)
+        (void)hipFree(*p);
+    *p = nullptr;
+    const uint64_t c = std::max<uint64_t>(need, *cap * 2);
+    if (hipMalloc(p, c * sizeof(T)) != hipSuccess)
+        return -1;
+    *cap = c;
+    return 0;
+}
+
+int IPFragmenter::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
+{
+    hipStream_t s = (hipStream_t)clk_ctx_stream(ctx_);
+    uint64_t pc = d_npkt_cap_, pc2 = d_npkt_cap_, pc3 = d_npkt_cap_;
+    if (dev_grow(&d_first_, &pc, b->n) || dev_grow(&d_ffirst_, &pc2, b->n) || dev_grow(&d_newid_, &pc3, b->n))
+        return CLK_EHIP;
+    d_npkt_cap_ = pc;
+    if (!d_totals_ && hipMalloc(&d_totals_, 16) != hipSuccess)
+        return CLK_EHIP;
+    const uint16_t *nid = nullptr;
+    if (!honor_df_) {                                   // click_random() for cleared DF bits (112-115)
+        h_newid_.resize(b->n);
+        for (auto &x : h_newid_)
+            x = (uint16_t)std::rand();
+        (void)hipMemcpyAsync(d_newid_, h_newid_.data(), b->n * 2, hipMemcpyHostToDevice, s);
+        nid = d_newid_;
+    }
+    clk_frag_cfg cfg{mtu_, honor_df_ ? 1 : 0, nid};
+    clk_frag_out sizing{nullptr, 0, nullptr, nullptr, nullptr, 0};
+    int r = clk_ip_fragment(ctx_, b, &cfg, d_codes, d_first_, nullptr, &sizing, d_totals_);
+    if (r)
+        return r;
+    uint64_t tot[2];
+    if (hipMemcpyAsync(tot, d_totals_, 16, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipStreamSynchronize(s) != hipSuccess)
+        return CLK_EHIP;
+    uint64_t fc = d_nfrag_cap_, fc2 = d_nfrag_cap_, fc3 = d_nfrag_cap_;
+    if (dev_grow(&d_frag_, &d_frag_cap_, std::max<uint64_t>(tot[1], 16)) ||
+        dev_grow(&d_foff_, &fc, std::max<uint64_t>(tot[0], 1)) || dev_grow(&d_flen_, &fc2, std::max<uint64_t>(tot[0], 1)) ||
+        dev_grow(&d_fsrc_, &fc3, std::max<uint64_t>(tot[0], 1)))
+        return CLK_EHIP;
+    d_nfrag_cap_ = fc;
+    clk_frag_out out{d_frag_, d_frag_cap_, d_foff_, d_flen_, d_fsrc_, d_nfrag_cap_};
+    if ((r = clk_ip_fragment(ctx_, b, &cfg, d_codes, d_first_, d_ffirst_, &out, d_totals_)))
+        return r;
+    nfrag_ = tot[0];
+    h_frag_.resize(tot[1]);
+    h_foff_.resize(tot[0]);
+    h_flen_.resize(tot[0]);
+    h_first_.resize(b->n);
+    h_ffirst_.resize(b->n);
+    (void)hipMemcpyAsync(h_frag_.data(), d_frag_, tot[1], hipMemcpyDeviceToHost, s);
+    (void)hipMemcpyAsync(h_foff_.data(), d_foff_, tot[0] * 8, hipMemcpyDeviceToHost, s);
+    (void)hipMemcpyAsync(h_flen_.data(), d_flen_, tot[0] * 4, hipMemcpyDeviceToHost, s);
+    (void)hipMemcpyAsync(h_first_.data(), d_first_, b->n * 4, hipMemcpyDeviceToHost, s);
+    (void)hipMemcpyAsync(h_ffirst_.data(), d_ffirst_, b->n * 8, hipMemcpyDeviceToHost, s);
+    return CLK_SUCCESS;                                  // flush() synchronizes
+}
+
+void IPFragmenter::route(Pending &p, int code, uint16_t, Result *r)
+{
+    if (p.host_code >= 0 || code == 0) {
+        r->port = 0;
+        return;
+    }
+    if (code == 1) {                                     // DF / too small (96-102)
+        if (verbose_ || drops_ < 5) {
+            const uint8_t *ip = p.data + p.span_off;
+            chatter("IPFragmenter(" + std::to_string(mtu_) + ") DF " + ip_text(ip + 12) + " " + ip_text(ip + 16) +
+                    " len=" + std::to_string(p.length));
+        }
+        drops_++;
+        r->port = noutputs_ >= 2 ? 1 : -1;
+        return;
+    }
+    // the first fragment: rewritten header, truncated (117-123)
+    const uint32_t first = h_first_[p.index];
+    const uint32_t hl = (uint32_t)(p.data[p.span_off] & 0xF) << 2;
+    write_back(p, hl);
+    r->length = p.span_off + first;
+    r->port = 0;
+    fragments_++;
+}
+
+void IPFragmenter::post_route(Pending &p, int code, std::deque<Result> &out)
+{
+    if (p.host_code >= 0 || code != 2)
+        return;
+    const uint64_t k0 = h_ffirst_[p.index];
+    const uint64_t k1 = p.index + 1 < (uint32_t)h_first_.size() ? h_ffirst_[p.index + 1] : nfrag_;
+    for (uint64_t k = k0; k < k1 && k < nfrag_; k++) {   // 129-159: the other fragments, in order
+        const uint32_t key = keep_packet(h_frag_.data() + h_foff_[k], h_flen_[k]);
+        out.push_back(Result{p.token, 0, h_flen_[k], key});
+        fragments_++;
+    }
+}
+
+std::string IPFragmenter::read_handler(const std::string &h) const
+{
+    if (h == "drops")
+        return std::to_string(drops_);
+    if (h == "fragments")
+        return std::to_string(fragments_);
+    return BatchElement::read_handler(h);
+}
+
 BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::string &name, int noutputs)
 {
     if (cls == "CheckICMPHeader")
@@ -919,6 +1395,14 @@ BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::stri
         return new (std::nothrow) SetL4Checksum(ctx, name, noutputs, 17);
     if (cls == "SetTCPChecksum")
         return new (std::nothrow) SetL4Checksum(ctx, name, noutputs, 6);
+    if (cls == "IPGWOptions")
+        return new (std::nothrow) IPGWOptions(ctx, name, noutputs);
+    if (cls == "FixIPSrc")
+        return new (std::nothrow) FixIPSrc(ctx, name, noutputs);
+    if (cls == "IPOutputCombo")
+        return new (std::nothrow) IPOutputCombo(ctx, name, noutputs);
+    if (cls == "IPFragmenter")
+        return new (std::nothrow) IPFragmenter(ctx, name, noutputs);
     return nullptr;
 }
 
@@ -936,7 +1420,7 @@ extern "C" {
 int clk_element_create(clk_ctx *ctx, const char *class_name, const char *config, const char *name,
                        int noutputs, clk_element **out)
 {
-    if (!ctx || !class_name || !out || (noutputs != 1 && noutputs != 2))
+    if (!ctx || !class_name || !out || noutputs < 1 || noutputs > 5)
         return CLK_EINVAL;
     *out = nullptr;
     std::string nm = name ? name : class_name;
@@ -977,6 +1461,14 @@ int clk_element_push(clk_element *w, uint8_t *data, uint32_t length, int32_t nh_
     return w->e->push(data, length, nh_offset, token);
 }
 
+int clk_element_push_anno(clk_element *w, uint8_t *data, uint32_t length, int32_t nh_offset, uint32_t anno,
+                          uint64_t token)
+{
+    if (!w || (!data && length))
+        return CLK_EINVAL;
+    return w->e->push(data, length, nh_offset, token, anno);
+}
+
 int clk_element_push_burst(clk_element *w, uint8_t *const *datas, const uint32_t *lengths,
                            const int32_t *nh_offsets, uint64_t first_token, uint32_t n)
 {
@@ -1003,7 +1495,22 @@ uint64_t clk_element_results(clk_element *w, uint64_t *tokens, int32_t *ports, u
 {
     if (!w)
         return 0;
-    return w->e->pop_results(tokens, ports, lengths, cap);
+    return w->e->pop_results(tokens, ports, lengths, nullptr, cap);
+}
+
+uint64_t clk_element_results_aux(clk_element *w, uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint32_t *aux,
+                                 uint64_t cap)
+{
+    if (!w)
+        return 0;
+    return w->e->pop_results(tokens, ports, lengths, aux, cap);
+}
+
+int64_t clk_element_take_packet(clk_element *w, uint32_t key, uint8_t *buf, size_t cap)
+{
+    if (!w)
+        return CLK_EINVAL;
+    return w->e->take_packet(key, buf, cap);
 }
 
 static int copy_out(const std::string &s, char *buf, size_t cap)

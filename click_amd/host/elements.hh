@@ -7,6 +7,7 @@
 #pragma once
 #include <cstdint>
 #include <deque>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -17,8 +18,9 @@ namespace host {
 
 struct Result {
     uint64_t token;
-    int32_t port;        // 0, 1, or -1 (kill)
+    int32_t port;        // 0..4, or -1 (kill)
     uint32_t length;     // packet length after the element
+    uint32_t aux;        // clk_element_results_aux (problem offset, clone flag, new-packet key)
 };
 
 // Click-style configuration: comma-separated arguments, "KEYWORD value".
@@ -39,9 +41,10 @@ class BatchElement {
     virtual ~BatchElement();
     virtual const char *class_name() const = 0;
     virtual int configure(ConfArgs &args, std::string *err);
-    int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token);
+    int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno = 0);
     int flush();
-    uint64_t pop_results(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint64_t cap);
+    uint64_t pop_results(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap);
+    int64_t take_packet(uint32_t key, uint8_t *buf, size_t cap);
     virtual std::string read_handler(const std::string &h) const;
     std::string take_messages();
     const std::string &name() const { return name_; }
@@ -59,6 +62,8 @@ class BatchElement {
         uint64_t slot;       // staging offset of the span
         uint32_t span_off;   // span start relative to data
         uint32_t span_len;
+        uint32_t anno;       // CLK_ANNO_* bits
+        uint32_t index;      // position in the GPU batch (staged packets)
     };
     // Bytes the kernel needs, relative to data; return false to decide on the
     // host with *code (routed like a kernel result).
@@ -66,6 +71,19 @@ class BatchElement {
     virtual int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) = 0;
     virtual void route(Pending &p, int code, uint16_t sum, Result *r) = 0;
     virtual bool wants_sums() const { return false; }
+    // copy the device batch back into the staging arena after run() (the
+    // kernel rewrote bytes route() writes back into the packet)
+    virtual bool wants_arena_back() const { return false; }
+    // upload anno & 0xFF of the staged packets; run() finds it in d_anno_
+    virtual bool wants_anno() const { return false; }
+    // called by flush() before route(): results() of the packet that precede
+    // its own (IPOutputCombo's clone)
+    virtual void pre_route(Pending &, std::deque<Result> &) {}
+    // called after route(): results that follow the packet's own (fragments)
+    virtual void post_route(Pending &, int, std::deque<Result> &) {}
+    const uint8_t *staged(const Pending &p) const { return h_arena_ + p.slot; }
+    void write_back(const Pending &p, uint32_t nbytes) const;   // staged span -> packet
+    uint32_t keep_packet(const uint8_t *bytes, uint32_t len);   // new packet, returns its key
     void chatter(const std::string &s) { msgs_.push_back(s); }
     static uint32_t be16(const uint8_t *p) { return (uint32_t(p[0]) << 8) | p[1]; }
 
@@ -75,6 +93,9 @@ class BatchElement {
     uint32_t batch_cap_ = 65536;
     std::string err_;
     uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0;
+    uint8_t *d_anno_ = nullptr;      // per staged packet (wants_anno)
+    uint8_t *d_aux8_ = nullptr;      // per staged packet, element use (problem offsets)
+    uint8_t *h_aux8_ = nullptr;
 
   private:
     int grow_host(size_t bytes, size_t n);
@@ -82,6 +103,9 @@ class BatchElement {
     std::vector<Pending> pend_;
     std::deque<Result> results_;
     std::vector<std::string> msgs_;
+    std::map<uint32_t, std::vector<uint8_t>> packets_kept_;
+    uint32_t next_key_ = 1;
+    uint8_t *h_anno_ = nullptr;
     uint8_t *h_arena_ = nullptr;
     size_t h_arena_cap_ = 0, h_used_ = 0;
     uint64_t *h_off_ = nullptr;
@@ -237,6 +261,106 @@ class DecIPTTL : public BatchElement {
   private:
     bool active_ = true, multicast_ = true;
     uint32_t drops_ = 0;
+};
+
+// IPGWOptions (elements/ip/ipgwoptions.cc): MYADDR, [OTHERADDRS]; parameter
+// problems to output 1 (or killed) with the offset as aux; handler drops.
+class IPGWOptions : public BatchElement {
+  public:
+    using BatchElement::BatchElement;
+    ~IPGWOptions() override;
+    const char *class_name() const override { return "IPGWOptions"; }
+    int configure(ConfArgs &args, std::string *err) override;
+    std::string read_handler(const std::string &h) const override;
+
+  protected:
+    bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
+    int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
+    void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    bool wants_arena_back() const override { return true; }
+
+  private:
+    uint32_t my_ip_ = 0;
+    std::vector<uint32_t> addrs_;        // OTHERADDRS + MYADDR (ipgwoptions.cc:46)
+    uint32_t *d_addrs_ = nullptr;
+    uint32_t drops_ = 0;
+};
+
+// FixIPSrc (elements/ip/fixipsrc.cc): IPADDR; rewrites ip_src and ip_sum of
+// packets pushed with CLK_ANNO_FIX_IP_SRC.
+class FixIPSrc : public BatchElement {
+  public:
+    using BatchElement::BatchElement;
+    const char *class_name() const override { return "FixIPSrc"; }
+    int configure(ConfArgs &args, std::string *err) override;
+
+  protected:
+    bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
+    int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
+    void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    bool wants_arena_back() const override { return true; }
+
+  private:
+    uint32_t my_ip_ = 0;
+};
+
+// IPOutputCombo (elements/ip/ipoutputcombo.cc): COLOR, IPADDR, MTU; five
+// outputs.
+class IPOutputCombo : public BatchElement {
+  public:
+    using BatchElement::BatchElement;
+    const char *class_name() const override { return "IPOutputCombo"; }
+    int configure(ConfArgs &args, std::string *err) override;
+    std::string read_handler(const std::string &h) const override;
+
+  protected:
+    bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
+    int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
+    void pre_route(Pending &p, std::deque<Result> &out) override;
+    void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    bool wants_arena_back() const override { return true; }
+    bool wants_anno() const override { return true; }
+
+  private:
+    long color_ = 0;
+    uint32_t my_ip_ = 0, mtu_ = 0;
+};
+
+// IPFragmenter (elements/ip/ipfragmenter.cc): MTU, [HONOR_DF], [VERBOSE],
+// HEADROOM; handlers drops, fragments.
+class IPFragmenter : public BatchElement {
+  public:
+    using BatchElement::BatchElement;
+    ~IPFragmenter() override;
+    const char *class_name() const override { return "IPFragmenter"; }
+    int configure(ConfArgs &args, std::string *err) override;
+    std::string read_handler(const std::string &h) const override;
+
+  protected:
+    bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
+    int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
+    void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    void post_route(Pending &p, int code, std::deque<Result> &out) override;
+    bool wants_arena_back() const override { return true; }
+
+  private:
+    uint32_t mtu_ = 0;
+    bool honor_df_ = true, verbose_ = false;
+    uint32_t drops_ = 0;
+    uint64_t fragments_ = 0;
+    // device / host fragment buffers of the last flush
+    uint8_t *d_frag_ = nullptr;
+    uint64_t d_frag_cap_ = 0;
+    uint64_t *d_foff_ = nullptr;
+    uint32_t *d_flen_ = nullptr, *d_fsrc_ = nullptr, *d_first_ = nullptr;
+    uint64_t *d_ffirst_ = nullptr, *d_totals_ = nullptr;
+    uint16_t *d_newid_ = nullptr;
+    uint64_t d_nfrag_cap_ = 0, d_npkt_cap_ = 0;
+    std::vector<uint8_t> h_frag_;
+    std::vector<uint64_t> h_foff_, h_ffirst_;
+    std::vector<uint32_t> h_flen_, h_first_;
+    std::vector<uint16_t> h_newid_;
+    uint64_t nfrag_ = 0;
 };
 
 BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::string &name, int noutputs);

@@ -247,6 +247,8 @@ int clk_ip_output_combo(clk_ctx *ctx, const clk_batch *batch, const clk_ip_out_c
  *                  appended to `out`.
  * out_first_len[i]: packet i's length after the element.
  * out_frag_first[i] (nullable): index of packet i's first appended fragment.
+ * out->arena == NULL makes a sizing call: out_port, out_first_len and totals
+ * are produced and nothing is written (packets untouched).
  * Appended fragments are packed in packet order at 16 B-aligned offsets of
  * out->arena; fragment k is out->frag_len[k] bytes at out->frag_off[k],
  * cut from packet out->frag_src[k].  totals (device u64[2]) receives the

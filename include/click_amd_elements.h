@@ -34,7 +34,23 @@
  *                   OFFSET 14, bad packets killed; the result length is the
  *                   length after Strip(14) and the ip_len trim, and the
  *                   adapter paints COLOR ("color" handler) and pulls 14 bytes
+ *   IPGWOptions     MYADDR, [OTHERADDRS] (elements/ip/ipgwoptions.cc:38-48);
+ *                   handler drops; parameter problems to output 1 (aux =
+ *                   ICMP_PARAMPROB_ANNO)
+ *   FixIPSrc        IPADDR             (elements/ip/fixipsrc.cc:40-49); acts
+ *                   on packets pushed with CLK_ANNO_FIX_IP_SRC (the adapter
+ *                   clears that annotation)
+ *   IPOutputCombo   COLOR, IPADDR, MTU (elements/ip/ipoutputcombo.cc:34-41);
+ *                   ports 0-4: broadcast/multicast killed, a painted clone to
+ *                   1 (aux CLK_AUX_CLONE), parameter problems to 2 (aux =
+ *                   offset), expired TTL to 3, longer than MTU to 4
+ *   IPFragmenter    MTU, [HONOR_DF], [VERBOSE], HEADROOM
+ *                   (elements/ip/ipfragmenter.cc:41-55); handlers drops,
+ *                   fragments; each fragment beyond the first is a new
+ *                   packet (aux = its key for clk_element_take_packet)
  * plus glue keywords BATCH (packets per GPU batch, default 65536).
+ * Elements that rewrite header bytes (IPGWOptions, FixIPSrc, IPOutputCombo,
+ * IPFragmenter) write them back into `data` at flush().
  */
 #ifndef CLICK_AMD_ELEMENTS_H
 #define CLICK_AMD_ELEMENTS_H
@@ -51,11 +67,14 @@ typedef struct clk_element clk_element;
 enum clk_port {
     CLK_PORT_OUT0 = 0,        /* output(0).push(p)                          */
     CLK_PORT_OUT1 = 1,        /* output(1).push(p) (drop port / SetUDP short) */
+    CLK_PORT_OUT2 = 2,        /* IPOutputCombo: parameter problem           */
+    CLK_PORT_OUT3 = 3,        /* IPOutputCombo: TTL expired                 */
+    CLK_PORT_OUT4 = 4,        /* IPOutputCombo: longer than the MTU         */
     CLK_PORT_KILL = -1        /* p->kill()                                   */
 };
 
 /* name: the element's name in messages (Click's name(); NULL = class name);
- * noutputs: 1 or 2 (whether output 1 is connected).
+ * noutputs: how many outputs are connected (1 or 2; IPOutputCombo 5).
  * Returns CLK_EINVAL with clk_last_error(ctx) set on a configure error,
  * worded like the reference's ErrorHandler messages.                      */
 int clk_element_create(clk_ctx *ctx, const char *class_name, const char *config,
@@ -78,6 +97,15 @@ int clk_element_push(clk_element *e, uint8_t *data, uint32_t length, int32_t nh_
 int clk_element_push_burst(clk_element *e, uint8_t *const *datas, const uint32_t *lengths,
                            const int32_t *nh_offsets, uint64_t first_token, uint32_t n);
 
+/* Packet annotations the output-path elements read (push_anno's `anno`). */
+#define CLK_ANNO_FIX_IP_SRC 0x1u       /* FIX_IP_SRC_ANNO (packet_anno.hh)           */
+#define CLK_ANNO_BCAST 0x2u            /* packet_type_anno() BROADCAST or MULTICAST  */
+#define CLK_ANNO_PAINT(c) (((uint32_t)(c) & 0xFFu) << 8)   /* PAINT_ANNO            */
+
+/* clk_element_push with the packet's annotations (CLK_ANNO_*). */
+int clk_element_push_anno(clk_element *e, uint8_t *data, uint32_t length, int32_t nh_offset,
+                          uint32_t anno, uint64_t token);
+
 /* Run the staged batch on the GPU and route it (synchronous).  Results are
  * appended to the element's result queue in push order.                  */
 int clk_element_flush(clk_element *e);
@@ -87,6 +115,22 @@ int clk_element_flush(clk_element *e);
  * otherwise unchanged).  Returns the number popped.                        */
 uint64_t clk_element_results(clk_element *e, uint64_t *tokens, int32_t *ports,
                              uint32_t *lengths, uint64_t cap);
+
+/* clk_element_results plus a per-result auxiliary word: the
+ * ICMP_PARAMPROB_ANNO offset of a parameter problem (IPGWOptions port 1,
+ * IPOutputCombo port 2), CLK_AUX_CLONE for IPOutputCombo's painted clone
+ * (a clone of the packet as pushed, before any rewrite), or for
+ * IPFragmenter the key of a new fragment packet (0 = the pushed packet
+ * itself, now the first fragment).                                         */
+#define CLK_AUX_CLONE 0x80000000u
+uint64_t clk_element_results_aux(clk_element *e, uint64_t *tokens, int32_t *ports,
+                                 uint32_t *lengths, uint32_t *aux, uint64_t cap);
+
+/* Copy out (and release) new packet `key` an element made (IPFragmenter's
+ * fragments after the first): its bytes start at the IP header.  Returns
+ * the packet length, or < 0 for an unknown key; copies min(len, cap).
+ * buf == NULL only queries the length (the packet is kept).               */
+int64_t clk_element_take_packet(clk_element *e, uint32_t key, uint8_t *buf, size_t cap);
 
 /* Handler text, as Click's read handlers print it ("drops",
  * "drop_details", plus the glue's "batches", "packets", "gpu_ns").
