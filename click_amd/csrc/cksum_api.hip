@@ -261,7 +261,10 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
     if (!code) return fail(ctx, CLK_EINVAL, "%s: null output", fn);
     uint32_t *work = nullptr;
     const bool bins = use_bins(ctx, b);
-    const bool two = SET && ctx->set_mode != 0;            // auto: two-phase for UDP/TCP Set
+    // auto (-1): two-phase for the fixed-geometry and size-class Set kernels,
+    // fused for the packet-stream kernel (its phase C stores)
+    const bool stream = bins && ctx->varlen == 2;
+    const bool two = SET && (ctx->set_mode == 1 || (ctx->set_mode < 0 && !stream));
     const ScratchLayout L = scratch_layout(b->n);
     if (two || bins) {
         if ((r = ensure_scratch(ctx, L.bytes))) return r;

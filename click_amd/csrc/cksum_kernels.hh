@@ -16,7 +16,7 @@
 #include "cksum_device.hh"
 
 #ifndef CLK_NT_LOADS
-#define CLK_NT_LOADS 0     // tuning knob: nontemporal chunk loads
+#define CLK_NT_LOADS -1    // nontemporal chunk loads: -1 auto (fixed-geometry Check kernels), 0 never, 1 always
 #endif
 #ifndef CLK_NT_STORES
 #define CLK_NT_STORES 0    // tuning knob: nontemporal checksum-field stores
@@ -164,22 +164,29 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
 // group.  `first` holds the chunks of pass 0, already loaded by the caller
 // so that they were in flight while the caller parsed the header.
 // ---------------------------------------------------------------------------
-template <int G, int K>
+// NT: nontemporal loads (once-read stream; measured faster for the
+// fixed-geometry Check kernels, slower for the Set and packet-stream ones,
+// DESIGN.md §6).
+template <bool NT_AUTO>
+struct UseNT {
+    static constexpr bool value = CLK_NT_LOADS < 0 ? NT_AUTO : CLK_NT_LOADS != 0;
+};
+
+template <int G, int K, bool NT = false>
 __device__ __forceinline__ void load_pass(const uint8_t *c0, uint32_t nch, uint32_t pass, uint32_t gl,
                                           u32x4 (&v)[K])
 {
 #pragma unroll
     for (int k = 0; k < K; k++) {
         const uint32_t idx = pass * (G * K) + (uint32_t)k * G + gl;
-#if CLK_NT_LOADS
-        v[k] = idx < nch ? __builtin_nontemporal_load((const u32x4 *)(c0 + 16ull * idx)) : u32x4{0, 0, 0, 0};
-#else
-        v[k] = idx < nch ? gload16((uint64_t)(c0 + 16ull * idx)) : u32x4{0, 0, 0, 0};
-#endif
+        if (NT)
+            v[k] = idx < nch ? __builtin_nontemporal_load((const u32x4 *)(c0 + 16ull * idx)) : u32x4{0, 0, 0, 0};
+        else
+            v[k] = idx < nch ? gload16((uint64_t)(c0 + 16ull * idx)) : u32x4{0, 0, 0, 0};
     }
 }
 
-template <int G, int K>
+template <int G, int K, bool NT = false>
 __device__ __forceinline__ uint32_t group_range_sum(const uint8_t *c0, uint32_t nch, uint32_t gl,
                                                     const u32x4 (&first)[K], uint64_t s, int len)
 {
@@ -194,7 +201,7 @@ __device__ __forceinline__ uint32_t group_range_sum(const uint8_t *c0, uint32_t 
     const uint32_t npass = (nch + G * K - 1) / (G * K);
     for (uint32_t p = 1; p < npass; p++) {
         u32x4 v[K];
-        load_pass<G, K>(c0, nch, p, gl, v);
+        load_pass<G, K, NT>(c0, nch, p, gl, v);
 #pragma unroll
         for (int k = 0; k < K; k++) {
             const uint32_t idx = p * (G * K) + (uint32_t)k * G + gl;
@@ -494,11 +501,12 @@ __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_
         const uint8_t *c0 = (const uint8_t *)(a & ~15ull);
         const uint32_t nch = (uint32_t)((((a + caplen + 15) & ~15ull) - (uint64_t)c0) / 16);
         u32x4 v[K];
-        load_pass<G, K>(c0, nch, 0, gl, v);      // issued before the header loads
+        constexpr bool NT = UseNT<!SET>::value;
+        load_pass<G, K, NT>(c0, nch, 0, gl, v);  // issued before the header loads
         L4State st;
         l4_parse<PROTO, SET>(nh, caplen, fixoff, st);
         // a lane whose packet needs no sum masks everything (len 0)
-        const uint32_t sum = group_range_sum<G, K>(c0, nch, gl, v, a + st.hl, st.summing ? st.rlen : 0);
+        const uint32_t sum = group_range_sum<G, K, NT>(c0, nch, gl, v, a + st.hl, st.summing ? st.rlen : 0);
         l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, gl == 0, out_code, out_sum, work);
     }
 }
@@ -757,7 +765,11 @@ __global__ void __launch_bounds__(256) l4_stream_kernel(BatchArgs b, int fixoff,
                 jk[k] = j;
                 Pk[k] = P;
                 const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
-                v[k] = c < total ? gload16(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
+                if (UseNT<false>::value)
+                    v[k] = c < total ? __builtin_nontemporal_load((const u32x4 *)(cf + 16ull * (c - P[2])))
+                                     : u32x4{0, 0, 0, 0};
+                else
+                    v[k] = c < total ? gload16(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
             }
             uint32_t cur = jk[0], part = 0;
 #pragma unroll

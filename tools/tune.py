@@ -27,6 +27,7 @@ VARIANTS = {
     "k8": (["-DCLK_K=8"], {}),
     "k16": (["-DCLK_K=16"], {}),
     "nt": (["-DCLK_NT_LOADS=1"], {}),
+    "nont": (["-DCLK_NT_LOADS=0"], {}),
     "g16": ([], {"CLK_FORCE_GROUP": "16"}),
     "g32": ([], {"CLK_FORCE_GROUP": "32"}),
     "fused": ([], {"CLK_SET_MODE": "0"}),
@@ -51,6 +52,11 @@ VARIANTS = {
     "skv1": (["-DCLK_SKV=1"], {"CLK_VARLEN": "2"}),
     "skv4": (["-DCLK_SKV=4"], {"CLK_VARLEN": "2"}),
     "skv8": (["-DCLK_SKV=8"], {"CLK_VARLEN": "2"}),
+    "fused_stream": ([], {"CLK_SET_MODE": "0", "CLK_VARLEN": "2"}),
+    "two_stream": ([], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
+    "g8": ([], {"CLK_FORCE_GROUP": "8"}),
+    "k4": (["-DCLK_K=4"], {}),
+    "k12": (["-DCLK_K=12"], {}),
 }
 
 
