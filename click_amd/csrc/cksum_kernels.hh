@@ -30,6 +30,14 @@
 
 namespace clk {
 
+// NT: nontemporal loads (once-read stream; measured faster for the
+// fixed-geometry Check kernels, slower for the Set and packet-stream ones,
+// DESIGN.md §6).
+template <bool NT_AUTO>
+struct UseNT {
+    static constexpr bool value = CLK_NT_LOADS < 0 ? NT_AUTO : CLK_NT_LOADS != 0;
+};
+
 struct BatchArgs {
     uint8_t *base;
     const uint64_t *off;
@@ -90,10 +98,19 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
             const uint64_t a = (uint64_t)ip;
             const uint32_t sh = (uint32_t)(a & 3);
             const uint8_t *q = (const uint8_t *)(a & ~3ull);
-            const u32x4 d0 = gload16_a4((uint64_t)q);
+            u32x4 d0;
             uint32_t d4, d5;
-            d4 = gload4((uint64_t)(q + 16));
-            d5 = sh ? gload4((uint64_t)(q + 20)) : 0u;
+            if (UseNT<MODE != IP_SET>::value) {
+                typedef __attribute__((address_space(1))) u32x4_a4 g4;
+                typedef __attribute__((address_space(1))) uint32_t g1;
+                d0 = __builtin_nontemporal_load((const g4 *)q);
+                d4 = __builtin_nontemporal_load((const g1 *)(q + 16));
+                d5 = sh ? __builtin_nontemporal_load((const g1 *)(q + 20)) : 0u;
+            } else {
+                d0 = gload16_a4((uint64_t)q);
+                d4 = gload4((uint64_t)(q + 16));
+                d5 = sh ? gload4((uint64_t)(q + 20)) : 0u;
+            }
             uint32_t h[5];
             h[0] = __builtin_amdgcn_alignbyte(d0[1], d0[0], sh);
             h[1] = __builtin_amdgcn_alignbyte(d0[2], d0[1], sh);
@@ -164,13 +181,6 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
 // group.  `first` holds the chunks of pass 0, already loaded by the caller
 // so that they were in flight while the caller parsed the header.
 // ---------------------------------------------------------------------------
-// NT: nontemporal loads (once-read stream; measured faster for the
-// fixed-geometry Check kernels, slower for the Set and packet-stream ones,
-// DESIGN.md §6).
-template <bool NT_AUTO>
-struct UseNT {
-    static constexpr bool value = CLK_NT_LOADS < 0 ? NT_AUTO : CLK_NT_LOADS != 0;
-};
 
 template <int G, int K, bool NT = false>
 __device__ __forceinline__ void load_pass(const uint8_t *c0, uint32_t nch, uint32_t pass, uint32_t gl,
@@ -1331,8 +1341,10 @@ __global__ void __launch_bounds__(256) read_stream_kernel(const u32x4 *p, uint64
     const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
     uint32_t acc = 0;
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * nthreads < n16; i += 4 * nthreads) {
-        const u32x4 a0 = p[i], a1 = p[i + nthreads], a2 = p[i + 2 * nthreads], a3 = p[i + 3 * nthreads];
+    for (; i + 3 * nthreads < n16; i += 4 * nthreads) {     // nontemporal, as the Check kernels' stream
+        const u32x4 a0 = __builtin_nontemporal_load(p + i), a1 = __builtin_nontemporal_load(p + i + nthreads),
+                    a2 = __builtin_nontemporal_load(p + i + 2 * nthreads),
+                    a3 = __builtin_nontemporal_load(p + i + 3 * nthreads);
         acc += (a0[0] ^ a0[1] ^ a0[2] ^ a0[3]) + (a1[0] ^ a1[1] ^ a1[2] ^ a1[3])
              + (a2[0] ^ a2[1] ^ a2[2] ^ a2[3]) + (a3[0] ^ a3[1] ^ a3[2] ^ a3[3]);
     }
