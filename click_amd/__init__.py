@@ -44,12 +44,14 @@ class Batch:
     def __init__(self, base, n, stride=0, fixed_len=0, off=None, length=None, max_len=0):
         self.base, self.off, self.length = base, off, length
         self.n, self.stride, self.fixed_len, self.max_len = int(n), int(stride), int(fixed_len), int(max_len)
-        if n and off is None and stride and (n - 1) * stride + fixed_len > base.numel():
+        if n and off is None and stride and hasattr(base, "numel") and (n - 1) * stride + fixed_len > base.numel():
             raise ValueError("batch exceeds its arena")
 
     def c(self):
         b = _abi.clk_batch()
-        b.base = self.base.data_ptr() if self.base is not None else None
+        # base: a device tensor, or an int device address (a registered host
+        # region's device base, Context.host_register)
+        b.base = (self.base if isinstance(self.base, int) else self.base.data_ptr()) if self.base is not None else None
         b.off = self.off.data_ptr() if self.off is not None else None
         b.stride = self.stride
         b.len = self.length.data_ptr() if self.length is not None else None
@@ -259,6 +261,18 @@ class Context:
                                              _ptr(first_len), _ptr(frag_first), ctypes.byref(out), _ptr(totals)))
         return dict(port=port[:b.n], first_len=first_len[:b.n], frag_first=frag_first[:b.n], frag_off=fo,
                     frag_len=fl, frag_src=fs, totals=totals)
+
+    # -- zero-copy host memory -----------------------------------------------------
+    def host_register(self, arr):
+        """Register a host numpy array for zero-copy kernel access; returns
+        the device base address (int) of its first byte."""
+        dev = ctypes.c_void_p()
+        self._check(self.lib.clk_host_register(self.h, ctypes.c_void_p(arr.ctypes.data), arr.nbytes,
+                                               ctypes.byref(dev)))
+        return dev.value
+
+    def host_unregister(self, arr):
+        self._check(self.lib.clk_host_unregister(self.h, ctypes.c_void_p(arr.ctypes.data)))
 
     # -- utilities ---------------------------------------------------------------
     def count_codes(self, codes, ncounts=8, counts=None):

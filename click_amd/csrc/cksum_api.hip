@@ -10,7 +10,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
+#include <vector>
 
 struct clk_ctx {
     int device;
@@ -663,6 +665,70 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, u
                        (const uint8_t *)out_port, (const uint32_t *)pl_n, (const uint32_t *)pl_b,
                        (const uint64_t *)tile_sums, ffirst);
     return check_launch(ctx, "clk_ip_fragment");
+}
+
+}   // extern "C"
+
+namespace {
+struct HostRegion {
+    uintptr_t host;
+    size_t bytes;
+    void *dev;
+};
+std::mutex g_regions_mu;
+std::vector<HostRegion> g_regions;
+}   // namespace
+
+extern "C" {
+
+int clk_host_register(clk_ctx *ctx, void *host, size_t bytes, void **dev_base)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if (!host || !bytes || !dev_base)
+        return fail(ctx, CLK_EINVAL, "clk_host_register: bad arguments");
+    hipError_t e = hipHostRegister(host, bytes, hipHostRegisterMapped);
+    if (e != hipSuccess)
+        return hip_fail(ctx, e, "hipHostRegister");
+    void *dev = nullptr;
+    e = hipHostGetDevicePointer(&dev, host, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(host);
+        return hip_fail(ctx, e, "hipHostGetDevicePointer");
+    }
+    std::lock_guard<std::mutex> g(g_regions_mu);
+    g_regions.push_back(HostRegion{(uintptr_t)host, bytes, dev});
+    *dev_base = dev;
+    return CLK_SUCCESS;
+}
+
+int clk_host_unregister(clk_ctx *ctx, void *host)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    {
+        std::lock_guard<std::mutex> g(g_regions_mu);
+        for (size_t i = 0; i < g_regions.size(); i++)
+            if (g_regions[i].host == (uintptr_t)host) {
+                g_regions.erase(g_regions.begin() + (long)i);
+                hipError_t e = hipHostUnregister(host);
+                return e == hipSuccess ? CLK_SUCCESS : hip_fail(ctx, e, "hipHostUnregister");
+            }
+    }
+    return fail(ctx, CLK_EINVAL, "clk_host_unregister: not registered");
+}
+
+int clk_host_lookup(const void *p, size_t len, void **host_start, void **dev_base)
+{
+    std::lock_guard<std::mutex> g(g_regions_mu);
+    const uintptr_t a = (uintptr_t)p;
+    for (const HostRegion &h : g_regions)
+        if (a >= h.host && a + len <= h.host + h.bytes) {
+            if (host_start) *host_start = (void *)h.host;
+            if (dev_base) *dev_base = h.dev;
+            return CLK_SUCCESS;
+        }
+    return CLK_EINVAL;
 }
 
 int clk_count_codes(clk_ctx *ctx, const uint8_t *codes, uint64_t n, uint64_t *counts, uint32_t ncounts)

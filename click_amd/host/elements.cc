@@ -205,6 +205,10 @@ int BatchElement::configure(ConfArgs &args, std::string *err)
         }
         batch_cap_ = (uint32_t)b;
     }
+    if (args.take("ZEROCOPY", &v) && !parse_bool(v, &zerocopy_)) {
+        *err = "ZEROCOPY: expected boolean";
+        return -1;
+    }
     if (!args.kw.empty()) {
         *err = "unknown keyword " + args.kw[0].first;
         return -1;
@@ -280,6 +284,32 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
     int32_t code = 0;
     if (!span(p, &off, &len, &code)) {
         p.host_code = code;
+    } else if (zerocopy_) {
+        // the kernel reads the span where it lies (clk_host_register)
+        void *hs = nullptr, *db = nullptr;
+        if (clk_host_lookup(data + off, len ? len : 1, &hs, &db) != CLK_SUCCESS) {
+            err_ = "ZEROCOPY: packet memory is not registered (clk_host_register)";
+            return CLK_EINVAL;
+        }
+        if (zc_host_ && hs != zc_host_) {            // one region per batch
+            int r = flush();
+            if (r)
+                return r;
+        }
+        bool any_staged = false;
+        for (const Pending &q : pend_)
+            any_staged |= q.host_code < 0;
+        if (!any_staged) {
+            zc_host_ = (const uint8_t *)hs;
+            zc_dev_ = (uint8_t *)db;
+        }
+        if (grow_host(64, pend_.size() + 1)) {
+            err_ = "out of pinned host memory";
+            return CLK_EINVAL;
+        }
+        p.slot = (uint64_t)(data + off - zc_host_);
+        p.span_off = off;
+        p.span_len = len;
     } else {
         const size_t slot = (h_used_ + 63) & ~size_t(63);
         if (grow_host(slot + len + 64, pend_.size() + 1)) {
@@ -316,8 +346,9 @@ int BatchElement::flush()
         }
     hipStream_t s = (hipStream_t)clk_ctx_stream(ctx_);
     float ms = 0;
+    in_place_ = zerocopy_;
     if (n) {
-        if (grow_dev(h_used_ + 64, n)) {
+        if (grow_dev(zerocopy_ ? 64 : h_used_ + 64, n)) {
             err_ = "out of device memory";
             return CLK_EHIP;
         }
@@ -325,13 +356,14 @@ int BatchElement::flush()
             (void)hipEventCreate((hipEvent_t *)&ev_[0]);
             (void)hipEventCreate((hipEvent_t *)&ev_[1]);
         }
-        (void)hipMemcpyAsync(d_arena_, h_arena_, h_used_, hipMemcpyHostToDevice, s);
+        if (!zerocopy_)
+            (void)hipMemcpyAsync(d_arena_, h_arena_, h_used_, hipMemcpyHostToDevice, s);
         (void)hipMemcpyAsync(d_off_, h_off_, n * 8, hipMemcpyHostToDevice, s);
         (void)hipMemcpyAsync(d_len_, h_len_, n * 4, hipMemcpyHostToDevice, s);
         if (wants_anno())
             (void)hipMemcpyAsync(d_anno_, h_anno_, n, hipMemcpyHostToDevice, s);
         clk_batch b;
-        b.base = d_arena_;
+        b.base = zerocopy_ ? zc_dev_ : d_arena_;
         b.off = d_off_;
         b.stride = 0;
         b.len = d_len_;
@@ -349,7 +381,8 @@ int BatchElement::flush()
         if (wants_sums())
             (void)hipMemcpyAsync(h_sums_, d_sums_, n * 2, hipMemcpyDeviceToHost, s);
         if (wants_arena_back()) {
-            (void)hipMemcpyAsync(h_arena_, d_arena_, h_used_, hipMemcpyDeviceToHost, s);
+            if (!zerocopy_)
+                (void)hipMemcpyAsync(h_arena_, d_arena_, h_used_, hipMemcpyDeviceToHost, s);
             (void)hipMemcpyAsync(h_aux8_, d_aux8_, n, hipMemcpyDeviceToHost, s);
         }
         hipError_t e = hipStreamSynchronize(s);
@@ -381,6 +414,8 @@ int BatchElement::flush()
     gpu_ns_ += (uint64_t)(ms * 1e6);
     pend_.clear();
     h_used_ = 0;
+    zc_host_ = nullptr;
+    in_place_ = false;
     return 0;
 }
 
@@ -402,6 +437,8 @@ uint64_t BatchElement::pop_results(uint64_t *tokens, int32_t *ports, uint32_t *l
 
 void BatchElement::write_back(const Pending &p, uint32_t nbytes) const
 {
+    if (in_place_)                       // zero-copy: the kernel wrote the packet itself
+        return;
     std::memcpy(p.data + p.span_off, h_arena_ + p.slot, std::min(nbytes, p.span_len));
 }
 
@@ -729,7 +766,8 @@ void SetIPChecksum::route(Pending &p, int code, uint16_t sum, Result *r)
 {
     if (code == CLK_SET_OK) {
         uint8_t *iph = p.data + (p.nh_off >= 0 ? p.nh_off : 0);
-        std::memcpy(iph + 10, &sum, 2);                        // ip_sum (85-86)
+        if (!in_place_)
+            std::memcpy(iph + 10, &sum, 2);                    // ip_sum (85-86)
         r->port = 0;
         return;
     }
@@ -854,6 +892,10 @@ int SetL4Checksum::run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums)
 
 void SetL4Checksum::route(Pending &p, int code, uint16_t sum, Result *r)
 {
+    if (code == CLK_SET_OK && in_place_) {
+        r->port = 0;
+        return;
+    }
     if (code == CLK_SET_OK) {
         uint8_t *iph = p.data + p.nh_off;
         const uint32_t hl = (uint32_t)(iph[0] & 0xF) << 2;
@@ -928,7 +970,7 @@ void DecIPTTL::route(Pending &p, int code, uint16_t sum, Result *r)
         r->port = noutputs_ == 2 ? 1 : -1;
         return;
     }
-    if (code == CLK_TTL_OK) {                                // 63, 72-73
+    if (code == CLK_TTL_OK && !in_place_) {                  // 63, 72-73
         uint8_t *iph = p.data + p.nh_off;
         iph[8]--;
         std::memcpy(iph + 10, &sum, 2);
@@ -1345,7 +1387,7 @@ void IPFragmenter::route(Pending &p, int code, uint16_t, Result *r)
     // the first fragment: rewritten header, truncated (117-123)
     const uint32_t first = h_first_[p.index];
     const uint32_t hl = (uint32_t)(p.data[p.span_off] & 0xF) << 2;
-    write_back(p, hl);
+    write_back(p, std::max(hl, 20u));                    // ip_len, ip_id, ip_off, ip_sum even when ip_hl < 5
     r->length = p.span_off + first;
     r->port = 0;
     fragments_++;

@@ -93,6 +93,8 @@ class BatchElement {
     uint32_t batch_cap_ = 65536;
     std::string err_;
     uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0;
+    bool zerocopy_ = false;          // ZEROCOPY: packets read/written in registered host memory
+    bool in_place_ = false;          // routing a zero-copy batch: the kernel already wrote the packets
     uint8_t *d_anno_ = nullptr;      // per staged packet (wants_anno)
     uint8_t *d_aux8_ = nullptr;      // per staged packet, element use (problem offsets)
     uint8_t *h_aux8_ = nullptr;
@@ -106,6 +108,8 @@ class BatchElement {
     std::map<uint32_t, std::vector<uint8_t>> packets_kept_;
     uint32_t next_key_ = 1;
     uint8_t *h_anno_ = nullptr;
+    const uint8_t *zc_host_ = nullptr;   // the batch's registered region (zero-copy)
+    uint8_t *zc_dev_ = nullptr;
     uint8_t *h_arena_ = nullptr;
     size_t h_arena_cap_ = 0, h_used_ = 0;
     uint64_t *h_off_ = nullptr;

@@ -273,6 +273,21 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *batch, const clk_frag_cfg *cf
                     uint32_t *out_first_len, uint64_t *out_frag_first, const clk_frag_out *out,
                     uint64_t *totals);
 
+/* ---- zero-copy host packet memory --------------------------------------------
+ * Register a host memory region (a DPDK mempool's hugepage area, a pcap
+ * ring, any buffer the packets live in) so that kernels read and write the
+ * packets in place over PCIe, with no staging copy: a batch may then use
+ * base = *dev_base (the region's device address) and off_i = the packet's
+ * offset from the region's host start.  Set elements then write their
+ * fields straight into host memory.  Wraps hipHostRegister(Mapped) +
+ * hipHostGetDevicePointer; regions are recorded process-wide so that the
+ * element glue can find them (clk_host_lookup).                            */
+int clk_host_register(clk_ctx *ctx, void *host, size_t bytes, void **dev_base);
+int clk_host_unregister(clk_ctx *ctx, void *host);
+/* The registered region containing [p, p + len): its host start and device
+ * base; returns 0, or CLK_EINVAL when no registered region contains it.    */
+int clk_host_lookup(const void *p, size_t len, void **host_start, void **dev_base);
+
 /* ---- batch utilities ------------------------------------------------------- */
 
 /* counts[c] += number of i with codes[i] == c, for c < ncounts (device u64). */

@@ -48,7 +48,11 @@
  *                   (elements/ip/ipfragmenter.cc:41-55); handlers drops,
  *                   fragments; each fragment beyond the first is a new
  *                   packet (aux = its key for clk_element_take_packet)
- * plus glue keywords BATCH (packets per GPU batch, default 65536).
+ * plus glue keywords BATCH (packets per GPU batch, default 65536) and
+ * ZEROCOPY (bool, default false): the kernels read -- and the Set /
+ * rewriting elements write -- the packets where they lie, in host memory
+ * registered with clk_host_register, instead of gathering them into a
+ * staging batch and copying it to HBM.
  * Elements that rewrite header bytes (IPGWOptions, FixIPSrc, IPOutputCombo,
  * IPFragmenter) write them back into `data` at flush().
  */
