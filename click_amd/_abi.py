@@ -120,7 +120,8 @@ SIGNATURES = {
                                        ctypes.POINTER(clk_frag_out), _P]),
     "clk_host_register": (ctypes.c_int, [_P, _P, ctypes.c_size_t, ctypes.POINTER(_P)]),
     "clk_host_unregister": (ctypes.c_int, [_P, _P]),
-    "clk_host_lookup": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    "clk_host_lookup": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_size_t),
+                                       ctypes.POINTER(_P)]),
     "clk_count_codes": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P, ctypes.c_uint32]),
     "clk_gen_packets": (ctypes.c_int, [_P, _BP, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
     "clk_gen_corrupt": (ctypes.c_int, [_P, _BP, ctypes.c_uint64, ctypes.c_uint32]),

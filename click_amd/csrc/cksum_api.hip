@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -677,6 +678,7 @@ struct HostRegion {
 };
 std::mutex g_regions_mu;
 std::vector<HostRegion> g_regions;
+std::atomic<uint64_t> g_regions_gen{1};
 }   // namespace
 
 extern "C" {
@@ -698,6 +700,7 @@ int clk_host_register(clk_ctx *ctx, void *host, size_t bytes, void **dev_base)
     }
     std::lock_guard<std::mutex> g(g_regions_mu);
     g_regions.push_back(HostRegion{(uintptr_t)host, bytes, dev});
+    g_regions_gen++;
     *dev_base = dev;
     return CLK_SUCCESS;
 }
@@ -711,6 +714,7 @@ int clk_host_unregister(clk_ctx *ctx, void *host)
         for (size_t i = 0; i < g_regions.size(); i++)
             if (g_regions[i].host == (uintptr_t)host) {
                 g_regions.erase(g_regions.begin() + (long)i);
+                g_regions_gen++;
                 hipError_t e = hipHostUnregister(host);
                 return e == hipSuccess ? CLK_SUCCESS : hip_fail(ctx, e, "hipHostUnregister");
             }
@@ -718,13 +722,16 @@ int clk_host_unregister(clk_ctx *ctx, void *host)
     return fail(ctx, CLK_EINVAL, "clk_host_unregister: not registered");
 }
 
-int clk_host_lookup(const void *p, size_t len, void **host_start, void **dev_base)
+uint64_t clk_host_generation_internal(void) { return g_regions_gen.load(std::memory_order_acquire); }
+
+int clk_host_lookup(const void *p, size_t len, void **host_start, size_t *bytes, void **dev_base)
 {
     std::lock_guard<std::mutex> g(g_regions_mu);
     const uintptr_t a = (uintptr_t)p;
     for (const HostRegion &h : g_regions)
         if (a >= h.host && a + len <= h.host + h.bytes) {
             if (host_start) *host_start = (void *)h.host;
+            if (bytes) *bytes = h.bytes;
             if (dev_base) *dev_base = h.dev;
             return CLK_SUCCESS;
         }

@@ -286,20 +286,28 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
         p.host_code = code;
     } else if (zerocopy_) {
         // the kernel reads the span where it lies (clk_host_register)
-        void *hs = nullptr, *db = nullptr;
-        if (clk_host_lookup(data + off, len ? len : 1, &hs, &db) != CLK_SUCCESS) {
-            err_ = "ZEROCOPY: packet memory is not registered (clk_host_register)";
-            return CLK_EINVAL;
+        const uint8_t *a = data + off;
+        const uint64_t gen = clk_host_generation_internal();
+        if (gen != zc_gen_ || !(a >= zc_last_ && a + len <= zc_last_ + zc_last_bytes_)) {
+            void *hs = nullptr, *db = nullptr;
+            size_t nb = 0;
+            if (clk_host_lookup(a, len ? len : 1, &hs, &nb, &db) != CLK_SUCCESS) {
+                err_ = "ZEROCOPY: packet memory is not registered (clk_host_register)";
+                return CLK_EINVAL;
+            }
+            zc_last_ = (const uint8_t *)hs;
+            zc_last_bytes_ = nb;
+            zc_last_dev_ = (uint8_t *)db;
+            zc_gen_ = gen;
         }
+        const void *hs = zc_last_;
+        uint8_t *db = zc_last_dev_;
         if (zc_host_ && hs != zc_host_) {            // one region per batch
             int r = flush();
             if (r)
                 return r;
         }
-        bool any_staged = false;
-        for (const Pending &q : pend_)
-            any_staged |= q.host_code < 0;
-        if (!any_staged) {
+        if (!zc_host_) {                             // the batch's first staged packet
             zc_host_ = (const uint8_t *)hs;
             zc_dev_ = (uint8_t *)db;
         }

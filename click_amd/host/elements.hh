@@ -110,6 +110,10 @@ class BatchElement {
     uint8_t *h_anno_ = nullptr;
     const uint8_t *zc_host_ = nullptr;   // the batch's registered region (zero-copy)
     uint8_t *zc_dev_ = nullptr;
+    const uint8_t *zc_last_ = nullptr;   // last region found (lookup cache)
+    size_t zc_last_bytes_ = 0;
+    uint8_t *zc_last_dev_ = nullptr;
+    uint64_t zc_gen_ = 0;                // clk_host_generation_internal() of the cache
     uint8_t *h_arena_ = nullptr;
     size_t h_arena_cap_ = 0, h_used_ = 0;
     uint64_t *h_off_ = nullptr;

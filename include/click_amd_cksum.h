@@ -284,9 +284,10 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *batch, const clk_frag_cfg *cf
  * element glue can find them (clk_host_lookup).                            */
 int clk_host_register(clk_ctx *ctx, void *host, size_t bytes, void **dev_base);
 int clk_host_unregister(clk_ctx *ctx, void *host);
-/* The registered region containing [p, p + len): its host start and device
- * base; returns 0, or CLK_EINVAL when no registered region contains it.    */
-int clk_host_lookup(const void *p, size_t len, void **host_start, void **dev_base);
+/* The registered region containing [p, p + len): its host start, size and
+ * device base (each nullable); returns 0, or CLK_EINVAL when no registered
+ * region contains it.                                                      */
+int clk_host_lookup(const void *p, size_t len, void **host_start, size_t *bytes, void **dev_base);
 
 /* ---- batch utilities ------------------------------------------------------- */
 
