@@ -21,6 +21,9 @@
 #ifndef CLK_NT_STORES
 #define CLK_NT_STORES 0    // tuning knob: nontemporal checksum-field stores
 #endif
+#ifndef CLK_BLOCK_WRITE
+#define CLK_BLOCK_WRITE 0  // tuning knob: fused Set stores rewrite the whole 64 B block (measured slower)
+#endif
 #ifndef CLK_DIAG_NO_FIELD_STORE
 #define CLK_DIAG_NO_FIELD_STORE 0   // diagnostic builds only (results wrong)
 #endif
@@ -267,6 +270,7 @@ struct L4State {
     uint32_t hl, b0, proto, src, dst;
     uint32_t fb0, fb1;   // Set: the stored field's two bytes
     uint32_t new_b12, fix_delta;
+    uint32_t caplen;
     bool fix, summing;
 };
 
@@ -304,6 +308,7 @@ __device__ __forceinline__ void l4_parse_words(uint8_t *nh, uint32_t caplen, int
     st.code = OK;
     st.rlen = 0;
     st.plen_ph = 0;
+    st.caplen = caplen;
     st.hl = hl;
     st.b0 = b0;
     st.proto = proto;
@@ -425,9 +430,60 @@ __device__ __forceinline__ void l4_parse(uint8_t *nh, uint32_t caplen, int fixof
 }
 
 // Finish one packet from its range sum.  `writer` lanes store.
+// Replace byte `val` at absolute address `at` if it lies in the 16 bytes of
+// v at absolute address `va`.
+__device__ __forceinline__ void patch_byte(u32x4 &v, uint64_t va, uint64_t at, uint32_t val)
+{
+    const uint64_t rel = at - va;
+    if (rel < 16) {
+        const uint32_t d = (uint32_t)rel >> 2, sh = 8 * ((uint32_t)rel & 3);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++)
+            if (k == d)
+                v[k] = (v[k] & ~(0xFFu << sh)) | ((val & 0xFF) << sh);
+    }
+}
+
+// Fused Set stores.  HBM rewrites a partially written 64 B block by
+// read-modify-write: alone, one 2 B store per 1536 B slot runs at 21.6 G
+// stores/s and a full 64 B block at 39 G/s (tools/probes/write_probe.hip).
+// With CLK_BLOCK_WRITE, when the 64 B-aligned block holding the field lies
+// inside this packet, the lanes re-read it, patch the field (and the FIXOFF
+// byte when it falls in the block) and store the whole block; lane `gl` of
+// `ng` takes quarters gl, gl+ng, ...  Inside the streaming kernels this
+// measured slower (C3 5.19 vs 4.94 ms, C4 7.11 vs 6.64 ms), so by default
+// the writer lane stores the bytes alone.
+template <int PROTO>
+__device__ __forceinline__ void set_field_store(uint8_t *nh, const L4State &st, uint32_t r, uint32_t gl,
+                                                uint32_t ng, bool writer)
+{
+    constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
+    const uint64_t a = (uint64_t)nh, fa = a + st.hl + FIELD, xa = a + st.hl + 12;
+    const uint64_t blk = fa & ~63ull;
+    if (CLK_BLOCK_WRITE && blk >= a && blk + 64 <= a + st.caplen) {
+        const bool fix_in = st.fix && (xa - blk) < 64;
+        for (uint32_t q = gl; q < 4; q += ng) {
+            const uint64_t qa = blk + 16 * q;
+            u32x4 v = gload16(qa);
+            patch_byte(v, qa, fa, r);
+            patch_byte(v, qa, fa + 1, r >> 8);
+            if (fix_in)
+                patch_byte(v, qa, xa, st.new_b12);
+            *(__attribute__((address_space(1))) u32x4 *)qa = v;
+        }
+        if (writer && st.fix && !fix_in)
+            nh[st.hl + 12] = (uint8_t)st.new_b12;
+    } else if (writer) {
+        if (st.fix)
+            nh[st.hl + 12] = (uint8_t)st.new_b12;
+        st_u16(nh + st.hl + FIELD, r);
+    }
+}
+
 template <int PROTO, bool SET, bool DEFER>
 __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum, L4State &st, bool writer,
-                                          uint8_t *out_code, uint16_t *out_sum, uint32_t *work)
+                                          uint8_t *out_code, uint16_t *out_sum, uint32_t *work,
+                                          uint32_t gl = 0, uint32_t ng = 1)
 {
     constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
     uint32_t stored = 0;
@@ -466,13 +522,14 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
         if (SET) {
             stored = r;
 #if !CLK_DIAG_NO_FIELD_STORE
-            if (writer) {
-                if (st.fix)
-                    nh[st.hl + 12] = (uint8_t)st.new_b12;
-                if (DEFER)       // the field is written by field_scatter_kernel
+            if (DEFER) {         // the field is written by field_scatter_kernel
+                if (writer) {
+                    if (st.fix)
+                        nh[st.hl + 12] = (uint8_t)st.new_b12;
                     work[i] = 0x80000000u | (st.hl << 16) | r;
-                else
-                    st_u16(nh + st.hl + FIELD, r);
+                }
+            } else {
+                set_field_store<PROTO>(nh, st, r, gl, ng, writer);
             }
 #endif
         } else if (r != 0) {
@@ -517,7 +574,7 @@ __global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_
         l4_parse<PROTO, SET>(nh, caplen, fixoff, st);
         // a lane whose packet needs no sum masks everything (len 0)
         const uint32_t sum = group_range_sum<G, K, NT>(c0, nch, gl, v, a + st.hl, st.summing ? st.rlen : 0);
-        l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, gl == 0, out_code, out_sum, work);
+        l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, gl == 0, out_code, out_sum, work, gl, G);
     }
 }
 
