@@ -764,7 +764,7 @@ __device__ __forceinline__ uint32_t chunk_outside(const u32x4 V, uint64_t ca, ui
 //            bytes) is re-summed from global memory by its lane.
 // The sum mod 2^32 is order-free (cksum_device.hh), so whole-chunk sums
 // minus the excluded bytes equal the reference's word sum exactly.
-template <int PROTO, bool SET, bool DEFER, int KV>
+template <int PROTO, bool SET, bool DEFER, int KV, bool PF>
 __global__ void __launch_bounds__(256) l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                         uint16_t *out_sum, uint32_t *work)
 {
@@ -807,7 +807,8 @@ __global__ void __launch_bounds__(256) l4_stream_kernel(BatchArgs b, int fixoff,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
+        // issue: find the packets of this lane's KV chunks at cb and load them
+        auto issue = [&](uint32_t cb, u32x4 (&v)[KV], uint32_t (&jk)[KV], u32x4 (&Pk)[KV]) {
             const uint32_t cl = cb + lane * KV;
             uint32_t j = 0;                                    // last packet whose chunk start <= cl
 #pragma unroll
@@ -816,9 +817,6 @@ __global__ void __launch_bounds__(256) l4_stream_kernel(BatchArgs b, int fixoff,
                     j += step;
             uint32_t nxt = cst[wv][j + 1];
             u32x4 P = pk[wv][j];
-            u32x4 v[KV];
-            uint32_t jk[KV];
-            u32x4 Pk[KV];
 #pragma unroll
             for (int k = 0; k < KV; k++) {
                 const uint32_t c = cl + k;
@@ -838,6 +836,10 @@ __global__ void __launch_bounds__(256) l4_stream_kernel(BatchArgs b, int fixoff,
                 else
                     v[k] = c < total ? gload16(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
             }
+        };
+        // consume: whole-chunk sums into the packets' accumulators, stash
+        auto consume = [&](uint32_t cb, const u32x4 (&v)[KV], const uint32_t (&jk)[KV], const u32x4 (&Pk)[KV]) {
+            const uint32_t cl = cb + lane * KV;
             uint32_t cur = jk[0], part = 0;
 #pragma unroll
             for (int k = 0; k < KV; k++) {
@@ -868,6 +870,35 @@ __global__ void __launch_bounds__(256) l4_stream_kernel(BatchArgs b, int fixoff,
             }
             if (cl < total)
                 atomicAdd(&acc[wv][cur], part);
+        };
+        if (PF) {                 // the next pass's loads are in flight while this pass is summed
+            u32x4 v[KV], Pk[KV];
+            uint32_t jk[KV];
+            if (total)
+                issue(0, v, jk, Pk);
+            for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
+                u32x4 v2[KV], P2[KV];
+                uint32_t j2[KV];
+                const bool more = cb + 64 * KV < total;
+                if (more)
+                    issue(cb + 64 * KV, v2, j2, P2);
+                consume(cb, v, jk, Pk);
+                if (more) {
+#pragma unroll
+                    for (int k = 0; k < KV; k++) {
+                        v[k] = v2[k];
+                        jk[k] = j2[k];
+                        Pk[k] = P2[k];
+                    }
+                }
+            }
+        } else {
+            for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
+                u32x4 v[KV], Pk[KV];
+                uint32_t jk[KV];
+                issue(cb, v, jk, Pk);
+                consume(cb, v, jk, Pk);
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

@@ -384,3 +384,42 @@ def test_fragmenter_matches_pyref_fuzz(mtu, honor_df):
         else:
             assert a[o:o + c].tobytes() == arena[o:o + c].tobytes()
     assert ports == ({0, 1, 2} if honor_df else {0, 2})
+
+
+def test_config1_fake_iprouter_plumbing_on_cpu():
+    """BASELINE config 1 (conf/fake-iprouter.click, CPU, no GPU): the
+    forwarding path of its 600,000 frames through the CPU restatement --
+    Strip(14) + CheckIPHeader(INTERFACES ...) -> IPGWOptions -> FixIPSrc ->
+    DecIPTTL -> IPFragmenter(300), and the click-xform combos
+    IPInputCombo -> IPOutputCombo(1, 18.26.4.24, 300) -- forwards every
+    frame (iprouter-01 expects 600000) with identical bytes both ways."""
+    L = oracle_lib.load_oracle()
+    v = [g for g in golden_vectors() if g["name"] == "fake-iprouter-ip-check"][0]
+    frame = bytes.fromhex("0000c0ae67ef0000000000000800") + bytes.fromhex(v["l3"])
+    n, fl = 600000, len(frame)
+    outs = []
+    for combo in (False, True):
+        arena = np.tile(np.frombuffer(frame, np.uint8), n).copy()
+        bad = np.array([0xFF041A12, 0x00041A12, 0xFF071A12, 0x00071A12, 0, 0xFFFFFFFF], np.uint32)
+        good = np.array([0x01041A12, 0x01071A12], np.uint32)
+        ok = [L.oracle_check_ip_header(arena[i * fl:].ctypes.data, fl, 14, 1, bad.ctypes.data, len(bad),
+                                       good.ctypes.data, len(good)) for i in range(0, n, 997)]
+        assert not any(ok)                      # a sample: every frame is the same
+        ip = arena.reshape(n, fl)[:, 14:].copy().reshape(-1)
+        if combo:
+            port, _, _ = oracle_lib.ip_out_batch("ip_output_combo", ip, n, stride=fl - 14, fixed_len=fl - 14,
+                                                 my_ip=0x18041A12, mtu=300)
+            assert not port.any()
+        else:
+            st, _, _ = oracle_lib.ip_out_batch("ip_gw_options", ip, n, stride=fl - 14, fixed_len=fl - 14,
+                                               my_ip=0x18041A12, my_addrs=np.array([0x18041A12], np.uint32))
+            assert not st.any()
+            oracle_lib.ip_out_batch("fix_ip_src", ip, n, stride=fl - 14, fixed_len=fl - 14,
+                                    flags=np.zeros(n, np.uint8), my_ip=0x18041A12)
+            st, _ = oracle_lib.batch("dec_ttl", ip, n, stride=fl - 14, fixed_len=fl - 14)
+            assert not st.any()
+            r = oracle_lib.ip_fragment(ip, n, 300, True, stride=fl - 14, fixed_len=fl - 14)
+            assert not r["port"].any() and not r["frags"]
+        outs.append(ip)
+    assert np.array_equal(outs[0], outs[1])
+    assert int(outs[0].reshape(n, -1)[:, 8].astype(np.int64).sum()) == n * 63     # TTL 64 -> 63 on all 600000

@@ -54,6 +54,9 @@ VARIANTS = {
     "skv8": (["-DCLK_SKV=8"], {"CLK_VARLEN": "2"}),
     "fused_stream": ([], {"CLK_SET_MODE": "0", "CLK_VARLEN": "2"}),
     "two_stream": ([], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
+    "spf": (["-DCLK_SPF=1"], {}),
+    "spf_kv1": (["-DCLK_SPF=1", "-DCLK_SKV=1"], {}),
+    "spf_kv4": (["-DCLK_SPF=1", "-DCLK_SKV=4"], {}),
     "block": (["-DCLK_BLOCK_WRITE=1"], {}),
     "fused_block": (["-DCLK_BLOCK_WRITE=1"], {"CLK_SET_MODE": "0"}),
     "g8": ([], {"CLK_FORCE_GROUP": "8"}),
