@@ -85,6 +85,14 @@ class Element:
             raise ClickAmdError("flush failed: %d" % rc)
         self._keep = []
 
+    def flush_async(self):
+        """Route the batch in flight, launch the staged one, do not wait
+        (the host buffers pushed since the previous flush must stay valid
+        until the next flush)."""
+        rc = self.lib.clk_element_flush_async(self.h)
+        if rc != 0:
+            raise ClickAmdError("flush_async failed: %d" % rc)
+
     def results(self, cap=1 << 20, aux=False):
         """(tokens, ports, lengths[, aux]) of every flushed packet, in order."""
         out = []

@@ -174,24 +174,28 @@ BatchElement::BatchElement(clk_ctx *ctx, const std::string &name, int noutputs)
 {
 }
 
+void BatchElement::free_stage(Stage &g)
+{
+    for (void *q : {(void *)g.h_arena, (void *)g.h_off, (void *)g.h_len, (void *)g.h_codes, (void *)g.h_sums,
+                    (void *)g.h_anno, (void *)g.h_aux8})
+        if (q)
+            (void)hipHostFree(q);
+    for (void *q : {(void *)g.d_arena, (void *)g.d_off, (void *)g.d_len, (void *)g.d_codes, (void *)g.d_sums,
+                    (void *)g.d_anno, (void *)g.d_aux8})
+        if (q)
+            (void)hipFree(q);
+    for (void *e : g.ev)
+        if (e)
+            (void)hipEventDestroy((hipEvent_t)e);
+}
+
 BatchElement::~BatchElement()
 {
-    if (h_arena_) (void)hipHostFree(h_arena_);
-    if (h_off_) (void)hipHostFree(h_off_);
-    if (h_len_) (void)hipHostFree(h_len_);
-    if (h_codes_) (void)hipHostFree(h_codes_);
-    if (h_sums_) (void)hipHostFree(h_sums_);
-    if (d_arena_) (void)hipFree(d_arena_);
-    if (d_off_) (void)hipFree(d_off_);
-    if (d_len_) (void)hipFree(d_len_);
-    if (d_codes_) (void)hipFree(d_codes_);
-    if (d_sums_) (void)hipFree(d_sums_);
-    if (d_anno_) (void)hipFree(d_anno_);
-    if (d_aux8_) (void)hipFree(d_aux8_);
-    if (h_anno_) (void)hipHostFree(h_anno_);
-    if (h_aux8_) (void)hipHostFree(h_aux8_);
-    for (void *e : ev_)
-        if (e) (void)hipEventDestroy((hipEvent_t)e);
+    for (Stage &g : st_) {
+        if (g.inflight)
+            (void)hipEventSynchronize((hipEvent_t)g.ev[2]);
+        free_stage(g);
+    }
 }
 
 int BatchElement::configure(ConfArgs &args, std::string *err)
@@ -234,45 +238,42 @@ static int host_grow(T **p, size_t *cap_elems, size_t need, size_t keep)
     return 0;
 }
 
-int BatchElement::grow_host(size_t bytes, size_t n)
+int BatchElement::grow_host(Stage &g, size_t bytes, size_t n)
 {
-    if (host_grow(&h_arena_, &h_arena_cap_, bytes, h_used_))
+    if (host_grow(&g.h_arena, &g.h_arena_cap, bytes, g.h_used))
         return -1;
-    if (h_n_cap_ < n) {
-        size_t c1 = h_n_cap_, c2 = h_n_cap_, c3 = h_n_cap_, c4 = h_n_cap_, c5 = h_n_cap_, c6 = h_n_cap_;
-        if (host_grow(&h_off_, &c1, n, 0) || host_grow(&h_len_, &c2, n, 0) ||
-            host_grow(&h_codes_, &c3, n, 0) || host_grow(&h_sums_, &c4, n, 0) ||
-            host_grow(&h_anno_, &c5, n, 0) || host_grow(&h_aux8_, &c6, n, 0))
+    if (g.h_n_cap < n) {
+        size_t c1 = g.h_n_cap, c2 = g.h_n_cap, c3 = g.h_n_cap, c4 = g.h_n_cap, c5 = g.h_n_cap, c6 = g.h_n_cap;
+        if (host_grow(&g.h_off, &c1, n, 0) || host_grow(&g.h_len, &c2, n, 0) || host_grow(&g.h_codes, &c3, n, 0) ||
+            host_grow(&g.h_sums, &c4, n, 0) || host_grow(&g.h_anno, &c5, n, 0) || host_grow(&g.h_aux8, &c6, n, 0))
             return -1;
-        h_n_cap_ = c1;
+        g.h_n_cap = c1;
     }
     return 0;
 }
 
-int BatchElement::grow_dev(size_t bytes, size_t n)
+int BatchElement::grow_dev(Stage &g, size_t bytes, size_t n)
 {
-    if (d_arena_cap_ < bytes) {
-        if (d_arena_)
-            (void)hipFree(d_arena_);
-        d_arena_ = nullptr;
-        size_t c = std::max(bytes, d_arena_cap_ * 2);
-        if (hipMalloc(&d_arena_, c) != hipSuccess)
+    if (g.d_arena_cap < bytes) {
+        if (g.d_arena)
+            (void)hipFree(g.d_arena);
+        g.d_arena = nullptr;
+        size_t c = std::max(bytes, g.d_arena_cap * 2);
+        if (hipMalloc(&g.d_arena, c) != hipSuccess)
             return -1;
-        d_arena_cap_ = c;
+        g.d_arena_cap = c;
     }
-    if (d_n_cap_ < n) {
-        size_t c = std::max(n, d_n_cap_ * 2);
-        if (d_off_) (void)hipFree(d_off_);
-        if (d_len_) (void)hipFree(d_len_);
-        if (d_codes_) (void)hipFree(d_codes_);
-        if (d_sums_) (void)hipFree(d_sums_);
-        if (d_anno_) (void)hipFree(d_anno_);
-        if (d_aux8_) (void)hipFree(d_aux8_);
-        if (hipMalloc(&d_off_, c * 8) != hipSuccess || hipMalloc(&d_len_, c * 4) != hipSuccess ||
-            hipMalloc(&d_codes_, c) != hipSuccess || hipMalloc(&d_sums_, c * 2) != hipSuccess ||
-            hipMalloc(&d_anno_, c) != hipSuccess || hipMalloc(&d_aux8_, c) != hipSuccess)
+    if (g.d_n_cap < n) {
+        size_t c = std::max(n, g.d_n_cap * 2);
+        for (void *q : {(void *)g.d_off, (void *)g.d_len, (void *)g.d_codes, (void *)g.d_sums, (void *)g.d_anno,
+                        (void *)g.d_aux8})
+            if (q)
+                (void)hipFree(q);
+        if (hipMalloc(&g.d_off, c * 8) != hipSuccess || hipMalloc(&g.d_len, c * 4) != hipSuccess ||
+            hipMalloc(&g.d_codes, c) != hipSuccess || hipMalloc(&g.d_sums, c * 2) != hipSuccess ||
+            hipMalloc(&g.d_anno, c) != hipSuccess || hipMalloc(&g.d_aux8, c) != hipSuccess)
             return -1;
-        d_n_cap_ = c;
+        g.d_n_cap = c;
     }
     return 0;
 }
@@ -300,115 +301,134 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
             zc_last_dev_ = (uint8_t *)db;
             zc_gen_ = gen;
         }
-        const void *hs = zc_last_;
-        uint8_t *db = zc_last_dev_;
-        if (zc_host_ && hs != zc_host_) {            // one region per batch
-            int r = flush();
+        if (st_[cur_].zc_host && zc_last_ != st_[cur_].zc_host) {   // one region per batch
+            int r = flush_async();
             if (r)
                 return r;
         }
-        if (!zc_host_) {                             // the batch's first staged packet
-            zc_host_ = (const uint8_t *)hs;
-            zc_dev_ = (uint8_t *)db;
+        Stage &g = st_[cur_];
+        if (!g.zc_host) {                                         // the batch's first staged packet
+            g.zc_host = zc_last_;
+            g.zc_dev = zc_last_dev_;
         }
-        if (grow_host(64, pend_.size() + 1)) {
+        if (grow_host(g, 64, g.pend.size() + 1)) {
             err_ = "out of pinned host memory";
             return CLK_EINVAL;
         }
-        p.slot = (uint64_t)(data + off - zc_host_);
+        p.slot = (uint64_t)(a - g.zc_host);
         p.span_off = off;
         p.span_len = len;
     } else {
-        const size_t slot = (h_used_ + 63) & ~size_t(63);
-        if (grow_host(slot + len + 64, pend_.size() + 1)) {
+        Stage &g = st_[cur_];
+        const size_t slot = (g.h_used + 63) & ~size_t(63);
+        if (grow_host(g, slot + len + 64, g.pend.size() + 1)) {
             err_ = "out of pinned host memory";
             return CLK_EINVAL;
         }
         if (len)
-            std::memcpy(h_arena_ + slot, data + off, len);
+            std::memcpy(g.h_arena + slot, data + off, len);
         p.slot = slot;
         p.span_off = off;
         p.span_len = len;
-        h_used_ = slot + len;
+        g.h_used = slot + len;
     }
-    pend_.push_back(p);
-    return pend_.size() >= batch_cap_ ? 1 : 0;
+    Stage &g = st_[cur_];
+    g.pend.push_back(p);
+    return g.pend.size() >= batch_cap_ ? 1 : 0;
 }
 
-int BatchElement::flush()
+// Copy the staged batch to the GPU, run the element, queue the copies back
+// and a completion event; nothing waits.
+int BatchElement::launch(Stage &g)
 {
-    if (pend_.empty())
-        return 0;
     size_t n = 0;
     uint32_t maxlen = 0;
-    if (grow_host(h_used_ + 64, pend_.size()))
+    if (grow_host(g, g.h_used + 64, g.pend.size()))
         return CLK_EINVAL;
-    for (Pending &p : pend_)
+    for (Pending &p : g.pend)
         if (p.host_code < 0) {
-            h_off_[n] = p.slot;
-            h_len_[n] = p.span_len;
-            h_anno_[n] = (uint8_t)p.anno;
+            g.h_off[n] = p.slot;
+            g.h_len[n] = p.span_len;
+            g.h_anno[n] = (uint8_t)p.anno;
             p.index = (uint32_t)n;
             maxlen = std::max(maxlen, p.span_len);
             n++;
         }
+    g.n = n;
+    g.zc = zerocopy_;
+    g.inflight = true;
     hipStream_t s = (hipStream_t)clk_ctx_stream(ctx_);
-    float ms = 0;
-    in_place_ = zerocopy_;
+    if (!g.ev[0])
+        for (void *&e : g.ev)
+            (void)hipEventCreate((hipEvent_t *)&e);
     if (n) {
-        if (grow_dev(zerocopy_ ? 64 : h_used_ + 64, n)) {
+        if (grow_dev(g, g.zc ? 64 : g.h_used + 64, n)) {
             err_ = "out of device memory";
             return CLK_EHIP;
         }
-        if (!ev_[0]) {
-            (void)hipEventCreate((hipEvent_t *)&ev_[0]);
-            (void)hipEventCreate((hipEvent_t *)&ev_[1]);
-        }
-        if (!zerocopy_)
-            (void)hipMemcpyAsync(d_arena_, h_arena_, h_used_, hipMemcpyHostToDevice, s);
-        (void)hipMemcpyAsync(d_off_, h_off_, n * 8, hipMemcpyHostToDevice, s);
-        (void)hipMemcpyAsync(d_len_, h_len_, n * 4, hipMemcpyHostToDevice, s);
+        if (!g.zc)
+            (void)hipMemcpyAsync(g.d_arena, g.h_arena, g.h_used, hipMemcpyHostToDevice, s);
+        (void)hipMemcpyAsync(g.d_off, g.h_off, n * 8, hipMemcpyHostToDevice, s);
+        (void)hipMemcpyAsync(g.d_len, g.h_len, n * 4, hipMemcpyHostToDevice, s);
         if (wants_anno())
-            (void)hipMemcpyAsync(d_anno_, h_anno_, n, hipMemcpyHostToDevice, s);
+            (void)hipMemcpyAsync(g.d_anno, g.h_anno, n, hipMemcpyHostToDevice, s);
         clk_batch b;
-        b.base = zerocopy_ ? zc_dev_ : d_arena_;
-        b.off = d_off_;
+        b.base = g.zc ? g.zc_dev : g.d_arena;
+        b.off = g.d_off;
         b.stride = 0;
-        b.len = d_len_;
+        b.len = g.d_len;
         b.fixed_len = 0;
         b.max_len = maxlen;
         b.n = n;
-        (void)hipEventRecord((hipEvent_t)ev_[0], s);
-        int r = run(&b, d_codes_, d_sums_);
+        d_anno_ = g.d_anno;
+        d_aux8_ = g.d_aux8;
+        (void)hipEventRecord((hipEvent_t)g.ev[0], s);
+        int r = run(&b, g.d_codes, g.d_sums);
         if (r) {
             err_ = clk_last_error(ctx_);
+            g.inflight = false;
             return r;
         }
-        (void)hipEventRecord((hipEvent_t)ev_[1], s);
-        (void)hipMemcpyAsync(h_codes_, d_codes_, n, hipMemcpyDeviceToHost, s);
+        (void)hipEventRecord((hipEvent_t)g.ev[1], s);
+        (void)hipMemcpyAsync(g.h_codes, g.d_codes, n, hipMemcpyDeviceToHost, s);
         if (wants_sums())
-            (void)hipMemcpyAsync(h_sums_, d_sums_, n * 2, hipMemcpyDeviceToHost, s);
+            (void)hipMemcpyAsync(g.h_sums, g.d_sums, n * 2, hipMemcpyDeviceToHost, s);
         if (wants_arena_back()) {
-            if (!zerocopy_)
-                (void)hipMemcpyAsync(h_arena_, d_arena_, h_used_, hipMemcpyDeviceToHost, s);
-            (void)hipMemcpyAsync(h_aux8_, d_aux8_, n, hipMemcpyDeviceToHost, s);
+            if (!g.zc)
+                (void)hipMemcpyAsync(g.h_arena, g.d_arena, g.h_used, hipMemcpyDeviceToHost, s);
+            (void)hipMemcpyAsync(g.h_aux8, g.d_aux8, n, hipMemcpyDeviceToHost, s);
         }
-        hipError_t e = hipStreamSynchronize(s);
-        if (e != hipSuccess) {
-            err_ = hipGetErrorString(e);
-            return CLK_EHIP;
-        }
-        (void)hipEventElapsedTime(&ms, (hipEvent_t)ev_[0], (hipEvent_t)ev_[1]);
     }
+    (void)hipEventRecord((hipEvent_t)g.ev[2], s);
+    return 0;
+}
+
+// Wait for a launched stage and route its packets, in push order.
+int BatchElement::complete(Stage &g)
+{
+    if (!g.inflight)
+        return 0;
+    hipError_t e = hipEventSynchronize((hipEvent_t)g.ev[2]);
+    g.inflight = false;
+    if (e != hipSuccess) {
+        err_ = hipGetErrorString(e);
+        return CLK_EHIP;
+    }
+    float ms = 0;
+    if (g.n)
+        (void)hipEventElapsedTime(&ms, (hipEvent_t)g.ev[0], (hipEvent_t)g.ev[1]);
+    rt_ = &g;
+    h_aux8_ = g.h_aux8;
+    in_place_ = g.zc;
     size_t k = 0;
-    for (Pending &p : pend_) {
+    for (Pending &p : g.pend) {
         int code;
         uint16_t sum = 0;
         if (p.host_code >= 0) {
             code = p.host_code;
         } else {
-            code = h_codes_[k];
-            sum = wants_sums() ? h_sums_[k] : 0;
+            code = g.h_codes[k];
+            sum = wants_sums() ? g.h_sums[k] : 0;
             k++;
         }
         Result r{p.token, 0, p.length, 0};
@@ -418,13 +438,36 @@ int BatchElement::flush()
         post_route(p, code, results_);
     }
     batches_++;
-    packets_ += pend_.size();
+    packets_ += g.pend.size();
     gpu_ns_ += (uint64_t)(ms * 1e6);
-    pend_.clear();
-    h_used_ = 0;
-    zc_host_ = nullptr;
+    g.pend.clear();
+    g.h_used = 0;
+    g.zc_host = nullptr;
     in_place_ = false;
     return 0;
+}
+
+int BatchElement::flush_async()
+{
+    Stage &other = st_[cur_ ^ 1];
+    int r = complete(other);              // results stay in push order
+    if (r)
+        return r;
+    Stage &g = st_[cur_];
+    if (g.pend.empty())
+        return 0;
+    if ((r = launch(g)))
+        return r;
+    cur_ ^= 1;
+    return 0;
+}
+
+int BatchElement::flush()
+{
+    int r = flush_async();
+    if (r)
+        return r;
+    return complete(st_[cur_ ^ 1]);
 }
 
 uint64_t BatchElement::pop_results(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint32_t *aux,
@@ -447,7 +490,7 @@ void BatchElement::write_back(const Pending &p, uint32_t nbytes) const
 {
     if (in_place_)                       // zero-copy: the kernel wrote the packet itself
         return;
-    std::memcpy(p.data + p.span_off, h_arena_ + p.slot, std::min(nbytes, p.span_len));
+    std::memcpy(p.data + p.span_off, rt_->h_arena + p.slot, std::min(nbytes, p.span_len));
 }
 
 uint32_t BatchElement::keep_packet(const uint8_t *bytes, uint32_t len)
@@ -1528,7 +1571,7 @@ int clk_element_push_burst(clk_element *w, uint8_t *const *datas, const uint32_t
         int r = w->e->push(datas[k], lengths[k], nh_offsets ? nh_offsets[k] : -1, first_token + k);
         if (r < 0)
             return r;
-        if (r == 1 && (r = w->e->flush()) != 0)
+        if (r == 1 && (r = w->e->flush_async()) != 0)   // stage the next batch while this one runs
             return r;
     }
     return CLK_SUCCESS;
@@ -1539,6 +1582,13 @@ int clk_element_flush(clk_element *w)
     if (!w)
         return CLK_EINVAL;
     return w->e->flush();
+}
+
+int clk_element_flush_async(clk_element *w)
+{
+    if (!w)
+        return CLK_EINVAL;
+    return w->e->flush_async();
 }
 
 uint64_t clk_element_results(clk_element *w, uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint64_t cap)

@@ -42,7 +42,8 @@ class BatchElement {
     virtual const char *class_name() const = 0;
     virtual int configure(ConfArgs &args, std::string *err);
     int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno = 0);
-    int flush();
+    int flush();          // run the staged batch, wait for every batch in flight, route
+    int flush_async();    // route the batch in flight (if any), launch the staged one, return
     uint64_t pop_results(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap);
     int64_t take_packet(uint32_t key, uint8_t *buf, size_t cap);
     virtual std::string read_handler(const std::string &h) const;
@@ -50,7 +51,7 @@ class BatchElement {
     const std::string &name() const { return name_; }
     std::string declaration() const { return name_ + " :: " + class_name(); }
     const std::string &last_error() const { return err_; }
-    size_t pending() const { return pend_.size(); }
+    size_t pending() const { return st_[cur_].pend.size(); }
 
   protected:
     struct Pending {
@@ -81,7 +82,7 @@ class BatchElement {
     virtual void pre_route(Pending &, std::deque<Result> &) {}
     // called after route(): results that follow the packet's own (fragments)
     virtual void post_route(Pending &, int, std::deque<Result> &) {}
-    const uint8_t *staged(const Pending &p) const { return h_arena_ + p.slot; }
+    const uint8_t *staged(const Pending &p) const { return rt_->h_arena + p.slot; }
     void write_back(const Pending &p, uint32_t nbytes) const;   // staged span -> packet
     uint32_t keep_packet(const uint8_t *bytes, uint32_t len);   // new packet, returns its key
     void chatter(const std::string &s) { msgs_.push_back(s); }
@@ -95,40 +96,56 @@ class BatchElement {
     uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0;
     bool zerocopy_ = false;          // ZEROCOPY: packets read/written in registered host memory
     bool in_place_ = false;          // routing a zero-copy batch: the kernel already wrote the packets
+    // the launching stage's buffers (valid in run()) and the routing
+    // stage's host results (valid in route())
     uint8_t *d_anno_ = nullptr;      // per staged packet (wants_anno)
     uint8_t *d_aux8_ = nullptr;      // per staged packet, element use (problem offsets)
     uint8_t *h_aux8_ = nullptr;
 
   private:
-    int grow_host(size_t bytes, size_t n);
-    int grow_dev(size_t bytes, size_t n);
-    std::vector<Pending> pend_;
+    // Double buffering: push() stages into st_[cur_]; flush_async() launches
+    // it and flips cur_, so the host stages batch k+1 while batch k is on
+    // the GPU.  At most one stage is in flight; its results are routed
+    // before the next launch (element state such as IPFragmenter's
+    // fragment buffers serves one batch at a time).
+    struct Stage {
+        std::vector<Pending> pend;
+        uint8_t *h_arena = nullptr;
+        size_t h_arena_cap = 0, h_used = 0;
+        uint64_t *h_off = nullptr;
+        uint32_t *h_len = nullptr;
+        uint8_t *h_codes = nullptr, *h_anno = nullptr, *h_aux8 = nullptr;
+        uint16_t *h_sums = nullptr;
+        size_t h_n_cap = 0;
+        uint8_t *d_arena = nullptr;
+        size_t d_arena_cap = 0;
+        uint64_t *d_off = nullptr;
+        uint32_t *d_len = nullptr;
+        uint8_t *d_codes = nullptr, *d_anno = nullptr, *d_aux8 = nullptr;
+        uint16_t *d_sums = nullptr;
+        size_t d_n_cap = 0;
+        const uint8_t *zc_host = nullptr;   // the batch's registered region (zero-copy)
+        uint8_t *zc_dev = nullptr;
+        void *ev[3] = {nullptr, nullptr, nullptr};   // kernel start, kernel end, batch done
+        size_t n = 0;                       // packets on the GPU
+        bool inflight = false, zc = false;
+    };
+    int grow_host(Stage &g, size_t bytes, size_t n);
+    int grow_dev(Stage &g, size_t bytes, size_t n);
+    int launch(Stage &g);
+    int complete(Stage &g);
+    void free_stage(Stage &g);
+    Stage st_[2];
+    int cur_ = 0;
+    const Stage *rt_ = &st_[0];          // the stage being routed
     std::deque<Result> results_;
     std::vector<std::string> msgs_;
     std::map<uint32_t, std::vector<uint8_t>> packets_kept_;
     uint32_t next_key_ = 1;
-    uint8_t *h_anno_ = nullptr;
-    const uint8_t *zc_host_ = nullptr;   // the batch's registered region (zero-copy)
-    uint8_t *zc_dev_ = nullptr;
     const uint8_t *zc_last_ = nullptr;   // last region found (lookup cache)
     size_t zc_last_bytes_ = 0;
     uint8_t *zc_last_dev_ = nullptr;
     uint64_t zc_gen_ = 0;                // clk_host_generation_internal() of the cache
-    uint8_t *h_arena_ = nullptr;
-    size_t h_arena_cap_ = 0, h_used_ = 0;
-    uint64_t *h_off_ = nullptr;
-    uint32_t *h_len_ = nullptr;
-    uint8_t *h_codes_ = nullptr;
-    uint16_t *h_sums_ = nullptr;
-    size_t h_n_cap_ = 0;
-    uint8_t *d_arena_ = nullptr;
-    size_t d_arena_cap_ = 0;
-    uint64_t *d_off_ = nullptr;
-    uint32_t *d_len_ = nullptr;
-    uint8_t *d_codes_ = nullptr;
-    uint16_t *d_sums_ = nullptr;
-    size_t d_n_cap_ = 0;
-    void *ev_[2] = {nullptr, nullptr};
 };
 
 // Check elements share drop(): elements/ip/checkipheader.cc:143-159 and the

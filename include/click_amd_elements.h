@@ -114,6 +114,12 @@ int clk_element_push_anno(clk_element *e, uint8_t *data, uint32_t length, int32_
  * appended to the element's result queue in push order.                  */
 int clk_element_flush(clk_element *e);
 
+/* Double-buffered flush: route the batch still on the GPU (if any), launch
+ * the staged one, and return without waiting, so the caller stages the
+ * next batch while this one runs (push_burst flushes this way).  Results
+ * of the launched batch arrive at the next flush / flush_async.           */
+int clk_element_flush_async(clk_element *e);
+
 /* Pop up to `cap` results: token, port (enum clk_port) and the packet's
  * new length (CheckIPHeader trims to ip_len, checkipheader.cc:216-217;
  * otherwise unchanged).  Returns the number popped.                        */
