@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CLK_ABI_VERSION 2
+#define CLK_ABI_VERSION 3
 
 /* ---- return codes -------------------------------------------------------- */
 #define CLK_SUCCESS 0

@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
         assert name in _abi.SIGNATURES, "ctypes binding lacks " + name
-    assert lib.clk_abi_version() == 2
+    assert lib.clk_abi_version() == 3
 
 
 def test_codes_agree_with_header_and_oracle():
@@ -69,6 +69,12 @@ int main(void) {
   printf("%zu %zu %zu %zu %zu %zu\n", sizeof(clk_ip_check_cfg), offsetof(clk_ip_check_cfg, checksum),
          offsetof(clk_ip_check_cfg, badsrc), offsetof(clk_ip_check_cfg, nbadsrc),
          offsetof(clk_ip_check_cfg, ngooddst), offsetof(clk_ip_check_cfg, gooddst));
+  printf("%zu %zu %zu %zu %zu\n", sizeof(clk_ip_out_cfg), offsetof(clk_ip_out_cfg, ts),
+         offsetof(clk_ip_out_cfg, my_addrs), offsetof(clk_ip_out_cfg, n_my_addrs), offsetof(clk_ip_out_cfg, mtu));
+  printf("%zu %zu %zu\n", sizeof(clk_frag_cfg), offsetof(clk_frag_cfg, honor_df), offsetof(clk_frag_cfg, new_id));
+  printf("%zu %zu %zu %zu %zu %zu\n", sizeof(clk_frag_out), offsetof(clk_frag_out, arena_bytes),
+         offsetof(clk_frag_out, frag_off), offsetof(clk_frag_out, frag_len), offsetof(clk_frag_out, frag_src),
+         offsetof(clk_frag_out, max_frags));
   return 0; }
 '''
     with tempfile.TemporaryDirectory() as d:
@@ -78,6 +84,14 @@ int main(void) {
         out = subprocess.run([os.path.join(d, "l")], capture_output=True, text=True, check=True).stdout.split("\n")
     b = [int(x) for x in out[0].split()]
     cfg = [int(x) for x in out[1].split()]
+    oc = [int(x) for x in out[2].split()]
+    fc = [int(x) for x in out[3].split()]
+    fo = [int(x) for x in out[4].split()]
+    O, F, FO = _abi.clk_ip_out_cfg, _abi.clk_frag_cfg, _abi.clk_frag_out
+    assert oc == [ctypes.sizeof(O), O.ts.offset, O.my_addrs.offset, O.n_my_addrs.offset, O.mtu.offset]
+    assert fc == [ctypes.sizeof(F), F.honor_df.offset, F.new_id.offset]
+    assert fo == [ctypes.sizeof(FO), FO.arena_bytes.offset, FO.frag_off.offset, FO.frag_len.offset,
+                  FO.frag_src.offset, FO.max_frags.offset]
     B = _abi.clk_batch
     assert b == [ctypes.sizeof(B), B.off.offset, B.stride.offset, B.len.offset, B.fixed_len.offset,
                  B.max_len.offset, B.n.offset]
