@@ -179,6 +179,65 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
     return out
 
 
+def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, seed=0x5EED):
+    """IPFragmenter(MTU 576, HONOR_DF true) over the C3 batch (16M x 1500 B
+    per GPU): every packet becomes a 572 B first fragment rewritten in place
+    plus 572 B and 396 B fragments appended to an HBM arena (16 B-aligned
+    slots).  The first-fragment header fields are restored between steps
+    (outside the HIP events); the numbers are kernel-time based.
+    Algorithmic bytes per packet: 1500 read + 968 appended + 8 rewritten."""
+    import click_amd
+    from click_amd import shard
+    w = WORKLOADS["c3"]
+    n, L, stride = w["n"], w["L"], w["stride"]
+    first, _ = shard.shard_range(rank, world, n * world)
+    arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    b = click_amd.Batch(arena, n, stride=stride, fixed_len=L)
+    ctx.gen_packets(b, proto=17, seed=seed, first_idx=first)
+    ctx.set_ip_checksum(b, want_sums=False)
+    hdr = arena.view(n, stride)[:, :12]
+    saved = hdr.clone()
+    out = torch.empty(n * (576 + 400), dtype=torch.uint8, device="cuda")
+    port = torch.empty(n, dtype=torch.uint8, device="cuda")
+    first_len = torch.empty(n, dtype=torch.int32, device="cuda")
+    frag_first = torch.empty(n, dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream()
+    r = None
+    for _ in range(warmup):
+        hdr.copy_(saved)
+        r = ctx.ip_fragment(b, mtu, True, arena=out, max_frags=2 * n, port=port, first_len=first_len,
+                            frag_first=frag_first)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    for k in range(steps):
+        hdr.copy_(saved)
+        ev[k][0].record(stream)
+        r = ctx.ip_fragment(b, mtu, True, arena=out, max_frags=2 * n, port=port, first_len=first_len,
+                            frag_first=frag_first)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    kms = [a.elapsed_time(z) for a, z in ev]
+    kernel_ms = sum(kms) / len(kms)
+    totals = [int(x) for x in r["totals"].cpu()]
+    ok = int((port == 2).sum()) if totals == [2 * n, 976 * n] else 0
+    dig = [ok, n, totals[0], 0]
+    _, kernel_ms, dig = shard.reduce_results(torch, dist, "cuda", 0.0, kernel_ms, dig)
+    del arena, out, saved, port, first_len, frag_first
+    torch.cuda.empty_cache()
+    alg = (1500 + 968 + 8) * n
+    ach = alg / (kernel_ms * 1e-3) / 1e9
+    return {"element": "IPFragmenter(576, HONOR_DF true)", "workload": w["desc"],
+            "kernel_ms": round(kernel_ms, 4), "kernel_ms_min": round(min(kms), 4),
+            "mpps": round(dig[1] / (kernel_ms * 1e-3) / 1e6, 1),
+            "fragments_per_s_M": round((dig[1] + dig[2]) / (kernel_ms * 1e-3) / 1e6, 1),
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg},
+            "verify": {"fragmented": dig[0], "packets": dig[1], "appended_fragments": dig[2]},
+            "note": "kernel time (plan + scan + write launches); first-fragment headers restored between steps"}
+
+
 def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5):
     """Measured HBM read-stream ceiling (16 B loads, grid-stride)."""
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
@@ -423,6 +482,7 @@ def main():
     ap.add_argument("--no-c2", action="store_true", help="skip the extra 64 B (C2) measurement")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-peak", action="store_true", help="skip the read-stream ceiling")
+    ap.add_argument("--no-frag", action="store_true", help="skip the IPFragmenter measurement (C3)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--e2e", action="store_true", help="measure the host-resident end-to-end rates instead")
     args = ap.parse_args()
@@ -459,6 +519,9 @@ def main():
     c2 = None
     if args.workload != "c2" and not args.no_c2:
         c2 = measure(torch, ctx, dist, rank, world, "c2", args.steps, args.warmup)
+    frag = None
+    if args.workload == "c3" and not args.no_frag:
+        frag = measure_fragmenter(torch, ctx, dist, rank, world, args.steps, args.warmup)
     peak_meas = None if args.no_peak else read_stream_peak(torch, ctx)
 
     if rank == 0:
@@ -484,6 +547,8 @@ def main():
             for e, r in c2.items():
                 line["c2_64b"]["elements"][e]["slot_GBs"] = round(
                     (64 + SLOT_EXTRA[e]) * r["n"] / (r["kernel_ms"] * 1e-3) / 1e9, 1)
+        if frag:
+            line["fragmenter"] = frag
         if world == 1 and not args.no_cpu and args.workload != "c4":
             try:
                 line["cpu_baseline"] = cpu_baseline(args.workload, head["element"], args.cpu_seconds)

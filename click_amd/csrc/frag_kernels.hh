@@ -8,12 +8,13 @@
 //                      slots); one (fragments, bytes) sum per 1024-packet tile.
 //   frag_scan_kernel   one block: exclusive scan of the tile sums, totals.
 //   frag_write_kernel  per tile: block scan of the per-packet counts; then
-//                      one wave per fragmenting packet rewrites the first
-//                      fragment's header in place (ip_len, MF, DF/ip_id,
-//                      ip_sum) and writes the other fragments -- header
-//                      (base header + copied options, per-fragment ip_off /
-//                      ip_len / ip_sum) and payload, 16 bytes per lane per
-//                      step from an unaligned source.
+//                      one 16-lane group per fragmenting packet (four per
+//                      wave) rewrites the first fragment's header in place
+//                      (ip_len, MF, DF/ip_id, ip_sum) and writes the other
+//                      fragments -- header (base header + copied options,
+//                      per-fragment ip_off / ip_len / ip_sum) and payload,
+//                      four 16 B chunks per lane in flight from an
+//                      unaligned source.
 // Appended fragments are packed in packet order, as the reference pushes
 // them, so the arena layout equals the oracle's (oracle_ip_fragment_batch).
 #pragma once
@@ -196,28 +197,34 @@ __device__ __forceinline__ void st_u32(uint8_t *p, uint32_t v)
     *(__attribute__((address_space(1))) uint32_t *)p = v;
 }
 
-// Header word sum over lanes [0, nw) of a wave (each lane one dword),
-// folded and complemented: click_in_cksum of the header with ip_sum = 0
-// (the caller zeroes lane 2's upper half).
-__device__ __forceinline__ uint32_t wave_header_cksum(uint32_t dw, uint32_t lane, uint32_t nw)
+// Header word sum over the lanes [0, nw) of a 16-lane group (each lane one
+// dword), folded and complemented: click_in_cksum of the header with
+// ip_sum = 0 (the caller zeroes the upper half of the group's lane 2).
+__device__ __forceinline__ uint32_t group_header_cksum(uint32_t dw, uint32_t gl, uint32_t nw)
 {
-    uint32_t s = lane < nw ? (dw & 0xFFFF) + (dw >> 16) : 0u;
-    for (int m = 32; m >= 1; m >>= 1)
+    uint32_t s = gl < nw ? (dw & 0xFFFF) + (dw >> 16) : 0u;
+#pragma unroll
+    for (int m = 8; m >= 1; m >>= 1)
         s += __shfl_xor(s, m, 64);
     return in_cksum_fold(s);
 }
 
-// K3: write.  Block = one tile.
+constexpr uint32_t FRAG_G = 16;          // lanes per fragmenting packet in frag_write_kernel
+constexpr int FRAG_U = 4;                // 16 B payload loads in flight per lane
+
+// K3: write.  Block = one tile; 16 groups of 16 lanes, group g takes the
+// tile's packets g, g+16, ...  (the same trip count for every group).
 __global__ void __launch_bounds__(256) frag_write_kernel(BatchArgs b, FragArgs f, const uint8_t *port,
                                                          const uint32_t *pl_n, const uint32_t *pl_b,
                                                          const uint64_t *tile_sums, uint64_t *out_frag_first)
 {
     __shared__ uint32_t pn[FRAG_TILE], pb[FRAG_TILE];     // exclusive prefixes within the tile
     __shared__ uint32_t wsum[2][4];
-    __shared__ uint32_t hdr[4][16];                        // per wave: header dwords, then copied options
-    __shared__ uint32_t optw[4][11];                       // per wave: copied options (<= 40 B + pad)
+    __shared__ uint32_t hdr[16][16];                       // per group: the rewritten header dwords
+    __shared__ uint32_t optw[16][11];                      // per group: copied options (<= 40 B + pad)
     const uint64_t tile = (uint64_t)blockIdx.x * FRAG_TILE;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t gl = lane & (FRAG_G - 1), grp = threadIdx.x / FRAG_G, g0 = lane & ~(FRAG_G - 1);
     // block exclusive scan of (nextra, bytes): thread t owns packets 4t..4t+3 of the tile
     uint32_t vn[4], vb[4], tn = 0, tb = 0;
 #pragma unroll
@@ -258,8 +265,8 @@ __global__ void __launch_bounds__(256) frag_write_kernel(BatchArgs b, FragArgs f
     const uint64_t fbase = tile_sums[2 * blockIdx.x], bbase = tile_sums[2 * blockIdx.x + 1];
     for (uint32_t j = threadIdx.x; j < FRAG_TILE && tile + j < b.n; j += blockDim.x)
         out_frag_first[tile + j] = fbase + pn[j];
-    // one wave per fragmenting packet
-    for (uint32_t j = wv; j < FRAG_TILE; j += 4) {
+    // one 16-lane group per fragmenting packet
+    for (uint32_t j = grp; j < FRAG_TILE; j += 256 / FRAG_G) {
         const uint64_t i = tile + j;
         if (i >= b.n)
             break;
@@ -267,38 +274,37 @@ __global__ void __launch_bounds__(256) frag_write_kernel(BatchArgs b, FragArgs f
             continue;
         uint8_t *ip = b.base + pkt_off(b, i);
         const uint32_t caplen = pkt_len(b, i);
-        const FragPlan p = frag_plan(ip, caplen, f.mtu, f.honor_df);   // wave-uniform; port 2
+        const FragPlan p = frag_plan(ip, caplen, f.mtu, f.honor_df);   // group-uniform; port 2
         const uint32_t nw = p.hlen >> 2;
-        uint32_t dw = lane < nw ? ld_u32_unaligned(ip + 4 * lane) : 0u;
+        uint32_t dw = gl < nw ? ld_u32_unaligned(ip + 4 * gl) : 0u;
         // the first fragment's header (112-120)
-        const bool df = (__shfl(dw, 1, 64) >> 16) & 0x40;
-        const bool had_mf = (__shfl(dw, 1, 64) >> 16) & 0x20;
-        if (lane == 0)
+        const uint32_t w1 = __shfl(dw, g0 + 1, 64);
+        const bool df = (w1 >> 16) & 0x40, had_mf = (w1 >> 16) & 0x20;
+        if (gl == 0)
             dw = (dw & 0xFFFF) | (bswap16(p.hlen + (uint32_t)p.first_dlen) << 16);
-        if (lane == 1) {
+        if (gl == 1) {
             if (df && f.new_id)
                 dw = (dw & 0xFFFF0000u) | f.new_id[i];
             dw = (dw & ~(0x40u << 16)) | (0x20u << 16);
         }
-        if (lane == 2)
+        if (gl == 2)
             dw &= 0xFFFF;
-        const uint32_t sum = wave_header_cksum(dw, lane, nw);
-        if (lane == 2)
+        const uint32_t sum = group_header_cksum(dw, gl, nw);
+        if (gl == 2)
             dw |= sum << 16;
-        if (lane < 16)
-            hdr[wv][lane] = dw;
+        hdr[grp][gl] = dw;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (lane == 0) {
-            const uint32_t h0 = hdr[wv][0], h1 = hdr[wv][1], h2 = hdr[wv][2];
+        if (gl == 0) {
+            const uint32_t h0 = hdr[grp][0], h1 = hdr[grp][1], h2 = hdr[grp][2];
             st_u16(ip + 2, h0 >> 16);
             st_u16(ip + 4, h1 & 0xFFFF);
             st_u16(ip + 6, h1 >> 16);
             st_u16(ip + 10, h2 >> 16);
             // copied options (53-86) into optw[], EOL-padded
-            const uint8_t *hb = (const uint8_t *)hdr[wv];
-            uint8_t *ob = (uint8_t *)optw[wv];
+            const uint8_t *hb = (const uint8_t *)hdr[grp];
+            uint8_t *ob = (uint8_t *)optw[grp];
             uint32_t k = 20, o = 0;
             while (k < p.hlen) {
                 const uint32_t t = hb[k];
@@ -326,14 +332,14 @@ __global__ void __launch_bounds__(256) frag_write_kernel(BatchArgs b, FragArgs f
         // header + copied options (140-144)
         const uint32_t qw = p.out_hlen >> 2;
         uint32_t tpl = 0;
-        if (lane < 5)
-            tpl = hdr[wv][lane];
-        else if (lane < qw)
-            tpl = optw[wv][lane - 5];
-        if (lane == 0)
+        if (gl < 5)
+            tpl = hdr[grp][gl];
+        else if (gl < qw)
+            tpl = optw[grp][gl - 5];
+        if (gl == 0)
             tpl = (tpl & ~0xFu) | (qw & 0xF);                // ip_hl (144)
-        const uint32_t off_first = bswap16(hdr[wv][1] >> 16);  // ntohs(ip->ip_off) after 112-118
-        uint64_t fidx = tile_sums[2 * blockIdx.x] + pn[j];
+        const uint32_t off_first = bswap16(hdr[grp][1] >> 16);  // ntohs(ip->ip_off) after 112-118
+        uint64_t fidx = fbase + pn[j];
         uint64_t bpos = bbase + pb[j];
         const uint64_t src_end = (uint64_t)ip + caplen;
         for (uint32_t k = 0; k < p.nextra; k++) {
@@ -346,37 +352,49 @@ __global__ void __launch_bounds__(256) frag_write_kernel(BatchArgs b, FragArgs f
             if (fits) {
                 uint8_t *q = f.arena + bpos;
                 uint32_t h = tpl;
-                if (lane == 0)
+                if (gl == 0)
                     h = (h & 0xFFFF) | (bswap16(qlen) << 16);     // 148
-                if (lane == 1) {
+                if (gl == 1) {
                     uint32_t fo = (off_first + ((uint32_t)off >> 3)) & 0xFFFF;   // 145
                     if ((int)dlen + off >= p.in_dlen && !had_mf)  // 146-147
                         fo &= ~0x2000u;
                     h = (h & 0xFFFF) | (bswap16(fo) << 16);
                 }
-                if (lane == 2)
+                if (gl == 2)
                     h &= 0xFFFF;                                  // 149
-                const uint32_t s = wave_header_cksum(h, lane, qw);
-                if (lane == 2)
+                const uint32_t s = group_header_cksum(h, gl, qw);
+                if (gl == 2)
                     h |= s << 16;                                 // 150
-                if (lane < qw)
-                    st_u32(q + 4 * lane, h);
-                // payload (142): 16 bytes per lane per step
+                if (gl < qw)
+                    st_u32(q + 4 * gl, h);
+                // payload (142): FRAG_U 16 B chunks per lane in flight
                 const uint64_t src0 = (uint64_t)ip + p.hlen + (uint32_t)off;
                 const uint64_t hi = src0 + dlen < src_end ? src0 + dlen : src_end;
-                for (uint32_t c = lane; 16 * c < dlen; c += 64) {
-                    const u32x4 v = load16_guarded(src0 + 16ull * c, hi);
-                    const uint32_t at = p.out_hlen + 16 * c;      // 4-aligned; the slot ends at `slot`
-                    if (at + 16 <= slot) {
-                        *(__attribute__((address_space(1))) u32x4_a4 *)(q + at) = v;
-                    } else {
+                const uint32_t nch = (dlen + 15) / 16;
+                for (uint32_t c0 = 0; c0 < nch; c0 += FRAG_G * FRAG_U) {
+                    u32x4 v[FRAG_U];
 #pragma unroll
-                        for (int d = 0; d < 4; d++)
-                            if (at + 4 * d < slot)
-                                st_u32(q + at + 4 * d, v[d]);
+                    for (int u = 0; u < FRAG_U; u++) {
+                        const uint32_t c = c0 + u * FRAG_G + gl;
+                        v[u] = c < nch ? load16_guarded(src0 + 16ull * c, hi) : u32x4{0, 0, 0, 0};
+                    }
+#pragma unroll
+                    for (int u = 0; u < FRAG_U; u++) {
+                        const uint32_t c = c0 + u * FRAG_G + gl;
+                        if (c >= nch)
+                            continue;
+                        const uint32_t at = p.out_hlen + 16 * c;  // 4-aligned; the slot ends at `slot`
+                        if (at + 16 <= slot) {
+                            *(__attribute__((address_space(1))) u32x4_a4 *)(q + at) = v[u];
+                        } else {
+#pragma unroll
+                            for (int d = 0; d < 4; d++)
+                                if (at + 4 * d < slot)
+                                    st_u32(q + at + 4 * d, v[u][d]);
+                        }
                     }
                 }
-                if (lane == 0) {
+                if (gl == 0) {
                     f.frag_off[fidx] = bpos;
                     f.frag_len[fidx] = qlen;
                     f.frag_src[fidx] = (uint32_t)i;
