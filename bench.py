@@ -185,7 +185,10 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
     plus 572 B and 396 B fragments appended to an HBM arena (16 B-aligned
     slots).  The first-fragment header fields are restored between steps
     (outside the HIP events); the numbers are kernel-time based.
-    Algorithmic bytes per packet: 1500 read + 968 appended + 8 rewritten."""
+    Algorithmic bytes per packet: the 20 B header and the 928 payload bytes
+    the appended fragments carry are read (the first fragment's payload
+    stays in place); 968 B of fragments are appended and 8 header bytes
+    rewritten in place: 1924 B."""
     import click_amd
     from click_amd import shard
     w = WORKLOADS["c3"]
@@ -226,7 +229,7 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
     _, kernel_ms, dig = shard.reduce_results(torch, dist, "cuda", 0.0, kernel_ms, dig)
     del arena, out, saved, port, first_len, frag_first
     torch.cuda.empty_cache()
-    alg = (1500 + 968 + 8) * n
+    alg = (20 + 928 + 968 + 8) * n
     ach = alg / (kernel_ms * 1e-3) / 1e9
     return {"element": "IPFragmenter(576, HONOR_DF true)", "workload": w["desc"],
             "kernel_ms": round(kernel_ms, 4), "kernel_ms_min": round(min(kms), 4),
