@@ -10,7 +10,9 @@ CheckUDPHeader (full-payload checksum + verdict, read-bound), and
 SetUDPChecksum (checksum written in place) is timed beside it under
 "elements".  The 64 B min-size batch (C2: CheckIPHeader and SetIPChecksum
 over 16M packets in 64 B slots) is measured in the same run under "c2_64b"
-because the metric names both sizes.
+because the metric names both sizes; the IMIX (C4, "c4_imix") and 9000 B
+(C5, "c5_jumbo": 16M per GPU, 128M at 8 GPUs) configurations and the
+IPFragmenter (C3 to MTU 576, "fragmenter") follow.
 Multi-GPU (torchrun, one process per GPU): every rank generates and
 processes its own shard of global packet indices -- packets are independent,
 so there is no collective in the data path (weak scaling); one RCCL
@@ -486,6 +488,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-peak", action="store_true", help="skip the read-stream ceiling")
     ap.add_argument("--no-frag", action="store_true", help="skip the IPFragmenter measurement (C3)")
+    ap.add_argument("--skip", default="", help="comma list of side configurations to skip: c4,c5")
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--e2e", action="store_true", help="measure the host-resident end-to-end rates instead")
     args = ap.parse_args()
@@ -522,6 +525,12 @@ def main():
     c2 = None
     if args.workload != "c2" and not args.no_c2:
         c2 = measure(torch, ctx, dist, rank, world, "c2", args.steps, args.warmup)
+    # the other configurations of BASELINE.json, reported beside the
+    # headline (C4: IMIX 64M; C5: 9000 B, 16M per GPU = 128M at N = 8)
+    extra = {}
+    for sect, wl in (("c4_imix", "c4"), ("c5_jumbo", "c5")):
+        if args.workload != wl and wl not in args.skip.split(","):
+            extra[sect] = (wl, measure(torch, ctx, dist, rank, world, wl, args.steps, args.warmup))
     frag = None
     if args.workload == "c3" and not args.no_frag:
         frag = measure_fragmenter(torch, ctx, dist, rank, world, args.steps, args.warmup)
@@ -550,6 +559,9 @@ def main():
             for e, r in c2.items():
                 line["c2_64b"]["elements"][e]["slot_GBs"] = round(
                     (64 + SLOT_EXTRA[e]) * r["n"] / (r["kernel_ms"] * 1e-3) / 1e9, 1)
+        for sect, (wl, res) in extra.items():
+            line[sect] = {"workload": WORKLOADS[wl]["desc"],
+                          "elements": {e: summarize(r, args.steps, wl) for e, r in res.items()}}
         if frag:
             line["fragmenter"] = frag
         if world == 1 and not args.no_cpu and args.workload != "c4":
