@@ -132,6 +132,9 @@ constexpr int K = CLK_K;   // 16-byte chunk loads in flight per lane per pass
 #ifndef CLK_SPF
 #define CLK_SPF 0          // packet-stream kernel: prefetch the next pass (tuning knob)
 #endif
+#ifndef CLK_SMARK
+#define CLK_SMARK 0        // packet-stream kernel: chunk->packet by marks + wave max-scan (tuning knob)
+#endif
 
 // Lanes per packet: the fewest (of 1, 4, 16, 64) whose K-deep pass covers
 // the largest packet in one pass; 64 beyond that (multi-pass).
@@ -283,10 +286,10 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
         if (blocks > (uint64_t)ctx->max_blocks)
             blocks = (uint64_t)ctx->max_blocks;
         if (work)
-            hipLaunchKernelGGL((clk::l4_stream_kernel<PROTO, SET, true, KV, CLK_SPF != 0>), dim3((unsigned)blocks), dim3(BLOCK), 0,
+            hipLaunchKernelGGL((clk::l4_stream_kernel<PROTO, SET, true, KV, CLK_SPF != 0, CLK_SMARK != 0>), dim3((unsigned)blocks), dim3(BLOCK), 0,
                                ctx->cur, args_of(b), fixoff, code, sum, work);
         else
-            hipLaunchKernelGGL((clk::l4_stream_kernel<PROTO, SET, false, KV, CLK_SPF != 0>), dim3((unsigned)blocks), dim3(BLOCK),
+            hipLaunchKernelGGL((clk::l4_stream_kernel<PROTO, SET, false, KV, CLK_SPF != 0, CLK_SMARK != 0>), dim3((unsigned)blocks), dim3(BLOCK),
                                0, ctx->cur, args_of(b), fixoff, code, sum, work);
     } else if (bins && ctx->varlen) {
         constexpr int KV = CLK_KV, VU = CLK_VU;

@@ -21,6 +21,12 @@
 #ifndef CLK_NT_STORES
 #define CLK_NT_STORES 0    // tuning knob: nontemporal checksum-field stores
 #endif
+#ifndef CLK_SHC_EXTRA
+#define CLK_SHC_EXTRA 0    // packet-stream kernel: head chunks stashed beyond the aligned-header minimum
+#endif
+#ifndef CLK_SWPE
+#define CLK_SWPE 8         // packet-stream kernel: request this many waves per SIMD (0: compiler default)
+#endif
 #ifndef CLK_BLOCK_WRITE
 #define CLK_BLOCK_WRITE 0  // tuning knob: fused Set stores rewrite the whole 64 B block (measured slower)
 #endif
@@ -764,17 +770,25 @@ __device__ __forceinline__ uint32_t chunk_outside(const u32x4 V, uint64_t ca, ui
 //            bytes) is re-summed from global memory by its lane.
 // The sum mod 2^32 is order-free (cksum_device.hh), so whole-chunk sums
 // minus the excluded bytes equal the reference's word sum exactly.
-template <int PROTO, bool SET, bool DEFER, int KV, bool PF>
-__global__ void __launch_bounds__(256) l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
+template <int PROTO, bool SET, bool DEFER, int KV, bool PF, bool MARKS>
+__global__ void __launch_bounds__(256)
+#if CLK_SWPE
+__attribute__((amdgpu_waves_per_eu(CLK_SWPE)))
+#endif
+l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                         uint16_t *out_sum, uint32_t *work)
 {
     constexpr int HDR_DW = L4Hdr<PROTO>::DW;
-    constexpr int HC = PROTO == TCP ? 4 : 3;        // stashed head chunks: (nh&~3) - c0 + 4*HDR_DW <= 16*HC
+    // stashed head chunks: every header dword when (nh&~3) - c0 + 4*HDR_DW <= 16*HC
+    // (always for HC = 4 / 3; for 16 B-aligned packets with 3 / 2), else
+    // the parse loads the missing dwords itself
+    constexpr int HC = PROTO == TCP ? 3 + CLK_SHC_EXTRA : 2 + CLK_SHC_EXTRA;
     __shared__ u32x4 head[4][64][HC];
     __shared__ u32x4 tail[4][64];
     __shared__ u32x4 pk[4][64];       // {c0 lo, c0 hi, chunk start, nch | odd << 31}
     __shared__ uint32_t cst[4][68];   // chunk starts; cst[64] = total
     __shared__ uint32_t acc[4][64];
+    __shared__ uint32_t mark[4][MARKS ? 64 * KV : 1];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t nruns = (b.n + 63) / 64;
     const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
@@ -808,26 +822,70 @@ __global__ void __launch_bounds__(256) l4_stream_kernel(BatchArgs b, int fixoff,
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // issue: find the packets of this lane's KV chunks at cb and load them
+        uint32_t carry = 0;          // MARKS: 1 + the packet of the chunk before this pass (wave-uniform)
         auto issue = [&](uint32_t cb, u32x4 (&v)[KV], uint32_t (&jk)[KV], u32x4 (&Pk)[KV]) {
             const uint32_t cl = cb + lane * KV;
-            uint32_t j = 0;                                    // last packet whose chunk start <= cl
+            if (MARKS) {
+                // each packet marks its first chunk in the pass window, a
+                // wave max-scan carries the packet index to every chunk:
+                // no dependent LDS chain
 #pragma unroll
-            for (int step = 32; step >= 1; step >>= 1)
-                if (cst[wv][j + step] <= cl)
-                    j += step;
-            uint32_t nxt = cst[wv][j + 1];
-            u32x4 P = pk[wv][j];
+                for (int k = 0; k < KV; k++)
+                    mark[wv][lane * KV + k] = 0;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t my_start = incl - nch;
+                if (nch && my_start >= cb && my_start - cb < 64u * KV)
+                    mark[wv][my_start - cb] = lane + 1;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                uint32_t m[KV], lm = 0;
+#pragma unroll
+                for (int k = 0; k < KV; k++) {
+                    m[k] = mark[wv][lane * KV + k];
+                    lm = m[k] > lm ? m[k] : lm;
+                }
+                uint32_t x = lm;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t t = __shfl_up(x, d, 64);
+                    if ((int)lane >= d)
+                        x = t > x ? t : x;
+                }
+                uint32_t run = __shfl_up(x, 1, 64);
+                run = lane == 0 ? carry : (run > carry ? run : carry);
+                const uint32_t last = __shfl(x, 63, 64);
+                carry = last > carry ? last : carry;
+#pragma unroll
+                for (int k = 0; k < KV; k++) {
+                    run = m[k] > run ? m[k] : run;
+                    jk[k] = run ? run - 1 : 0;
+                }
+            } else {
+                uint32_t j = 0;                                    // last packet whose chunk start <= cl
+#pragma unroll
+                for (int step = 32; step >= 1; step >>= 1)
+                    if (cst[wv][j + step] <= cl)
+                        j += step;
+                uint32_t nxt = cst[wv][j + 1];
+#pragma unroll
+                for (int k = 0; k < KV; k++) {
+                    const uint32_t c = cl + k;
+                    if (c < total && c >= nxt) {
+                        do {
+                            j++;
+                            nxt = cst[wv][j + 1];
+                        } while (c >= nxt);
+                    }
+                    jk[k] = j;
+                }
+            }
 #pragma unroll
             for (int k = 0; k < KV; k++) {
                 const uint32_t c = cl + k;
-                if (c < total && c >= nxt) {
-                    do {
-                        j++;
-                        nxt = cst[wv][j + 1];
-                    } while (c >= nxt);
-                    P = pk[wv][j];
-                }
-                jk[k] = j;
+                const u32x4 P = pk[wv][jk[k]];
                 Pk[k] = P;
                 const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
                 if (UseNT<false>::value)
@@ -910,7 +968,9 @@ __global__ void __launch_bounds__(256) l4_stream_kernel(BatchArgs b, int fixoff,
             uint32_t d[HDR_DW];
 #pragma unroll
             for (int k = 0; k < HDR_DW; k++)
-                d[k] = (a & ~3ull) + 4 * k < end ? hw[q0 + k] : 0u;
+                d[k] = (a & ~3ull) + 4 * k >= end ? 0u
+                       : q0 + k < 4u * HC      ? hw[q0 + k]
+                                               : gload4((a & ~3ull) + 4 * k);
             L4State st;
             l4_parse_words<PROTO, SET>(nh, caplen, fixoff, d, st);
             uint32_t sum = 0;

@@ -54,6 +54,11 @@ VARIANTS = {
     "skv8": (["-DCLK_SKV=8"], {"CLK_VARLEN": "2"}),
     "fused_stream": ([], {"CLK_SET_MODE": "0", "CLK_VARLEN": "2"}),
     "two_stream": ([], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
+    "hc2": (["-DCLK_SHC_EXTRA=0"], {}),
+    "hc2w8": (["-DCLK_SHC_EXTRA=0", "-DCLK_SWPE=8"], {}),
+    "w8": (["-DCLK_SWPE=8"], {}),
+    "smark": (["-DCLK_SMARK=1"], {}),
+    "smark_kv4": (["-DCLK_SMARK=1", "-DCLK_SKV=4"], {}),
     "spf": (["-DCLK_SPF=1"], {}),
     "spf_kv1": (["-DCLK_SPF=1", "-DCLK_SKV=1"], {}),
     "spf_kv4": (["-DCLK_SPF=1", "-DCLK_SKV=4"], {}),
