@@ -13,8 +13,9 @@
 //                      (ip_len, MF, DF/ip_id, ip_sum) and writes the other
 //                      fragments -- header (base header + copied options,
 //                      per-fragment ip_off / ip_len / ip_sum) and payload,
-//                      four 16 B chunks per lane in flight from an
-//                      unaligned source.
+//                      four unaligned 16 B loads per lane in flight, all
+//                      issued before the packet's stores; the next
+//                      packet's header is prefetched meanwhile.
 // Appended fragments are packed in packet order, as the reference pushes
 // them, so the arena layout equals the oracle's (oracle_ip_fragment_batch).
 #pragma once
@@ -192,6 +193,39 @@ __device__ __forceinline__ u32x4 load16_guarded(uint64_t p, uint64_t hi)
     return r;
 }
 
+#ifndef CLK_FRAG_HDR_FIRST
+#define CLK_FRAG_HDR_FIRST 0
+#endif
+#ifndef CLK_FRAG_UA
+#define CLK_FRAG_UA 1
+#endif
+#ifndef CLK_FRAG_NT_STORE
+#define CLK_FRAG_NT_STORE 0
+#endif
+#ifndef CLK_FRAG_NT_LOAD
+#define CLK_FRAG_NT_LOAD 0
+#endif
+// load16_guarded at ip + o with the bound ip + hi (offsets < 64 KiB).
+__device__ __forceinline__ u32x4 load16_rel(const uint8_t *ip, uint32_t o, uint32_t hi)
+{
+#if CLK_FRAG_UA
+    typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
+    if (o + 16 <= hi)                    // one global_load_dwordx4 (the HSA queues run in unaligned mode)
+        return *(const __attribute__((address_space(1))) u32x4_a1 *)(ip + o);
+#endif
+    const uint32_t q = o & ~3u, sh = o & 3;
+    uint32_t d[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        d[k] = q + 4 * k < hi ? (CLK_FRAG_NT_LOAD ? __builtin_nontemporal_load((const __attribute__((address_space(1))) uint32_t *)(ip + q + 4 * k))
+                                                  : gload4((uint64_t)ip + q + 4 * k)) : 0u;
+    u32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        r[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh) & lowmask((int)(hi - (o + 4 * j)));
+    return r;
+}
+
 __device__ __forceinline__ void st_u32(uint8_t *p, uint32_t v)
 {
     *(__attribute__((address_space(1))) uint32_t *)p = v;
@@ -204,24 +238,47 @@ __device__ __forceinline__ uint32_t group_header_cksum(uint32_t dw, uint32_t gl,
 {
     uint32_t s = gl < nw ? (dw & 0xFFFF) + (dw >> 16) : 0u;
 #pragma unroll
-    for (int m = 8; m >= 1; m >>= 1)
+    for (int m = 8; m >= 1; m >>= 1)              // the header is within the group's first 16 lanes
         s += __shfl_xor(s, m, 64);
     return in_cksum_fold(s);
 }
 
-constexpr uint32_t FRAG_G = 16;          // lanes per fragmenting packet in frag_write_kernel
-constexpr int FRAG_U = 4;                // 16 B payload loads in flight per lane
+#ifndef CLK_FRAG_G
+#define CLK_FRAG_G 16
+#endif
+#ifndef CLK_FRAG_U
+#define CLK_FRAG_U 4
+#endif
+constexpr uint32_t FRAG_G = CLK_FRAG_G;  // lanes per fragmenting packet in frag_write_kernel (16, 32, 64)
+constexpr int FRAG_U = CLK_FRAG_U;       // 16 B payload loads in flight per lane
+#ifndef CLK_FRAG_WPE
+#define CLK_FRAG_WPE 4
+#endif
+
+// Header dword gl (< 15) of a packet, 0 past caplen: the prefetch of the
+// next fragmenting packet's header (port 2 implies caplen > mtu >= hlen + 8).
+__device__ __forceinline__ uint32_t frag_hdr_dword(const uint8_t *ip, uint32_t caplen, uint32_t gl)
+{
+    return gl < 15 && 4 * gl + 4 <= caplen ? ld_u32_unaligned(ip + 4 * gl) : 0u;
+}
 
 // K3: write.  Block = one tile; 16 groups of 16 lanes, group g takes the
-// tile's packets g, g+16, ...  (the same trip count for every group).
-__global__ void __launch_bounds__(256) frag_write_kernel(BatchArgs b, FragArgs f, const uint8_t *port,
+// tile's fragmenting packets among g, g+16, ...  Per packet the only
+// dependent global round trip is the payload's: the next packet's header is
+// prefetched while this one is written, the plan is rebuilt from the header
+// registers (options from LDS), and the payload of all appended fragments
+// is one chunk space loaded before any store of the packet is issued (gfx9
+// counts stores in vmcnt too).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FRAG_WPE))) frag_write_kernel(BatchArgs b, FragArgs f, const uint8_t *port,
                                                          const uint32_t *pl_n, const uint32_t *pl_b,
                                                          const uint64_t *tile_sums, uint64_t *out_frag_first)
 {
+    constexpr uint32_t NG = 256 / FRAG_G;
     __shared__ uint32_t pn[FRAG_TILE], pb[FRAG_TILE];     // exclusive prefixes within the tile
+    __shared__ uint8_t lport[FRAG_TILE];
     __shared__ uint32_t wsum[2][4];
-    __shared__ uint32_t hdr[16][16];                       // per group: the rewritten header dwords
-    __shared__ uint32_t optw[16][11];                      // per group: copied options (<= 40 B + pad)
+    __shared__ uint32_t hdr[NG][16];                       // per group: the packet's header dwords
+    __shared__ uint32_t optw[NG][11];                      // per group: copied options (<= 40 B + pad)
     const uint64_t tile = (uint64_t)blockIdx.x * FRAG_TILE;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t gl = lane & (FRAG_G - 1), grp = threadIdx.x / FRAG_G, g0 = lane & ~(FRAG_G - 1);
@@ -232,6 +289,7 @@ __global__ void __launch_bounds__(256) frag_write_kernel(BatchArgs b, FragArgs f
         const uint64_t i = tile + 4 * threadIdx.x + k;
         vn[k] = i < b.n ? pl_n[i] : 0u;
         vb[k] = i < b.n ? pl_b[i] : 0u;
+        lport[4 * threadIdx.x + k] = i < b.n ? port[i] : 0u;
         tn += vn[k];
         tb += vb[k];
     }
@@ -265,23 +323,84 @@ __global__ void __launch_bounds__(256) frag_write_kernel(BatchArgs b, FragArgs f
     const uint64_t fbase = tile_sums[2 * blockIdx.x], bbase = tile_sums[2 * blockIdx.x + 1];
     for (uint32_t j = threadIdx.x; j < FRAG_TILE && tile + j < b.n; j += blockDim.x)
         out_frag_first[tile + j] = fbase + pn[j];
-    // one 16-lane group per fragmenting packet
-    for (uint32_t j = grp; j < FRAG_TILE; j += 256 / FRAG_G) {
+    const uint32_t lim = b.n - tile < FRAG_TILE ? (uint32_t)(b.n - tile) : FRAG_TILE;
+    auto next_j = [&](uint32_t j) {
+        while (j < lim && lport[j] != 2)
+            j += NG;
+        return j;
+    };
+    uint32_t j = next_j(grp);
+    const uint8_t *nip = nullptr;
+    uint32_t ncap = 0, ndw = 0;
+    if (j < lim) {
+        nip = b.base + pkt_off(b, tile + j);
+        ncap = pkt_len(b, tile + j);
+        ndw = frag_hdr_dword(nip, ncap, gl);
+    }
+    while (j < lim) {
         const uint64_t i = tile + j;
-        if (i >= b.n)
-            break;
-        if (port[i] != 2)
-            continue;
-        uint8_t *ip = b.base + pkt_off(b, i);
-        const uint32_t caplen = pkt_len(b, i);
-        const FragPlan p = frag_plan(ip, caplen, f.mtu, f.honor_df);   // group-uniform; port 2
-        const uint32_t nw = p.hlen >> 2;
-        uint32_t dw = gl < nw ? ld_u32_unaligned(ip + 4 * gl) : 0u;
-        // the first fragment's header (112-120)
-        const uint32_t w1 = __shfl(dw, g0 + 1, 64);
+        uint8_t *ip = (uint8_t *)nip;
+        const uint32_t caplen = ncap;
+        uint32_t dw = ndw;
+        const uint32_t jn = next_j(j + NG);
+        if (jn < lim) {                                    // prefetch the group's next packet
+            nip = b.base + pkt_off(b, tile + jn);
+            ncap = pkt_len(b, tile + jn);
+            ndw = frag_hdr_dword(nip, ncap, gl);
+        }
+        // the plan (frag_plan for a port-2 packet), from the header registers
+        const uint32_t w0 = __shfl(dw, g0, 64), w1 = __shfl(dw, g0 + 1, 64);
+        const uint32_t hlen = (w0 & 0xF) << 2, nw = hlen >> 2;                 // 92
+        const int first_dlen = (int)((f.mtu - hlen) & ~7u);                     // 93
+        const int in_dlen = (int)bswap16(w0 >> 16) - (int)hlen;                // 94
+        if (gl < 16)
+            hdr[grp][gl] = gl < nw ? dw : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // copied options (53-86): every lane walks the LDS bytes, lane 0 copies
+        uint32_t olen = 0;
+        {
+            const uint8_t *hb = (const uint8_t *)hdr[grp];
+            uint8_t *ob = (uint8_t *)optw[grp];
+            uint32_t k = 20;
+            while (k < hlen) {
+                const uint32_t t = hb[k];
+                if (t == 1) {
+                    k++;
+                    continue;
+                }
+                if (t == 0 || k + 1 == hlen)
+                    break;
+                const uint32_t l = hb[k + 1];
+                if (l < 2 || k + l > hlen)
+                    break;
+                if (t & 0x80) {
+                    if (gl == 0)
+                        for (uint32_t c = 0; c < l; c++)
+                            ob[olen + c] = hb[k + c];
+                    olen += l;
+                }
+                k += l;
+            }
+            if (gl == 0)
+                for (uint32_t c = olen; c & 3; c++)
+                    ob[c] = 0;
+            olen = (olen + 3) & ~3u;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t out_hlen = 20 + olen, qw = out_hlen >> 2;               // 127
+        const uint32_t step = (f.mtu - out_hlen) & ~7u;                         // 131
+        const int rem = in_dlen - first_dlen;
+        const uint32_t nextra = rem > 0 ? ((uint32_t)rem + step - 1) / step : 0u;
+        const uint32_t last = rem > 0 ? (uint32_t)rem - (nextra - 1) * step : 0u;
+        const uint32_t slot_f = slot16(out_hlen + step);
+        // the first fragment's header (112-120), in the lanes' registers
         const bool df = (w1 >> 16) & 0x40, had_mf = (w1 >> 16) & 0x20;
         if (gl == 0)
-            dw = (dw & 0xFFFF) | (bswap16(p.hlen + (uint32_t)p.first_dlen) << 16);
+            dw = (dw & 0xFFFF) | (bswap16(hlen + (uint32_t)first_dlen) << 16);
         if (gl == 1) {
             if (df && f.new_id)
                 dw = (dw & 0xFFFF0000u) | f.new_id[i];
@@ -292,117 +411,113 @@ __global__ void __launch_bounds__(256) frag_write_kernel(BatchArgs b, FragArgs f
         const uint32_t sum = group_header_cksum(dw, gl, nw);
         if (gl == 2)
             dw |= sum << 16;
-        hdr[grp][gl] = dw;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (gl == 0) {
-            const uint32_t h0 = hdr[grp][0], h1 = hdr[grp][1], h2 = hdr[grp][2];
-            st_u16(ip + 2, h0 >> 16);
-            st_u16(ip + 4, h1 & 0xFFFF);
-            st_u16(ip + 6, h1 >> 16);
-            st_u16(ip + 10, h2 >> 16);
-            // copied options (53-86) into optw[], EOL-padded
-            const uint8_t *hb = (const uint8_t *)hdr[grp];
-            uint8_t *ob = (uint8_t *)optw[grp];
-            uint32_t k = 20, o = 0;
-            while (k < p.hlen) {
-                const uint32_t t = hb[k];
-                if (t == 1) {
-                    k++;
-                    continue;
-                }
-                if (t == 0 || k + 1 == p.hlen)
-                    break;
-                const uint32_t l = hb[k + 1];
-                if (l < 2 || k + l > p.hlen)
-                    break;
-                if (t & 0x80)
-                    for (uint32_t c = 0; c < l; c++)
-                        ob[o++] = hb[k + c];
-                k += l;
-            }
-            while (o & 3)
-                ob[o++] = 0;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // the fragment header template: base 20 bytes of the rewritten
         // header + copied options (140-144)
-        const uint32_t qw = p.out_hlen >> 2;
-        uint32_t tpl = 0;
-        if (gl < 5)
-            tpl = hdr[grp][gl];
-        else if (gl < qw)
-            tpl = optw[grp][gl - 5];
+        uint32_t tpl = gl < 5 ? dw : (gl < qw ? optw[grp][gl - 5] : 0u);
         if (gl == 0)
-            tpl = (tpl & ~0xFu) | (qw & 0xF);                // ip_hl (144)
-        const uint32_t off_first = bswap16(hdr[grp][1] >> 16);  // ntohs(ip->ip_off) after 112-118
-        uint64_t fidx = fbase + pn[j];
-        uint64_t bpos = bbase + pb[j];
-        const uint64_t src_end = (uint64_t)ip + caplen;
-        for (uint32_t k = 0; k < p.nextra; k++) {
-            const int off = p.first_dlen + (int)(k * p.step);
-            uint32_t dlen = p.step;
-            if ((int)dlen + off > p.in_dlen)                       // 132-133
-                dlen = (uint32_t)(p.in_dlen - off);
-            const uint32_t qlen = p.out_hlen + dlen, slot = slot16(qlen);
-            const bool fits = fidx < f.max_frags && bpos + slot <= f.arena_bytes;
-            if (fits) {
-                uint8_t *q = f.arena + bpos;
+            tpl = (tpl & ~0xFu) | (qw & 0xF);                                   // ip_hl (144)
+        const uint32_t off_first = bswap16(__shfl(dw, g0 + 1, 64) >> 16);      // ntohs(ip->ip_off) after 112-118
+        const uint64_t fidx = fbase + pn[j];
+        const uint64_t bpos = bbase + pb[j];
+        // payload offsets are relative to ip (32-bit): fragment k's payload
+        // starts at pay0 + k * step and ends at min(that + dlen_k, caplen)
+        const uint32_t pay0 = hlen + (uint32_t)first_dlen;
+        // payload chunk space: fragment k < nextra-1 has nch_f chunks, the last nch_l
+        const uint32_t nch_f = (step + 15) / 16, nch_l = (last + 15) / 16;
+        const uint32_t total = nextra ? (nextra - 1) * nch_f + nch_l : 0u;
+        auto write_headers = [&]() {
+            // the first fragment's header fields, in place (112-120)
+            if (gl == 0)
+                st_u16(ip + 2, dw >> 16);
+            if (gl == 1) {
+                st_u16(ip + 4, dw & 0xFFFF);
+                st_u16(ip + 6, dw >> 16);
+            }
+            if (gl == 2)
+                st_u16(ip + 10, dw >> 16);
+            // the appended fragments' headers (140-150) and descriptors
+            for (uint32_t k = 0; k < nextra; k++) {
+                const int off = first_dlen + (int)(k * step);
+                const uint32_t dlen = k + 1 < nextra ? step : last;
+                const uint32_t qlen = out_hlen + dlen;
+                const uint64_t bp = bpos + (uint64_t)k * slot_f;
+                const bool fits = fidx + k < f.max_frags && bp + slot16(qlen) <= f.arena_bytes;
                 uint32_t h = tpl;
                 if (gl == 0)
-                    h = (h & 0xFFFF) | (bswap16(qlen) << 16);     // 148
+                    h = (h & 0xFFFF) | (bswap16(qlen) << 16);                // 148
                 if (gl == 1) {
-                    uint32_t fo = (off_first + ((uint32_t)off >> 3)) & 0xFFFF;   // 145
-                    if ((int)dlen + off >= p.in_dlen && !had_mf)  // 146-147
+                    uint32_t fo = (off_first + ((uint32_t)off >> 3)) & 0xFFFF;  // 145
+                    if ((int)dlen + off >= in_dlen && !had_mf)              // 146-147
                         fo &= ~0x2000u;
                     h = (h & 0xFFFF) | (bswap16(fo) << 16);
                 }
                 if (gl == 2)
-                    h &= 0xFFFF;                                  // 149
+                    h &= 0xFFFF;                                            // 149
                 const uint32_t s = group_header_cksum(h, gl, qw);
                 if (gl == 2)
-                    h |= s << 16;                                 // 150
-                if (gl < qw)
-                    st_u32(q + 4 * gl, h);
-                // payload (142): FRAG_U 16 B chunks per lane in flight
-                const uint64_t src0 = (uint64_t)ip + p.hlen + (uint32_t)off;
-                const uint64_t hi = src0 + dlen < src_end ? src0 + dlen : src_end;
-                const uint32_t nch = (dlen + 15) / 16;
-                for (uint32_t c0 = 0; c0 < nch; c0 += FRAG_G * FRAG_U) {
-                    u32x4 v[FRAG_U];
-#pragma unroll
-                    for (int u = 0; u < FRAG_U; u++) {
-                        const uint32_t c = c0 + u * FRAG_G + gl;
-                        v[u] = c < nch ? load16_guarded(src0 + 16ull * c, hi) : u32x4{0, 0, 0, 0};
+                    h |= s << 16;                                           // 150
+                if (fits) {
+                    if (gl < qw)
+                        st_u32(f.arena + bp + 4 * gl, h);
+                    if (gl == (k & (FRAG_G - 1))) {
+                        f.frag_off[fidx + k] = bp;
+                        f.frag_len[fidx + k] = qlen;
+                        f.frag_src[fidx + k] = (uint32_t)i;
                     }
-#pragma unroll
-                    for (int u = 0; u < FRAG_U; u++) {
-                        const uint32_t c = c0 + u * FRAG_G + gl;
-                        if (c >= nch)
-                            continue;
-                        const uint32_t at = p.out_hlen + 16 * c;  // 4-aligned; the slot ends at `slot`
-                        if (at + 16 <= slot) {
-                            *(__attribute__((address_space(1))) u32x4_a4 *)(q + at) = v[u];
-                        } else {
-#pragma unroll
-                            for (int d = 0; d < 4; d++)
-                                if (at + 4 * d < slot)
-                                    st_u32(q + at + 4 * d, v[u][d]);
-                        }
-                    }
-                }
-                if (gl == 0) {
-                    f.frag_off[fidx] = bpos;
-                    f.frag_len[fidx] = qlen;
-                    f.frag_src[fidx] = (uint32_t)i;
                 }
             }
-            fidx++;
-            bpos += slot;
+        };
+#if CLK_FRAG_HDR_FIRST
+        write_headers();
+#endif
+        uint32_t ck = 0, cc = gl;                          // this lane's next (fragment, chunk)
+        for (uint32_t c0 = 0; c0 == 0 || c0 < total; c0 += FRAG_G * FRAG_U) {
+            u32x4 v[FRAG_U];
+            uint32_t vkc[FRAG_U];                          // k << 16 | chunk, ~0u: none
+#pragma unroll
+            for (int u = 0; u < FRAG_U; u++) {
+                while (ck + 1 < nextra && cc >= nch_f) {
+                    cc -= nch_f;
+                    ck++;
+                }
+                const bool ok = ck < nextra && cc < (ck + 1 < nextra ? nch_f : nch_l);
+                const uint32_t fs = pay0 + ck * step;
+                const uint32_t fe = fs + (ck + 1 < nextra ? step : last);
+                v[u] = ok ? load16_rel(ip, fs + 16 * cc, fe < caplen ? fe : caplen) : u32x4{0, 0, 0, 0};
+                vkc[u] = ok ? (ck << 16) | cc : 0xFFFFFFFFu;
+                cc += FRAG_G;
+            }
+#if !CLK_FRAG_HDR_FIRST
+            if (c0 == 0)
+                write_headers();
+#endif
+#pragma unroll
+            for (int u = 0; u < FRAG_U; u++) {
+                if (vkc[u] == 0xFFFFFFFFu)
+                    continue;
+                const uint32_t k = vkc[u] >> 16, c = vkc[u] & 0xFFFF;
+                const uint32_t dlen = k + 1 < nextra ? step : last;
+                const uint32_t slot = slot16(out_hlen + dlen);
+                const uint64_t bp = bpos + (uint64_t)k * slot_f;
+                if (fidx + k >= f.max_frags || bp + slot > f.arena_bytes)
+                    continue;
+                uint8_t *q = f.arena + bp;
+                const uint32_t at = out_hlen + 16 * c;    // 4-aligned; the slot ends at `slot`
+                if (at + 16 <= slot) {
+#if CLK_FRAG_NT_STORE
+                    __builtin_nontemporal_store(v[u], (__attribute__((address_space(1))) u32x4_a4 *)(q + at));
+#else
+                    *(__attribute__((address_space(1))) u32x4_a4 *)(q + at) = v[u];
+#endif
+                } else {
+#pragma unroll
+                    for (int d = 0; d < 4; d++)
+                        if (at + 4 * d < slot)
+                            st_u32(q + at + 4 * d, v[u][d]);
+                }
+            }
         }
+        j = jn;
     }
 }
 

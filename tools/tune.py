@@ -54,6 +54,23 @@ VARIANTS = {
     "skv8": (["-DCLK_SKV=8"], {"CLK_VARLEN": "2"}),
     "fused_stream": ([], {"CLK_SET_MODE": "0", "CLK_VARLEN": "2"}),
     "two_stream": ([], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
+    "fua": (["-DCLK_FRAG_UA=1"], {}),
+    "fuah": (["-DCLK_FRAG_UA=1", "-DCLK_FRAG_HDR_FIRST=1"], {}),
+    "fuahu2": (["-DCLK_FRAG_UA=1", "-DCLK_FRAG_HDR_FIRST=1", "-DCLK_FRAG_U=2"], {}),
+    "fuau8": (["-DCLK_FRAG_UA=1", "-DCLK_FRAG_U=8"], {}),
+    "fuau2": (["-DCLK_FRAG_UA=1", "-DCLK_FRAG_U=2"], {}),
+    "fnts": (["-DCLK_FRAG_NT_STORE=1"], {}),
+    "fntl": (["-DCLK_FRAG_NT_LOAD=1"], {}),
+    "fnt": (["-DCLK_FRAG_NT_STORE=1", "-DCLK_FRAG_NT_LOAD=1"], {}),
+    "fw6": (["-DCLK_FRAG_WPE=6"], {}),
+    "fw8": (["-DCLK_FRAG_WPE=8"], {}),
+    "fu2w6": (["-DCLK_FRAG_U=2", "-DCLK_FRAG_WPE=6"], {}),
+    "fu2w8": (["-DCLK_FRAG_U=2", "-DCLK_FRAG_WPE=8"], {}),
+    "fg32": (["-DCLK_FRAG_G=32"], {}),
+    "fg64": (["-DCLK_FRAG_G=64"], {}),
+    "fu2": (["-DCLK_FRAG_U=2"], {}),
+    "fu8": (["-DCLK_FRAG_U=8"], {}),
+    "fg32u8": (["-DCLK_FRAG_G=32", "-DCLK_FRAG_U=8"], {}),
     "hc2": (["-DCLK_SHC_EXTRA=0"], {}),
     "hc2w8": (["-DCLK_SHC_EXTRA=0", "-DCLK_SWPE=8"], {}),
     "w8": (["-DCLK_SWPE=8"], {}),
@@ -139,7 +156,18 @@ def main():
                 "SetIPChecksum": lambda c: c.set_ip_checksum(b, status=status, want_sums=False),
                 "CheckUDPHeader": lambda c: c.check_udp_header(b, out=status),
                 "CheckTCPHeader": lambda c: c.check_tcp_header(b, out=status),
-                "CheckIPHeader": lambda c: c.check_ip_header(b, out=status)}
+                "CheckIPHeader": lambda c: c.check_ip_header(b, out=status),
+                "IPFragmenter": lambda c: frag(c)}
+    if os.environ.get("TUNE_ELEMENT") == "IPFragmenter":       # C3 to MTU 576; headers restored per call
+        hdr = arena.view(n, w["stride"])[:, :12]
+        saved = hdr.clone()
+        fout = torch.empty(n * 976, dtype=torch.uint8, device="cuda")
+        ff = torch.empty(n, dtype=torch.int64, device="cuda")
+        fl = torch.empty(n, dtype=torch.int32, device="cuda")
+
+        def frag(c):
+            hdr.copy_(saved)
+            c.ip_fragment(b, 576, True, arena=fout, max_frags=2 * n, port=status, first_len=fl, frag_first=ff)
     element = os.environ.get("TUNE_ELEMENT", w["elements"][-1])
     run = elements[element]
     times = {nm: [] for nm in names}
@@ -161,7 +189,10 @@ def main():
             e.record()
             torch.cuda.synchronize()
             times[nm].append(s.elapsed_time(e) / args.launches)
-    alg = bench.ALG[element](w["L"]) * n if args.workload != "c4" else sum_l + (bench.ALG[element](0) + 12) * n
+    if element == "IPFragmenter":
+        alg = 1924 * n
+    else:
+        alg = bench.ALG[element](w["L"]) * n if args.workload != "c4" else sum_l + (bench.ALG[element](0) + 12) * n
     out = {nm: {"median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
                 "GBs": round(alg / (statistics.median(t) * 1e-3) / 1e9, 1)} for nm, t in times.items()}
     print(json.dumps({"workload": args.workload, "element": element,
