@@ -192,6 +192,48 @@ __device__ __noinline__ uint32_t pseudohdr_hard(uint32_t csum, const uint8_t *ip
     return pseudohdr_raw(csum, src, dst, proto, packet_len);
 }
 
+// The destination the pseudo-header uses: the final hop of the first
+// SSRR/LSRR option (in_cksum.c:86-108), else `dst`.  Options only.
+__device__ __noinline__ uint32_t route_dst(const uint8_t *iph, uint32_t hl, uint32_t dst)
+{
+    uint32_t o = 20;
+    while (o < hl) {
+        const uint32_t t = ld_u8(iph + o);
+        if (t == 1) {               // IPOPT_NOP
+            o++;
+            continue;
+        } else if (t == 0)          // IPOPT_EOL
+            break;
+        if (o + 1 >= hl)
+            break;
+        const uint32_t l = ld_u8(iph + o + 1);
+        if (l < 2 || o + l > hl)
+            break;
+        if ((t == 137 || t == 131) && l >= 7)      // IPOPT_SSRR / IPOPT_LSRR
+            return ld_u32_unaligned(iph + o + l - 4);
+        o += l;
+    }
+    return dst;
+}
+
+// pseudohdr_raw split in two (in_cksum.c:74-78): the header terms, summed
+// at parse time (< 7 * 0xFFFF, no carry out of 32 bits) ...
+__device__ __forceinline__ uint32_t pseudohdr_partial(uint32_t src, uint32_t dst, uint32_t proto,
+                                                      uint32_t packet_len)
+{
+    return (src & 0xffffu) + (src >> 16) + (dst & 0xffffu) + (dst >> 16) + bswap16(packet_len & 0xFFFFu) +
+           bswap16(proto & 0xFFFFu);
+}
+// ... and the fold with the payload checksum: equal to pseudohdr_raw(csum,
+// src, dst, proto, packet_len) for ph = pseudohdr_partial(src, dst, proto,
+// packet_len), as the u32 sum is order-free.
+__device__ __forceinline__ uint32_t pseudohdr_ph(uint32_t csum, uint32_t ph)
+{
+    uint32_t c = (~csum & 0xFFFFu) + ph;
+    c = (c & 0xffffu) + (c >> 16);
+    return ~(c + (c >> 16)) & 0xFFFFu;
+}
+
 // include/clicknet/ip.h:152-160
 __device__ __forceinline__ uint32_t pseudohdr(uint32_t csum, const uint8_t *iph, uint32_t b0,
                                               uint32_t src, uint32_t dst, uint32_t proto,

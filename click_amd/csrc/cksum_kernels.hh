@@ -269,13 +269,18 @@ __global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_s
 // The header parse reads the first 28 (UDP) / 40 (TCP) bytes as aligned
 // dwords and is speculative on ip_hl = 5; other header lengths re-read.
 // ---------------------------------------------------------------------------
+// What the finish needs once the header is parsed.  The pseudo-header is
+// reduced to one partial sum at parse time (ph), and a Set's corrections
+// (its zeroed field, FIXOFF's rewritten byte) to one u32 added to the range
+// sum (adj), so few registers stay live across the payload sum.
 struct L4State {
     uint32_t code;
     int rlen;            // summed range length (int, as click_in_cksum's)
     uint32_t plen_ph;    // packet_len for the pseudo-header
-    uint32_t hl, b0, proto, src, dst;
-    uint32_t fb0, fb1;   // Set: the stored field's two bytes
-    uint32_t new_b12, fix_delta;
+    uint32_t hl;
+    uint32_t ph;         // src + dst (+ SSRR/LSRR) halves + htons(len) + htons(proto)
+    uint32_t adj;        // Set: added to the range sum (mod 2^32)
+    uint32_t new_b12;
     uint32_t caplen;
     bool fix, summing;
 };
@@ -316,12 +321,9 @@ __device__ __forceinline__ void l4_parse_words(uint8_t *nh, uint32_t caplen, int
     st.plen_ph = 0;
     st.caplen = caplen;
     st.hl = hl;
-    st.b0 = b0;
-    st.proto = proto;
-    st.src = h[3];
-    st.dst = h[4];
-    st.fb0 = st.fb1 = 0;
-    st.new_b12 = st.fix_delta = 0;
+    st.new_b12 = 0;
+    st.adj = st.ph = 0;
+    uint32_t fix_delta = 0;
     st.fix = false;
     if (caplen < 20) {
         st.code = PROTO == UDP ? (SET ? SET_OUTPUT1 : L4_BAD_LENGTH) : (SET ? SET_KILL : L4_BAD_LENGTH);
@@ -409,15 +411,41 @@ __device__ __forceinline__ void l4_parse_words(uint8_t *nh, uint32_t caplen, int
                         st.fix = true;
                     }
                     if (st.fix)
-                        st.fix_delta = st.new_b12 - ob;
+                        fix_delta = st.new_b12 - ob;
                 }
             }
         }
     }
     st.summing = (st.code == OK) && (st.rlen != 0 || st.plen_ph != 0 || SET);
     if (SET && st.summing) {
-        st.fb0 = (int)FIELD < st.rlen ? tbyte(FIELD) : 0;
-        st.fb1 = (int)FIELD + 1 < st.rlen ? tbyte(FIELD + 1) : 0;
+        // the field is zeroed before summing (setudpchecksum.cc:64,
+        // settcpchecksum.cc:65): remove its bytes that lie in range; FIXOFF's
+        // rewritten th_off byte is summed as rewritten (57-63)
+        const uint32_t fb0 = (int)FIELD < st.rlen ? tbyte(FIELD) : 0;
+        const uint32_t fb1 = (int)FIELD + 1 < st.rlen ? tbyte(FIELD + 1) : 0;
+        st.adj = (st.fix && 12 < st.rlen ? fix_delta : 0u) - (fb0 + (fb1 << 8));
+    }
+    if (PROTO != ICMP && st.summing) {
+        uint32_t s2 = h[3], d2 = h[4];
+        if (SET && hl < 20) {
+            // ip_hl < 5: the transport header overlaps the IP header.  The
+            // reference zeroes the field (and FIXOFF rewrites th_off)
+            // BEFORE the pseudo-header reads ip_src/ip_dst, and the option
+            // walk is empty (in_cksum.c:86-88), so patch those bytes in.
+            auto patch = [&](uint32_t pos, uint32_t val) {
+                if (pos >= 12 && pos < 16)
+                    s2 = (s2 & ~(0xFFu << (8 * (pos - 12)))) | (val << (8 * (pos - 12)));
+                else if (pos >= 16 && pos < 20)
+                    d2 = (d2 & ~(0xFFu << (8 * (pos - 16)))) | (val << (8 * (pos - 16)));
+            };
+            if (st.fix)
+                patch(hl + 12, st.new_b12);
+            patch(hl + FIELD, 0);
+            patch(hl + FIELD + 1, 0);
+        } else if ((b0 & 0xF) != 5) {
+            d2 = route_dst(nh, hl, d2);              // ip.h:156-159 -> in_cksum.c:83-108
+        }
+        st.ph = pseudohdr_partial(s2, d2, proto, st.plen_ph);
     }
 }
 
@@ -494,37 +522,11 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
     constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
     uint32_t stored = 0;
     if (st.code == OK && st.summing) {
-        if (SET) {
-            // the field was zeroed before summing (setudpchecksum.cc:64,
-            // settcpchecksum.cc:65): remove its bytes that lie in range
-            sum -= st.fb0 + (st.fb1 << 8);
-            if (st.fix && 12 < st.rlen)
-                sum += st.fix_delta;
-        }
+        if (SET)
+            sum += st.adj;
         const uint32_t csum = in_cksum_fold(sum);
-        uint32_t r;
-        if (PROTO == ICMP) {
-            r = csum;                           // click_in_cksum(icmph, icmp_len) != 0, 136-138
-        } else if (SET && st.hl < 20) {
-            // ip_hl < 5: the transport header overlaps the IP header.  The
-            // reference zeroes the field (and FIXOFF rewrites th_off)
-            // BEFORE the pseudo-header reads ip_src/ip_dst, and the option
-            // walk is empty (in_cksum.c:86-88), so patch those bytes in.
-            uint32_t s2 = st.src, d2 = st.dst;
-            auto patch = [&](uint32_t pos, uint32_t val) {
-                if (pos >= 12 && pos < 16)
-                    s2 = (s2 & ~(0xFFu << (8 * (pos - 12)))) | (val << (8 * (pos - 12)));
-                else if (pos >= 16 && pos < 20)
-                    d2 = (d2 & ~(0xFFu << (8 * (pos - 16)))) | (val << (8 * (pos - 16)));
-            };
-            if (st.fix)
-                patch(st.hl + 12, st.new_b12);
-            patch(st.hl + FIELD, 0);
-            patch(st.hl + FIELD + 1, 0);
-            r = pseudohdr_raw(csum, s2, d2, st.proto, st.plen_ph);
-        } else {
-            r = pseudohdr(csum, nh, st.b0, st.src, st.dst, st.proto, st.plen_ph);
-        }
+        // click_in_cksum(icmph, icmp_len) != 0 (checkicmpheader.cc:136-138), else the pseudo-header
+        const uint32_t r = PROTO == ICMP ? csum : pseudohdr_ph(csum, st.ph);
         if (SET) {
             stored = r;
 #if !CLK_DIAG_NO_FIELD_STORE
@@ -559,8 +561,15 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
 // packet's pass-0 chunk loads for [nh, nh+caplen) AND the header dwords
 // (same addresses across the group: one request per wave instruction), so
 // one memory round trip serves the parse and the sum.
+#ifndef CLK_L4_WPE_SET
+#define CLK_L4_WPE_SET 5
+#endif
+#ifndef CLK_L4_WPE_CHECK
+#define CLK_L4_WPE_CHECK 1
+#endif
 template <int PROTO, bool SET, int G, int K, bool DEFER>
-__global__ void __launch_bounds__(256) l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SET ? CLK_L4_WPE_SET : CLK_L4_WPE_CHECK)))
+l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                  uint16_t *out_sum, uint32_t *work)
 {
     const uint32_t lane = threadIdx.x & 63, gl = lane & (G - 1);

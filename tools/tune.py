@@ -54,6 +54,11 @@ VARIANTS = {
     "skv8": (["-DCLK_SKV=8"], {"CLK_VARLEN": "2"}),
     "fused_stream": ([], {"CLK_SET_MODE": "0", "CLK_VARLEN": "2"}),
     "two_stream": ([], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
+    "prev": (["(built by hand from the previous commit's sources)"], {}),
+    "sw5": (["-DCLK_L4_WPE_SET=5"], {}),
+    "sw6": (["-DCLK_L4_WPE_SET=6"], {}),
+    "cw6": (["-DCLK_L4_WPE_CHECK=6"], {}),
+    "cw8": (["-DCLK_L4_WPE_CHECK=8"], {}),
     "fua": (["-DCLK_FRAG_UA=1"], {}),
     "fuah": (["-DCLK_FRAG_UA=1", "-DCLK_FRAG_HDR_FIRST=1"], {}),
     "fuahu2": (["-DCLK_FRAG_UA=1", "-DCLK_FRAG_HDR_FIRST=1", "-DCLK_FRAG_U=2"], {}),
