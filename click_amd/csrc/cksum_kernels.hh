@@ -25,7 +25,7 @@
 #define CLK_SHC_EXTRA 0    // packet-stream kernel: head chunks stashed beyond the aligned-header minimum
 #endif
 #ifndef CLK_SWPE
-#define CLK_SWPE 8         // packet-stream kernel: request this many waves per SIMD (0: compiler default)
+#define CLK_SWPE 8         // packet-stream kernel: request this many waves per SIMD (TCP: at most 7, its 3 stashed head chunks)
 #endif
 #ifndef CLK_BLOCK_WRITE
 #define CLK_BLOCK_WRITE 0  // tuning knob: fused Set stores rewrite the whole 64 B block (measured slower)
@@ -519,7 +519,6 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
                                           uint8_t *out_code, uint16_t *out_sum, uint32_t *work,
                                           uint32_t gl = 0, uint32_t ng = 1)
 {
-    constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
     uint32_t stored = 0;
     if (st.code == OK && st.summing) {
         if (SET)
@@ -782,7 +781,7 @@ __device__ __forceinline__ uint32_t chunk_outside(const u32x4 V, uint64_t ca, ui
 template <int PROTO, bool SET, bool DEFER, int KV, bool PF, bool MARKS>
 __global__ void __launch_bounds__(256)
 #if CLK_SWPE
-__attribute__((amdgpu_waves_per_eu(CLK_SWPE)))
+__attribute__((amdgpu_waves_per_eu(PROTO == TCP && CLK_SWPE > 7 ? 7 : CLK_SWPE)))
 #endif
 l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                         uint16_t *out_sum, uint32_t *work)

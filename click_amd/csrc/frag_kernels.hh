@@ -66,7 +66,17 @@ __device__ __forceinline__ uint32_t frag_optcopy_len(const uint8_t *ip, uint32_t
 
 __device__ __forceinline__ uint32_t slot16(uint32_t b) { return (b + 15) & ~15u; }
 
-__device__ __forceinline__ FragPlan frag_plan(const uint8_t *ip, uint32_t caplen, uint32_t mtu, int honor_df)
+// Whether frag_plan reads the header (it does only for packets longer than the MTU).
+__device__ __forceinline__ bool frag_reads_header(uint32_t caplen, uint32_t mtu)
+{
+    return (int)caplen > (int)mtu && caplen >= 20;
+}
+
+// The element's decision for one packet (ipfragmenter.cc:88-171), from the
+// header's bytes 0-3 (w0) and 4-7 (w4), loaded by the caller when
+// frag_reads_header().
+__device__ __forceinline__ FragPlan frag_plan_words(const uint8_t *ip, uint32_t caplen, uint32_t mtu, int honor_df,
+                                                    uint32_t w0, uint32_t w4)
 {
     FragPlan p;
     p.port = 0;
@@ -79,7 +89,6 @@ __device__ __forceinline__ FragPlan frag_plan(const uint8_t *ip, uint32_t caplen
         p.port = 1;
         return p;
     }
-    const uint32_t w0 = ld_u32_unaligned(ip), w4 = ld_u32_unaligned(ip + 4);
     p.hlen = (w0 & 0xF) << 2;                          // 92
     p.first_dlen = (int)((mtu - p.hlen) & ~7u);        // 93 (unsigned MTU, int result)
     p.in_dlen = (int)bswap16(w0 >> 16) - (int)p.hlen;  // 94
@@ -108,11 +117,22 @@ __global__ void __launch_bounds__(256) frag_plan_kernel(BatchArgs b, FragArgs f,
     __shared__ uint64_t red[2][4];
     const uint64_t tile = (uint64_t)blockIdx.x * FRAG_TILE;
     uint64_t sn = 0, sb = 0;
+    // all four packets' header words in flight before any is planned
+    uint32_t cl[4], w0[4], w4[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint64_t i = tile + threadIdx.x + 256u * k;
+        cl[k] = i < b.n ? pkt_len(b, i) : 0u;
+        const bool rd = i < b.n && frag_reads_header(cl[k], f.mtu);
+        const uint8_t *ip = b.base + (i < b.n ? pkt_off(b, i) : 0);
+        w0[k] = rd ? ld_u32_unaligned(ip) : 0u;
+        w4[k] = rd ? ld_u32_unaligned(ip + 4) : 0u;
+    }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const uint64_t i = tile + threadIdx.x + 256u * k;
         if (i < b.n) {
-            const FragPlan p = frag_plan(b.base + pkt_off(b, i), pkt_len(b, i), f.mtu, f.honor_df);
+            const FragPlan p = frag_plan_words(b.base + pkt_off(b, i), cl[k], f.mtu, f.honor_df, w0[k], w4[k]);
             out_port[i] = (uint8_t)p.port;
             out_first_len[i] = p.first_len;
             pl_n[i] = p.nextra;

@@ -1,4 +1,4 @@
 set -o pipefail
 mkdir -p gpurun_out/sp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/sp/gpu_all.log 2>&1 || exit 1
-timeout -k 10 400 python bench.py > gpurun_out/sp/bench.json 2>gpurun_out/sp/bench.err || exit 2
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_fragment.py tests/test_gpu_output_elements.py > gpurun_out/sp/frag.log 2>&1 || exit 1
+TUNE_ELEMENT=IPFragmenter timeout -k 10 240 python tools/tune.py --workload c3 --variants prev,base --rounds 6 --launches 3 > gpurun_out/sp/fr.json 2>gpurun_out/sp/fr.err || exit 2
