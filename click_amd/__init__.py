@@ -17,8 +17,11 @@ from ._abi import (CLK_OK, CLK_IP_MINISCULE_PACKET, CLK_IP_BAD_VERSION, CLK_IP_B
                    CLK_IP_BAD_IP_LEN, CLK_IP_BAD_CHECKSUM, CLK_IP_BAD_SADDR, CLK_L4_NOT_PROTO,
                    CLK_L4_BAD_LENGTH, CLK_L4_BAD_CHECKSUM, CLK_SET_OK, CLK_SET_OUTPUT1, CLK_SET_KILL)
 import ctypes
+import os
 
-__all__ = ["Context", "Batch", "ClickAmdError", "lib"]
+import numpy as np
+
+__all__ = ["Context", "Batch", "ClickAmdError", "lib", "read_pcap", "Pcap"]
 
 
 class ClickAmdError(RuntimeError):
@@ -59,6 +62,56 @@ class Batch:
         b.max_len = self.max_len
         b.n = self.n
         return b
+
+
+class Pcap:
+    """A tcpdump file read by clk_pcap_read (FromDump(FILENAME, FORCE_IP)):
+    `arena` (page-aligned uint8 numpy array, so it can be registered for
+    zero-copy), per record `off`, `caplen`, `wire_len`, `ts_ns` and `nh`
+    (the IP header's offset in the record, -1 when FORCE_IP found none),
+    and the file's `info` (clk_pcap_info as a dict)."""
+
+    def __init__(self, arena, off, caplen, wire_len, ts_ns, nh, info):
+        self.arena, self.off, self.caplen, self.wire_len, self.ts_ns, self.nh = arena, off, caplen, wire_len, ts_ns, nh
+        self.info = info
+
+    def ip_records(self):
+        """Indices of the records FORCE_IP kept (FromDump's output 0)."""
+        return np.nonzero(self.nh >= 0)[0]
+
+    def ip_layout(self):
+        """(off, length) of the kept records' IP packets within the arena:
+        the SoA of a clk_batch over them (nh applied)."""
+        k = self.ip_records()
+        return (self.off[k] + self.nh[k].astype(np.uint64)).astype(np.uint64), \
+            (self.caplen[k] - self.nh[k].astype(np.uint32)).astype(np.uint32)
+
+
+def read_pcap(path, force_ip=True, max_records=None):
+    """Read a tcpdump file through the library (include/click_amd_ingest.h)."""
+    L = lib()
+    info = _abi.clk_pcap_info()
+    p = os.fsencode(path)
+    rc = L.clk_pcap_read(p, 1 if force_ip else 0, None, 0, None, None, None, None, None, 0, ctypes.byref(info))
+    if rc < 0:
+        raise ClickAmdError(L.clk_last_error(None).decode())
+    n = info.records if max_records is None else min(info.records, max_records)
+    page = 4096
+    raw = np.zeros(int(info.arena_bytes) + 2 * page, np.uint8)
+    start = (-raw.ctypes.data) % page
+    arena = raw[start:start + ((int(info.arena_bytes) + page - 1) // page) * page]
+    off = np.zeros(max(n, 1), np.uint64)
+    cap = np.zeros(max(n, 1), np.uint32)
+    wl = np.zeros(max(n, 1), np.uint32)
+    ts = np.zeros(max(n, 1), np.uint64)
+    nh = np.zeros(max(n, 1), np.int32)
+    rc = L.clk_pcap_read(p, 1 if force_ip else 0, arena.ctypes.data, arena.size, off.ctypes.data, cap.ctypes.data,
+                         wl.ctypes.data, ts.ctypes.data, nh.ctypes.data, n, ctypes.byref(info))
+    if rc < 0:
+        raise ClickAmdError(L.clk_last_error(None).decode())
+    d = {f: getattr(info, f) for f, _ in _abi.clk_pcap_info._fields_}
+    d["stopped"] = L.clk_last_error(None).decode() if rc == 1 else None
+    return Pcap(arena, off[:n], cap[:n], wl[:n], ts[:n], nh[:n], d)
 
 
 class Context:

@@ -88,6 +88,18 @@ class clk_frag_out(ctypes.Structure):
     ]
 
 
+class clk_pcap_info(ctypes.Structure):
+    _fields_ = [
+        ("linktype", ctypes.c_int32),
+        ("nanosecond", ctypes.c_int32),
+        ("swapped", ctypes.c_int32),
+        ("force_ip", ctypes.c_int32),
+        ("records", ctypes.c_uint64),
+        ("arena_bytes", ctypes.c_uint64),
+        ("ip_records", ctypes.c_uint64),
+    ]
+
+
 _P = ctypes.c_void_p
 _BP = ctypes.POINTER(clk_batch)
 _OP = ctypes.POINTER(clk_ip_out_cfg)
@@ -123,6 +135,9 @@ SIGNATURES = {
     "clk_host_lookup": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_size_t),
                                        ctypes.POINTER(_P)]),
     "clk_count_codes": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P, ctypes.c_uint32]),
+    "clk_pcap_read": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, _P, ctypes.c_uint64, _P, _P, _P, _P, _P,
+                                     ctypes.c_uint64, ctypes.POINTER(clk_pcap_info)]),
+    "clk_pcap_force_ip": (ctypes.c_int32, [_P, ctypes.c_uint32, ctypes.c_int32]),
     "clk_gen_packets": (ctypes.c_int, [_P, _BP, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
     "clk_gen_corrupt": (ctypes.c_int, [_P, _BP, ctypes.c_uint64, ctypes.c_uint32]),
     "clk_read_stream": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P]),

@@ -13,11 +13,12 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "click_amd")
 LIB = os.path.join(PKG, "libclick_amd_cksum.so")
-SOURCES = [os.path.join(PKG, "csrc", "cksum_api.hip"), os.path.join(PKG, "host", "elements.cc")]
+SOURCES = [os.path.join(PKG, "csrc", "cksum_api.hip"), os.path.join(PKG, "host", "elements.cc"),
+           os.path.join(PKG, "host", "ingest.cc")]
 DEPS = SOURCES + [os.path.join(PKG, "csrc", f) for f in ("cksum_kernels.hh", "cksum_device.hh", "frag_kernels.hh",
                                                                     "internal.hh")] + [
     os.path.join(PKG, "host", "elements.hh")] + [
-    os.path.join(ROOT, "include", f) for f in ("click_amd_cksum.h", "click_amd_elements.h")]
+    os.path.join(ROOT, "include", f) for f in ("click_amd_cksum.h", "click_amd_elements.h", "click_amd_ingest.h")]
 ARCH = "gfx950"
 
 

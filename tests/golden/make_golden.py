@@ -140,6 +140,9 @@ def main():
     i = data.index(hdr) + len(hdr)
     blob = data[i:i + 431]
     src = "%s:%d" % (rel, data[:i].count(b"\n"))
+    # the file itself, for the pcap ingest tests (tests/test_ingest.py)
+    with open(os.path.join(HERE, "dump_trace.pcap"), "wb") as f:
+        f.write(blob)
     p = 24
     k = 0
     while p < len(blob):

@@ -412,3 +412,179 @@ def ip_fragment(pkt, mtu, honor_df=False, new_id=None):
         frags.append(bytes(q))
         pos += size
     return 2, first, frags
+
+
+# ---------------------------------------------------------------------------
+# pcap ingest: FromDump's record loop (elements/userlevel/fromdump.cc:226-290,
+# 328-413) and FORCE_IP (elements/userlevel/fakepcap.cc:121-330), written
+# from the pcap format and the link-layer headers.
+# ---------------------------------------------------------------------------
+FORCE_IPABLE = {101, 12, 1, 123, 10, 100, 113, 104, 105, 119, 50, 9, 0, 127}
+
+
+def _is_ip_ethertype(b, i):
+    return i + 2 <= len(b) and ((b[i] << 8) | b[i + 1]) in (0x0800, 0x86DD)
+
+
+def force_ip(rec, dlt):
+    """Offset of the IP header FORCE_IP finds in record bytes `rec`, or -1."""
+    n = len(rec)
+
+    def eth(i):
+        if i + 14 <= n:
+            et = (rec[i + 12] << 8) | rec[i + 13]
+            if et in (0x0800, 0x86DD):
+                return i + 14
+            if et == 0x8100 and i + 18 <= n and _is_ip_ethertype(rec, i + 16):
+                return i + 18
+        return None
+
+    def fddi(i):
+        if i + 21 > n or (rec[i] & 0xF0) != 0x50:
+            return None
+        return rfc1483(i + 13)
+
+    def rfc1483(i):
+        if i + 8 <= n and bytes(rec[i:i + 6]) == b"\xAA\xAA\x03\x00\x00\x00" and _is_ip_ethertype(rec, i + 6):
+            return i + 8
+        if i + 4 <= n and rec[i] == 0x06 and rec[i + 1] == 0x06:
+            return i + 4
+        if i + 8 <= n and rec[i] == 0xAA and rec[i + 1] == 0xAA:
+            org = (rec[i + 3] << 16) | (rec[i + 4] << 8) | rec[i + 5]
+            if org in (0, 0xF8):
+                return eth(i - 6)
+            if org == 0x0080C2:
+                et = (rec[i + 6] << 8) | rec[i + 7]
+                if et in (1, 7):
+                    return eth(i + 8)
+                if et in (4, 0xA):
+                    return fddi(i + 9)
+        return None
+
+    def wifi(i):
+        if i + 24 <= n and (rec[i] & 0x0C) == 0x08:
+            return rfc1483(i + (30 if (rec[i + 1] & 3) == 3 else 24))
+        return None
+
+    def chdlc(i):
+        return i + 4 if i + 4 <= n and _is_ip_ethertype(rec, i + 2) else None
+
+    ip = None
+    if dlt in (101, 12):
+        ip = 0
+    elif dlt == 1:
+        ip = eth(0)
+    elif dlt == 10:
+        ip = fddi(0)
+    elif dlt == 123:
+        ip = rfc1483(4)
+    elif dlt == 100:
+        ip = rfc1483(0)
+    elif dlt == 113:
+        ip = 16 if n >= 16 and _is_ip_ethertype(rec, 14) else None
+    elif dlt == 104:
+        ip = chdlc(0)
+    elif dlt == 50:
+        if n >= 4:
+            if rec[0] == 0xFF:
+                ip = 4 if rec[2] == 0 and rec[3] in (0x21, 0x57) else None
+            elif rec[0] in (0x0F, 0x8F):
+                ip = chdlc(0)
+    elif dlt == 9:
+        i = 2 if n >= 2 and rec[0] == 0xFF and rec[1] == 0x03 else 0
+        if i + 2 <= n:
+            if rec[i] in (0x21, 0x57):
+                ip = i + 1
+            elif rec[i] == 0 and rec[i + 1] in (0x21, 0x57):
+                ip = i + 2
+    elif dlt == 119:
+        ip = wifi(144)
+    elif dlt == 105:
+        ip = wifi(0)
+    elif dlt == 127:
+        if n >= 4:
+            ln = (rec[3] << 8) | rec[2]
+            if ln >= 8:
+                ip = wifi(ln)
+    elif dlt == 0:
+        if n >= 4:
+            fam = rec[0] | (rec[1] << 8)
+            if fam == 0:
+                fam = (rec[2] << 8) | rec[3]
+            if fam in (2, 24, 28, 30):
+                ip = 4
+    # fakepcap.cc:318-330 (plus the domain guard: the header byte must exist)
+    if ip is None or ip < 0 or ip >= n:
+        return -1
+    v = rec[ip] >> 4
+    if v == 4:
+        hl = rec[ip] & 0xF
+        return ip if hl >= 5 and ip + 4 * hl <= n else -1
+    if v == 6:
+        return ip if ip + 40 <= n else -1
+    return -1
+
+
+def read_pcap(data, want_force_ip=True):
+    """(info, records): records = [(bytes, wire_len, ts_ns, nh)] as FromDump
+    would emit them, or raises ValueError(message)."""
+    if len(data) < 24:
+        raise ValueError("not a tcpdump file (too short)")
+    magics = (0xA1B2C3D4, 0xA1B23C4D, 0xA1B2CD34)
+    end = "<"
+    magic = struct.unpack_from("<I", data, 0)[0]
+    if magic not in magics:
+        end = ">"
+        magic = struct.unpack_from(">I", data, 0)[0]
+    if magic not in magics:
+        raise ValueError("not a tcpdump file (bad magic number)")
+    vmaj, vmin = struct.unpack_from(end + "HH", data, 4)
+    dlt = struct.unpack_from(end + "I", data, 20)[0]
+    if vmaj != 2:
+        raise ValueError("unknown major version %d" % vmaj)
+    dlt = 101 if dlt == 12 else dlt
+    fip = want_force_ip
+    if fip and dlt not in FORCE_IPABLE:
+        raise ValueError("unknown linktype %d; can't force IP packets" % dlt)
+    if dlt == 101:
+        fip = True
+    extra = 8 if magic == 0xA1B2CD34 else 0
+    nano = magic == 0xA1B23C4D
+    pos, recs, stopped = 24, [], False
+    while pos + 16 <= len(data):
+        sec, sub, a, b = struct.unpack_from(end + "iiII", data, pos)
+        if vmin > 3 or (vmin == 3 and a <= b):
+            cap, ln = a, b
+        else:
+            cap, ln = b, a
+        if cap > 65535:
+            stopped = True
+            break
+        skip = 0
+        if cap > ln:
+            skip, cap = cap - ln, ln
+        pos += 16 + extra
+        if pos + cap > len(data):
+            break
+        rec = data[pos:pos + cap]
+        recs.append((rec, ln, sec * 1000000000 + (sub if nano else sub * 1000),
+                     force_ip(rec, dlt) if fip else -1))
+        pos += cap + skip
+    return {"linktype": dlt, "nanosecond": int(nano), "swapped": int(end == ">"), "force_ip": int(fip),
+            "stopped": stopped}, recs
+
+
+def write_pcap(records, linktype=1, magic=0xA1B2C3D4, big_endian=False, vmin=4, lens=None, raw_headers=None):
+    """A tcpdump file: records = [(bytes, sec, subsec)]; lens = wire lengths
+    (default: the captured length); raw_headers[k] = (a, b) written as the
+    record's caplen/len words verbatim."""
+    e = ">" if big_endian else "<"
+    out = bytearray(struct.pack(e + "IHHiIII", magic, 2, vmin, 0, 0, 65535, linktype))
+    for k, (rec, sec, sub) in enumerate(records):
+        ln = len(rec) if lens is None else lens[k]
+        a, b = (len(rec), ln) if raw_headers is None or raw_headers[k] is None else raw_headers[k]
+        out += struct.pack(e + "iiII", sec, sub, a, b)
+        if magic == 0xA1B2CD34:
+            out += bytes(8)
+        out += rec
+    return bytes(out)

@@ -13,7 +13,7 @@ from click_amd import _abi, build
 
 ROOT = build.ROOT
 HEADER = os.path.join(ROOT, "include", "click_amd_cksum.h")
-HEADERS = [HEADER, os.path.join(ROOT, "include", "click_amd_elements.h")]
+HEADERS = [HEADER, os.path.join(ROOT, "include", "click_amd_elements.h"), os.path.join(ROOT, "include", "click_amd_ingest.h")]
 
 
 def declared_functions():
@@ -62,6 +62,7 @@ def test_struct_layouts_match_c():
 #include <stdio.h>
 #include <stddef.h>
 #include "click_amd_cksum.h"
+#include "click_amd_ingest.h"
 int main(void) {
   printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(clk_batch), offsetof(clk_batch, off),
          offsetof(clk_batch, stride), offsetof(clk_batch, len), offsetof(clk_batch, fixed_len),
@@ -75,6 +76,8 @@ int main(void) {
   printf("%zu %zu %zu %zu %zu %zu\n", sizeof(clk_frag_out), offsetof(clk_frag_out, arena_bytes),
          offsetof(clk_frag_out, frag_off), offsetof(clk_frag_out, frag_len), offsetof(clk_frag_out, frag_src),
          offsetof(clk_frag_out, max_frags));
+  printf("%zu %zu %zu %zu\n", sizeof(clk_pcap_info), offsetof(clk_pcap_info, force_ip),
+         offsetof(clk_pcap_info, records), offsetof(clk_pcap_info, ip_records));
   return 0; }
 '''
     with tempfile.TemporaryDirectory() as d:
@@ -87,6 +90,9 @@ int main(void) {
     oc = [int(x) for x in out[2].split()]
     fc = [int(x) for x in out[3].split()]
     fo = [int(x) for x in out[4].split()]
+    pc = [int(x) for x in out[5].split()]
+    P = _abi.clk_pcap_info
+    assert pc == [ctypes.sizeof(P), P.force_ip.offset, P.records.offset, P.ip_records.offset]
     O, F, FO = _abi.clk_ip_out_cfg, _abi.clk_frag_cfg, _abi.clk_frag_out
     assert oc == [ctypes.sizeof(O), O.ts.offset, O.my_addrs.offset, O.n_my_addrs.offset, O.mtu.offset]
     assert fc == [ctypes.sizeof(F), F.honor_df.offset, F.new_id.offset]
@@ -104,7 +110,8 @@ def test_header_is_plain_c():
     """The boundary header compiles as C99 with no C++ or torch types."""
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "h.c")
-        open(c, "w").write('#include "click_amd_cksum.h"\n#include "click_amd_elements.h"\nint main(void){return 0;}\n')
+        open(c, "w").write('#include "click_amd_cksum.h"\n#include "click_amd_elements.h"\n#include "click_amd_ingest.h"\n'
+                           'int main(void){return 0;}\n')
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-pedantic", "-I", os.path.dirname(HEADER),
                         "-c", "-o", os.path.join(d, "h.o"), c], check=True)
     text = open(HEADER).read()
