@@ -645,9 +645,14 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, u
     if (!out_port || !out_first_len)
         return fail(ctx, CLK_EINVAL, "clk_ip_fragment: null output");
     const uint32_t ntiles = (uint32_t)((b->n + clk::FRAG_TILE - 1) / clk::FRAG_TILE);
-    // scratch: [nextra u32 x n][bytes u32 x n][tile sums u64 x 2 x ntiles][frag_first u64 x n if not given]
+    // single pass (plan + look-back scan + write) when the fragments are written
+    const bool fused = out->arena && CLK_FRAG_FUSED;
+    // scratch, two-pass: [nextra u32 x n][bytes u32 x n][tile sums u64 x 2 x ntiles]
+    //          single pass: [ticket, err u32 | 256 B][tagged words u64 x 2 x ntiles]
+    //          then [frag_first u64 x n] if the caller gives none
     const size_t pl = (b->n * 4 + 255) & ~size_t(255);
-    const size_t ts_end = 2 * pl + (((size_t)ntiles * 16 + 255) & ~size_t(255));
+    const size_t tb = (((size_t)ntiles * 16 + 255) & ~size_t(255));
+    const size_t ts_end = fused ? 256 + tb : 2 * pl + tb;
     if ((r = ensure_scratch(ctx, ts_end + (out_frag_first ? 0 : b->n * 8)))) return r;
     uint8_t *sc = (uint8_t *)ctx->scratch;
     uint32_t *pl_n = (uint32_t *)sc, *pl_b = (uint32_t *)(sc + pl);
@@ -663,14 +668,31 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, u
     f.frag_len = out->frag_len;
     f.frag_src = out->frag_src;
     f.max_frags = out->frag_off ? out->max_frags : 0;
+    if (fused) {
+        clk::FragLookback lb;
+        lb.ticket = (uint32_t *)sc;
+        lb.err = (uint32_t *)sc + 1;
+        lb.word = (uint64_t *)(sc + 256);
+        lb.totals = totals;
+        lb.out_port = out_port;
+        lb.out_first_len = out_first_len;
+        lb.ntiles = ntiles;
+        e = hipMemsetAsync(sc, 0, 256 + (size_t)ntiles * 16, ctx->cur);
+        if (e != hipSuccess)
+            return hip_fail(ctx, e, "hipMemsetAsync");
+        hipLaunchKernelGGL(clk::frag_write_kernel<true>, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f,
+                           (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr,
+                           (const uint64_t *)nullptr, ffirst, lb);
+        return check_launch(ctx, "clk_ip_fragment");
+    }
     hipLaunchKernelGGL(clk::frag_plan_kernel, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f, out_port,
                        out_first_len, pl_n, pl_b, tile_sums);
     hipLaunchKernelGGL(clk::frag_scan_kernel, dim3(1), dim3(1024), 0, ctx->cur, tile_sums, ntiles, totals);
     if (!out->arena)                         // sizing call: nothing is written
         return check_launch(ctx, "clk_ip_fragment");
-    hipLaunchKernelGGL(clk::frag_write_kernel, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f,
+    hipLaunchKernelGGL(clk::frag_write_kernel<false>, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f,
                        (const uint8_t *)out_port, (const uint32_t *)pl_n, (const uint32_t *)pl_b,
-                       (const uint64_t *)tile_sums, ffirst);
+                       (const uint64_t *)tile_sums, ffirst, clk::FragLookback{});
     return check_launch(ctx, "clk_ip_fragment");
 }
 

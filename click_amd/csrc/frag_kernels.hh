@@ -1,7 +1,10 @@
 // frag_kernels.hh -- IPFragmenter (elements/ip/ipfragmenter.cc:53-171) on
 // gfx950, for whole batches.
 //
-// Three launches, no host round trip:
+// When the fragments are written (arena given) one launch does it all
+// (frag_write_kernel<true>: plan + decoupled look-back scan + write); a
+// sizing call (no arena), or CLK_FRAG_FUSED=0, runs three launches, no
+// host round trip:
 //   frag_plan_kernel   lane per packet: the element's decision (port 0 / 1 /
 //                      2), the first fragment's length, how many fragments
 //                      it appends and their arena bytes (16 B-aligned
@@ -23,7 +26,12 @@
 
 namespace clk {
 
-constexpr uint32_t FRAG_TILE = 1024;    // packets per block (256 threads x 4)
+#ifndef CLK_FRAG_TILE
+#define CLK_FRAG_TILE 1024
+#endif
+constexpr uint32_t FRAG_TILE = CLK_FRAG_TILE;   // packets per block (256 threads x FRAG_PER)
+constexpr int FRAG_PER = FRAG_TILE / 256;
+static_assert(FRAG_TILE % 256 == 0 && FRAG_PER >= 1 && FRAG_PER <= 8, "tile of 256..2048 packets");
 
 struct FragArgs {
     uint32_t mtu;
@@ -118,9 +126,9 @@ __global__ void __launch_bounds__(256) frag_plan_kernel(BatchArgs b, FragArgs f,
     const uint64_t tile = (uint64_t)blockIdx.x * FRAG_TILE;
     uint64_t sn = 0, sb = 0;
     // all four packets' header words in flight before any is planned
-    uint32_t cl[4], w0[4], w4[4];
+    uint32_t cl[FRAG_PER], w0[FRAG_PER], w4[FRAG_PER];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < FRAG_PER; k++) {
         const uint64_t i = tile + threadIdx.x + 256u * k;
         cl[k] = i < b.n ? pkt_len(b, i) : 0u;
         const bool rd = i < b.n && frag_reads_header(cl[k], f.mtu);
@@ -129,7 +137,7 @@ __global__ void __launch_bounds__(256) frag_plan_kernel(BatchArgs b, FragArgs f,
         w4[k] = rd ? ld_u32_unaligned(ip + 4) : 0u;
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < FRAG_PER; k++) {
         const uint64_t i = tile + threadIdx.x + 256u * k;
         if (i < b.n) {
             const FragPlan p = frag_plan_words(b.base + pkt_off(b, i), cl[k], f.mtu, f.honor_df, w0[k], w4[k]);
@@ -213,6 +221,9 @@ __device__ __forceinline__ u32x4 load16_guarded(uint64_t p, uint64_t hi)
     return r;
 }
 
+#ifndef CLK_FRAG_FUSED
+#define CLK_FRAG_FUSED 1       // one launch (plan + look-back scan + write) when fragments are written
+#endif
 #ifndef CLK_FRAG_HDR_FIRST
 #define CLK_FRAG_HDR_FIRST 0
 #endif
@@ -289,9 +300,43 @@ __device__ __forceinline__ uint32_t frag_hdr_dword(const uint8_t *ip, uint32_t c
 // registers (options from LDS), and the payload of all appended fragments
 // is one chunk space loaded before any store of the packet is issued (gfx9
 // counts stores in vmcnt too).
+// Single-pass mode (FUSED): the block plans its own tile (frag_plan_words,
+// writing port / first_len) and gets its tile's exclusive prefix by a
+// decoupled look-back over the tiles before it.  Each tile publishes two
+// words, (fragments, bytes), each tagged in its top bits with 1 =
+// aggregate of the tile or 2 = inclusive prefix; relaxed agent-scope
+// atomics keep a word whole and coherent across XCDs without cache
+// invalidation.  Wave 0 reads 64 predecessors at once and stops at the
+// nearest inclusive one.  Tiles are numbered by an atomic ticket in start
+// order, so every tile waited on has started and publishes its aggregate
+// without waiting: the wait always ends.  The spin is bounded anyway (a bug
+// cannot hang the GPU; a timeout sets err).
+struct FragLookback {
+    uint32_t *ticket;           // 1 word, zeroed before the launch
+    uint32_t *err;              // set when a look-back spin times out
+    uint64_t *word;             // per tile: tagged (fragments, bytes), zeroed before the launch
+    uint64_t *totals;           // {fragments, arena bytes} of the batch
+    uint8_t *out_port;
+    uint32_t *out_first_len;
+    uint32_t ntiles;
+};
+
+constexpr uint64_t LB_VAL = (1ull << 62) - 1;
+
+__device__ __forceinline__ uint64_t lb_load(uint64_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool FUSED>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FRAG_WPE))) frag_write_kernel(BatchArgs b, FragArgs f, const uint8_t *port,
                                                          const uint32_t *pl_n, const uint32_t *pl_b,
-                                                         const uint64_t *tile_sums, uint64_t *out_frag_first)
+                                                         const uint64_t *tile_sums, uint64_t *out_frag_first,
+                                                         FragLookback lb)
 {
     constexpr uint32_t NG = 256 / FRAG_G;
     __shared__ uint32_t pn[FRAG_TILE], pb[FRAG_TILE];     // exclusive prefixes within the tile
@@ -299,19 +344,57 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
     __shared__ uint32_t wsum[2][4];
     __shared__ uint32_t hdr[NG][16];                       // per group: the packet's header dwords
     __shared__ uint32_t optw[NG][11];                      // per group: copied options (<= 40 B + pad)
-    const uint64_t tile = (uint64_t)blockIdx.x * FRAG_TILE;
+    __shared__ uint64_t lb_base[2];
+    __shared__ uint32_t lb_tile;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t gl = lane & (FRAG_G - 1), grp = threadIdx.x / FRAG_G, g0 = lane & ~(FRAG_G - 1);
+    uint32_t tix = blockIdx.x;
+    if (FUSED) {
+        if (threadIdx.x == 0)
+            lb_tile = atomicAdd(lb.ticket, 1u);
+        __syncthreads();
+        tix = lb_tile;
+    }
+    const uint64_t tile = (uint64_t)tix * FRAG_TILE;
     // block exclusive scan of (nextra, bytes): thread t owns packets 4t..4t+3 of the tile
-    uint32_t vn[4], vb[4], tn = 0, tb = 0;
+    uint32_t vn[FRAG_PER], vb[FRAG_PER], tn = 0, tb = 0;
+    if (FUSED) {                           // the plan (frag_plan_kernel), header words loaded first
+        uint32_t cl[FRAG_PER], w0[FRAG_PER], w4[FRAG_PER];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint64_t i = tile + 4 * threadIdx.x + k;
-        vn[k] = i < b.n ? pl_n[i] : 0u;
-        vb[k] = i < b.n ? pl_b[i] : 0u;
-        lport[4 * threadIdx.x + k] = i < b.n ? port[i] : 0u;
-        tn += vn[k];
-        tb += vb[k];
+        for (int k = 0; k < FRAG_PER; k++) {
+            const uint64_t i = tile + FRAG_PER * threadIdx.x + k;
+            cl[k] = i < b.n ? pkt_len(b, i) : 0u;
+            const bool rd = i < b.n && frag_reads_header(cl[k], f.mtu);
+            const uint8_t *ip = b.base + (i < b.n ? pkt_off(b, i) : 0);
+            w0[k] = rd ? ld_u32_unaligned(ip) : 0u;
+            w4[k] = rd ? ld_u32_unaligned(ip + 4) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < FRAG_PER; k++) {
+            const uint64_t i = tile + FRAG_PER * threadIdx.x + k;
+            vn[k] = vb[k] = 0;
+            lport[FRAG_PER * threadIdx.x + k] = 0;
+            if (i < b.n) {
+                const FragPlan p = frag_plan_words(b.base + pkt_off(b, i), cl[k], f.mtu, f.honor_df, w0[k], w4[k]);
+                lb.out_port[i] = (uint8_t)p.port;
+                lb.out_first_len[i] = p.first_len;
+                lport[FRAG_PER * threadIdx.x + k] = (uint8_t)p.port;
+                vn[k] = p.nextra;
+                vb[k] = p.bytes;
+            }
+            tn += vn[k];
+            tb += vb[k];
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < FRAG_PER; k++) {
+            const uint64_t i = tile + FRAG_PER * threadIdx.x + k;
+            vn[k] = i < b.n ? pl_n[i] : 0u;
+            vb[k] = i < b.n ? pl_b[i] : 0u;
+            lport[FRAG_PER * threadIdx.x + k] = i < b.n ? port[i] : 0u;
+            tn += vn[k];
+            tb += vb[k];
+        }
     }
     uint32_t in_ = tn, ib = tb;
     for (int d = 1; d < 64; d <<= 1) {
@@ -333,14 +416,83 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
     }
     uint32_t rn = bn + in_ - tn, rb = bb + ib - tb;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        pn[4 * threadIdx.x + k] = rn;
-        pb[4 * threadIdx.x + k] = rb;
+    for (int k = 0; k < FRAG_PER; k++) {
+        pn[FRAG_PER * threadIdx.x + k] = rn;
+        pb[FRAG_PER * threadIdx.x + k] = rb;
         rn += vn[k];
         rb += vb[k];
     }
+    if (FUSED && wv == 0) {                // decoupled look-back over the tiles before this one
+        const uint64_t an = (uint64_t)wsum[0][0] + wsum[0][1] + wsum[0][2] + wsum[0][3];
+        const uint64_t ab = (uint64_t)wsum[1][0] + wsum[1][1] + wsum[1][2] + wsum[1][3];
+        if (lane == 0) {
+            const uint64_t tag = (tix == 0 ? 2ull : 1ull) << 62;
+            lb_store(&lb.word[2 * tix + 1], tag | ab);
+            lb_store(&lb.word[2 * tix], tag | an);
+        }
+        uint64_t en = 0, eb = 0;
+        int64_t top = (int64_t)tix - 1;
+        uint32_t spins = 0;
+        while (top >= 0) {
+            const int64_t j = top - (int64_t)lane;
+            uint64_t vn = 0, vb = 0;
+            uint32_t st = 2;                           // before tile 0: an inclusive 0
+            if (j >= 0) {
+                vn = lb_load(&lb.word[2 * j]);
+                vb = lb_load(&lb.word[2 * j + 1]);
+                st = (uint32_t)(vn >> 62);
+                if ((uint32_t)(vb >> 62) != st)        // the pair is being rewritten: read again
+                    st = 0;
+                vn &= LB_VAL;
+                vb &= LB_VAL;
+            }
+            const uint64_t m2 = __ballot(st == 2), m0 = __ballot(st == 0);
+            const uint32_t first2 = m2 ? (uint32_t)__builtin_ctzll(m2) : 64u;
+            const uint64_t below = first2 >= 64 ? ~0ull : ((1ull << first2) - 1);
+            if (m0 & below) {                          // a nearer tile has not published yet
+                __builtin_amdgcn_s_sleep(1);
+                if (++spins > (1u << 22)) {            // never reached when the tiles start in ticket order
+                    if (lane == 0)
+                        atomicOr(lb.err, 1u);
+                    break;
+                }
+                continue;
+            }
+            uint32_t n_lo = lane <= first2 ? (uint32_t)vn : 0u, n_hi = lane <= first2 ? (uint32_t)(vn >> 32) : 0u;
+            uint32_t b_lo = lane <= first2 ? (uint32_t)vb : 0u, b_hi = lane <= first2 ? (uint32_t)(vb >> 32) : 0u;
+            uint64_t sn = 0, sb = 0;
+            // exact 64-bit sum of the 64 lanes' values: sum halves separately (each < 2^38 over 64 lanes)
+            uint64_t a0 = n_lo, a1 = n_hi, c0 = b_lo, c1 = b_hi;
+#pragma unroll
+            for (int m = 32; m >= 1; m >>= 1) {
+                a0 += __shfl_xor(a0, m, 64);
+                a1 += __shfl_xor(a1, m, 64);
+                c0 += __shfl_xor(c0, m, 64);
+                c1 += __shfl_xor(c1, m, 64);
+            }
+            sn = a0 + (a1 << 32);
+            sb = c0 + (c1 << 32);
+            en += sn;
+            eb += sb;
+            if (first2 < 64)
+                break;
+            top -= 64;
+        }
+        if (lane == 0) {
+            if (tix != 0) {
+                lb_store(&lb.word[2 * tix + 1], (2ull << 62) | (eb + ab));
+                lb_store(&lb.word[2 * tix], (2ull << 62) | (en + an));
+            }
+            if (tix == lb.ntiles - 1) {
+                lb.totals[0] = en + an;
+                lb.totals[1] = eb + ab;
+            }
+            lb_base[0] = en;
+            lb_base[1] = eb;
+        }
+    }
     __syncthreads();
-    const uint64_t fbase = tile_sums[2 * blockIdx.x], bbase = tile_sums[2 * blockIdx.x + 1];
+    const uint64_t fbase = FUSED ? lb_base[0] : tile_sums[2 * tix], bbase = FUSED ? lb_base[1] : tile_sums[2 * tix + 1];
     for (uint32_t j = threadIdx.x; j < FRAG_TILE && tile + j < b.n; j += blockDim.x)
         out_frag_first[tile + j] = fbase + pn[j];
     const uint32_t lim = b.n - tile < FRAG_TILE ? (uint32_t)(b.n - tile) : FRAG_TILE;

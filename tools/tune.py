@@ -59,6 +59,10 @@ VARIANTS = {
     "sw6": (["-DCLK_L4_WPE_SET=6"], {}),
     "cw6": (["-DCLK_L4_WPE_CHECK=6"], {}),
     "cw8": (["-DCLK_L4_WPE_CHECK=8"], {}),
+    "ffu0": (["-DCLK_FRAG_FUSED=0"], {}),
+    "ft256": (["-DCLK_FRAG_TILE=256"], {}),
+    "ft512": (["-DCLK_FRAG_TILE=512"], {}),
+    "ft2048": (["-DCLK_FRAG_TILE=2048"], {}),
     "fua": (["-DCLK_FRAG_UA=1"], {}),
     "fuah": (["-DCLK_FRAG_UA=1", "-DCLK_FRAG_HDR_FIRST=1"], {}),
     "fuahu2": (["-DCLK_FRAG_UA=1", "-DCLK_FRAG_HDR_FIRST=1", "-DCLK_FRAG_U=2"], {}),
