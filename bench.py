@@ -240,7 +240,7 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg},
             "verify": {"fragmented": dig[0], "packets": dig[1], "appended_fragments": dig[2]},
-            "note": "kernel time (plan + scan + write launches); first-fragment headers restored between steps"}
+            "note": "kernel time (one plan + look-back + write launch, after a small memset); first-fragment headers restored between steps"}
 
 
 def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5):
