@@ -561,13 +561,13 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
 // (same addresses across the group: one request per wave instruction), so
 // one memory round trip serves the parse and the sum.
 #ifndef CLK_L4_WPE_SET
-#define CLK_L4_WPE_SET 5
+#define CLK_L4_WPE_SET 5     // UDP Set l4_kernels: 5 waves/SIMD (C3 -4 %); TCP Set keeps 4 (C5 +0.6 % at 5)
 #endif
 #ifndef CLK_L4_WPE_CHECK
 #define CLK_L4_WPE_CHECK 1
 #endif
 template <int PROTO, bool SET, int G, int K, bool DEFER>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SET ? CLK_L4_WPE_SET : CLK_L4_WPE_CHECK)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SET && PROTO == UDP ? CLK_L4_WPE_SET : SET ? 1 : CLK_L4_WPE_CHECK)))
 l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                  uint16_t *out_sum, uint32_t *work)
 {

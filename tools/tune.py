@@ -56,6 +56,7 @@ VARIANTS = {
     "two_stream": ([], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
     "prev": (["(built by hand from the previous commit's sources)"], {}),
     "sw5": (["-DCLK_L4_WPE_SET=5"], {}),
+    "sw1": (["-DCLK_L4_WPE_SET=1"], {}),
     "sw6": (["-DCLK_L4_WPE_SET=6"], {}),
     "cw6": (["-DCLK_L4_WPE_CHECK=6"], {}),
     "cw8": (["-DCLK_L4_WPE_CHECK=8"], {}),
