@@ -341,7 +341,8 @@ def summarize(r, steps, wname):
     }
 
 
-def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24, glue_pkts=1 << 18):
+def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24, glue_pkts=1 << 18,
+        glue_threads=int(os.environ.get("CLK_E2E_THREADS", 2))):
     """End-to-end rates with the packets in HOST memory (DESIGN.md "E2E").
 
     (a) device C ABI over pinned SoA chunks: per chunk, hipMemcpyAsync H2D of
@@ -456,6 +457,38 @@ def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24, glue_pkts=1 
         _, ports, _ = e.results()
         ok_d = int((ports == 0).sum())
         e.close()
+        # (e) as (d) from `glue_threads` host threads, one context (own
+        # stream) and one element per thread ("Threads"),
+        # each pushing a contiguous quarter of the packets
+        import threading
+        T = glue_threads
+        parts = np.array_split(np.arange(glue_pkts), T)
+        ctxs = [click_amd.Context(0, stream="own") for _ in range(T)]
+        els = [Element(c, element, ", ".join(x for x in (ELEMENT_CONF.get(element, ""),
+                                                          "BATCH 65536, ZEROCOPY true") if x), noutputs=2)
+               for c in ctxs]
+        ok_e = [0] * T
+
+        sl = [(zptrs[p_], lens[p_], nhs[p_], int(p_[0])) for p_ in parts]
+
+        def work(k):
+            els[k].push_burst(sl[k][0], sl[k][1], sl[k][2], first_token=sl[k][3])
+            els[k].flush()
+
+        for timed in (False, False, True):                # two warm-ups (both staging buffers of every element), then timed
+            ths = [threading.Thread(target=work, args=(k,)) for k in range(T)]
+            t0 = time.perf_counter()
+            for t in ths:
+                t.start()
+            for t in ths:
+                t.join()
+            dt_e = time.perf_counter() - t0
+            for k in range(T):                            # results are read outside the timed region, as in (d)
+                _, pts, _ = els[k].results()
+                ok_e[k] = int((pts == 0).sum())
+        for el, c in zip(els, ctxs):
+            el.close()
+            c.close()
     finally:
         ctx.host_unregister(hostnp)
     return {
@@ -471,6 +504,10 @@ def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24, glue_pkts=1 
         "element_glue_zero_copy": {"value": round(glue_pkts * L / dt_d / GIB, 3), "unit": "GiB/s",
                                    "mpps": round(glue_pkts / dt_d / 1e6, 3), "packets": glue_pkts, "ok": ok_d,
                                    "note": "C++ push() per packet records the packet's offset in the registered region (no gather), 64K-packet batches double-buffered, 1 host thread"},
+        "element_glue_zero_copy_threads": {"value": round(glue_pkts * L / dt_e / GIB, 3), "unit": "GiB/s",
+                                           "mpps": round(glue_pkts / dt_e / 1e6, 3), "packets": glue_pkts,
+                                           "threads": glue_threads, "ok": sum(ok_e),
+                                           "note": "as element_glue_zero_copy from %d host threads, one context (own stream) and element per thread" % glue_threads},
         "element_glue": {"value": round(glue_pkts * L / dt_b / GIB, 3), "unit": "GiB/s",
                          "mpps": round(glue_pkts / dt_b / 1e6, 3), "packets": glue_pkts, "ok": ok_b,
                          "gpu_ms": round(gpu_ns / 1e6, 3), "wall_ms": round(dt_b * 1e3, 3),
