@@ -1,14 +1,6 @@
-# GPU box: the given pytest selection, then optional bench workloads.
-# Usage: bash tools/gpu_check.sh "<pytest -k expr or ''>" [workload ...]
+# Round-end check on the GPU box: every -m gpu test, smoke(), the default bench.
 set -o pipefail
-mkdir -p gpurun_out
-K="$1"; shift
-if [ -n "$K" ]; then
-  timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -k "$K" --timeout 120 --timeout-method thread \
-      > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 1; }
-  tail -2 gpurun_out/gpu_tests.log
-fi
-for wl in "$@"; do
-  timeout -k 10 300 python bench.py --workload $wl --no-cpu --no-peak --no-c2 --steps 10 \
-      > gpurun_out/bench_$wl.json 2> gpurun_out/bench_$wl.err || { tail -20 gpurun_out/bench_$wl.err; exit 2; }
-done
+mkdir -p gpurun_out/check
+timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/check/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/check/smoke.log 2>&1 || exit 2
+timeout -k 10 600 python bench.py > gpurun_out/check/bench.json 2> gpurun_out/check/bench.err || exit 3
