@@ -195,3 +195,46 @@ def test_sizing_and_small_arena(tmp_path):
     assert b"arena too small" in L.clk_last_error(None)
     p = click_amd.read_pcap(TRACE, max_records=2)
     assert p.info["records"] == 5 and len(p.off) == 2
+
+
+def test_parser_under_sanitizers(tmp_path):
+    """The pcap reader parses untrusted files: build it with ASan + UBSan
+    (host code; tests/native/pcap_fuzz_main.cc) and run it over mutated
+    files of every link type -- flipped bytes, truncations, huge lengths."""
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if not gxx:
+        pytest.skip("no g++")
+    root = os.path.dirname(HERE)
+    exe = str(tmp_path / "pcap_fuzz")
+    r = subprocess.run([gxx, "-std=c++17", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                        "-I", os.path.join(root, "include"), os.path.join(HERE, "native", "pcap_fuzz_main.cc"),
+                        os.path.join(root, "click_amd", "host", "ingest.cc"), "-o", exe],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rng = np.random.default_rng(77)
+    paths = []
+    for dlt in sorted(pyref.FORCE_IPABLE) + [147]:
+        for v in range(12):
+            recs = []
+            for _ in range(int(rng.integers(0, 12))):
+                ip = _ip4(rng, payload=int(rng.integers(0, 80)), hl=int(rng.integers(5, 16)))
+                fr = [rec for d, rec in _framings(rng, ip) if d == dlt] or [ip]
+                recs.append((fr[int(rng.integers(0, len(fr)))], 1, 2))
+            data = bytearray(pyref.write_pcap(recs, linktype=dlt, magic=[0xA1B2C3D4, 0xA1B23C4D, 0xA1B2CD34][v % 3],
+                                              big_endian=bool(v & 4), vmin=int(rng.integers(1, 5))))
+            for _ in range(int(rng.integers(0, 6))):                   # byte flips (headers included)
+                if data:
+                    data[int(rng.integers(0, len(data)))] = int(rng.integers(0, 256))
+            if v % 5 == 4 and len(data) > 24:                          # a record length far past the file
+                struct.pack_into("<I", data, min(24 + 8, len(data) - 4), int(rng.integers(0, 2 ** 32)))
+            if v % 3 == 2:
+                data = data[:int(rng.integers(0, len(data) + 1))]        # truncation
+            p = tmp_path / ("f%d_%d.pcap" % (dlt, v))
+            p.write_bytes(bytes(data))
+            paths.append(str(p))
+    r = subprocess.run([exe] + paths, capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
+    assert r.returncode == 0, (r.returncode, r.stderr[-3000:])
+    assert int(r.stdout.strip()) > 0
