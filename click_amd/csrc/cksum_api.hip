@@ -28,6 +28,8 @@ struct clk_ctx {
                        // wave-cooperative range kernel, 0 the size-class partition (CLK_VARLEN)
     void *scratch;     // two-phase work array (grown on demand)
     size_t scratch_bytes;
+    uint32_t *dev_flags;   // device word kernels report internal faults in (fragmenter look-back timeout)
+    bool check_flags;      // a launch since the last clk_ctx_sync may have set dev_flags
     char err[512];
 };
 
@@ -399,6 +401,13 @@ int clk_ctx_create(int device, clk_ctx **out)
         return hip_fail(nullptr, e, "hipStreamCreateWithFlags");
     }
     c->cur = c->own;
+    c->check_flags = false;
+    c->dev_flags = nullptr;
+    if ((e = hipMalloc(&c->dev_flags, 256)) != hipSuccess || (e = hipMemset(c->dev_flags, 0, 256)) != hipSuccess) {
+        (void)hipStreamDestroy(c->own);
+        delete c;
+        return hip_fail(nullptr, e, "hipMalloc");
+    }
     *out = c;
     return CLK_SUCCESS;
 }
@@ -412,6 +421,8 @@ int clk_ctx_destroy(clk_ctx *ctx)
     (void)hipStreamDestroy(ctx->own);
     if (ctx->scratch)
         (void)hipFree(ctx->scratch);
+    if (ctx->dev_flags)
+        (void)hipFree(ctx->dev_flags);
     delete ctx;
     return CLK_SUCCESS;
 }
@@ -442,6 +453,17 @@ int clk_ctx_sync(clk_ctx *ctx)
     hipError_t e = hipStreamSynchronize(ctx->cur);
     if (e != hipSuccess)
         return hip_fail(ctx, e, "hipStreamSynchronize");
+    if (ctx->check_flags) {              // a kernel's internal fault report (see dev_flags)
+        ctx->check_flags = false;
+        uint32_t f = 0;
+        if ((e = hipMemcpy(&f, ctx->dev_flags, 4, hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(ctx, e, "hipMemcpy");
+        if (f) {
+            (void)hipMemset(ctx->dev_flags, 0, 4);
+            return fail(ctx, CLK_EHIP, "clk_ip_fragment: the tile look-back timed out (internal error; "
+                                       "fragment offsets of that call are wrong)");
+        }
+    }
     return CLK_SUCCESS;
 }
 
@@ -671,7 +693,8 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, u
     if (fused) {
         clk::FragLookback lb;
         lb.ticket = (uint32_t *)sc;
-        lb.err = (uint32_t *)sc + 1;
+        lb.err = ctx->dev_flags;
+        ctx->check_flags = true;
         lb.word = (uint64_t *)(sc + 256);
         lb.totals = totals;
         lb.out_port = out_port;

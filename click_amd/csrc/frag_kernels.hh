@@ -313,7 +313,7 @@ __device__ __forceinline__ uint32_t frag_hdr_dword(const uint8_t *ip, uint32_t c
 // cannot hang the GPU; a timeout sets err).
 struct FragLookback {
     uint32_t *ticket;           // 1 word, zeroed before the launch
-    uint32_t *err;              // set when a look-back spin times out
+    uint32_t *err;              // set when a look-back spin times out (the context's fault word, read by clk_ctx_sync)
     uint64_t *word;             // per tile: tagged (fragments, bytes), zeroed before the launch
     uint64_t *totals;           // {fragments, arena bytes} of the batch
     uint8_t *out_port;

@@ -84,6 +84,8 @@ int clk_ctx_destroy(clk_ctx *ctx);
 int clk_ctx_set_stream(clk_ctx *ctx, void *hip_stream);
 void *clk_ctx_stream(clk_ctx *ctx);
 void *clk_ctx_own_stream(clk_ctx *ctx);
+/* Wait for the context's stream.  Also reports a kernel's internal fault
+ * flag (the IPFragmenter look-back's bounded wait timing out: CLK_EHIP). */
 int clk_ctx_sync(clk_ctx *ctx);
 int clk_ctx_device(clk_ctx *ctx);
 /* Pre-size the context's device scratch for batches of up to max_packets
