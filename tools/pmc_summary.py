@@ -35,7 +35,7 @@ ELEMENT_KERNELS = {
     "SetIPChecksum": ["ip_header_kernel<2", "field_scatter_kernel<10"],
     "DecIPTTL": ["dec_ttl_kernel"],
     "IPOutputCombo": ["ip_out_kernel<2"],
-    "IPFragmenter": ["frag_plan_kernel", "frag_scan_kernel", "frag_write_kernel"],
+    "IPFragmenter": ["frag_plan_kernel", "frag_scan_kernel", "frag_write_kernel"],   # one launch (frag_write_kernel<true>) or three
 }
 
 
