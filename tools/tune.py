@@ -31,6 +31,7 @@ VARIANTS = {
     "g16": ([], {"CLK_FORCE_GROUP": "16"}),
     "g32": ([], {"CLK_FORCE_GROUP": "32"}),
     "fused": ([], {"CLK_SET_MODE": "0"}),
+    "fusednt": (["-DCLK_NT_LOADS=1"], {"CLK_SET_MODE": "0"}),
     "two": ([], {"CLK_SET_MODE": "1"}),
     "mb8k": ([], {"CLK_MAX_BLOCKS": "8192"}),
     "mb64k": ([], {"CLK_MAX_BLOCKS": "65536"}),
