@@ -57,8 +57,33 @@ def build_oracle(force=False):
     return target
 
 
+EXAMPLES = ["pcap_check"]
+
+
+def build_examples(force=False):
+    """Plain-C programs over the ABI (examples/*.c) -> examples/bin/, linked
+    against the in-tree library (rpath relative to the binary)."""
+    lib = build_library()
+    edir = os.path.join(ROOT, "examples")
+    os.makedirs(os.path.join(edir, "bin"), exist_ok=True)
+    out = []
+    for name in EXAMPLES:
+        src = os.path.join(edir, name + ".c")
+        exe = os.path.join(edir, "bin", name)
+        deps = [src, lib] + [os.path.join(ROOT, "include", h) for h in ("click_amd_cksum.h", "click_amd_ingest.h")]
+        if force or _stale(exe, deps):
+            subprocess.run(["gcc", "-std=c11", "-O2", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__",
+                            "-I" + os.path.join(ROOT, "include"), "-I/opt/rocm/include", src,
+                            "-L" + PKG, "-lclick_amd_cksum", "-L/opt/rocm/lib", "-lamdhip64",
+                            "-Wl,-rpath,$ORIGIN/../../click_amd", "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
+        out.append(exe)
+    return out
+
+
 if __name__ == "__main__":
     force = "--force" in sys.argv
     print(build_library(force=force, verbose=True))
     if "--oracle" in sys.argv:
         print(build_oracle(force=force))
+    if "--examples" in sys.argv:
+        print(build_examples(force=force))

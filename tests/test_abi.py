@@ -121,3 +121,10 @@ def test_header_is_plain_c():
 def test_missing_library_fails_loudly(tmp_path):
     with pytest.raises(OSError):
         _abi.load(str(tmp_path / "nope.so"))
+
+
+def test_c_example_builds():
+    """examples/pcap_check.c uses only the C headers (+ the HIP runtime for
+    its device arrays) and links against the library with -Werror."""
+    exes = build.build_examples()
+    assert all(os.access(e, os.X_OK) for e in exes)

@@ -90,3 +90,18 @@ def test_reference_trace_through_glue(ctx):
         ports[cls] = list(port)
     assert ports["CheckIPHeader"] == [0, 0, 0, 0, 1]      # the fifth frame's ip_sum is 0 (golden vectors)
     assert ports["CheckTCPHeader"] == [0, 0, 0, 0, 1]     # ... and th_sum 0 (BAD_CHECKSUM)
+
+
+def test_c_example_on_reference_trace(ctx):
+    """The plain-C program (examples/pcap_check.c): pcap -> zero-copy ->
+    CheckIPHeader + CheckTCPHeader, no Python in the data path."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(HERE), "examples", "bin", "pcap_check")
+    if not os.path.exists(exe):
+        pytest.skip("examples not built (python -m click_amd.build --examples)")
+    r = subprocess.run([exe, os.path.join(HERE, "golden", "dump_trace.pcap")], capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0, r.stderr
+    # record, CheckIPHeader verdict, CheckTCPHeader verdict (the golden vectors: the fifth
+    # frame's ip_sum and th_sum are 0 -> BAD_CHECKSUM, 1 + Reason = 5 and 3)
+    assert r.stdout.split("\n")[:5] == ["0 0 0", "1 0 0", "2 0 0", "3 0 0", "4 5 3"]
