@@ -221,6 +221,9 @@ __device__ __forceinline__ u32x4 load16_guarded(uint64_t p, uint64_t hi)
     return r;
 }
 
+#ifndef CLK_FRAG_PRO
+#define CLK_FRAG_PRO 1         // fused: plain headers rewritten in place by the tile prologue
+#endif
 #ifndef CLK_FRAG_FUSED
 #define CLK_FRAG_FUSED 1       // one launch (plan + look-back scan + write) when fragments are written
 #endif
@@ -346,6 +349,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
     __shared__ uint32_t optw[NG][11];                      // per group: copied options (<= 40 B + pad)
     __shared__ uint64_t lb_base[2];
     __shared__ uint32_t lb_tile;
+    // fused: the original 20-byte headers of the tile's plain (ip_hl 5)
+    // fragmenting packets, whose first-fragment header the prologue already
+    // rewrote in place (word 0 = 0 marks "not done here")
+    __shared__ uint32_t lhdr[FUSED && CLK_FRAG_PRO ? FRAG_TILE : 1][5];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t gl = lane & (FRAG_G - 1), grp = threadIdx.x / FRAG_G, g0 = lane & ~(FRAG_G - 1);
     uint32_t tix = blockIdx.x;
@@ -359,28 +366,60 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
     // block exclusive scan of (nextra, bytes): thread t owns packets 4t..4t+3 of the tile
     uint32_t vn[FRAG_PER], vb[FRAG_PER], tn = 0, tb = 0;
     if (FUSED) {                           // the plan (frag_plan_kernel), header words loaded first
-        uint32_t cl[FRAG_PER], w0[FRAG_PER], w4[FRAG_PER];
+        constexpr int HW = CLK_FRAG_PRO ? 5 : 2;   // header dwords loaded per packet
+        uint32_t cl[FRAG_PER], hw[FRAG_PER][HW];
 #pragma unroll
         for (int k = 0; k < FRAG_PER; k++) {
             const uint64_t i = tile + FRAG_PER * threadIdx.x + k;
             cl[k] = i < b.n ? pkt_len(b, i) : 0u;
-            const bool rd = i < b.n && frag_reads_header(cl[k], f.mtu);
+            const bool rd = i < b.n && frag_reads_header(cl[k], f.mtu);   // caplen >= 20
             const uint8_t *ip = b.base + (i < b.n ? pkt_off(b, i) : 0);
-            w0[k] = rd ? ld_u32_unaligned(ip) : 0u;
-            w4[k] = rd ? ld_u32_unaligned(ip + 4) : 0u;
+#pragma unroll
+            for (int d = 0; d < HW; d++)
+                hw[k][d] = rd ? ld_u32_unaligned(ip + 4 * d) : 0u;
         }
 #pragma unroll
         for (int k = 0; k < FRAG_PER; k++) {
             const uint64_t i = tile + FRAG_PER * threadIdx.x + k;
+            const uint32_t pk = FRAG_PER * threadIdx.x + k;
             vn[k] = vb[k] = 0;
-            lport[FRAG_PER * threadIdx.x + k] = 0;
+            lport[pk] = 0;
+            if (CLK_FRAG_PRO)
+                lhdr[pk][0] = 0;
             if (i < b.n) {
-                const FragPlan p = frag_plan_words(b.base + pkt_off(b, i), cl[k], f.mtu, f.honor_df, w0[k], w4[k]);
+                uint8_t *ip = b.base + pkt_off(b, i);
+                const FragPlan p = frag_plan_words(ip, cl[k], f.mtu, f.honor_df, hw[k][0], hw[k][1]);
                 lb.out_port[i] = (uint8_t)p.port;
                 lb.out_first_len[i] = p.first_len;
-                lport[FRAG_PER * threadIdx.x + k] = (uint8_t)p.port;
+                lport[pk] = (uint8_t)p.port;
                 vn[k] = p.nextra;
                 vb[k] = p.bytes;
+                if (CLK_FRAG_PRO && p.port == 2 && p.hlen == 20) {
+                    // the first fragment's header (112-120) while its line is in the
+                    // cache: ip_len, MF set / DF cleared (ip_id when DF and new_id),
+                    // ip_sum over the rewritten 20 bytes
+                    uint32_t h[5];
+#pragma unroll
+                    for (int d = 0; d < 5; d++) {
+                        h[d] = hw[k][d];
+                        lhdr[pk][d] = hw[k][d];
+                    }
+                    const bool df = (h[1] >> 16) & 0x40;
+                    h[0] = (h[0] & 0xFFFF) | (bswap16(p.first_len) << 16);
+                    if (df && f.new_id)
+                        h[1] = (h[1] & 0xFFFF0000u) | f.new_id[i];
+                    h[1] = (h[1] & ~(0x40u << 16)) | (0x20u << 16);
+                    h[2] &= 0xFFFF;
+                    uint32_t sum = 0;
+#pragma unroll
+                    for (int d = 0; d < 5; d++)
+                        sum += (h[d] & 0xFFFF) + (h[d] >> 16);
+                    const uint32_t ck = in_cksum_fold(sum);
+                    st_u16(ip + 2, h[0] >> 16);
+                    st_u16(ip + 4, h[1] & 0xFFFF);
+                    st_u16(ip + 6, h[1] >> 16);
+                    st_u16(ip + 10, ck);
+                }
             }
             tn += vn[k];
             tb += vb[k];
@@ -501,13 +540,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
             j += NG;
         return j;
     };
+    // header dword gl of tile packet jj: from LDS when the prologue rewrote
+    // its header (the original words), else from memory
+    auto hdr_word = [&](uint32_t jj, const uint8_t *ipp, uint32_t cap) -> uint32_t {
+        if (FUSED && CLK_FRAG_PRO && lhdr[jj][0] != 0u)
+            return gl < 5 ? lhdr[jj][gl] : 0u;
+        return frag_hdr_dword(ipp, cap, gl);
+    };
     uint32_t j = next_j(grp);
     const uint8_t *nip = nullptr;
     uint32_t ncap = 0, ndw = 0;
     if (j < lim) {
         nip = b.base + pkt_off(b, tile + j);
         ncap = pkt_len(b, tile + j);
-        ndw = frag_hdr_dword(nip, ncap, gl);
+        ndw = hdr_word(j, nip, ncap);
     }
     while (j < lim) {
         const uint64_t i = tile + j;
@@ -518,7 +564,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
         if (jn < lim) {                                    // prefetch the group's next packet
             nip = b.base + pkt_off(b, tile + jn);
             ncap = pkt_len(b, tile + jn);
-            ndw = frag_hdr_dword(nip, ncap, gl);
+            ndw = hdr_word(jn, nip, ncap);
         }
         // the plan (frag_plan for a port-2 packet), from the header registers
         const uint32_t w0 = __shfl(dw, g0, 64), w1 = __shfl(dw, g0 + 1, 64);
@@ -598,15 +644,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
         const uint32_t nch_f = (step + 15) / 16, nch_l = (last + 15) / 16;
         const uint32_t total = nextra ? (nextra - 1) * nch_f + nch_l : 0u;
         auto write_headers = [&]() {
-            // the first fragment's header fields, in place (112-120)
-            if (gl == 0)
-                st_u16(ip + 2, dw >> 16);
-            if (gl == 1) {
-                st_u16(ip + 4, dw & 0xFFFF);
-                st_u16(ip + 6, dw >> 16);
+            // the first fragment's header fields, in place (112-120), unless
+            // the prologue wrote them
+            if (!(FUSED && CLK_FRAG_PRO && lhdr[j][0] != 0u)) {
+                if (gl == 0)
+                    st_u16(ip + 2, dw >> 16);
+                if (gl == 1) {
+                    st_u16(ip + 4, dw & 0xFFFF);
+                    st_u16(ip + 6, dw >> 16);
+                }
+                if (gl == 2)
+                    st_u16(ip + 10, dw >> 16);
             }
-            if (gl == 2)
-                st_u16(ip + 10, dw >> 16);
             // the appended fragments' headers (140-150) and descriptors
             for (uint32_t k = 0; k < nextra; k++) {
                 const int off = first_dlen + (int)(k * step);

@@ -1,4 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out/sp
-TUNE_ELEMENT=SetUDPChecksum timeout -k 10 200 python tools/tune.py --workload c3 --variants base,fused,fusednt --rounds 6 --launches 3 > gpurun_out/sp/s3.json 2>gpurun_out/sp/s.err || exit 3
-TUNE_ELEMENT=SetTCPChecksum timeout -k 10 300 python tools/tune.py --workload c5 --variants base,fused,fusednt --rounds 3 --launches 2 > gpurun_out/sp/s5.json 2>>gpurun_out/sp/s.err || exit 2
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_fragment.py tests/test_gpu_output_elements.py tests/test_gpu_zerocopy.py > gpurun_out/sp/frag.log 2>&1 || exit 1
+TUNE_ELEMENT=IPFragmenter timeout -k 10 240 python tools/tune.py --workload c3 --variants base,fpro0 --rounds 8 --launches 3 > gpurun_out/sp/fr.json 2>gpurun_out/sp/fr.err || exit 2
+timeout -k 10 300 python bench.py --workload c3 --no-c2 --skip c4,c5 --no-cpu > gpurun_out/sp/b_c3.json 2>gpurun_out/sp/b_c3.err || exit 3

@@ -62,6 +62,7 @@ VARIANTS = {
     "cw6": (["-DCLK_L4_WPE_CHECK=6"], {}),
     "cw8": (["-DCLK_L4_WPE_CHECK=8"], {}),
     "ffu0": (["-DCLK_FRAG_FUSED=0"], {}),
+    "fpro0": (["-DCLK_FRAG_PRO=0"], {}),
     "ft256": (["-DCLK_FRAG_TILE=256"], {}),
     "ft512": (["-DCLK_FRAG_TILE=512"], {}),
     "ft2048": (["-DCLK_FRAG_TILE=2048"], {}),
