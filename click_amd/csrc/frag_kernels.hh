@@ -2,7 +2,9 @@
 // gfx950, for whole batches.
 //
 // When the fragments are written (arena given) one launch does it all
-// (frag_write_kernel<true>: plan + decoupled look-back scan + write); a
+// (frag_write_kernel<true>: plan + decoupled look-back scan + write; the
+// plan prologue also rewrites plain 20-byte first-fragment headers in
+// place while their line is cached); a
 // sizing call (no arena), or CLK_FRAG_FUSED=0, runs three launches, no
 // host round trip:
 //   frag_plan_kernel   lane per packet: the element's decision (port 0 / 1 /
