@@ -233,12 +233,14 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
     torch.cuda.empty_cache()
     alg = (20 + 928 + 968 + 8) * n
     ach = alg / (kernel_ms * 1e-3) / 1e9
+    traffic, tsrc = load_traffic("c3", "IPFragmenter")
     return {"element": "IPFragmenter(576, HONOR_DF true)", "workload": w["desc"],
             "kernel_ms": round(kernel_ms, 4), "kernel_ms_min": round(min(kms), 4),
             "mpps": round(dig[1] / (kernel_ms * 1e-3) / 1e6, 1),
             "fragments_per_s_M": round((dig[1] + dig[2]) / (kernel_ms * 1e-3) / 1e6, 1),
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg},
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "alg_bytes_per_launch": alg,
+                         "traffic_source": tsrc},
             "verify": {"fragmented": dig[0], "packets": dig[1], "appended_fragments": dig[2]},
             "note": "kernel time (one plan + look-back + write launch, after a small memset); first-fragment headers restored between steps"}
 
