@@ -96,6 +96,8 @@ VARIANTS = {
     "g8": ([], {"CLK_FORCE_GROUP": "8"}),
     "k4": (["-DCLK_K=4"], {}),
     "k12": (["-DCLK_K=12"], {}),
+    "k9": (["-DCLK_K=9"], {}),
+    "k10": (["-DCLK_K=10"], {}),
 }
 
 
