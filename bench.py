@@ -112,15 +112,18 @@ def run_element(ctx, name, b, status):
         raise ValueError(name)
 
 
-def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
+def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, packets=None, coll_dev="cuda"):
     """Generate the shard in HBM, make every checksum valid (untimed), then
     time each of the workload's elements: warmup + `steps` launches between
     barriers + synchronize; HIP events on the launch stream give the kernel
-    time.  Returns {element: result}."""
+    time.  Check elements run over a batch with 1 in 1024 packets corrupted
+    (one flipped bit), so the drop path is inside the timed
+    region; the corruption is undone before the next element.
+    Returns {element: result}."""
     import click_amd
     from click_amd import shard
     w = dict(WORKLOADS[wname])
-    n = w["n"]
+    n = packets or w["n"]
     first, _ = shard.shard_range(rank, world, n * world)   # this rank's global packet indices
     if wname == "c4":
         off, ln, total, sum_l = imix_layout(torch, n, seed, first)
@@ -137,14 +140,29 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
     ctx.reserve(n)
     ctx.gen_packets(b, proto=w["proto"], seed=seed, first_idx=first)
     ctx.set_ip_checksum(b, status=status, want_sums=False)
-    run_element(ctx, "SetTCPChecksum" if w["proto"] == 6 else "SetUDPChecksum", b, status)
+    l4sums = torch.empty(n, dtype=torch.uint16, device="cuda")
+    (ctx.set_tcp_checksum if w["proto"] == 6 else ctx.set_udp_checksum)(b, status=status, sums=l4sums)
     stream = torch.cuda.current_stream()
     out = {}
+    picks = corrupt_picks(first, n)
     for e in w["elements"]:
         if e in ("DecIPTTL", "IPOutputCombo"):
             # untimed: TTL 255 so that every timed pass decrements (<= 254 passes)
             arena.view(n, w["stride"])[:, 8] = 255
             ctx.set_ip_checksum(b, status=status, want_sums=False)
+        corrupt = None
+        expect_drops = 0
+        if e.startswith("Check"):
+            # IP: a bit of ip_src/ip_dst (only the checksum can see it);
+            # L4: a payload bit (CheckUDPHeader skips uh_sum == 0,
+            # checkudpheader.cc:100, so those picks pass)
+            corrupt = dict(seed=CORRUPT_SEED, rate_log2=CORRUPT_LOG2, first_idx=first,
+                           lo=12 if e == "CheckIPHeader" else None, hi=20 if e == "CheckIPHeader" else 0)
+            ctx.gen_corrupt(b, **corrupt)
+            if e == "CheckUDPHeader":
+                expect_drops = int((picks & (l4sums.cpu().numpy() != 0)).sum())
+            else:
+                expect_drops = int(picks.sum())
         for _ in range(warmup):
             run_element(ctx, e, b, status)
         torch.cuda.synchronize()
@@ -171,17 +189,39 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED):
              "SetIPChecksum": ctx.set_ip_checksum}[e](b, status=status, sums=sums)
         torch.cuda.synchronize()
         dig = shard.digest(torch, status, sums)
-        wall, kernel_ms, dig = shard.reduce_results(torch, dist, "cuda", wall, kernel_ms, dig)
+        if corrupt:
+            ctx.gen_corrupt(b, **corrupt)             # flip the same bits back (untimed)
+        dig.append(expect_drops)
+        wall, kernel_ms, dig = shard.reduce_results(torch, dist, coll_dev, wall, kernel_ms, dig)
         out[e] = dict(wall=wall, kernel_ms=kernel_ms, kernel_ms_min=min(kms), n=n, ck_bytes=ck_bytes,
                       alg_bytes=alg[e], w=w, element=e, ok_total=dig[0], n_total=dig[1],
-                      digest={"ok": dig[0], "packets": dig[1], "sum16": dig[2], "xor16": dig[3]})
+                      digest={"ok": dig[0], "packets": dig[1], "sum16": dig[2], "xor16": dig[3],
+                              "drops": dig[1] - dig[0], "expected_drops": dig[4],
+                              "drops_exact": dig[1] - dig[0] == dig[4]})
         del sums
-    del arena, status, b
+    del arena, status, b, l4sums
     torch.cuda.empty_cache()
     return out
 
 
-def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, seed=0x5EED):
+CORRUPT_SEED, CORRUPT_LOG2 = 0xBAD, 10
+
+
+def corrupt_picks(first, n, seed=CORRUPT_SEED, rate_log2=CORRUPT_LOG2):
+    """The packets clk_gen_corrupt_span picks (cksum_kernels.hh corrupt_kernel):
+    the low rate_log2 bits of splitmix64(seed ^ (first + i) * C) are zero."""
+    import numpy as np
+    i = np.arange(first, first + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (np.uint64(seed) ^ (i * np.uint64(0xD1B54A32D192ED03))) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z ^= z >> np.uint64(31)
+    return (z & np.uint64((1 << rate_log2) - 1)) == 0
+
+
+def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, seed=0x5EED, packets=None,
+                       coll_dev="cuda"):
     """IPFragmenter(MTU 576, HONOR_DF true) over the C3 batch (16M x 1500 B
     per GPU): every packet becomes a 572 B first fragment rewritten in place
     plus 572 B and 396 B fragments appended to an HBM arena (16 B-aligned
@@ -194,7 +234,7 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
     import click_amd
     from click_amd import shard
     w = WORKLOADS["c3"]
-    n, L, stride = w["n"], w["L"], w["stride"]
+    n, L, stride = packets or w["n"], w["L"], w["stride"]
     first, _ = shard.shard_range(rank, world, n * world)
     arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
     b = click_amd.Batch(arena, n, stride=stride, fixed_len=L)
@@ -228,7 +268,7 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
     totals = [int(x) for x in r["totals"].cpu()]
     ok = int((port == 2).sum()) if totals == [2 * n, 976 * n] else 0
     dig = [ok, n, totals[0], 0]
-    _, kernel_ms, dig = shard.reduce_results(torch, dist, "cuda", 0.0, kernel_ms, dig)
+    _, kernel_ms, dig = shard.reduce_results(torch, dist, coll_dev, 0.0, kernel_ms, dig)
     del arena, out, saved, port, first_len, frag_first
     torch.cuda.empty_cache()
     alg = (20 + 928 + 968 + 8) * n
@@ -265,35 +305,50 @@ def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5):
     return nbytes / (best * 1e-3) / 1e9
 
 
-def cpu_baseline(wname, element, seconds=8.0):
-    """Oracle (restated lib/in_cksum.c + the element, -O2 -g) over a bounded
-    sample of the same workload in host DRAM, on the host cores: one thread
-    and `threads` threads on disjoint contiguous shards."""
-    import numpy as np
-    from tests import oracle_lib
-    w = WORKLOADS[wname]
-    L_ = oracle_lib.load_oracle()
-    op = {"SetUDPChecksum": oracle_lib.OP_SET_UDP, "SetTCPChecksum": oracle_lib.OP_SET_TCP,
-          "SetIPChecksum": oracle_lib.OP_SET_IP, "CheckUDPHeader": oracle_lib.OP_CHECK_UDP,
-          "CheckTCPHeader": oracle_lib.OP_CHECK_TCP, "CheckIPHeader": oracle_lib.OP_CHECK_IP}[element]
-    n = max(1, min(w["n"], (256 << 20) // w["stride"]))      # <= 256 MB sample
-    arena = np.zeros(n * w["stride"], np.uint8)
-    oracle_lib.gen(arena, n, stride=w["stride"], fixed_len=w["L"], proto=w["proto"])
-    oracle_lib.batch("set_ip", arena, n, stride=w["stride"], fixed_len=w["L"])
-    if w["L"] >= 28:
-        oracle_lib.batch("set_tcp" if w["proto"] == 6 else "set_udp", arena, n, stride=w["stride"],
-                         fixed_len=w["L"], arg=0)
-    ptr = arena.ctypes.data
-    L_.oracle_bench(op, ptr, w["stride"], w["L"], n, 1, 1)                 # warm
-    one = L_.oracle_bench(op, ptr, w["stride"], w["L"], n, 1, 1)
-    reps1 = max(1, int(seconds / 2 / max(one, 1e-6)))
-    t1 = L_.oracle_bench(op, ptr, w["stride"], w["L"], n, reps1, 1)
-    threads = int(os.environ.get("CLK_CPU_THREADS", min(16, os.cpu_count() or 1)))
-    tn_one = L_.oracle_bench(op, ptr, w["stride"], w["L"], n, 1, threads)
-    repsn = max(1, int(seconds / 2 / max(tn_one, 1e-6)))
-    tn = L_.oracle_bench(op, ptr, w["stride"], w["L"], n, repsn, threads)
-    pk1 = n * reps1 / t1
-    pkn = n * repsn / tn
+def host_topology():
+    """Logical CPUs this process may run on, one per physical core (the first
+    sibling), ordered round-robin over sockets so a leg with fewer threads
+    than cores still uses every socket's memory; plus the cgroup CPU quota
+    (cpu.max; None: unlimited), the L3 bytes of the whole machine and the
+    CPU model."""
+    allowed = sorted(os.sched_getaffinity(0))
+    cores = {}
+    for c in allowed:
+        base = "/sys/devices/system/cpu/cpu%d/topology/" % c
+        try:
+            pkg = int(open(base + "physical_package_id").read())
+            core = int(open(base + "core_id").read())
+        except (OSError, ValueError):
+            pkg, core = 0, c
+        cores.setdefault((pkg, core), c)
+    by_pkg = {}
+    for (pkg, core), c in sorted(cores.items()):
+        by_pkg.setdefault(pkg, []).append(c)
+    order = []
+    for k in range(max(len(v) for v in by_pkg.values())):
+        for pkg in sorted(by_pkg):
+            if k < len(by_pkg[pkg]):
+                order.append(by_pkg[pkg][k])
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    l3 = 0
+    seen = set()
+    for c in allowed:
+        d = "/sys/devices/system/cpu/cpu%d/cache/index3/" % c
+        try:
+            ids = open(d + "shared_cpu_list").read().strip()
+            if ids in seen:
+                continue
+            seen.add(ids)
+            sz = open(d + "size").read().strip()
+            l3 += int(sz[:-1]) * {"K": 1 << 10, "M": 1 << 20}.get(sz[-1], 1) if sz[-1] in "KM" else int(sz)
+        except (OSError, ValueError):
+            pass
     model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -302,14 +357,78 @@ def cpu_baseline(wname, element, seconds=8.0):
                 break
     except OSError:
         pass
-    return {
-        "value": round(pkn * w["ck"] / GIB, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "mpps": round(pkn / 1e6, 3),
-        "single_thread": {"value": round(pk1 * w["ck"] / GIB, 3), "mpps": round(pk1 / 1e6, 3), "cores": 1},
-        "sample": "%s over %d x %d B packets (%d B slots) in host DRAM, %d + %d passes; oracle/cksum_oracle.c -O2 -g"
-                  % (element, n, w["L"], w["stride"], reps1, repsn),
-        "cpu": model,
-    }
+    return dict(cpus=order, sockets=len(by_pkg), physical_cores=len(cores), logical_cpus=len(allowed),
+                quota=quota, l3_bytes=l3, model=model)
+
+
+# CPU legs: workload -> (element, oracle op, metric bytes/pkt)
+CPU_LEGS = {"c2": ("CheckIPHeader", 20), "c3": ("CheckUDPHeader", 1500), "c4": ("CheckUDPHeader", None),
+            "c5": ("CheckTCPHeader", 9000)}
+
+
+def cpu_baseline(legs=("c2", "c3", "c4", "c5"), reps=5):
+    """The oracle restatement of lib/in_cksum.c + the element (-O2 -g) on the
+    host cores, per BASELINE.md §2: one thread, then one thread pinned per
+    physical core (capped by the cgroup CPU quota; CLK_CPU_THREADS
+    overrides), each pinned BEFORE it first-touches its own DRAM-resident
+    shard (>= 4 GiB in all and >= 4x the machine's L3; C5: a 1M-packet
+    subset); warm-up, then the median of `reps` passes."""
+    import ctypes
+    from tests import oracle_lib
+    L_ = oracle_lib.load_oracle()
+
+    class Cfg(ctypes.Structure):
+        _fields_ = [("op", ctypes.c_int), ("arg", ctypes.c_int), ("proto", ctypes.c_int), ("imix", ctypes.c_int),
+                    ("fixed_len", ctypes.c_uint32), ("stride", ctypes.c_uint64),
+                    ("bytes_per_thread", ctypes.c_uint64), ("seed", ctypes.c_uint64), ("reps", ctypes.c_int)]
+
+    class Res(ctypes.Structure):
+        _fields_ = [("median_s", ctypes.c_double), ("min_s", ctypes.c_double), ("max_s", ctypes.c_double),
+                    ("gen_s", ctypes.c_double), ("packets", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
+                    ("ok", ctypes.c_uint64), ("pinned", ctypes.c_int)]
+
+    L_.oracle_cpu_baseline.restype = ctypes.c_int
+    L_.oracle_cpu_baseline.argtypes = [ctypes.POINTER(Cfg), ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Res)]
+    topo = host_topology()
+    nthr = len(topo["cpus"])
+    if topo["quota"]:
+        nthr = min(nthr, max(1, int(topo["quota"])))
+    nthr = int(os.environ.get("CLK_CPU_THREADS", nthr))
+    total = int(os.environ.get("CLK_CPU_SAMPLE_BYTES", max(4 << 30, 4 * topo["l3_bytes"])))   # env: tests only
+    ops = {"CheckIPHeader": oracle_lib.OP_CHECK_IP, "CheckUDPHeader": oracle_lib.OP_CHECK_UDP,
+           "CheckTCPHeader": oracle_lib.OP_CHECK_TCP}
+    out = {}
+    for wl in legs:
+        element, ck = CPU_LEGS[wl]
+        w = WORKLOADS[wl]
+        res = {}
+        for label, t in (("single_thread", 1), ("all_cores", nthr)):
+            cfg = Cfg()
+            cfg.op, cfg.arg, cfg.proto, cfg.imix = ops[element], 1, w["proto"], 1 if wl == "c4" else 0
+            cfg.fixed_len, cfg.stride = w["L"], w["stride"]
+            sample = min(1 << 30, total) if t == 1 else total
+            if wl == "c5" and t > 1 and "CLK_CPU_SAMPLE_BYTES" not in os.environ:
+                sample = (1 << 20) * w["stride"]                # the 1M-packet subset
+            cfg.bytes_per_thread = max(sample // t, 64 << 10)
+            cfg.seed, cfg.reps = 0x5EED, reps
+            cpus = (ctypes.c_int * t)(*topo["cpus"][:t])
+            r = Res()
+            rc = L_.oracle_cpu_baseline(ctypes.byref(cfg), cpus, t, ctypes.byref(r))
+            if rc != 0:
+                res[label] = {"error": "oracle_cpu_baseline rc %d" % rc}
+                continue
+            pps = r.packets / r.median_s
+            ckb = r.bytes if ck is None else r.packets * ck
+            res[label] = {"value": round(ckb / r.median_s / GIB, 3), "unit": "GiB/s", "mpps": round(pps / 1e6, 3),
+                          "threads": t, "pinned": r.pinned, "packets": r.packets,
+                          "sample_bytes": r.packets * w["stride"] if wl != "c4" else cfg.bytes_per_thread * t,
+                          "median_s": round(r.median_s, 5), "min_s": round(r.min_s, 5), "max_s": round(r.max_s, 5),
+                          "ok": r.ok}
+        out[wl] = {"element": element, "workload": w["desc"], **res}
+    return {"legs": out, "threads": nthr, "host": topo | {"cpus": None},
+            "method": "oracle/cksum_oracle.c (-O2 -g restatement of lib/in_cksum.c + the element), one thread "
+                      "pinned per physical core (round-robin over sockets, capped by the cgroup CPU quota), "
+                      "NUMA-local first touch of a DRAM-resident shard per thread, warm-up + median of %d" % reps}
 
 
 def load_traffic(wname, element):
@@ -517,33 +636,158 @@ def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24, glue_pkts=1 
     }
 
 
+# BASELINE config 1: conf/fake-iprouter.click's forwarding path
+# (fake-iprouter.click:38-100) on the 86 B frame of its InfiniteSource,
+# 600000 packets (test/userlevel/iprouter-01.clicktest:243), run through the
+# element glue as the separate elements and as iprouter-01's click-xform
+# combos (IPInputCombo / IPOutputCombo; OUTA == OUTB, iprouter-01:57).
+C1_PACKETS = 600000
+C1_CHAINS = {
+    "elements": [("CheckIPHeader", "INTERFACES 18.26.4.1/24 18.26.7.1/24, OFFSET 14", 2),
+                 ("IPGWOptions", "18.26.4.24", 2), ("FixIPSrc", "18.26.4.24", 1),
+                 ("DecIPTTL", "", 2), ("IPFragmenter", "300", 2)],
+    "combos": [("IPInputCombo", "1, INTERFACES 18.26.4.1/24 18.26.7.1/24", 1),
+               ("IPOutputCombo", "1, 18.26.4.24, 300", 5)],
+}
+
+
+def c1_frame():
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden_vectors.json")))["vectors"]
+    l3 = bytes.fromhex([v for v in g if v["name"] == "fake-iprouter-ip-check"][0]["l3"])
+    return bytes.fromhex("0000c0ae67ef0000000000000800") + l3          # fake-iprouter.click:42-44
+
+
+def config1(ctx, n=C1_PACKETS, batch=65536):
+    """Config 1 through the element glue on the GPU: every element of the
+    chain takes all n frames by push_burst (C++ push() per packet, batches of
+    `batch` double-buffered), flushes and routes them; the next element takes
+    the survivors.  One untimed warm-up run on a copy allocates the staging
+    buffers.  Asserts all n forwarded on port 0 and identical bytes both
+    ways (OUTA == OUTB)."""
+    import numpy as np
+    from click_amd.elements import Element
+    frame = c1_frame()
+    out, arenas = {}, {}
+    for name, chain in C1_CHAINS.items():
+        els = [Element(ctx, cls, ", ".join(x for x in (conf, "BATCH %d" % batch) if x), noutputs=nout)
+               for cls, conf, nout in chain]
+        for timed in (False, True):
+            arena = np.tile(np.frombuffer(frame, np.uint8), n)
+            ptrs = np.uint64(arena.ctypes.data) + np.arange(n, dtype=np.uint64) * np.uint64(len(frame))
+            lens = np.full(n, len(frame), np.uint32)
+            nhs = np.full(n, 14, np.int32)
+            t0 = time.perf_counter()
+            fwd = n
+            for e in els:
+                e.push_burst(ptrs, lens, nhs, first_token=0)
+                e.flush()
+                tok, port, _ = e.results()
+                keep = port == 0
+                fwd = int(keep.sum())
+                ptrs, lens, nhs = ptrs[tok[keep].astype(np.int64)], lens[keep], nhs[keep]
+            dt = time.perf_counter() - t0
+        for e in els:
+            e.close()
+        arenas[name] = arena
+        out[name] = {"chain": [c[0] for c in chain], "forwarded": fwd, "wall_s": round(dt, 4),
+                     "mpps": round(n / dt / 1e6, 2)}
+    same = bool(np.array_equal(arenas["elements"], arenas["combos"]))
+    return {"workload": "C1: conf/fake-iprouter.click forwarding path, %d x %d B frames, element glue on the GPU"
+                        % (n, len(frame)),
+            "packets": n, "expect_forwarded": n, "outa_eq_outb": same,
+            "ok": same and all(v["forwarded"] == n for v in out.values()), **out}
+
+
+def config1_cpu(n=C1_PACKETS):
+    """The same chains on one host thread through the oracle restatement
+    (the byte-touching elements only; Click's scheduler, Classifier and
+    queues are not part of it): CheckIPHeader + IPGWOptions + FixIPSrc +
+    DecIPTTL + IPFragmenter(300), and IPInputCombo + IPOutputCombo."""
+    import numpy as np
+    from tests import oracle_lib
+    frame = c1_frame()
+    fl = len(frame)
+    res = {}
+    for name in ("elements", "combos"):
+        arena = np.tile(np.frombuffer(frame, np.uint8), n)
+        l3 = arena[14:]
+        t0 = time.perf_counter()
+        codes, _ = oracle_lib.batch("check_ip", l3, n, stride=fl, fixed_len=fl - 14)
+        if name == "elements":
+            oracle_lib.ip_out_batch("ip_gw_options", l3, n, stride=fl, fixed_len=fl - 14, my_ip=0x18041A12)
+            oracle_lib.ip_out_batch("fix_ip_src", l3, n, stride=fl, fixed_len=fl - 14, my_ip=0x18041A12,
+                                    flags=np.zeros(n, np.uint8))
+            c2, _ = oracle_lib.batch("dec_ttl", l3, n, stride=fl, fixed_len=fl - 14)
+            fr = oracle_lib.ip_fragment(l3, n, 300, False, stride=fl, fixed_len=fl - 14)
+            fwd = int(((codes == 0) & (c2 == 0) & (fr["port"] == 0)).sum())
+        else:
+            port, _, _ = oracle_lib.ip_out_batch("ip_output_combo", l3, n, stride=fl, fixed_len=fl - 14,
+                                                 my_ip=0x18041A12, mtu=300)
+            fwd = int(((codes == 0) & (port == 0)).sum())
+        dt = time.perf_counter() - t0
+        res[name] = {"forwarded": fwd, "wall_s": round(dt, 4), "mpps": round(n / dt / 1e6, 2)}
+    return {"threads": 1, "kind": "port", **res,
+            "note": "oracle restatement of the byte-touching elements, one host thread; the reference's own "
+                    "`click -t conf/fake-iprouter.click` (Click runtime included) measured 4.3-6.7 Mpps on the "
+                    "survey VM (BASELINE.md §3)"}
+
+
+def spawn_ranks(args):
+    """--gpus N > 1 without a torchrun environment: launch N ranks (one per
+    GPU) under torch.distributed.run as a child process before anything
+    touches the GPU, and exit with its status."""
+    import socket
+    import subprocess
+    s_ = socket.socket()
+    s_.bind(("127.0.0.1", 0))
+    port = s_.getsockname()[1]
+    s_.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log("bench: --gpus %d without WORLD_SIZE: launching %s" % (args.gpus, " ".join(cmd)))
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: the workload's)")
     ap.add_argument("--no-c2", action="store_true", help="skip the extra 64 B (C2) measurement")
+    ap.add_argument("--no-c1", action="store_true", help="skip the config-1 (fake-iprouter) measurement")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-peak", action="store_true", help="skip the read-stream ceiling")
     ap.add_argument("--no-frag", action="store_true", help="skip the IPFragmenter measurement (C3)")
     ap.add_argument("--skip", default="", help="comma list of side configurations to skip: c4,c5")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--e2e", action="store_true", help="measure the host-resident end-to-end rates instead")
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        log("bench: WORLD_SIZE=%d but --gpus %d: refusing to report a mislabelled run" % (world, args.gpus))
+        sys.exit(2)
+    same_dev = os.environ.get("CLK_BENCH_SAME_DEVICE") == "1"
+
     import torch
+    if world > 1 and not same_dev and torch.cuda.device_count() < world:
+        log("bench: --gpus %d but %d GPUs visible" % (world, torch.cuda.device_count()))
+        sys.exit(2)
     import click_amd
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # CLK_BENCH_SAME_DEVICE=1 + CLK_BENCH_BACKEND=gloo rehearse the
     # multi-rank code path with every rank on GPU 0 (RCCL refuses duplicate
     # GPUs); the driver's N>1 runs use RCCL, one rank per GPU.
-    dev = 0 if os.environ.get("CLK_BENCH_SAME_DEVICE") == "1" else local
+    dev = 0 if same_dev else local
     torch.cuda.set_device(dev)
     dist = None
+    coll_dev = "cuda"
     if world > 1:
         import torch.distributed as dist
         backend = os.environ.get("CLK_BENCH_BACKEND", "nccl")
@@ -551,6 +795,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
+            coll_dev = "cpu"
     ctx = click_amd.Context(dev)
     if args.e2e:
         w = WORKLOADS[args.workload]
@@ -559,21 +804,27 @@ def main():
             print(json.dumps({"e2e": res}), flush=True)
         ctx.close()
         return
-
-    main_res = measure(torch, ctx, dist, rank, world, args.workload, args.steps, args.warmup)
+    pk = args.packets or None
+    meas = lambda wl: measure(torch, ctx, dist, rank, world, wl, args.steps, args.warmup, packets=pk,
+                              coll_dev=coll_dev)
+    main_res = meas(args.workload)
     c2 = None
     if args.workload != "c2" and not args.no_c2:
-        c2 = measure(torch, ctx, dist, rank, world, "c2", args.steps, args.warmup)
+        c2 = meas("c2")
     # the other configurations of BASELINE.json, reported beside the
     # headline (C4: IMIX 64M; C5: 9000 B, 16M per GPU = 128M at N = 8)
     extra = {}
     for sect, wl in (("c4_imix", "c4"), ("c5_jumbo", "c5")):
         if args.workload != wl and wl not in args.skip.split(","):
-            extra[sect] = (wl, measure(torch, ctx, dist, rank, world, wl, args.steps, args.warmup))
+            extra[sect] = (wl, meas(wl))
     frag = None
     if args.workload == "c3" and not args.no_frag:
-        frag = measure_fragmenter(torch, ctx, dist, rank, world, args.steps, args.warmup)
+        frag = measure_fragmenter(torch, ctx, dist, rank, world, args.steps, args.warmup, packets=pk,
+                                  coll_dev=coll_dev)
     peak_meas = None if args.no_peak else read_stream_peak(torch, ctx)
+    c1 = None
+    if rank == 0 and world == 1 and not args.no_c1:
+        c1 = config1(ctx)
 
     if rank == 0:
         w = WORKLOADS[args.workload]
@@ -603,9 +854,21 @@ def main():
                           "elements": {e: summarize(r, args.steps, wl) for e, r in res.items()}}
         if frag:
             line["fragmenter"] = frag
-        if world == 1 and not args.no_cpu and args.workload != "c4":
+        if c1:
+            line["c1_fake_iprouter"] = c1
+        if world == 1 and not args.no_cpu:
             try:
-                line["cpu_baseline"] = cpu_baseline(args.workload, head["element"], args.cpu_seconds)
+                cb = cpu_baseline()
+                if c1:
+                    cb["legs"]["c1"] = config1_cpu()
+                head_leg = cb["legs"].get(args.workload, {}).get("all_cores", {})
+                line["cpu_baseline"] = {
+                    "value": head_leg.get("value"), "unit": "GiB/s", "cores": cb["threads"], "kind": "port",
+                    "mpps": head_leg.get("mpps"),
+                    "sample": "%s over %s packets (%s B, DRAM-resident, NUMA-local shards), median of 5"
+                              % (cb["legs"][args.workload]["element"], head_leg.get("packets"),
+                                 head_leg.get("sample_bytes")),
+                    "cpu": cb["host"]["model"], **cb}
             except Exception as e:        # reported, not fatal
                 line["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(line), flush=True)

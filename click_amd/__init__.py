@@ -338,9 +338,17 @@ class Context:
         cb = b.c()
         self._check(self.lib.clk_gen_packets(self.h, ctypes.byref(cb), proto, seed, first_idx))
 
-    def gen_corrupt(self, b, seed=0xBAD, rate_log2=10):
+    def gen_corrupt(self, b, seed=0xBAD, rate_log2=10, first_idx=None, lo=None, hi=0):
+        """Flip one bit in 1 of 2^rate_log2 packets (clk_gen_corrupt, or
+        clk_gen_corrupt_span when first_idx / lo / hi are given: the pick
+        hashed on the global index first_idx + i, the byte drawn from
+        [lo, min(hi, len_i))).  Calling it twice restores the batch."""
         cb = b.c()
-        self._check(self.lib.clk_gen_corrupt(self.h, ctypes.byref(cb), seed, rate_log2))
+        if first_idx is None and lo is None and not hi:
+            self._check(self.lib.clk_gen_corrupt(self.h, ctypes.byref(cb), seed, rate_log2))
+        else:
+            self._check(self.lib.clk_gen_corrupt_span(self.h, ctypes.byref(cb), seed, first_idx or 0, rate_log2,
+                                                      0xFFFFFFFF if lo is None else lo, hi))
 
     def read_stream(self, t, nbytes=None, out=None):
         if out is None:

@@ -140,6 +140,8 @@ SIGNATURES = {
     "clk_pcap_force_ip": (ctypes.c_int32, [_P, ctypes.c_uint32, ctypes.c_int32]),
     "clk_gen_packets": (ctypes.c_int, [_P, _BP, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64]),
     "clk_gen_corrupt": (ctypes.c_int, [_P, _BP, ctypes.c_uint64, ctypes.c_uint32]),
+    "clk_gen_corrupt_span": (ctypes.c_int, [_P, _BP, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.c_uint32, ctypes.c_uint32]),
     "clk_read_stream": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P]),
     # include/click_amd_elements.h
     "clk_element_create": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,

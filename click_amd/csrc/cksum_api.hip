@@ -272,9 +272,11 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
     if (!code) return fail(ctx, CLK_EINVAL, "%s: null output", fn);
     uint32_t *work = nullptr;
     const bool bins = use_bins(ctx, b);
-    // auto (-1): two-phase for the fixed-geometry and size-class Set kernels,
-    // fused for the packet-stream kernel (its phase C stores)
     const bool stream = bins && ctx->varlen == 2;
+    // auto (-1): two-phase for the fixed-geometry and size-class Set
+    // kernels (a read-only compute pass, then field_scatter_kernel), fused
+    // for the packet-stream kernel (phase C stores the field's 64 B block
+    // from its LDS stash); DESIGN.md §6
     const bool two = SET && (ctx->set_mode == 1 || (ctx->set_mode < 0 && !stream));
     const ScratchLayout L = scratch_layout(b->n);
     if (two || bins) {
@@ -814,15 +816,21 @@ int clk_gen_packets(clk_ctx *ctx, const clk_batch *b, int proto, uint64_t seed, 
     return check_launch(ctx, "clk_gen_packets");
 }
 
-int clk_gen_corrupt(clk_ctx *ctx, const clk_batch *b, uint64_t seed, uint32_t rate_log2)
+int clk_gen_corrupt_span(clk_ctx *ctx, const clk_batch *b, uint64_t seed, uint64_t first_idx, uint32_t rate_log2,
+                         uint32_t lo, uint32_t hi)
 {
     int r = enter(ctx);
     if (r) return r;
     if ((r = check_batch(ctx, b, "clk_gen_corrupt"))) return r;
     if (b->n == 0) return CLK_SUCCESS;
     hipLaunchKernelGGL(clk::corrupt_kernel, dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0, ctx->cur,
-                       args_of(b), seed, rate_log2);
+                       args_of(b), seed, first_idx, rate_log2, lo, hi);
     return check_launch(ctx, "clk_gen_corrupt");
+}
+
+int clk_gen_corrupt(clk_ctx *ctx, const clk_batch *b, uint64_t seed, uint32_t rate_log2)
+{
+    return clk_gen_corrupt_span(ctx, b, seed, 0, rate_log2, ~0u, 0);
 }
 
 int clk_read_stream(clk_ctx *ctx, const void *base, uint64_t bytes, uint64_t *out_sum)

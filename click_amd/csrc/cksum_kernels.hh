@@ -514,10 +514,94 @@ __device__ __forceinline__ void set_field_store(uint8_t *nh, const L4State &st, 
     }
 }
 
-template <int PROTO, bool SET, bool DEFER>
-__device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum, L4State &st, bool writer,
-                                          uint8_t *out_code, uint16_t *out_sum, uint32_t *work,
-                                          uint32_t gl = 0, uint32_t ng = 1)
+// Set stores from registers (CLK_SET_REGBLK).  When the 64 B-aligned block
+// holding the checksum field lies inside the packet, the lanes that loaded
+// its four 16 B chunks in pass 0 still hold them: they patch the field (and
+// the FIXOFF byte) and store the whole block, so HBM sees a full-block write
+// and no read-modify-write, with no re-read.  Returns false when the block
+// is not available (the caller stores the field bytes alone).
+//   v[k] holds chunk k*G + gl of [c0, ...) (group_range_sum's layout); the
+//   block's chunks are q0..q0+3 with q0 <= 4, so only v[k] with k*G < 8 can
+//   hold one and the rest need not stay live across later passes.
+#ifndef CLK_SET_REGBLK
+#define CLK_SET_REGBLK 1
+#endif
+__device__ __forceinline__ void store_block16(uint64_t ca, u32x4 w)
+{
+    if (CLK_NT_STORES)
+        __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x4 *)ca);
+    else
+        *(__attribute__((address_space(1))) u32x4 *)ca = w;
+}
+
+template <int PROTO, int G, int K>
+__device__ __forceinline__ bool set_block_store_regs(uint8_t *nh, const L4State &st, uint32_t r, uint32_t gl,
+                                                     uint64_t c0, const u32x4 (&v)[K])
+{
+    constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
+    const uint64_t a = (uint64_t)nh, fa = a + st.hl + FIELD, xa = a + st.hl + 12;
+    const uint64_t blk = fa & ~63ull;
+    // fa + 1 in the block too (an odd field at byte 63 straddles two blocks)
+    if (!(blk >= a && blk + 64 <= a + st.caplen && fa + 1 < blk + 64))
+        return false;
+    const uint32_t q0 = (uint32_t)(blk - c0) >> 4;          // 0..4
+    if (q0 + 4 > (uint32_t)(G * K))
+        return false;
+    const bool fix_in = st.fix && xa >= blk && xa < blk + 64;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        if (k * G >= 8)
+            break;
+        const uint32_t c = (uint32_t)(k * G) + gl;
+        if (c >= q0 && c < q0 + 4) {
+            u32x4 w = v[k];
+            const uint64_t ca = c0 + 16ull * c;
+            patch_byte(w, ca, fa, r);
+            patch_byte(w, ca, fa + 1, r >> 8);
+            if (fix_in)
+                patch_byte(w, ca, xa, st.new_b12);
+            store_block16(ca, w);
+        }
+    }
+    if (gl == 0 && st.fix && !fix_in)
+        nh[st.hl + 12] = (uint8_t)st.new_b12;
+    return true;
+}
+
+// l4_finish with the fused Set store given as store(r).
+// The same from the packet-stream kernel's LDS stash: chunks 0..HC-1 of
+// [c0, ...) of this lane's packet.
+template <int PROTO, int HC>
+__device__ __forceinline__ bool set_block_store_stash(uint8_t *nh, const L4State &st, uint32_t r, uint64_t c0,
+                                                      const u32x4 (&hs)[HC])
+{
+    constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
+    const uint64_t a = (uint64_t)nh, fa = a + st.hl + FIELD, xa = a + st.hl + 12;
+    const uint64_t blk = fa & ~63ull;
+    if (!(blk >= a && blk + 64 <= a + st.caplen && fa + 1 < blk + 64))
+        return false;
+    const uint32_t q0 = (uint32_t)(blk - c0) >> 4;
+    if (q0 + 4 > (uint32_t)HC)
+        return false;
+    const bool fix_in = st.fix && xa >= blk && xa < blk + 64;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        u32x4 w = hs[q0 + q];
+        const uint64_t ca = blk + 16ull * q;
+        patch_byte(w, ca, fa, r);
+        patch_byte(w, ca, fa + 1, r >> 8);
+        if (fix_in)
+            patch_byte(w, ca, xa, st.new_b12);
+        store_block16(ca, w);
+    }
+    if (st.fix && !fix_in)
+        nh[st.hl + 12] = (uint8_t)st.new_b12;
+    return true;
+}
+
+template <int PROTO, bool SET, bool DEFER, typename Store>
+__device__ __forceinline__ void l4_finish_with(uint8_t *nh, uint64_t i, uint32_t sum, L4State &st, bool writer,
+                                               uint8_t *out_code, uint16_t *out_sum, uint32_t *work, Store &&store)
 {
     uint32_t stored = 0;
     if (st.code == OK && st.summing) {
@@ -536,7 +620,7 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
                     work[i] = 0x80000000u | (st.hl << 16) | r;
                 }
             } else {
-                set_field_store<PROTO>(nh, st, r, gl, ng, writer);
+                store(r);
             }
 #endif
         } else if (r != 0) {
@@ -554,6 +638,15 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
         if (SET && out_sum)
             out_sum[i] = (uint16_t)stored;
     }
+}
+
+template <int PROTO, bool SET, bool DEFER>
+__device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum, L4State &st, bool writer,
+                                          uint8_t *out_code, uint16_t *out_sum, uint32_t *work,
+                                          uint32_t gl = 0, uint32_t ng = 1)
+{
+    l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, writer, out_code, out_sum, work,
+                                      [&](uint32_t r) { set_field_store<PROTO>(nh, st, r, gl, ng, writer); });
 }
 
 // Fixed geometry: G lanes per packet.  Every lane of a group issues the
@@ -582,13 +675,21 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         const uint8_t *c0 = (const uint8_t *)(a & ~15ull);
         const uint32_t nch = (uint32_t)((((a + caplen + 15) & ~15ull) - (uint64_t)c0) / 16);
         u32x4 v[K];
-        constexpr bool NT = UseNT<!SET>::value;
+        // nontemporal for Check and for the read-only compute pass of a
+        // two-phase Set
+        constexpr bool NT = UseNT<!SET || DEFER>::value;
         load_pass<G, K, NT>(c0, nch, 0, gl, v);  // issued before the header loads
         L4State st;
         l4_parse<PROTO, SET>(nh, caplen, fixoff, st);
         // a lane whose packet needs no sum masks everything (len 0)
         const uint32_t sum = group_range_sum<G, K, NT>(c0, nch, gl, v, a + st.hl, st.summing ? st.rlen : 0);
-        l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, gl == 0, out_code, out_sum, work, gl, G);
+        if (SET && !DEFER && CLK_SET_REGBLK)
+            l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, gl == 0, out_code, out_sum, work, [&](uint32_t r) {
+                if (!set_block_store_regs<PROTO, G, K>(nh, st, r, gl, (uint64_t)c0, v))
+                    set_field_store<PROTO>(nh, st, r, gl, G, gl == 0);
+            });
+        else
+            l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, gl == 0, out_code, out_sum, work, gl, G);
     }
 }
 
@@ -781,7 +882,7 @@ __device__ __forceinline__ uint32_t chunk_outside(const u32x4 V, uint64_t ca, ui
 template <int PROTO, bool SET, bool DEFER, int KV, bool PF, bool MARKS>
 __global__ void __launch_bounds__(256)
 #if CLK_SWPE
-__attribute__((amdgpu_waves_per_eu(PROTO == TCP && CLK_SWPE > 7 ? 7 : CLK_SWPE)))
+__attribute__((amdgpu_waves_per_eu(SET && CLK_SET_REGBLK && CLK_SWPE > 6 ? 6 : PROTO == TCP && CLK_SWPE > 7 ? 7 : CLK_SWPE)))
 #endif
 l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                         uint16_t *out_sum, uint32_t *work)
@@ -790,7 +891,9 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
     // stashed head chunks: every header dword when (nh&~3) - c0 + 4*HDR_DW <= 16*HC
     // (always for HC = 4 / 3; for 16 B-aligned packets with 3 / 2), else
     // the parse loads the missing dwords itself
-    constexpr int HC = PROTO == TCP ? 3 + CLK_SHC_EXTRA : 2 + CLK_SHC_EXTRA;
+    // A Set stashes 4 (the field's 64 B block, stored whole from the stash).
+    constexpr int HC0 = PROTO == TCP ? 3 + CLK_SHC_EXTRA : 2 + CLK_SHC_EXTRA;
+    constexpr int HC = SET && CLK_SET_REGBLK && HC0 < 4 ? 4 : HC0;
     __shared__ u32x4 head[4][64][HC];
     __shared__ u32x4 tail[4][64];
     __shared__ u32x4 pk[4][64];       // {c0 lo, c0 hi, chunk start, nch | odd << 31}
@@ -1000,7 +1103,13 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                     sum = lane_range_sum(s, rlen);
                 }
             }
-            l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work);
+            if (SET && !DEFER && CLK_SET_REGBLK)
+                l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work, [&](uint32_t r) {
+                    if (!set_block_store_stash<PROTO, HC>(nh, st, r, c0, head[wv][lane]))
+                        set_field_store<PROTO>(nh, st, r, 0, 1, true);
+                });
+            else
+                l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work);
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -1474,19 +1583,26 @@ __global__ void __launch_bounds__(256) gen_kernel(BatchArgs b, int proto, uint64
     }
 }
 
-__global__ void __launch_bounds__(256) corrupt_kernel(BatchArgs b, uint64_t seed, uint32_t rate_log2)
+// Packet i (global index first_idx + i) is picked when the low rate_log2
+// bits of h = splitmix64(seed ^ (first_idx + i) * C) are zero; one bit of
+// byte lo + (h >> 20) % (hi' - lo) is flipped, hi' = min(hi, len) (hi = 0:
+// len; lo = ~0u: 40 / 20 / 0 by length, the payload past the headers).
+// Flipping twice restores the batch.  bench.py recomputes the picks.
+__global__ void __launch_bounds__(256) corrupt_kernel(BatchArgs b, uint64_t seed, uint64_t first_idx,
+                                                      uint32_t rate_log2, uint32_t lo_arg, uint32_t hi_arg)
 {
     const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t mask = rate_log2 >= 64 ? ~0ull : ((1ull << rate_log2) - 1);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += nthreads) {
-        const uint64_t h = splitmix64(seed ^ (i * 0xD1B54A32D192ED03ull));
+        const uint64_t h = splitmix64(seed ^ ((first_idx + i) * 0xD1B54A32D192ED03ull));
         if ((h & mask) != 0)
             continue;
         const uint32_t len = pkt_len(b, i);
-        const uint32_t lo = len > 40 ? 40 : (len > 20 ? 20 : 0);
-        if (len <= lo)
+        const uint32_t lo = lo_arg != ~0u ? lo_arg : (len > 40 ? 40 : (len > 20 ? 20 : 0));
+        const uint32_t hi = hi_arg && hi_arg < len ? hi_arg : len;
+        if (hi <= lo)
             continue;
-        const uint32_t pos = lo + (uint32_t)((h >> 20) % (uint64_t)(len - lo));
+        const uint32_t pos = lo + (uint32_t)((h >> 20) % (uint64_t)(hi - lo));
         uint8_t *p = b.base + pkt_off(b, i) + pos;
         *p ^= (uint8_t)(1u << ((h >> 8) & 7));
     }

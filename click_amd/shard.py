@@ -46,12 +46,15 @@ def digest(torch, codes, sums=None):
 
 def reduce_results(torch, dist, device, wall_s, kernel_ms, dig):
     """All-reduce the timing (MAX) and the digest (SUM / XOR) over ranks.
-    Returns (wall_s, kernel_ms, digest) as seen by every rank."""
+    dig = [ok, packets, sum16, xor16, extra counts...]: entry 3 is
+    xor-folded, every other entry summed.  Returns (wall_s, kernel_ms,
+    digest) as seen by every rank."""
     if dist is None:
         return wall_s, kernel_ms, list(dig)
     t = torch.tensor([wall_s, kernel_ms], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    d = torch.tensor(dig[:3], dtype=torch.int64, device=device)
+    summed = list(dig[:3]) + list(dig[4:])           # entries past the xor-fold are counts too
+    d = torch.tensor(summed, dtype=torch.int64, device=device)
     dist.all_reduce(d, op=dist.ReduceOp.SUM)
     x = torch.tensor([dig[3]], dtype=torch.int64, device=device)
     gathered = [torch.zeros_like(x) for _ in range(dist.get_world_size())]
@@ -59,4 +62,5 @@ def reduce_results(torch, dist, device, wall_s, kernel_ms, dig):
     xr = 0
     for g in gathered:
         xr ^= int(g.item())
-    return float(t[0]), float(t[1]), [int(d[0]), int(d[1]), int(d[2]), xr]
+    d = [int(v) for v in d.tolist()]
+    return float(t[0]), float(t[1]), d[:3] + [xr] + d[3:]

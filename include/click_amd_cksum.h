@@ -308,6 +308,12 @@ int clk_gen_packets(clk_ctx *ctx, const clk_batch *batch, int proto,
  * `rate_log2` bits zero (1 in 2^rate_log2), for Check-mode drop tests.      */
 int clk_gen_corrupt(clk_ctx *ctx, const clk_batch *batch, uint64_t seed,
                     uint32_t rate_log2);
+/* The same with the pick hashed on the global index first_idx + i and the
+ * flipped byte drawn from [lo, min(hi, len_i)) (hi = 0: len_i; lo = ~0u:
+ * the default payload span of clk_gen_corrupt).  Calling it twice with the
+ * same arguments restores the batch.                                        */
+int clk_gen_corrupt_span(clk_ctx *ctx, const clk_batch *batch, uint64_t seed, uint64_t first_idx,
+                         uint32_t rate_log2, uint32_t lo, uint32_t hi);
 
 /* Sum of `bytes` starting at device `base`, read once as 16-byte loads: the
  * measured HBM read-stream ceiling for the roofline (bench only).          */

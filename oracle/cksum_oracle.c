@@ -856,3 +856,172 @@ double oracle_bench(int op, uint8_t *base, uint64_t stride, uint32_t fixed_len,
     free(th);
     return dt;
 }
+
+/* ---- CPU baseline per BASELINE.md §2 ---------------------------------------
+ * One thread per entry of cpus[] (the caller passes one logical CPU of each
+ * physical core), pinned before it allocates and generates its own shard, so
+ * every shard is first-touched on the thread's NUMA node.  Each shard holds
+ * bytes_per_thread of packets -- sized by the caller well above the last-level
+ * cache, so the timed passes stream from DRAM -- generated with the same
+ * splitmix64 packets as the GPU (oracle_gen_packet, global index
+ * t * npkt + i), checksums set, then: one warm-up pass, and `reps` timed
+ * passes, each between two barriers (all threads start together; a pass ends
+ * when the slowest shard is done).  imix = 1: packet sizes 64/576/1500 by
+ * the same hash and 7:4:1 odds as bench.py's C4 layout, packed at 64-byte
+ * aligned offsets; otherwise fixed_len-byte packets in stride-byte slots. */
+struct cb_thread {
+    const struct oracle_cb_cfg *cfg;
+    int t, cpu;
+    pthread_barrier_t *bar;
+    double *rep_s;               /* thread 0 writes the pass times */
+    uint64_t packets, bytes, ok, gen_ns;
+    int pinned, err;
+};
+
+static uint64_t imix_len(uint64_t seed, uint64_t i)
+{
+    /* bench.py imix_layout: splitmix64 finalizer of i*golden + seed, mod 12 */
+    uint64_t x = i * 0x9E3779B97F4A7C15ull + seed;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    x ^= x >> 31;
+    const uint64_t r = x % 12;
+    return r < 7 ? 64 : (r < 11 ? 576 : 1500);
+}
+
+static void *cb_run(void *vp)
+{
+    struct cb_thread *a = (struct cb_thread *)vp;
+    const struct oracle_cb_cfg *c = a->cfg;
+    if (a->cpu >= 0) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(a->cpu, &set);
+        a->pinned = pthread_setaffinity_np(pthread_self(), sizeof set, &set) == 0;
+    }
+    /* shard layout: fixed slots, or IMIX packed at 64 B-aligned offsets */
+    uint64_t n, bytes;
+    uint64_t *off = 0;
+    uint32_t *len = 0;
+    if (c->imix) {
+        /* packets until the shard bytes are used; mean slot ~ 384 B */
+        uint64_t cap = c->bytes_per_thread / 64 + 1;
+        off = malloc(cap * sizeof *off);
+        len = malloc(cap * sizeof *len);
+        if (!off || !len) { a->err = 1; free(off); free(len); return 0; }
+        uint64_t pos = 0, k = 0;
+        const uint64_t first = (uint64_t)a->t * cap;
+        for (; k < cap; k++) {
+            const uint64_t L = imix_len(c->seed, first + k);
+            const uint64_t slot = (L + 63) & ~63ull;
+            if (pos + slot > c->bytes_per_thread)
+                break;
+            off[k] = pos;
+            len[k] = (uint32_t)L;
+            pos += slot;
+        }
+        n = k;
+        bytes = pos;
+    } else {
+        n = c->bytes_per_thread / c->stride;
+        bytes = n * c->stride;
+    }
+    uint8_t *arena = 0;
+    if (posix_memalign((void **)&arena, 4096, bytes ? bytes : 4096)) {
+        a->err = 1;
+        free(off); free(len);
+        return 0;
+    }
+    struct timespec g0, g1;
+    clock_gettime(CLOCK_MONOTONIC, &g0);
+    /* first touch + generation on this thread's node */
+    const uint64_t first_idx = (uint64_t)a->t * (n + 1);
+    oracle_gen_batch(arena, off, c->stride, len, c->fixed_len, n, c->proto, c->seed, first_idx);
+    uint16_t s;
+    for (uint64_t i = 0; i < n; i++) {
+        uint8_t *p = arena + (off ? off[i] : i * c->stride);
+        const uint32_t l = len ? len[i] : c->fixed_len;
+        run_one(ORACLE_OP_SET_IP, p, l, 1, &s);
+        if (l >= 28)
+            run_one(c->proto == 6 ? ORACLE_OP_SET_TCP : ORACLE_OP_SET_UDP, p, l, 0, &s);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &g1);
+    a->gen_ns = (uint64_t)((g1.tv_sec - g0.tv_sec) * 1000000000ll + (g1.tv_nsec - g0.tv_nsec));
+    a->packets = n;
+    uint64_t sum_len = 0;
+    for (uint64_t i = 0; i < n; i++)
+        sum_len += len ? len[i] : c->fixed_len;
+    a->bytes = sum_len;
+    uint64_t ok = 0;
+    for (int r = -1; r < c->reps; r++) {          /* r = -1: warm-up */
+        pthread_barrier_wait(a->bar);
+        struct timespec t0, t1;
+        if (a->t == 0)
+            clock_gettime(CLOCK_MONOTONIC, &t0);
+        ok = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            uint8_t *p = arena + (off ? off[i] : i * c->stride);
+            ok += run_one(c->op, p, len ? len[i] : c->fixed_len, c->arg, &s) == 0;
+        }
+        pthread_barrier_wait(a->bar);
+        if (a->t == 0 && r >= 0) {
+            clock_gettime(CLOCK_MONOTONIC, &t1);
+            a->rep_s[r] = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+        }
+    }
+    a->ok = ok;
+    free(arena);
+    free(off);
+    free(len);
+    return 0;
+}
+
+static int cmp_double(const void *x, const void *y)
+{
+    const double a = *(const double *)x, b = *(const double *)y;
+    return a < b ? -1 : a > b;
+}
+
+int oracle_cpu_baseline(const struct oracle_cb_cfg *cfg, const int *cpus, int nthreads,
+                        struct oracle_cb_result *res)
+{
+    if (!cfg || !res || nthreads < 1 || cfg->reps < 1 || cfg->reps > 64 ||
+        (!cfg->imix && (cfg->stride == 0 || cfg->fixed_len > cfg->stride)))
+        return -1;
+    memset(res, 0, sizeof *res);
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, 0, (unsigned)nthreads);
+    struct cb_thread *a = calloc((size_t)nthreads, sizeof *a);
+    pthread_t *th = calloc((size_t)nthreads, sizeof *th);
+    double rep_s[64];
+    for (int t = 0; t < nthreads; t++) {
+        a[t].cfg = cfg;
+        a[t].t = t;
+        a[t].cpu = cpus ? cpus[t] : -1;
+        a[t].bar = &bar;
+        a[t].rep_s = rep_s;
+    }
+    for (int t = 1; t < nthreads; t++)
+        pthread_create(&th[t], 0, cb_run, &a[t]);
+    cb_run(&a[0]);
+    for (int t = 1; t < nthreads; t++)
+        pthread_join(th[t], 0);
+    pthread_barrier_destroy(&bar);
+    int err = 0;
+    for (int t = 0; t < nthreads; t++) {
+        err |= a[t].err;
+        res->packets += a[t].packets;
+        res->bytes += a[t].bytes;
+        res->ok += a[t].ok;
+        res->pinned += a[t].pinned;
+        if ((double)a[t].gen_ns * 1e-9 > res->gen_s)
+            res->gen_s = (double)a[t].gen_ns * 1e-9;
+    }
+    qsort(rep_s, (size_t)cfg->reps, sizeof rep_s[0], cmp_double);
+    res->median_s = rep_s[cfg->reps / 2];
+    res->min_s = rep_s[0];
+    res->max_s = rep_s[cfg->reps - 1];
+    free(a);
+    free(th);
+    return err ? -2 : 0;
+}

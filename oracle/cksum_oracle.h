@@ -105,6 +105,25 @@ void oracle_gen_batch(uint8_t *base, const uint64_t *off, uint64_t stride,
 double oracle_bench(int op, uint8_t *base, uint64_t stride, uint32_t fixed_len,
                     uint64_t n, int reps, int nthreads);
 
+/* CPU baseline per BASELINE.md §2 (bench.py cpu_baseline): `nthreads`
+ * threads, thread t pinned to cpus[t] (NULL: unpinned) BEFORE it allocates
+ * and generates its own DRAM-resident shard of bytes_per_thread (NUMA-local
+ * first touch); a warm-up pass, then `reps` passes between barriers; the
+ * median / min / max pass wall time and the per-pass totals are returned.  */
+struct oracle_cb_cfg {
+    int op, arg, proto, imix;
+    uint32_t fixed_len;
+    uint64_t stride, bytes_per_thread, seed;
+    int reps;
+};
+struct oracle_cb_result {
+    double median_s, min_s, max_s, gen_s;
+    uint64_t packets, bytes, ok;      /* per pass, all threads */
+    int pinned;                       /* threads whose affinity call succeeded */
+};
+int oracle_cpu_baseline(const struct oracle_cb_cfg *cfg, const int *cpus, int nthreads,
+                        struct oracle_cb_result *res);
+
 #ifdef __cplusplus
 }
 #endif

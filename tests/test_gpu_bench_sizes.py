@@ -1,0 +1,137 @@
+"""GPU tests at the bench's own sizes (BASELINE configs 4 and 5) and of the
+bench's multi-rank path.
+
+* C4: the full 64M-packet IMIX batch of bench.py (64/576/1500 B, 7:4:1,
+  packed at 64 B-aligned offsets) through the packet-stream kernels: Set
+  then Check pass everywhere, a random sample matches the oracle byte for
+  byte, and one flipped bit in 1/1024 packets is caught exactly on those
+  packets (except where SetUDPChecksum stored uh_sum = 0, which
+  CheckUDPHeader does not verify: checkudpheader.cc:100).
+* C5: one GPU's 16M x 9000 B TCP shard (128M over 8 GPUs), same checks.
+* bench.py --gpus 2 (two gloo ranks on GPU 0) reports n_gpus 2 and the
+  same digest as one rank over both shards.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from tests import oracle_lib
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+@pytest.fixture(scope="module")
+def ctx(torch):
+    import click_amd
+    c = click_amd.Context(0)
+    yield c
+    c.close()
+
+
+def oracle_packet(L, proto, idx):
+    ref = np.zeros(L, np.uint8)
+    oracle_lib.gen(ref, 1, fixed_len=L, proto=proto, first_idx=idx)
+    oracle_lib.batch("set_ip", ref, 1, fixed_len=L)
+    oracle_lib.batch("set_udp" if proto == 17 else "set_tcp", ref, 1, fixed_len=L, arg=0)
+    return ref
+
+
+def check_full_batch(torch, ctx, b, n, proto, off_np, len_np, sample=384):
+    import bench
+    st, _ = ctx.set_ip_checksum(b, want_sums=False)
+    assert int(ctx.count_codes(st)[0]) == n
+    st, sums = ctx.set_udp_checksum(b) if proto == 17 else ctx.set_tcp_checksum(b)
+    assert int(ctx.count_codes(st)[0]) == n
+    v = ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)
+    assert int(ctx.count_codes(v)[0]) == n
+    assert int(ctx.count_codes(ctx.check_ip_header(b))[0]) == n
+    # a sample of packets, byte for byte against the oracle
+    rng = np.random.default_rng(proto * 1000 + n % 997)
+    idx = np.sort(rng.choice(n, sample, replace=False))
+    for i in idx:
+        o, L = int(off_np[i]), int(len_np[i])
+        got = b.base[o:o + L].cpu().numpy()
+        assert np.array_equal(got, oracle_packet(L, proto, int(i))), "packet %d" % i
+    # corruption caught exactly (the bench's timed Check batches)
+    picks = bench.corrupt_picks(0, n)
+    ctx.gen_corrupt(b, seed=bench.CORRUPT_SEED, rate_log2=bench.CORRUPT_LOG2, first_idx=0)
+    v = (ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)).cpu().numpy()
+    detect = picks & (sums.cpu().numpy() != 0) if proto == 17 else picks
+    assert detect.sum() > 0
+    assert np.array_equal(v == 3, detect)
+    assert np.array_equal(v == 0, ~detect)
+    ctx.gen_corrupt(b, seed=bench.CORRUPT_SEED, rate_log2=bench.CORRUPT_LOG2, first_idx=0)   # restore
+    v = ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)
+    assert int(ctx.count_codes(v)[0]) == n
+
+
+def test_c4_full_imix_batch(torch, ctx):
+    import bench
+    import click_amd
+    n = bench.WORKLOADS["c4"]["n"]
+    off, ln, total, _ = bench.imix_layout(torch, n, 0x5EED, 0)
+    arena = torch.empty(total, dtype=torch.uint8, device="cuda")
+    b = click_amd.Batch(arena, n, off=off, length=ln, max_len=1500)
+    ctx.gen_packets(b, proto=17)
+    try:
+        check_full_batch(torch, ctx, b, n, 17, off.cpu().numpy(), ln.cpu().numpy())
+    finally:
+        del arena, b
+        torch.cuda.empty_cache()
+
+
+def test_c5_full_jumbo_shard(torch, ctx):
+    import bench
+    import click_amd
+    w = bench.WORKLOADS["c5"]
+    n, L, stride = w["n"], w["L"], w["stride"]
+    arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda")
+    b = click_amd.Batch(arena, n, stride=stride, fixed_len=L)
+    ctx.gen_packets(b, proto=6)
+    try:
+        check_full_batch(torch, ctx, b, n, 6, np.arange(n, dtype=np.uint64) * np.uint64(stride),
+                         np.full(n, L, np.uint32), sample=128)
+    finally:
+        del arena, b
+        torch.cuda.empty_cache()
+
+
+def run_bench(gpus, packets, extra_env=None):
+    env = dict(os.environ, CLK_BENCH_SAME_DEVICE="1", CLK_BENCH_BACKEND="gloo", **(extra_env or {}))
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--packets", str(packets),
+           "--steps", "2", "--warmup", "1", "--no-c2", "--no-c1", "--no-cpu", "--no-peak", "--no-frag",
+           "--skip", "c4,c5"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_two_ranks_match_one(torch):
+    """bench.py --gpus 2 launches two ranks itself (no WORLD_SIZE), reports
+    n_gpus 2, and the reduced digests equal one rank's over both shards."""
+    n = 1 << 17
+    two = run_bench(2, n)
+    one = run_bench(1, 2 * n)
+    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["packets_per_gpu"] == n
+    for e in ("CheckUDPHeader", "SetUDPChecksum"):
+        assert two["elements"][e]["verify"] == one["elements"][e]["verify"], e
+        assert two["elements"][e]["verify"]["packets"] == 2 * n
+    chk = two["elements"]["CheckUDPHeader"]["verify"]
+    assert chk["drops_exact"] and chk["drops"] > 0

@@ -98,6 +98,13 @@ VARIANTS = {
     "k12": (["-DCLK_K=12"], {}),
     "k9": (["-DCLK_K=9"], {}),
     "k10": (["-DCLK_K=10"], {}),
+    "regblk0": (["-DCLK_SET_REGBLK=0"], {}),
+    "ntst": (["-DCLK_NT_STORES=1"], {}),
+    "nt_ntst": (["-DCLK_NT_LOADS=1", "-DCLK_NT_STORES=1"], {}),
+    "two_nt": (["-DCLK_NT_LOADS=1"], {"CLK_SET_MODE": "1"}),
+    "regblk_fused": ([], {"CLK_SET_MODE": "0"}),
+    "two_stream_nt": (["-DCLK_NT_LOADS=1"], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
+    "regblk0_fused": (["-DCLK_SET_REGBLK=0"], {"CLK_SET_MODE": "0"}),
 }
 
 
