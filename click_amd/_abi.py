@@ -107,6 +107,7 @@ _OP = ctypes.POINTER(clk_ip_out_cfg)
 # name -> (restype, argtypes); every symbol include/*.h declares
 SIGNATURES = {
     "clk_abi_version": (ctypes.c_int, []),
+    "clk_device_count": (ctypes.c_int, []),
     "clk_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_P)]),
     "clk_ctx_destroy": (ctypes.c_int, [_P]),
     "clk_ctx_set_stream": (ctypes.c_int, [_P, _P]),
@@ -147,6 +148,7 @@ SIGNATURES = {
     "clk_element_create": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                           ctypes.POINTER(_P)]),
     "clk_element_destroy": (ctypes.c_int, [_P]),
+    "clk_element_last_error": (ctypes.c_char_p, [_P]),
     "clk_element_push": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64]),
     "clk_element_push_burst": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_uint64, ctypes.c_uint32]),
     "clk_element_push_anno": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint32,

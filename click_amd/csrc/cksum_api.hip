@@ -345,6 +345,20 @@ extern "C" {
 
 int clk_abi_version(void) { return CLK_ABI_VERSION; }
 
+int clk_device_count(void)
+{
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e == hipErrorNoDevice)
+        return 0;
+    if (e != hipSuccess)
+        return hip_fail(nullptr, e, "hipGetDeviceCount");
+    int n = 0;
+    for (int d = 0; d < ndev; d++)
+        n += is_gfx950(d) ? 1 : 0;
+    return n;
+}
+
 int clk_ctx_create(int device, clk_ctx **out)
 {
     if (!out)

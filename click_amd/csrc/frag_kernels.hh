@@ -316,6 +316,19 @@ __device__ __forceinline__ uint32_t frag_hdr_dword(const uint8_t *ip, uint32_t c
 // order, so every tile waited on has started and publishes its aggregate
 // without waiting: the wait always ends.  The spin is bounded anyway (a bug
 // cannot hang the GPU; a timeout sets err).
+constexpr uint8_t FRAG_PORT_NOROOM = 3;     // CLK_FRAG_NOROOM (include/click_amd_cksum.h)
+constexpr uint8_t FRAG_PORT_FAULT = 0xFF;   // CLK_FRAG_FAULT
+
+// Put back the four header fields the first-fragment rewrite changes
+// (ip_len, ip_id, ip_off, ip_sum) from the original dwords h[0..2].
+__device__ __forceinline__ void frag_restore_header(uint8_t *ip, const uint32_t *h)
+{
+    st_u16(ip + 2, h[0] >> 16);
+    st_u16(ip + 4, h[1] & 0xFFFF);
+    st_u16(ip + 6, h[1] >> 16);
+    st_u16(ip + 10, h[2] >> 16);
+}
+
 struct FragLookback {
     uint32_t *ticket;           // 1 word, zeroed before the launch
     uint32_t *err;              // set when a look-back spin times out (the context's fault word, read by clk_ctx_sync)
@@ -350,7 +363,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
     __shared__ uint32_t hdr[NG][16];                       // per group: the packet's header dwords
     __shared__ uint32_t optw[NG][11];                      // per group: copied options (<= 40 B + pad)
     __shared__ uint64_t lb_base[2];
-    __shared__ uint32_t lb_tile;
+    __shared__ uint32_t lb_tile, lb_fault;
     // fused: the original 20-byte headers of the tile's plain (ip_hl 5)
     // fragmenting packets, whose first-fragment header the prologue already
     // rewrote in place (word 0 = 0 marks "not done here")
@@ -359,8 +372,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
     const uint32_t gl = lane & (FRAG_G - 1), grp = threadIdx.x / FRAG_G, g0 = lane & ~(FRAG_G - 1);
     uint32_t tix = blockIdx.x;
     if (FUSED) {
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
             lb_tile = atomicAdd(lb.ticket, 1u);
+            lb_fault = 0;
+        }
         __syncthreads();
         tix = lb_tile;
     }
@@ -493,8 +508,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
             if (m0 & below) {                          // a nearer tile has not published yet
                 __builtin_amdgcn_s_sleep(1);
                 if (++spins > (1u << 22)) {            // never reached when the tiles start in ticket order
-                    if (lane == 0)
+                    if (lane == 0) {
                         atomicOr(lb.err, 1u);
+                        lb_fault = 1;
+                    }
                     break;
                 }
                 continue;
@@ -533,6 +550,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
         }
     }
     __syncthreads();
+    if (FUSED && lb_fault) {
+        // this tile's prefix is unknown: put back the headers the prologue
+        // rewrote, mark every packet of the tile CLK_FRAG_FAULT, write nothing
+        for (uint32_t j = threadIdx.x; j < FRAG_TILE && tile + j < b.n; j += blockDim.x) {
+            if (FUSED && CLK_FRAG_PRO && lhdr[j][0] != 0u)
+                frag_restore_header(b.base + pkt_off(b, tile + j), lhdr[j]);
+            lb.out_port[tile + j] = FRAG_PORT_FAULT;
+        }
+        return;
+    }
     const uint64_t fbase = FUSED ? lb_base[0] : tile_sums[2 * tix], bbase = FUSED ? lb_base[1] : tile_sums[2 * tix + 1];
     for (uint32_t j = threadIdx.x; j < FRAG_TILE && tile + j < b.n; j += blockDim.x)
         out_frag_first[tile + j] = fbase + pn[j];
@@ -639,6 +666,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
         const uint32_t off_first = bswap16(__shfl(dw, g0 + 1, 64) >> 16);      // ntohs(ip->ip_off) after 112-118
         const uint64_t fidx = fbase + pn[j];
         const uint64_t bpos = bbase + pb[j];
+        // all of the packet's fragments fit the caller's buffers, or none is
+        // written and the packet keeps its bytes (port CLK_FRAG_NOROOM)
+        if (!(fidx + nextra <= f.max_frags &&
+              bpos + (nextra ? (uint64_t)(nextra - 1) * slot16(out_hlen + step) + slot16(out_hlen + last) : 0) <=
+                  f.arena_bytes)) {
+            if (gl == 0) {
+                if (FUSED && CLK_FRAG_PRO && lhdr[j][0] != 0u)
+                    frag_restore_header(ip, lhdr[j]);
+                (FUSED ? lb.out_port : (uint8_t *)port)[i] = FRAG_PORT_NOROOM;
+            }
+            j = jn;
+            continue;
+        }
         // payload offsets are relative to ip (32-bit): fragment k's payload
         // starts at pay0 + k * step and ends at min(that + dlen_k, caplen)
         const uint32_t pay0 = hlen + (uint32_t)first_dlen;

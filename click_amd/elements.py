@@ -28,14 +28,24 @@ def anno_paint(color):
 
 class Element:
     def __init__(self, ctx, class_name, config="", name=None, noutputs=1):
+        """ctx: a click_amd.Context, or None: the element makes its own
+        context on the GPU its DEVICE keyword names (default 0)."""
         self.ctx = ctx
-        self.lib = ctx.lib
+        self.lib = ctx.lib if ctx is not None else _abi.load()
+        ch = ctx.h if ctx is not None else None
         h = ctypes.c_void_p()
-        rc = self.lib.clk_element_create(ctx.h, class_name.encode(), config.encode(),
+        rc = self.lib.clk_element_create(ch, class_name.encode(), config.encode(),
                                          name.encode() if name else None, noutputs, ctypes.byref(h))
+        self.rc = rc
         if rc != 0:
-            raise ClickAmdError("%s(%s): %s" % (class_name, config, (self.lib.clk_last_error(ctx.h) or b"").decode()))
+            err = ClickAmdError("%s(%s): %s" % (class_name, config, (self.lib.clk_last_error(ch) or b"").decode()))
+            err.rc = rc
+            raise err
         self.h = h
+        self._keep = []          # host buffers that must outlive flush()
+
+    def last_error(self):
+        return (self.lib.clk_element_last_error(self.h) or b"").decode()
         self._keep = []          # host buffers that must outlive flush()
 
     def close(self):
@@ -77,12 +87,14 @@ class Element:
                                              None if nh is None else nh.ctypes.data_as(ctypes.c_void_p),
                                              first_token, len(ptrs))
         if rc != 0:
-            raise ClickAmdError("push_burst failed: %d" % rc)
+            raise ClickAmdError("push_burst failed: %d (%s)" % (rc, self.last_error()))
 
     def flush(self):
         rc = self.lib.clk_element_flush(self.h)
         if rc != 0:
-            raise ClickAmdError("flush failed: %d" % rc)
+            err = ClickAmdError("flush failed: %d (%s)" % (rc, self.last_error()))
+            err.rc = rc
+            raise err
         self._keep = []
 
     def flush_async(self):
@@ -91,7 +103,7 @@ class Element:
         until the next flush)."""
         rc = self.lib.clk_element_flush_async(self.h)
         if rc != 0:
-            raise ClickAmdError("flush_async failed: %d" % rc)
+            raise ClickAmdError("flush_async failed: %d (%s)" % (rc, self.last_error()))
 
     def results(self, cap=1 << 20, aux=False):
         """(tokens, ports, lengths[, aux]) of every flushed packet, in order."""

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <cstdio>
 #include <cstdlib>
@@ -337,14 +338,41 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
     return g.pend.size() >= batch_cap_ ? 1 : 0;
 }
 
+// Test hook (clk_glue_inject_fault_internal): the n-th checked HIP call of
+// the flush path from now on fails as if the runtime had returned an error.
+static std::atomic<int> g_fault_at{0};
+
+static hipError_t checked(hipError_t e)
+{
+    int v = g_fault_at.load(std::memory_order_relaxed);
+    while (v > 0 && !g_fault_at.compare_exchange_weak(v, v - 1, std::memory_order_relaxed))
+        ;
+    return v == 1 ? hipErrorInvalidValue : e;
+}
+
+// A launch step failed: drain what was queued on the stream so no copy or
+// kernel still uses the stage's buffers, leave the batch staged (a later
+// flush retries it) and report.  Nothing of the batch is routed.
+int BatchElement::launch_failed(Stage &g, hipError_t e, const char *what)
+{
+    (void)hipStreamSynchronize((hipStream_t)clk_ctx_stream(ctx_));
+    g.inflight = false;
+    err_ = std::string(what) + ": " + hipGetErrorString(e);
+    return CLK_EHIP;
+}
+
 // Copy the staged batch to the GPU, run the element, queue the copies back
-// and a completion event; nothing waits.
+// and a completion event; nothing waits.  Every HIP call is checked: a
+// failure fails the flush before any packet is routed.
 int BatchElement::launch(Stage &g)
 {
+    err_.clear();
     size_t n = 0;
     uint32_t maxlen = 0;
-    if (grow_host(g, g.h_used + 64, g.pend.size()))
+    if (grow_host(g, g.h_used + 64, g.pend.size())) {
+        err_ = "out of pinned host memory";
         return CLK_EINVAL;
+    }
     for (Pending &p : g.pend)
         if (p.host_code < 0) {
             g.h_off[n] = p.slot;
@@ -356,22 +384,34 @@ int BatchElement::launch(Stage &g)
         }
     g.n = n;
     g.zc = zerocopy_;
-    g.inflight = true;
     hipStream_t s = (hipStream_t)clk_ctx_stream(ctx_);
-    if (!g.ev[0])
-        for (void *&e : g.ev)
-            (void)hipEventCreate((hipEvent_t *)&e);
+    hipError_t e;
+    for (void *&ev : g.ev)
+        if (!ev) {
+            hipEvent_t h = nullptr;
+            if ((e = checked(hipEventCreate(&h))) != hipSuccess) {
+                if (h)
+                    (void)hipEventDestroy(h);
+                return launch_failed(g, e, "hipEventCreate");
+            }
+            ev = (void *)h;
+        }
+    g.inflight = true;
     if (n) {
         if (grow_dev(g, g.zc ? 64 : g.h_used + 64, n)) {
+            g.inflight = false;
             err_ = "out of device memory";
             return CLK_EHIP;
         }
-        if (!g.zc)
-            (void)hipMemcpyAsync(g.d_arena, g.h_arena, g.h_used, hipMemcpyHostToDevice, s);
-        (void)hipMemcpyAsync(g.d_off, g.h_off, n * 8, hipMemcpyHostToDevice, s);
-        (void)hipMemcpyAsync(g.d_len, g.h_len, n * 4, hipMemcpyHostToDevice, s);
-        if (wants_anno())
-            (void)hipMemcpyAsync(g.d_anno, g.h_anno, n, hipMemcpyHostToDevice, s);
+        if (!g.zc && (e = checked(hipMemcpyAsync(g.d_arena, g.h_arena, g.h_used, hipMemcpyHostToDevice, s))) !=
+                         hipSuccess)
+            return launch_failed(g, e, "hipMemcpyAsync(packets)");
+        if ((e = checked(hipMemcpyAsync(g.d_off, g.h_off, n * 8, hipMemcpyHostToDevice, s))) != hipSuccess ||
+            (e = checked(hipMemcpyAsync(g.d_len, g.h_len, n * 4, hipMemcpyHostToDevice, s))) != hipSuccess)
+            return launch_failed(g, e, "hipMemcpyAsync(descriptors)");
+        if (wants_anno() &&
+            (e = checked(hipMemcpyAsync(g.d_anno, g.h_anno, n, hipMemcpyHostToDevice, s))) != hipSuccess)
+            return launch_failed(g, e, "hipMemcpyAsync(annotations)");
         clk_batch b;
         b.base = g.zc ? g.zc_dev : g.d_arena;
         b.off = g.d_off;
@@ -382,24 +422,32 @@ int BatchElement::launch(Stage &g)
         b.n = n;
         d_anno_ = g.d_anno;
         d_aux8_ = g.d_aux8;
-        (void)hipEventRecord((hipEvent_t)g.ev[0], s);
+        if ((e = checked(hipEventRecord((hipEvent_t)g.ev[0], s))) != hipSuccess)
+            return launch_failed(g, e, "hipEventRecord");
         int r = run(&b, g.d_codes, g.d_sums);
         if (r) {
-            err_ = clk_last_error(ctx_);
-            g.inflight = false;
+            const std::string why = err_.empty() ? clk_last_error(ctx_) : err_;
+            launch_failed(g, hipSuccess, "run");
+            err_ = why;
             return r;
         }
-        (void)hipEventRecord((hipEvent_t)g.ev[1], s);
-        (void)hipMemcpyAsync(g.h_codes, g.d_codes, n, hipMemcpyDeviceToHost, s);
-        if (wants_sums())
-            (void)hipMemcpyAsync(g.h_sums, g.d_sums, n * 2, hipMemcpyDeviceToHost, s);
+        if ((e = checked(hipEventRecord((hipEvent_t)g.ev[1], s))) != hipSuccess)
+            return launch_failed(g, e, "hipEventRecord");
+        if ((e = checked(hipMemcpyAsync(g.h_codes, g.d_codes, n, hipMemcpyDeviceToHost, s))) != hipSuccess)
+            return launch_failed(g, e, "hipMemcpyAsync(verdicts)");
+        if (wants_sums() &&
+            (e = checked(hipMemcpyAsync(g.h_sums, g.d_sums, n * 2, hipMemcpyDeviceToHost, s))) != hipSuccess)
+            return launch_failed(g, e, "hipMemcpyAsync(checksums)");
         if (wants_arena_back()) {
-            if (!g.zc)
-                (void)hipMemcpyAsync(g.h_arena, g.d_arena, g.h_used, hipMemcpyDeviceToHost, s);
-            (void)hipMemcpyAsync(g.h_aux8, g.d_aux8, n, hipMemcpyDeviceToHost, s);
+            if (!g.zc &&
+                (e = checked(hipMemcpyAsync(g.h_arena, g.d_arena, g.h_used, hipMemcpyDeviceToHost, s))) != hipSuccess)
+                return launch_failed(g, e, "hipMemcpyAsync(packets back)");
+            if ((e = checked(hipMemcpyAsync(g.h_aux8, g.d_aux8, n, hipMemcpyDeviceToHost, s))) != hipSuccess)
+                return launch_failed(g, e, "hipMemcpyAsync(aux)");
         }
     }
-    (void)hipEventRecord((hipEvent_t)g.ev[2], s);
+    if ((e = checked(hipEventRecord((hipEvent_t)g.ev[2], s))) != hipSuccess)
+        return launch_failed(g, e, "hipEventRecord");
     return 0;
 }
 
@@ -408,11 +456,16 @@ int BatchElement::complete(Stage &g)
 {
     if (!g.inflight)
         return 0;
-    hipError_t e = hipEventSynchronize((hipEvent_t)g.ev[2]);
+    hipError_t e = checked(hipEventSynchronize((hipEvent_t)g.ev[2]));
     g.inflight = false;
     if (e != hipSuccess) {
-        err_ = hipGetErrorString(e);
-        return CLK_EHIP;
+        err_ = std::string("hipEventSynchronize: ") + hipGetErrorString(e);
+        return CLK_EHIP;       // the batch stays staged; nothing is routed
+    }
+    if (g.n) {
+        int r = verify(g.h_codes, g.n);      // a kernel's internal fault report
+        if (r)
+            return r;
     }
     float ms = 0;
     if (g.n)
@@ -451,6 +504,10 @@ int BatchElement::flush_async()
 {
     Stage &other = st_[cur_ ^ 1];
     int r = complete(other);              // results stay in push order
+    if (r)
+        return r;
+    if (!other.pend.empty() && (r = launch(other)) == 0)   // its completion failed earlier: retry it first
+        r = complete(other);
     if (r)
         return r;
     Stage &g = st_[cur_];
@@ -523,6 +580,8 @@ std::string BatchElement::read_handler(const std::string &h) const
         return std::to_string(packets_);
     if (h == "gpu_ns")
         return std::to_string(gpu_ns_);
+    if (h == "device")
+        return std::to_string(clk_ctx_device(ctx_));
     return std::string();
 }
 
@@ -1384,7 +1443,8 @@ int IPFragmenter::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
         h_newid_.resize(b->n);
         for (auto &x : h_newid_)
             x = (uint16_t)std::rand();
-        (void)hipMemcpyAsync(d_newid_, h_newid_.data(), b->n * 2, hipMemcpyHostToDevice, s);
+        if (hipMemcpyAsync(d_newid_, h_newid_.data(), b->n * 2, hipMemcpyHostToDevice, s) != hipSuccess)
+            return CLK_EHIP;
         nid = d_newid_;
     }
     clk_frag_cfg cfg{mtu_, honor_df_ ? 1 : 0, nid};
@@ -1411,12 +1471,28 @@ int IPFragmenter::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
     h_flen_.resize(tot[0]);
     h_first_.resize(b->n);
     h_ffirst_.resize(b->n);
-    (void)hipMemcpyAsync(h_frag_.data(), d_frag_, tot[1], hipMemcpyDeviceToHost, s);
-    (void)hipMemcpyAsync(h_foff_.data(), d_foff_, tot[0] * 8, hipMemcpyDeviceToHost, s);
-    (void)hipMemcpyAsync(h_flen_.data(), d_flen_, tot[0] * 4, hipMemcpyDeviceToHost, s);
-    (void)hipMemcpyAsync(h_first_.data(), d_first_, b->n * 4, hipMemcpyDeviceToHost, s);
-    (void)hipMemcpyAsync(h_ffirst_.data(), d_ffirst_, b->n * 8, hipMemcpyDeviceToHost, s);
+    if (hipMemcpyAsync(h_frag_.data(), d_frag_, tot[1], hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(h_foff_.data(), d_foff_, tot[0] * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(h_flen_.data(), d_flen_, tot[0] * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(h_first_.data(), d_first_, b->n * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipMemcpyAsync(h_ffirst_.data(), d_ffirst_, b->n * 8, hipMemcpyDeviceToHost, s) != hipSuccess)
+        return CLK_EHIP;
     return CLK_SUCCESS;                                  // flush() synchronizes
+}
+
+// The single-pass kernel marks every packet of a tile whose look-back timed
+// out CLK_FRAG_FAULT (and leaves those packets whole): fail this flush, and
+// consume the context's fault word so no later call reports it.
+int IPFragmenter::verify(const uint8_t *codes, size_t n)
+{
+    for (size_t k = 0; k < n; k++)
+        if (codes[k] == CLK_FRAG_FAULT || codes[k] == CLK_FRAG_NOROOM) {
+            (void)clk_ctx_sync(ctx_);
+            err_ = codes[k] == CLK_FRAG_FAULT ? "IPFragmenter: fragment look-back timed out (internal fault)"
+                                              : "IPFragmenter: fragment buffers too small (internal error)";
+            return CLK_EHIP;
+        }
+    return 0;
 }
 
 void IPFragmenter::route(Pending &p, int code, uint16_t, Result *r)
@@ -1506,6 +1582,7 @@ BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::stri
 
 struct clk_element {
     clk::host::BatchElement *e;
+    clk_ctx *own_ctx;          // created for DEVICE when the caller passed no context
 };
 
 extern "C" {
@@ -1513,27 +1590,65 @@ extern "C" {
 int clk_element_create(clk_ctx *ctx, const char *class_name, const char *config, const char *name,
                        int noutputs, clk_element **out)
 {
-    if (!ctx || !class_name || !out || noutputs < 1 || noutputs > 5)
-        return CLK_EINVAL;
+    if (!class_name || !out || noutputs < 1 || noutputs > 5)
+        return clk_ctx_set_error_internal(ctx, "clk_element_create: bad arguments");
     *out = nullptr;
     std::string nm = name ? name : class_name;
-    clk::host::BatchElement *e = clk::host::make_element(ctx, class_name, nm, noutputs);
-    if (!e)
-        return CLK_EINVAL;
     clk::host::ConfArgs args;
     std::string err;
-    if (!clk::host::ConfArgs::split(config ? config : "", &args, &err) || e->configure(args, &err)) {
+    if (!clk::host::ConfArgs::split(config ? config : "", &args, &err)) {
+        clk_ctx_set_error_internal(ctx, (nm + ": " + err).c_str());
+        return CLK_EINVAL;
+    }
+    // DEVICE (glue keyword): the GPU this element's batches run on.  With a
+    // context it must name the context's device; without one (ctx NULL) the
+    // element makes its own context there (default 0).
+    long dev = ctx ? clk_ctx_device(ctx) : 0;
+    std::string v;
+    if (args.take("DEVICE", &v)) {
+        if (!clk::host::parse_int(v, &dev) || dev < 0) {
+            clk_ctx_set_error_internal(ctx, (nm + ": DEVICE: expected GPU number").c_str());
+            return CLK_EINVAL;
+        }
+        const int nd = clk_device_count();
+        if (dev >= nd) {
+            clk_ctx_set_error_internal(ctx, (nm + ": DEVICE " + std::to_string(dev) + ": no such GPU (" +
+                                             std::to_string(nd < 0 ? 0 : nd) + " gfx950 devices)").c_str());
+            return CLK_ENODEV;
+        }
+        if (ctx && dev != clk_ctx_device(ctx)) {
+            clk_ctx_set_error_internal(ctx, (nm + ": DEVICE " + std::to_string(dev) + " but the context is on device " +
+                                             std::to_string(clk_ctx_device(ctx))).c_str());
+            return CLK_EINVAL;
+        }
+    }
+    clk_ctx *own = nullptr;
+    if (!ctx) {
+        int r = clk_ctx_create((int)dev, &own);
+        if (r)
+            return r;                           // clk_last_error(NULL) says why
+        ctx = own;
+    }
+    clk::host::BatchElement *e = clk::host::make_element(ctx, class_name, nm, noutputs);
+    if (!e) {
+        clk_ctx_destroy(own);
+        return clk_ctx_set_error_internal(own ? nullptr : ctx, ("unknown element class " + std::string(class_name)).c_str());
+    }
+    if (e->configure(args, &err)) {
         delete e;
         // report through the context's error text, like a configure-time errh
-        clk_ctx_set_error_internal(ctx, (nm + ": " + err).c_str());
+        clk_ctx_set_error_internal(own ? nullptr : ctx, (nm + ": " + err).c_str());
+        clk_ctx_destroy(own);
         return CLK_EINVAL;
     }
     clk_element *w = new (std::nothrow) clk_element;
     if (!w) {
         delete e;
+        clk_ctx_destroy(own);
         return CLK_EINVAL;
     }
     w->e = e;
+    w->own_ctx = own;
     *out = w;
     return CLK_SUCCESS;
 }
@@ -1542,9 +1657,20 @@ int clk_element_destroy(clk_element *w)
 {
     if (w) {
         delete w->e;
+        clk_ctx_destroy(w->own_ctx);
         delete w;
     }
     return CLK_SUCCESS;
+}
+
+const char *clk_element_last_error(clk_element *w)
+{
+    return w ? w->e->last_error().c_str() : "null element";
+}
+
+void clk_glue_inject_fault_internal(int nth)
+{
+    clk::host::g_fault_at.store(nth, std::memory_order_relaxed);
 }
 
 int clk_element_push(clk_element *w, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token)

@@ -11,6 +11,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/click_amd_cksum.h"
 
 namespace clk {
@@ -82,6 +84,9 @@ class BatchElement {
     virtual void pre_route(Pending &, std::deque<Result> &) {}
     // called after route(): results that follow the packet's own (fragments)
     virtual void post_route(Pending &, int, std::deque<Result> &) {}
+    // after the batch completed, before any packet is routed: nonzero fails
+    // the flush (a kernel's internal fault report in the codes)
+    virtual int verify(const uint8_t *, size_t) { return 0; }
     const uint8_t *staged(const Pending &p) const { return rt_->h_arena + p.slot; }
     void write_back(const Pending &p, uint32_t nbytes) const;   // staged span -> packet
     uint32_t keep_packet(const uint8_t *bytes, uint32_t len);   // new packet, returns its key
@@ -133,6 +138,7 @@ class BatchElement {
     int grow_host(Stage &g, size_t bytes, size_t n);
     int grow_dev(Stage &g, size_t bytes, size_t n);
     int launch(Stage &g);
+    int launch_failed(Stage &g, hipError_t e, const char *what);
     int complete(Stage &g);
     void free_stage(Stage &g);
     Stage st_[2];
@@ -365,6 +371,7 @@ class IPFragmenter : public BatchElement {
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    int verify(const uint8_t *codes, size_t n) override;
     void post_route(Pending &p, int code, std::deque<Result> &out) override;
     bool wants_arena_back() const override { return true; }
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CLK_ABI_VERSION 3
+#define CLK_ABI_VERSION 4
 
 /* ---- return codes -------------------------------------------------------- */
 #define CLK_SUCCESS 0
@@ -74,6 +74,11 @@ enum clk_ttl_status {                 /* DecIPTTL outcome (decipttl.cc:45-77) */
 
 /* ---- context ------------------------------------------------------------- */
 typedef struct clk_ctx clk_ctx;
+
+/* Number of gfx950 devices visible (HIP ordinals 0..n-1 are scanned; a
+ * negative CLK_E* code on a runtime error).  An adapter maps its threads
+ * to devices with it ("Devices").                          */
+int clk_device_count(void);
 
 /* Create a context on HIP device `device` with its own non-blocking stream. */
 int clk_ctx_create(int device, clk_ctx **out);
@@ -247,6 +252,12 @@ int clk_ip_output_combo(clk_ctx *ctx, const clk_batch *batch, const clk_ip_out_c
  *                  fragment (ip_len, IP_MF, DF/ip_id, ip_sum) and keeps its
  *                  first out_first_len[i] bytes; its other fragments are
  *                  appended to `out`.
+ *              3 = CLK_FRAG_NOROOM: its fragments do not all fit out->arena /
+ *                  out->max_frags: nothing of it is written, the packet
+ *                  keeps its bytes (size the buffers from `totals`, retry);
+ *              0xFF = CLK_FRAG_FAULT: internal fault (the single-pass tile
+ *                  look-back timed out, also reported by clk_ctx_sync):
+ *                  the packet keeps its bytes, nothing of it is written.
  * out_first_len[i]: packet i's length after the element.
  * out_frag_first[i] (nullable): index of packet i's first appended fragment.
  * out->arena == NULL makes a sizing call: out_port, out_first_len and totals
@@ -254,10 +265,12 @@ int clk_ip_output_combo(clk_ctx *ctx, const clk_batch *batch, const clk_ip_out_c
  * Appended fragments are packed in packet order at 16 B-aligned offsets of
  * out->arena; fragment k is out->frag_len[k] bytes at out->frag_off[k],
  * cut from packet out->frag_src[k].  totals (device u64[2]) receives the
- * fragments and arena bytes the batch needs; fragments beyond out->max_frags
- * or out->arena_bytes are not written (compare after clk_ctx_sync).
+ * fragments and arena bytes the batch needs; a packet whose fragments would
+ * pass out->max_frags or out->arena_bytes is left whole (CLK_FRAG_NOROOM).
  * Domain guards (as the oracle): len_i < 20 with len_i > MTU -> port 1;
  * fragment bytes past len_i (ip_len > network_length) are written as 0. */
+#define CLK_FRAG_NOROOM 3
+#define CLK_FRAG_FAULT 0xFF
 typedef struct clk_frag_cfg {
     uint32_t mtu;
     int32_t honor_df;

@@ -48,7 +48,8 @@
  *                   (elements/ip/ipfragmenter.cc:41-55); handlers drops,
  *                   fragments; each fragment beyond the first is a new
  *                   packet (aux = its key for clk_element_take_packet)
- * plus glue keywords BATCH (packets per GPU batch, default 65536) and
+ * plus glue keywords BATCH (packets per GPU batch, default 65536), DEVICE
+ * (the GPU, see clk_element_create; handler "device") and
  * ZEROCOPY (bool, default false): the kernels read -- and the Set /
  * rewriting elements write -- the packets where they lie, in host memory
  * registered with clk_host_register, instead of gathering them into a
@@ -79,11 +80,20 @@ enum clk_port {
 
 /* name: the element's name in messages (Click's name(); NULL = class name);
  * noutputs: how many outputs are connected (1 or 2; IPOutputCombo 5).
- * Returns CLK_EINVAL with clk_last_error(ctx) set on a configure error,
- * worded like the reference's ErrorHandler messages.                      */
+ * ctx: the context (device + stream) the element's batches run on; NULL
+ * makes the element create (and destroy) its own, on the GPU its DEVICE
+ * keyword names (default 0).  With a context, DEVICE must be the
+ * context's device.  DEVICE past the gfx950 devices present: CLK_ENODEV.
+ * Returns CLK_EINVAL with clk_last_error(ctx) (clk_last_error(NULL) when
+ * ctx is NULL) set on a configure error, worded like the reference's
+ * ErrorHandler messages.                                                  */
 int clk_element_create(clk_ctx *ctx, const char *class_name, const char *config,
                        const char *name, int noutputs, clk_element **out);
 int clk_element_destroy(clk_element *e);
+/* Why the element's last flush / push failed.  A flush that fails (a HIP
+ * runtime error, or a kernel's internal fault report) routes nothing: the
+ * batch stays staged and the next flush retries it.                       */
+const char *clk_element_last_error(clk_element *e);
 
 /* Stage one host packet.  data/length = Packet::data()/length();
  * nh_offset = network_header_offset() (-1 = no network header: the IP

@@ -94,20 +94,63 @@ def test_fragment_fuzz_parity(torch, ctx, mtu, honor_df):
 
 
 def test_fragment_capacity_limit(torch, ctx):
-    """Fragments past the caller's capacity are not written (and nothing
-    past the arena is touched); totals still report the need."""
+    """A packet whose fragments do not all fit the caller's arena /
+    max_frags is left whole (port CLK_FRAG_NOROOM = 3, bytes untouched,
+    nothing of it written); every packet that fits is exact; totals still
+    report the need."""
     rng = np.random.default_rng(5)
     arena, off, caplen = fuzz.frag_batch(rng, 300)
     h = gpu_fragment(torch, ctx, arena.copy(), off, caplen, 300, False, slack=40)
-    r = oracle_lib.ip_fragment(arena.copy(), len(off), 300, False, off=off, length=caplen)
+    ref = arena.copy()
+    r = oracle_lib.ip_fragment(ref, len(off), 300, False, off=off, length=caplen)
     assert (h["nf"], h["nb"]) == (len(r["frags"]), r["arena_bytes"])
-    written = 0
-    for k in range(h["nf"] - 1):
-        o, l = int(r["frag_off"][k]), int(r["frag_len"][k])
-        if o + ((l + 15) & ~15) <= h["nb"] - 40:
-            assert h["arena"][o:o + l].tobytes() == r["frags"][k]
-            written += 1
-    assert written > 0
+    cap_b, cap_f = h["nb"] - 40, h["nf"] - 1
+    nfr = np.bincount(r["frag_src"].astype(np.int64), minlength=len(off))
+    fitted = noroom = 0
+    for i in range(len(off)):
+        o, c = int(off[i]), int(caplen[i])
+        ks = range(int(r["frag_first"][i]), int(r["frag_first"][i]) + int(nfr[i]))
+        fits = all(k < cap_f and int(r["frag_off"][k]) + ((int(r["frag_len"][k]) + 15) & ~15) <= cap_b for k in ks)
+        if r["port"][i] != 2 or fits:
+            assert h["port"][i] == r["port"][i], i
+            assert np.array_equal(h["base"][o:o + c], ref[o:o + c]), i
+            for k in ks:
+                fo, fl = int(r["frag_off"][k]), int(r["frag_len"][k])
+                assert h["arena"][fo:fo + fl].tobytes() == r["frags"][k]
+            fitted += r["port"][i] == 2
+        else:
+            assert h["port"][i] == 3, i
+            assert np.array_equal(h["base"][o:o + c], arena[o:o + c]), i     # untouched
+            for k in ks:
+                fo = int(r["frag_off"][k])
+                assert not h["arena"][fo:min(fo + int(r["frag_len"][k]), len(h["arena"]))].any()
+            noroom += 1
+    assert fitted > 0 and noroom > 0
+
+
+def test_fragment_many_tiles_uneven(torch, ctx):
+    """The single-pass look-back over more than 64 predecessor tiles (1024
+    packets each) with uneven tile sums: a fuzzed batch of 70,000 packets of
+    mixed lengths, options, DF/MF and fragment counts, exact against the
+    oracle (ports, first lengths, fragment indices and every fragment)."""
+    rng = np.random.default_rng(70)
+    arena, off, caplen = fuzz.frag_batch(rng, 70000, max_total=1600)
+    n = len(off)
+    nid = rng.integers(0, 65536, n).astype(np.uint16)
+    h = gpu_fragment(torch, ctx, arena.copy(), off, caplen, 296, False, nid)
+    ref = arena.copy()
+    r = oracle_lib.ip_fragment(ref, n, 296, False, off=off, length=caplen, new_id=nid)
+    assert np.array_equal(h["port"], r["port"])
+    assert np.array_equal(h["first_len"].view(np.uint32), r["first_len"])
+    assert np.array_equal(h["frag_first"].view(np.uint64), r["frag_first"])
+    assert (h["nf"], h["nb"]) == (len(r["frags"]), r["arena_bytes"])
+    assert np.array_equal(h["frag_off"][:h["nf"]].view(np.uint64), r["frag_off"])
+    assert np.array_equal(h["frag_len"][:h["nf"]].view(np.uint32), r["frag_len"])
+    assert np.array_equal(h["frag_src"][:h["nf"]].view(np.uint32), r["frag_src"])
+    assert np.array_equal(h["arena"][:r["arena_bytes"]], r["arena"])
+    assert np.array_equal(h["base"], ref)
+    tiles = np.bincount(np.arange(n) // 1024, weights=np.bincount(r["frag_src"].astype(np.int64), minlength=n))
+    assert len(tiles) > 65 and tiles.min() != tiles.max()
 
 
 def test_fragment_full_size(torch, ctx):
