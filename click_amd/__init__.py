@@ -247,6 +247,28 @@ class Context:
         return status[:b.n], (sums[:b.n] if sums is not None else None)
 
     # -- IP output path ----------------------------------------------------------
+    def update_in_cksum(self, b, sum_off, hw_off, new_hw, zero_fix=False, zero_lo=0, status=None, sums=None,
+                        want_sums=True):
+        """click_update_in_cksum (+ click_update_zero_in_cksum) in place:
+        new_hw is a uint16 device tensor of the words stored at hw_off."""
+        status = self._out(b.n, self._torch.uint8) if status is None else status
+        if sums is None and want_sums:
+            sums = self._out(b.n, self._torch.uint16)
+        cfg = _abi.clk_cksum_update_cfg(sum_off, hw_off, 1 if zero_fix else 0, zero_lo)
+        cb = b.c()
+        self._check(self.lib.clk_update_in_cksum(self.h, ctypes.byref(cb), ctypes.byref(cfg), _ptr(new_hw),
+                                                 _ptr(status), _ptr(sums)))
+        return status[:b.n], (sums[:b.n] if sums is not None else None)
+
+    def update_zero_in_cksum(self, b, sum_off, zero_lo=0, status=None, sums=None, want_sums=True):
+        status = self._out(b.n, self._torch.uint8) if status is None else status
+        if sums is None and want_sums:
+            sums = self._out(b.n, self._torch.uint16)
+        cb = b.c()
+        self._check(self.lib.clk_update_zero_in_cksum(self.h, ctypes.byref(cb), sum_off, zero_lo, _ptr(status),
+                                                      _ptr(sums)))
+        return status[:b.n], (sums[:b.n] if sums is not None else None)
+
     def _out_cfg(self, my_ip=0, ts=0, my_addrs=None, mtu=0xFFFFFFFF):
         cfg = _abi.clk_ip_out_cfg()
         cfg.my_ip, cfg.ts, cfg.mtu = my_ip & 0xFFFFFFFF, ts & 0xFFFFFFFF, mtu & 0xFFFFFFFF

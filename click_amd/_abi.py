@@ -104,6 +104,11 @@ _P = ctypes.c_void_p
 _BP = ctypes.POINTER(clk_batch)
 _OP = ctypes.POINTER(clk_ip_out_cfg)
 
+
+class clk_cksum_update_cfg(ctypes.Structure):
+    _fields_ = [("sum_off", ctypes.c_uint32), ("hw_off", ctypes.c_uint32), ("zero_fix", ctypes.c_int32),
+                ("zero_lo", ctypes.c_uint32)]
+
 # name -> (restype, argtypes); every symbol include/*.h declares
 SIGNATURES = {
     "clk_abi_version": (ctypes.c_int, []),
@@ -126,6 +131,8 @@ SIGNATURES = {
     "clk_set_tcp_checksum": (ctypes.c_int, [_P, _BP, ctypes.c_int, _P, _P]),
     "clk_check_icmp_header": (ctypes.c_int, [_P, _BP, _P]),
     "clk_dec_ip_ttl": (ctypes.c_int, [_P, _BP, ctypes.c_int, _P, _P]),
+    "clk_update_in_cksum": (ctypes.c_int, [_P, _BP, ctypes.POINTER(clk_cksum_update_cfg), _P, _P, _P]),
+    "clk_update_zero_in_cksum": (ctypes.c_int, [_P, _BP, ctypes.c_uint32, ctypes.c_uint32, _P, _P]),
     "clk_ip_gw_options": (ctypes.c_int, [_P, _BP, _OP, _P, _P, _P]),
     "clk_fix_ip_src": (ctypes.c_int, [_P, _BP, _OP, _P, _P]),
     "clk_ip_output_combo": (ctypes.c_int, [_P, _BP, _OP, _P, _P, _P, _P]),

@@ -603,6 +603,34 @@ int clk_dec_ip_ttl(clk_ctx *ctx, const clk_batch *b, int multicast, uint8_t *out
     return check_launch(ctx, "clk_dec_ip_ttl");
 }
 
+int clk_update_in_cksum(clk_ctx *ctx, const clk_batch *b, const clk_cksum_update_cfg *cfg, const uint16_t *new_hw,
+                        uint8_t *out_status, uint16_t *out_sum)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, "clk_update_in_cksum"))) return r;
+    if (!cfg) return fail(ctx, CLK_EINVAL, "clk_update_in_cksum: null cfg");
+    if (b->n == 0) return CLK_SUCCESS;
+    if (!new_hw) return fail(ctx, CLK_EINVAL, "clk_update_in_cksum: null new_hw");
+    clk::UpdateArgs u{cfg->sum_off, cfg->hw_off, cfg->zero_lo, cfg->zero_fix ? 1 : 0, 1};
+    hipLaunchKernelGGL(clk::update_kernel, dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0, ctx->cur, args_of(b), u,
+                       new_hw, out_status, out_sum);
+    return check_launch(ctx, "clk_update_in_cksum");
+}
+
+int clk_update_zero_in_cksum(clk_ctx *ctx, const clk_batch *b, uint32_t sum_off, uint32_t zero_lo,
+                             uint8_t *out_status, uint16_t *out_sum)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if ((r = check_batch(ctx, b, "clk_update_zero_in_cksum"))) return r;
+    if (b->n == 0) return CLK_SUCCESS;
+    clk::UpdateArgs u{sum_off, 0, zero_lo, 1, 0};
+    hipLaunchKernelGGL(clk::update_kernel, dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0, ctx->cur, args_of(b), u,
+                       (const uint16_t *)nullptr, out_status, out_sum);
+    return check_launch(ctx, "clk_update_zero_in_cksum");
+}
+
 }   // extern "C"
 
 namespace {

@@ -1154,6 +1154,71 @@ __global__ void __launch_bounds__(256) dec_ttl_kernel(BatchArgs b, int multicast
 }
 
 // ---------------------------------------------------------------------------
+// RFC 1624 incremental update (include/clicknet/ip.h:177-185) and the zero
+// fixup (ip.h:196-201, lib/in_cksum.c:113-121), one lane per packet.  Words
+// are read and stored as the reference's uint16_t accesses do (host order).
+// Codes: 0 updated, 1 a field lies past len_i (nothing written).
+// ---------------------------------------------------------------------------
+struct UpdateArgs {
+    uint32_t sum_off, hw_off, zero_lo;
+    int32_t zero_fix, replace;
+};
+
+__device__ __forceinline__ uint32_t ld_u16_any(const uint8_t *p)
+{
+    return ld_u8(p) | (ld_u8(p + 1) << 8);
+}
+
+// click_update_zero_in_cksum_hard: all bytes of [x, x + len) zero?
+__device__ __noinline__ bool all_zero(const uint8_t *x, int len)
+{
+    for (; len > 0 && ((uint64_t)x & 3); --len, ++x)
+        if (ld_u8(x))
+            return false;
+    for (; len >= 4; len -= 4, x += 4)
+        if (gload4((uint64_t)x))
+            return false;
+    for (; len > 0; --len, ++x)
+        if (ld_u8(x))
+            return false;
+    return true;
+}
+
+__global__ void __launch_bounds__(256) update_kernel(BatchArgs b, UpdateArgs u, const uint16_t *new_hw,
+                                                     uint8_t *out_code, uint16_t *out_sum)
+{
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += nthreads) {
+        uint8_t *p = b.base + pkt_off(b, i);
+        const uint32_t len = pkt_len(b, i);
+        uint32_t code = 0, csum = 0;
+        if ((uint64_t)u.sum_off + 2 > len || (u.replace && (uint64_t)u.hw_off + 2 > len)) {
+            code = 1;
+        } else {
+            csum = ld_u16_any(p + u.sum_off);
+            if (u.replace) {
+                const uint32_t old_hw = ld_u16_any(p + u.hw_off), nw = new_hw[i];
+                st_u16(p + u.hw_off, nw);
+                uint32_t sum = (~csum & 0xFFFFu) + (~old_hw & 0xFFFFu) + nw;    // ip.h:182
+                sum = (sum & 0xFFFFu) + (sum >> 16);                            // 183
+                csum = ~(sum + (sum >> 16)) & 0xFFFFu;                          // 184
+                st_u16(p + u.sum_off, csum);
+            }
+            // ip.h:196-201: a zero checksum of all-zero data is ~0
+            if (u.zero_fix && csum == 0 && all_zero(p + u.zero_lo, (int)len - (int)u.zero_lo)) {
+                csum = 0xFFFFu;
+                st_u16(p + u.sum_off, csum);
+                code = 2;
+            }
+        }
+        if (out_code)
+            out_code[i] = (uint8_t)code;
+        if (out_sum)
+            out_sum[i] = (uint16_t)csum;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // IP output path, one lane per packet: IPGWOptions (ipgwoptions.cc:53-172),
 // FixIPSrc (fixipsrc.cc:52-72) and IPOutputCombo after its annotation-only
 // steps (ipoutputcombo.cc:59-199).  Option-free headers (ip_hl = 5, the

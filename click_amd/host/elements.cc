@@ -756,6 +756,13 @@ bool CheckIPHeader::span(const Pending &p, uint32_t *off, uint32_t *len, int32_t
     return true;
 }
 
+std::string CheckIPHeader::read_handler(const std::string &h) const
+{
+    if (h == "offset")
+        return std::to_string(offset_);
+    return CheckElement::read_handler(h);
+}
+
 int CheckIPHeader::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
 {
     clk_ip_check_cfg cfg;
@@ -1386,7 +1393,7 @@ int IPFragmenter::configure(ConfArgs &args, std::string *err)
             return -1;
         }
     }
-    if (args.take("HEADROOM", &v) && (!parse_int(v, &mtu) || mtu < 0)) {   // Packet::make headroom: host side
+    if (args.take("HEADROOM", &v) && (!parse_int(v, &headroom_) || headroom_ < 0)) {   // Packet::make headroom: host side
         *err = "HEADROOM: expected unsigned integer";
         return -1;
     }
@@ -1539,6 +1546,10 @@ std::string IPFragmenter::read_handler(const std::string &h) const
         return std::to_string(drops_);
     if (h == "fragments")
         return std::to_string(fragments_);
+    if (h == "mtu")
+        return std::to_string(mtu_);
+    if (h == "headroom")
+        return std::to_string(headroom_);
     return BatchElement::read_handler(h);
 }
 

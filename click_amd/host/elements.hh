@@ -179,6 +179,7 @@ class CheckIPHeader : public CheckElement {
     ~CheckIPHeader() override;
     const char *class_name() const override { return checksum_default_ ? "CheckIPHeader" : "CheckIPHeader2"; }
     int configure(ConfArgs &args, std::string *err) override;
+    std::string read_handler(const std::string &h) const override;   // + "offset" (OFFSET)
 
   protected:
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
@@ -377,6 +378,7 @@ class IPFragmenter : public BatchElement {
 
   private:
     uint32_t mtu_ = 0;
+    long headroom_ = 28;   // Packet::default_headroom (packet.hh:45; 48 on MiniOS)
     bool honor_df_ = true, verbose_ = false;
     uint32_t drops_ = 0;
     uint64_t fragments_ = 0;

@@ -1,0 +1,81 @@
+// -*- c-basic-offset: 4 -*-
+/*
+ * hipcheck.{cc,hh} -- GPU-backed CheckIPHeader, CheckIPHeader2,
+ * IPInputCombo, CheckUDPHeader, CheckTCPHeader and CheckICMPHeader.
+ * The verdict comes from the GPU batch; what the reference does with a
+ * passing packet after its checksum is done here, on the host.
+ */
+#include <click/config.h>
+#include "hipcheck.hh"
+#include <click/packet_anno.hh>
+#include <clicknet/ip.h>
+#include <stdlib.h>
+CLICK_DECLS
+
+int
+HIPCheckIPHeader::initialize(ErrorHandler *errh)
+{
+    if (HIPBatchElement::initialize(errh) < 0)
+	return -1;
+    _offset = atoi(glue_handler("offset").c_str());		// OFFSET, parsed by the glue
+    return 0;
+}
+
+void
+HIPCheckIPHeader::deliver(PerThread &, Held &h, int32_t port, uint32_t len, uint32_t)
+{
+    Packet *p = h.p;
+    if (port != CLK_PORT_OUT0) {		// drop(): output 1 if connected, else kill (143-159)
+	kill_or_output1(p, port);
+	return;
+    }
+    // checkipheader.cc:213-223: network header, trim to ip_len, dst annotation
+    const click_ip *ip = reinterpret_cast<const click_ip *>(p->data() + _offset);
+    p->set_ip_header(ip, ip->ip_hl << 2);
+    if (p->length() > len)			// len: the packet's length after the trim
+	p->take(p->length() - len);
+    p->set_dst_ip_anno(ip->ip_dst);
+    output(0).push(p);
+}
+
+int
+HIPIPInputCombo::initialize(ErrorHandler *errh)
+{
+    if (HIPBatchElement::initialize(errh) < 0)
+	return -1;
+    _color = atoi(glue_handler("color").c_str());		// COLOR, parsed by the glue
+    return 0;
+}
+
+void
+HIPIPInputCombo::deliver(PerThread &, Held &h, int32_t port, uint32_t len, uint32_t)
+{
+    Packet *p = h.p;
+    if (port != CLK_PORT_OUT0) {		// bad: killed (ipinputcombo.cc:134-139)
+	p->kill();
+	return;
+    }
+    SET_PAINT_ANNO(p, _color);			// Paint (71)
+    p->pull(14);				// Strip(14) (74)
+    const click_ip *ip = reinterpret_cast<const click_ip *>(p->data());
+    p->set_ip_header(ip, ip->ip_hl << 2);	// 125
+    if (p->length() > len)			// 128-129
+	p->take(p->length() - len);
+    p->set_dst_ip_anno(ip->ip_dst);		// 132
+    output(0).push(p);
+}
+
+void
+HIPCheckL4Header::deliver(PerThread &, Held &h, int32_t port, uint32_t, uint32_t)
+{
+    if (port == CLK_PORT_OUT0)
+	output(0).push(h.p);
+    else
+	kill_or_output1(h.p, port);
+}
+
+CLICK_ENDDECLS
+ELEMENT_REQUIRES(HIPBatchElement)
+ELEMENT_PROVIDES(HIPCheckImpl)
+// the classes are exported by hipdropin.cc (reference names) and
+// hipparity.cc (HIP-prefixed names, for parity graphs beside the CPU ones)

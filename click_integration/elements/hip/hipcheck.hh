@@ -1,0 +1,65 @@
+#ifndef CLICK_HIPCHECK_HH
+#define CLICK_HIPCHECK_HH
+#include "hipbatch.hh"
+CLICK_DECLS
+
+/*
+ * GPU-backed header checks, registered under the reference class names so
+ * an unchanged .click graph uses them (build with
+ * --enable-skip-elements=CheckIPHeader,... : INTEGRATION.md).  Each keeps the
+ * reference's keywords (parsed by the glue), ports, handlers and messages;
+ * PROCESSING is push only (batching holds packets).
+ *
+ *   CheckIPHeader   checkipheader.cc:161-226    (glue CheckIPHeader)
+ *   CheckIPHeader2  checkipheader2.cc:27-31     (glue CheckIPHeader2)
+ *   IPInputCombo    ipinputcombo.cc:66-140      (glue IPInputCombo)
+ *   CheckUDPHeader  checkudpheader.cc:84-107
+ *   CheckTCPHeader  checktcpheader.cc:85-107
+ *   CheckICMPHeader checkicmpheader.cc:83-141
+ */
+
+class HIPCheckIPHeader : public HIPBatchElement { public:
+    const char *class_name() const	{ return "CheckIPHeader"; }
+    const char *port_count() const	{ return PORTS_1_1X2; }
+    const char *flags() const		{ return "A"; }
+    int initialize(ErrorHandler *errh) CLICK_COLD;
+  protected:
+    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+    int _offset;
+};
+
+class HIPCheckIPHeader2 : public HIPCheckIPHeader { public:
+    const char *class_name() const	{ return "CheckIPHeader2"; }
+};
+
+class HIPIPInputCombo : public HIPBatchElement { public:
+    const char *class_name() const	{ return "IPInputCombo"; }
+    const char *port_count() const	{ return PORTS_1_1; }
+    const char *flags() const		{ return "A"; }
+    int initialize(ErrorHandler *errh) CLICK_COLD;
+  protected:
+    int nh_offset(const Packet *) const	{ return 14; }   // Strip(14): the header is at data() + 14
+    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+    int _color;
+};
+
+class HIPCheckL4Header : public HIPBatchElement { public:
+    const char *port_count() const	{ return PORTS_1_1X2; }
+  protected:
+    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+};
+
+class HIPCheckUDPHeader : public HIPCheckL4Header { public:
+    const char *class_name() const	{ return "CheckUDPHeader"; }
+};
+
+class HIPCheckTCPHeader : public HIPCheckL4Header { public:
+    const char *class_name() const	{ return "CheckTCPHeader"; }
+};
+
+class HIPCheckICMPHeader : public HIPCheckL4Header { public:
+    const char *class_name() const	{ return "CheckICMPHeader"; }
+};
+
+CLICK_ENDDECLS
+#endif

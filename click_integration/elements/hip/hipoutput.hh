@@ -1,0 +1,58 @@
+#ifndef CLICK_HIPOUTPUT_HH
+#define CLICK_HIPOUTPUT_HH
+#include "hipbatch.hh"
+CLICK_DECLS
+
+/*
+ * GPU-backed IP output path, under the reference class names:
+ *
+ *   IPGWOptions    ipgwoptions.cc:53-172
+ *   FixIPSrc       fixipsrc.cc:52-72
+ *   IPOutputCombo  ipoutputcombo.cc:44-205 (ports 0-4)
+ *   IPFragmenter   ipfragmenter.cc:88-171 (fragments after the first are
+ *                  new packets the glue made; the adapter copies them into
+ *                  Packet::make(HEADROOM, ...) packets)
+ */
+
+class HIPIPGWOptions : public HIPBatchElement { public:
+    const char *class_name() const	{ return "IPGWOptions"; }
+    const char *port_count() const	{ return PORTS_1_1X2; }
+  protected:
+    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
+    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+};
+
+class HIPFixIPSrc : public HIPBatchElement { public:
+    const char *class_name() const	{ return "FixIPSrc"; }
+    const char *port_count() const	{ return PORTS_1_1; }
+  protected:
+    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
+    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+};
+
+class HIPIPOutputCombo : public HIPBatchElement { public:
+    const char *class_name() const	{ return "IPOutputCombo"; }
+    const char *port_count() const	{ return "1/5"; }
+    int initialize(ErrorHandler *errh) CLICK_COLD;
+  protected:
+    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
+    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+    bool primary(int32_t port, uint32_t aux) const	{ (void) port; return aux != CLK_AUX_CLONE; }
+    int _color;
+};
+
+class HIPIPFragmenter : public HIPBatchElement { public:
+    const char *class_name() const	{ return "IPFragmenter"; }
+    const char *port_count() const	{ return PORTS_1_1X2; }
+    int initialize(ErrorHandler *errh) CLICK_COLD;
+  protected:
+    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
+    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+    bool primary(int32_t port, uint32_t aux) const	{ (void) port; return aux == 0; }
+    void end_of_batch(PerThread &t);
+    uint32_t _mtu;
+    uint32_t _headroom;
+};
+
+CLICK_ENDDECLS
+#endif

@@ -1,0 +1,49 @@
+#ifndef CLICK_HIPSET_HH
+#define CLICK_HIPSET_HH
+#include "hipbatch.hh"
+CLICK_DECLS
+
+/*
+ * GPU-backed checksum writers, under the reference class names:
+ *
+ *   SetIPChecksum   setipchecksum.cc:74-95
+ *   SetUDPChecksum  setudpchecksum.cc:37-69
+ *   SetTCPChecksum  settcpchecksum.cc:44-75 (FIXOFF)
+ *   DecIPTTL        decipttl.cc:45-77 (RFC 1624 update of ip_sum)
+ *
+ * As the reference does, the packet is made writable (uniqueify()) before
+ * it is staged; the glue writes the new checksum (and TTL) into that
+ * writable packet when its batch is routed.
+ */
+
+class HIPSetChecksum : public HIPBatchElement { public:
+  protected:
+    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
+    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+};
+
+class HIPSetIPChecksum : public HIPSetChecksum { public:
+    const char *class_name() const	{ return "SetIPChecksum"; }
+    const char *port_count() const	{ return PORTS_1_1; }
+};
+
+class HIPSetUDPChecksum : public HIPSetChecksum { public:
+    const char *class_name() const	{ return "SetUDPChecksum"; }
+    const char *port_count() const	{ return PORTS_1_1X2; }
+};
+
+class HIPSetTCPChecksum : public HIPSetChecksum { public:
+    const char *class_name() const	{ return "SetTCPChecksum"; }
+    const char *port_count() const	{ return PORTS_1_1; }
+};
+
+class HIPDecIPTTL : public HIPBatchElement { public:
+    const char *class_name() const	{ return "DecIPTTL"; }
+    const char *port_count() const	{ return PORTS_1_1X2; }
+  protected:
+    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
+    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+};
+
+CLICK_ENDDECLS
+#endif

@@ -190,6 +190,31 @@ int clk_check_icmp_header(clk_ctx *ctx, const clk_batch *batch, uint8_t *out_ver
 int clk_dec_ip_ttl(clk_ctx *ctx, const clk_batch *batch, int multicast,
                    uint8_t *out_status, uint16_t *out_sum);
 
+/* ---- incremental update ------------------------------------------------------
+ * click_update_in_cksum (include/clicknet/ip.h:177-185) applied in place to
+ * every packet: the 16-bit word at off_i + cfg->hw_off is replaced by
+ * new_hw[i] (device u16, stored as the reference stores a uint16_t) and the
+ * checksum at off_i + cfg->sum_off is updated by RFC 1624 from the old and
+ * new words.  With cfg->zero_fix, click_update_zero_in_cksum follows
+ * (ip.h:196-201, lib/in_cksum.c:113-121): a resulting 0 over all-zero
+ * data [off_i + zero_lo, off_i + len_i) becomes 0xFFFF.
+ * out_status[i] (nullable): 0 updated, 1 a field past len_i (nothing
+ * written), 2 updated and zero-fixed.  out_sum (nullable): the checksum
+ * stored (as read back in host order).                                    */
+typedef struct clk_cksum_update_cfg {
+    uint32_t sum_off, hw_off;
+    int32_t zero_fix;
+    uint32_t zero_lo;
+} clk_cksum_update_cfg;
+int clk_update_in_cksum(clk_ctx *ctx, const clk_batch *batch, const clk_cksum_update_cfg *cfg,
+                        const uint16_t *new_hw, uint8_t *out_status, uint16_t *out_sum);
+/* click_update_zero_in_cksum alone on every packet (the ICMP responders'
+ * call after their own updates, e.g. icmppingresponder.cc:89): the stored
+ * checksum at off_i + sum_off becomes 0xFFFF when it is 0 and every byte of
+ * [off_i + zero_lo, off_i + len_i) is 0.  Status / sums as above.          */
+int clk_update_zero_in_cksum(clk_ctx *ctx, const clk_batch *batch, uint32_t sum_off, uint32_t zero_lo,
+                             uint8_t *out_status, uint16_t *out_sum);
+
 /* ---- IP output path ---------------------------------------------------------
  * The batch points at each packet's IP header (= data() for these elements
  * in an IP router graph); len_i = bytes from it to end_data().
