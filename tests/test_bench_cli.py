@@ -54,3 +54,17 @@ def test_config1_cpu_forwards_everything():
     import bench
     r = bench.config1_cpu(20000)
     assert r["elements"]["forwarded"] == 20000 and r["combos"]["forwarded"] == 20000
+
+
+def test_cpu_baseline_object_code(oracle):
+    """The timed restatement is the scalar movzwl/add word loop SURVEY §6
+    describes for the reference at -O2, called (not inlined or vectorized)
+    by every element function (oracle/objdump_check.py; the committed
+    oracle/objdump_in_cksum.txt is its output)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("objdump_check", os.path.join(ROOT, "oracle", "objdump_check.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    ok, rep, body = m.check()
+    assert ok, rep
+    assert any(i.startswith("movzwl") for i in body)
