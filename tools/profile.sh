@@ -12,7 +12,7 @@ OUT=gpurun_out/prof_${TAG}_${WL}
 mkdir -p "$OUT"
 # FRAG=1 keeps the IPFragmenter section (C3 only)
 NOFRAG=--no-frag; [ "${FRAG:-0}" = 1 ] && NOFRAG=
-ARGS="--workload $WL --no-cpu --no-peak --no-c2 $NOFRAG --skip c4,c5 $*"
+ARGS="--workload $WL --no-cpu --no-peak --no-c2 --no-c1 $NOFRAG --skip c4,c5 $*"
 # summaries land in gpurun_out/profiles/ (merged back); copy them into profiles/
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
     python3 bench.py --steps 10 --warmup 2 $ARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
