@@ -106,13 +106,14 @@ class Element:
             raise ClickAmdError("flush_async failed: %d (%s)" % (rc, self.last_error()))
 
     def results(self, cap=1 << 20, aux=False):
-        """(tokens, ports, lengths[, aux]) of every flushed packet, in order."""
+        """(tokens, ports, lengths[, aux]) of every flushed packet, in order
+        (popped `cap` at a time: pass about the number expected)."""
         out = []
         while True:
-            t = np.zeros(cap, np.uint64)
-            p = np.zeros(cap, np.int32)
-            ln = np.zeros(cap, np.uint32)
-            ax = np.zeros(cap, np.uint32)
+            t = np.empty(cap, np.uint64)
+            p = np.empty(cap, np.int32)
+            ln = np.empty(cap, np.uint32)
+            ax = np.empty(cap, np.uint32)
             n = self.lib.clk_element_results_aux(self.h, t.ctypes.data_as(ctypes.c_void_p),
                                                  p.ctypes.data_as(ctypes.c_void_p),
                                                  ln.ctypes.data_as(ctypes.c_void_p),
