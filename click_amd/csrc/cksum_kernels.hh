@@ -463,6 +463,39 @@ __device__ __forceinline__ void l4_parse(uint8_t *nh, uint32_t caplen, int fixof
     l4_parse_words<PROTO, SET>(nh, caplen, fixoff, d, st);
 }
 
+// The header dwords from the group's pass-0 registers instead of loads of
+// their own (CLK_HDR_FROM_CHUNKS, G >= 4): lanes 0..3 of the group hold
+// chunks 0..3 = [c0, c0 + 64) in v[0], which cover every aligned header
+// dword (at most 3 + 11 dwords past c0).  Same values as l4_parse: dwords at
+// or past nh + caplen read as 0.
+// Used by the two-phase Set compute pass (C3 Set 5.30 -> 5.14 ms); the
+// Check kernels keep their own header loads (C3 Check 3.83 vs 3.86 ms).
+#ifndef CLK_HDR_FROM_CHUNKS
+#define CLK_HDR_FROM_CHUNKS 1
+#endif
+template <int PROTO, bool SET, int G, int K>
+__device__ __forceinline__ void l4_parse_from_chunks(uint8_t *nh, uint32_t caplen, int fixoff, uint64_t c0,
+                                                     uint32_t lane, const u32x4 (&v)[K], L4State &st)
+{
+    constexpr int HDR_DW = L4Hdr<PROTO>::DW;
+    const int gbase = (int)(lane & ~(uint32_t)(G - 1));
+    uint32_t D[16];
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int w = 0; w < 4; w++)
+            D[4 * q + w] = __shfl(v[0][w], gbase + q, 64);
+    const uint64_t a = (uint64_t)nh, qa = a & ~3ull, end = a + caplen;
+    const uint32_t q0 = (uint32_t)(qa - c0) >> 2;           // 0..3
+    uint32_t d[HDR_DW];
+#pragma unroll
+    for (int k = 0; k < HDR_DW; k++) {
+        const uint32_t x = q0 == 0 ? D[k] : q0 == 1 ? D[k + 1] : q0 == 2 ? D[k + 2] : D[k + 3];
+        d[k] = qa + 4 * k < end ? x : 0u;
+    }
+    l4_parse_words<PROTO, SET>(nh, caplen, fixoff, d, st);
+}
+
 // Finish one packet from its range sum.  `writer` lanes store.
 // Replace byte `val` at absolute address `at` if it lies in the 16 bytes of
 // v at absolute address `va`.
@@ -657,7 +690,7 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
 #define CLK_L4_WPE_SET 5     // UDP Set l4_kernels: 5 waves/SIMD (C3 -4 %); TCP Set keeps 4 (C5 +0.6 % at 5)
 #endif
 #ifndef CLK_L4_WPE_CHECK
-#define CLK_L4_WPE_CHECK 1
+#define CLK_L4_WPE_CHECK 5   // 5 waves/SIMD: C5 Check 22.86 vs 23.01 ms (98 -> 96 VGPRs), C3 unchanged
 #endif
 template <int PROTO, bool SET, int G, int K, bool DEFER>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SET && PROTO == UDP ? CLK_L4_WPE_SET : SET ? 1 : CLK_L4_WPE_CHECK)))
@@ -680,7 +713,10 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         constexpr bool NT = UseNT<!SET || DEFER>::value;
         load_pass<G, K, NT>(c0, nch, 0, gl, v);  // issued before the header loads
         L4State st;
-        l4_parse<PROTO, SET>(nh, caplen, fixoff, st);
+        if (SET && DEFER && CLK_HDR_FROM_CHUNKS && G >= 4)    // two-phase compute pass
+            l4_parse_from_chunks<PROTO, SET, G, K>(nh, caplen, fixoff, (uint64_t)c0, lane, v, st);
+        else
+            l4_parse<PROTO, SET>(nh, caplen, fixoff, st);
         // a lane whose packet needs no sum masks everything (len 0)
         const uint32_t sum = group_range_sum<G, K, NT>(c0, nch, gl, v, a + st.hl, st.summing ? st.rlen : 0);
         if (SET && !DEFER && CLK_SET_REGBLK)

@@ -99,6 +99,8 @@ VARIANTS = {
     "k9": (["-DCLK_K=9"], {}),
     "k10": (["-DCLK_K=10"], {}),
     "regblk0": (["-DCLK_SET_REGBLK=0"], {}),
+    "hdrc0": (["-DCLK_HDR_FROM_CHUNKS=0"], {}),
+    "cw1": (["-DCLK_L4_WPE_CHECK=1"], {}),
     "ntst": (["-DCLK_NT_STORES=1"], {}),
     "nt_ntst": (["-DCLK_NT_LOADS=1", "-DCLK_NT_STORES=1"], {}),
     "two_nt": (["-DCLK_NT_LOADS=1"], {"CLK_SET_MODE": "1"}),
