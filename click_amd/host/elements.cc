@@ -334,6 +334,8 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
         g.h_used = slot + len;
     }
     Stage &g = st_[cur_];
+    if (g.pend.capacity() < batch_cap_ && g.pend.empty())
+        g.pend.reserve(std::min<size_t>(batch_cap_, 1u << 20));
     g.pend.push_back(p);
     return g.pend.size() >= batch_cap_ ? 1 : 0;
 }
@@ -540,7 +542,7 @@ uint64_t BatchElement::pop_results(uint64_t *tokens, int32_t *ports, uint32_t *l
         results_.pop_front();
         i++;
     }
-    return i;
+    return i;       // (the queue's storage is reused once it is empty)
 }
 
 void BatchElement::write_back(const Pending &p, uint32_t nbytes) const
@@ -1321,7 +1323,7 @@ int IPOutputCombo::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
     return clk_ip_output_combo(ctx_, b, &cfg, d_anno_, d_codes, d_aux8_, nullptr);
 }
 
-void IPOutputCombo::pre_route(Pending &p, std::deque<Result> &out)
+void IPOutputCombo::pre_route(Pending &p, ResultQueue &out)
 {
     // PaintTee: a clone of the packet as it arrived goes to output 1 first (56-57)
     if (!(p.anno & CLK_ANNO_BCAST) && (long)((p.anno >> 8) & 0xFF) == color_)
@@ -1527,7 +1529,7 @@ void IPFragmenter::route(Pending &p, int code, uint16_t, Result *r)
     fragments_++;
 }
 
-void IPFragmenter::post_route(Pending &p, int code, std::deque<Result> &out)
+void IPFragmenter::post_route(Pending &p, int code, ResultQueue &out)
 {
     if (p.host_code >= 0 || code != 2)
         return;

@@ -6,7 +6,6 @@
 // (include/click_amd_cksum.h).  See include/click_amd_elements.h.
 #pragma once
 #include <cstdint>
-#include <deque>
 #include <map>
 #include <string>
 #include <vector>
@@ -23,6 +22,35 @@ struct Result {
     int32_t port;        // 0..4, or -1 (kill)
     uint32_t length;     // packet length after the element
     uint32_t aux;        // clk_element_results_aux (problem offset, clone flag, new-packet key)
+};
+
+// Routed results in push order: appended by flush(), popped by the caller.
+// A vector with a read index (no per-block allocations as in std::deque);
+// storage is reused once everything has been popped.
+class ResultQueue {
+  public:
+    void push_back(const Result &r)
+    {
+        if (head_ > 4096 && head_ * 2 > v_.size()) {     // a caller that never drains: drop the popped prefix
+            v_.erase(v_.begin(), v_.begin() + (long)head_);
+            head_ = 0;
+        }
+        v_.push_back(r);
+    }
+    bool empty() const { return head_ == v_.size(); }
+    const Result &front() const { return v_[head_]; }
+    void pop_front()
+    {
+        if (++head_ == v_.size()) {
+            v_.clear();
+            head_ = 0;
+        }
+    }
+    size_t size() const { return v_.size() - head_; }
+
+  private:
+    std::vector<Result> v_;
+    size_t head_ = 0;
 };
 
 // Click-style configuration: comma-separated arguments, "KEYWORD value".
@@ -81,9 +109,9 @@ class BatchElement {
     virtual bool wants_anno() const { return false; }
     // called by flush() before route(): results() of the packet that precede
     // its own (IPOutputCombo's clone)
-    virtual void pre_route(Pending &, std::deque<Result> &) {}
+    virtual void pre_route(Pending &, ResultQueue &) {}
     // called after route(): results that follow the packet's own (fragments)
-    virtual void post_route(Pending &, int, std::deque<Result> &) {}
+    virtual void post_route(Pending &, int, ResultQueue &) {}
     // after the batch completed, before any packet is routed: nonzero fails
     // the flush (a kernel's internal fault report in the codes)
     virtual int verify(const uint8_t *, size_t) { return 0; }
@@ -144,7 +172,7 @@ class BatchElement {
     Stage st_[2];
     int cur_ = 0;
     const Stage *rt_ = &st_[0];          // the stage being routed
-    std::deque<Result> results_;
+    ResultQueue results_;
     std::vector<std::string> msgs_;
     std::map<uint32_t, std::vector<uint8_t>> packets_kept_;
     uint32_t next_key_ = 1;
@@ -348,7 +376,7 @@ class IPOutputCombo : public BatchElement {
   protected:
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
-    void pre_route(Pending &p, std::deque<Result> &out) override;
+    void pre_route(Pending &p, ResultQueue &out) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
     bool wants_arena_back() const override { return true; }
     bool wants_anno() const override { return true; }
@@ -373,7 +401,7 @@ class IPFragmenter : public BatchElement {
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
     int verify(const uint8_t *codes, size_t n) override;
-    void post_route(Pending &p, int code, std::deque<Result> &out) override;
+    void post_route(Pending &p, int code, ResultQueue &out) override;
     bool wants_arena_back() const override { return true; }
 
   private:

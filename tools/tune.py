@@ -98,6 +98,8 @@ VARIANTS = {
     "k12": (["-DCLK_K=12"], {}),
     "k9": (["-DCLK_K=9"], {}),
     "k10": (["-DCLK_K=10"], {}),
+    "k6": (["-DCLK_K=6"], {}),
+    "k7": (["-DCLK_K=7"], {}),
     "regblk0": (["-DCLK_SET_REGBLK=0"], {}),
     "hdrc0": (["-DCLK_HDR_FROM_CHUNKS=0"], {}),
     "cw1": (["-DCLK_L4_WPE_CHECK=1"], {}),
