@@ -323,7 +323,7 @@ HIPBatchElement::add_handlers()
     static const char *const names[] = {"drops", "drop_details", "fragments", "batches", "packets",
 					"gpu_ns", "device", "color", "active"};
     for (unsigned i = 0; i < sizeof(names) / sizeof(names[0]); i++)
-	add_read_handler(names[i], read_handler, const_cast<char *>(names[i]));
+	add_read_handler(String(names[i]), read_handler, static_cast<const void *>(names[i]));
 }
 
 CLICK_ENDDECLS
