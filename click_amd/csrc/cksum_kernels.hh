@@ -970,7 +970,10 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // issue: find the packets of this lane's KV chunks at cb and load them
         uint32_t carry = 0;          // MARKS: 1 + the packet of the chunk before this pass (wave-uniform)
-        auto issue = [&](uint32_t cb, u32x4 (&v)[KV], uint32_t (&jk)[KV], u32x4 (&Pk)[KV]) {
+        // per chunk the consumer needs its packet (jk) and inf = its index r in
+        // the packet | last chunk << 30 | odd packet << 31 (2 VGPRs per chunk
+        // rather than the packet's 4-word record: KV = 4 fits 8 waves)
+        auto issue = [&](uint32_t cb, u32x4 (&v)[KV], uint32_t (&jk)[KV], uint32_t (&inf)[KV]) {
             const uint32_t cl = cb + lane * KV;
             if (MARKS) {
                 // each packet marks its first chunk in the pass window, a
@@ -1033,7 +1036,8 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             for (int k = 0; k < KV; k++) {
                 const uint32_t c = cl + k;
                 const u32x4 P = pk[wv][jk[k]];
-                Pk[k] = P;
+                const uint32_t r = c - P[2];
+                inf[k] = r | (r == (P[3] & 0x7FFFFFFFu) - 1 ? 1u << 30 : 0u) | (P[3] & 0x80000000u);
                 const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
                 if (UseNT<false>::value)
                     v[k] = c < total ? __builtin_nontemporal_load((const u32x4 *)(cf + 16ull * (c - P[2])))
@@ -1043,7 +1047,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             }
         };
         // consume: whole-chunk sums into the packets' accumulators, stash
-        auto consume = [&](uint32_t cb, const u32x4 (&v)[KV], const uint32_t (&jk)[KV], const u32x4 (&Pk)[KV]) {
+        auto consume = [&](uint32_t cb, const u32x4 (&v)[KV], const uint32_t (&jk)[KV], const uint32_t (&inf)[KV]) {
             const uint32_t cl = cb + lane * KV;
             uint32_t cur = jk[0], part = 0;
 #pragma unroll
@@ -1057,13 +1061,13 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                     cur = jk[k];
                 }
                 const u32x4 V = v[k];
-                const uint32_t r = c - Pk[k][2];               // chunk index within the packet
+                const uint32_t r = inf[k] & 0x3FFFFFFFu;       // chunk index within the packet
                 if (r < (uint32_t)HC)
                     head[wv][jk[k]][r] = V;
-                if (r == (Pk[k][3] & 0x7FFFFFFFu) - 1)
+                if (inf[k] & (1u << 30))
                     tail[wv][jk[k]] = V;
                 if (anyodd) {
-                    const uint32_t sel = (Pk[k][3] >> 31) ? 0x02030001u : 0x03020100u;
+                    const uint32_t sel = (inf[k] >> 31) ? 0x02030001u : 0x03020100u;
 #pragma unroll
                     for (int q = 0; q < 4; q++)
                         part = dot_words(__builtin_amdgcn_perm(V[q], V[q], sel), part);
@@ -1077,32 +1081,32 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                 atomicAdd(&acc[wv][cur], part);
         };
         if (PF) {                 // the next pass's loads are in flight while this pass is summed
-            u32x4 v[KV], Pk[KV];
-            uint32_t jk[KV];
+            u32x4 v[KV];
+            uint32_t jk[KV], inf[KV];
             if (total)
-                issue(0, v, jk, Pk);
+                issue(0, v, jk, inf);
             for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
-                u32x4 v2[KV], P2[KV];
-                uint32_t j2[KV];
+                u32x4 v2[KV];
+                uint32_t j2[KV], i2[KV];
                 const bool more = cb + 64 * KV < total;
                 if (more)
-                    issue(cb + 64 * KV, v2, j2, P2);
-                consume(cb, v, jk, Pk);
+                    issue(cb + 64 * KV, v2, j2, i2);
+                consume(cb, v, jk, inf);
                 if (more) {
 #pragma unroll
                     for (int k = 0; k < KV; k++) {
                         v[k] = v2[k];
                         jk[k] = j2[k];
-                        Pk[k] = P2[k];
+                        inf[k] = i2[k];
                     }
                 }
             }
         } else {
             for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
-                u32x4 v[KV], Pk[KV];
-                uint32_t jk[KV];
-                issue(cb, v, jk, Pk);
-                consume(cb, v, jk, Pk);
+                u32x4 v[KV];
+                uint32_t jk[KV], inf[KV];
+                issue(cb, v, jk, inf);
+                consume(cb, v, jk, inf);
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

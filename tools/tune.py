@@ -52,6 +52,9 @@ VARIANTS = {
     "stream": ([], {"CLK_VARLEN": "2"}),
     "skv1": (["-DCLK_SKV=1"], {"CLK_VARLEN": "2"}),
     "skv4": (["-DCLK_SKV=4"], {"CLK_VARLEN": "2"}),
+    "skv3": (["-DCLK_SKV=3"], {"CLK_VARLEN": "2"}),
+    "skv4w7": (["-DCLK_SKV=4", "-DCLK_SWPE=7"], {"CLK_VARLEN": "2"}),
+    "skv3w7": (["-DCLK_SKV=3", "-DCLK_SWPE=7"], {"CLK_VARLEN": "2"}),
     "skv8": (["-DCLK_SKV=8"], {"CLK_VARLEN": "2"}),
     "fused_stream": ([], {"CLK_SET_MODE": "0", "CLK_VARLEN": "2"}),
     "two_stream": ([], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
