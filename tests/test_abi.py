@@ -128,3 +128,34 @@ def test_c_example_builds():
     its device arrays) and links against the library with -Werror."""
     exes = build.build_examples()
     assert all(os.access(e, os.X_OK) for e in exes)
+
+
+def test_click_adapters_use_only_the_public_abi():
+    """The Click element sources (click_integration/elements/hip, not
+    compilable here: they need Click's generated <click/config.h>) call only
+    functions and constants the public headers declare, and every adapter
+    class is exported under the reference name (hipdropin.cc) and a HIP
+    name (hipparity.cc)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    inc = os.path.join(root, "include")
+    declared = set()
+    for h in os.listdir(inc):
+        declared |= set(re.findall(r"\b(clk_\w+)\s*\(", open(os.path.join(inc, h)).read()))
+        declared |= set(re.findall(r"\b(CLK_\w+)\b", open(os.path.join(inc, h)).read()))
+    hip = os.path.join(root, "click_integration", "elements", "hip")
+    used = set()
+    for f in os.listdir(hip):
+        text = re.sub(r"//.*|/\*.*?\*/", "", open(os.path.join(hip, f)).read(), flags=re.S)
+        used |= set(re.findall(r"\b(clk_\w+)\s*\(", text)) | set(re.findall(r"\b(CLK_\w+)\b", text))
+    assert used and used <= declared, sorted(used - declared)
+    dropin = open(os.path.join(hip, "hipdropin.cc")).read()
+    parity = open(os.path.join(hip, "hipparity.cc")).read()
+    ref_names = ["CheckIPHeader", "CheckIPHeader2", "SetIPChecksum", "CheckUDPHeader", "SetUDPChecksum",
+                 "CheckTCPHeader", "SetTCPChecksum", "CheckICMPHeader", "DecIPTTL", "IPInputCombo", "IPGWOptions",
+                 "FixIPSrc", "IPOutputCombo", "IPFragmenter"]
+    hh = "".join(open(os.path.join(hip, f)).read() for f in os.listdir(hip) if f.endswith(".hh"))
+    for n in ref_names:
+        assert "EXPORT_ELEMENT(HIP%s)" % n in dropin and "EXPORT_ELEMENT(HIP%sX)" % n in parity, n
+        # click-buildtool reads class names from single-line class_name() methods
+        assert re.search(r'class HIP%s\b.*?\n\s*const char \*class_name\(\) const\s*\{ return "%s"; \}' % (n, n), hh,
+                         re.S), n
