@@ -238,12 +238,21 @@ template <int PROTO, bool SET, int G>
 void launch_l4_g(clk_ctx *ctx, const clk::BatchArgs &a, unsigned grid, int fixoff, uint8_t *code, uint16_t *sum,
                  uint32_t *work)
 {
-    if (SET && work)
-        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, true>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a, fixoff,
-                           code, sum, work);
+    // runs of 64 packets per wave for packets 0..n-1 (CLK_L4_RUNS), the
+    // grid-stride group loop for a size-class pass
+    constexpr bool RUNS = CLK_L4_RUNS != 0 && (!SET || G >= CLK_L4_RUNS_SET_G);
+    if (SET && work && !a.perm)
+        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, true, RUNS>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a,
+                           fixoff, code, sum, work);
+    else if (SET && work)
+        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, true, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a,
+                           fixoff, code, sum, work);
+    else if (!a.perm)
+        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, false, RUNS>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a,
+                           fixoff, code, sum, work);
     else
-        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a, fixoff,
-                           code, sum, work);
+        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, false, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a,
+                           fixoff, code, sum, work);
 }
 
 template <int PROTO, bool SET>
@@ -320,7 +329,11 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
         }
     } else {
         const int g = pick_group(ctx, b);
-        launch_l4_dispatch<PROTO, SET>(ctx, args_of(b), grid_for(ctx, b->n * (uint64_t)g), fixoff, code, sum, work, g);
+        // runs of CLK_L4_RUN packets per wave (CLK_L4_RUNS): a wave per run
+        const uint64_t run = (uint64_t)(CLK_L4_RUN < 64 / g ? 64 / g : CLK_L4_RUN);
+        const bool runs = CLK_L4_RUNS && (!SET || g >= CLK_L4_RUNS_SET_G);
+        const uint64_t threads = runs ? (b->n + run - 1) / run * 64 : b->n * (uint64_t)g;
+        launch_l4_dispatch<PROTO, SET>(ctx, args_of(b), grid_for(ctx, threads), fixoff, code, sum, work, g);
     }
     if (work) {
         constexpr int FIELD = PROTO == clk::UDP ? 6 : 16;

@@ -33,8 +33,14 @@
 #ifndef CLK_DIAG_NO_FIELD_STORE
 #define CLK_DIAG_NO_FIELD_STORE 0   // diagnostic builds only (results wrong)
 #endif
-#ifndef CLK_DIAG_NO_STATUS_STORE
-#define CLK_DIAG_NO_STATUS_STORE 0  // diagnostic builds only (results wrong)
+#ifndef CLK_L4_RUNS
+#define CLK_L4_RUNS 1      // l4_kernel: a wave owns runs of CLK_L4_RUN packets and stores their outputs whole
+#endif
+#ifndef CLK_L4_RUN
+#define CLK_L4_RUN 64      // packets per run (at least 64 / G)
+#endif
+#ifndef CLK_L4_RUNS_SET_G
+#define CLK_L4_RUNS_SET_G 32   // Set kernels use runs from this G up (C5 -6 %; C3's G = 16 Set +1-2 %: DESIGN.md §6)
 #endif
 
 namespace clk {
@@ -632,11 +638,15 @@ __device__ __forceinline__ bool set_block_store_stash(uint8_t *nh, const L4State
     return true;
 }
 
+// A packet's outputs: status code, two-phase work word, Set checksum.
+struct L4Out {
+    uint32_t code, work, sum;
+};
+
 template <int PROTO, bool SET, bool DEFER, typename Store>
-__device__ __forceinline__ void l4_finish_with(uint8_t *nh, uint64_t i, uint32_t sum, L4State &st, bool writer,
-                                               uint8_t *out_code, uint16_t *out_sum, uint32_t *work, Store &&store)
+__device__ __forceinline__ L4Out l4_result(uint8_t *nh, uint32_t sum, L4State &st, bool writer, Store &&store)
 {
-    uint32_t stored = 0;
+    L4Out o{0, 0, 0};
     if (st.code == OK && st.summing) {
         if (SET)
             sum += st.adj;
@@ -644,14 +654,12 @@ __device__ __forceinline__ void l4_finish_with(uint8_t *nh, uint64_t i, uint32_t
         // click_in_cksum(icmph, icmp_len) != 0 (checkicmpheader.cc:136-138), else the pseudo-header
         const uint32_t r = PROTO == ICMP ? csum : pseudohdr_ph(csum, st.ph);
         if (SET) {
-            stored = r;
+            o.sum = r;
 #if !CLK_DIAG_NO_FIELD_STORE
             if (DEFER) {         // the field is written by field_scatter_kernel
-                if (writer) {
-                    if (st.fix)
-                        nh[st.hl + 12] = (uint8_t)st.new_b12;
-                    work[i] = 0x80000000u | (st.hl << 16) | r;
-                }
+                if (writer && st.fix)
+                    nh[st.hl + 12] = (uint8_t)st.new_b12;
+                o.work = 0x80000000u | (st.hl << 16) | r;
             } else {
                 store(r);
             }
@@ -660,16 +668,23 @@ __device__ __forceinline__ void l4_finish_with(uint8_t *nh, uint64_t i, uint32_t
             st.code = L4_BAD_CHECKSUM;
         }
     }
+    o.code = st.code;
+    if (SET && DEFER && st.code != OK)
+        o.work = 0;
+    return o;
+}
+
+template <int PROTO, bool SET, bool DEFER, typename Store>
+__device__ __forceinline__ void l4_finish_with(uint8_t *nh, uint64_t i, uint32_t sum, L4State &st, bool writer,
+                                               uint8_t *out_code, uint16_t *out_sum, uint32_t *work, Store &&store)
+{
+    const L4Out o = l4_result<PROTO, SET, DEFER>(nh, sum, st, writer, store);
     if (writer) {
-#if !CLK_DIAG_NO_STATUS_STORE
-        out_code[i] = (uint8_t)st.code;
-#else
-        if (st.code == 0xFF) out_code[i] = 0;
-#endif
-        if (SET && DEFER && st.code != OK)
-            work[i] = 0;
+        out_code[i] = (uint8_t)o.code;
+        if (SET && DEFER)
+            work[i] = o.work;
         if (SET && out_sum)
-            out_sum[i] = (uint16_t)stored;
+            out_sum[i] = (uint16_t)o.sum;
     }
 }
 
@@ -690,42 +705,108 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
 #define CLK_L4_WPE_SET 5     // UDP Set l4_kernels: 5 waves/SIMD (C3 -4 %); TCP Set keeps 4 (C5 +0.6 % at 5)
 #endif
 #ifndef CLK_L4_WPE_CHECK
-#define CLK_L4_WPE_CHECK 5   // 5 waves/SIMD: C5 Check 22.86 vs 23.01 ms (98 -> 96 VGPRs), C3 unchanged
+#define CLK_L4_WPE_CHECK 4   // 4 waves/SIMD: the run loop spills at 5 (C3 Check 4.14 vs 3.81 ms)
 #endif
-template <int PROTO, bool SET, int G, int K, bool DEFER>
+// One packet by its G-lane group: parse, sum, and (fused Set) the field store.
+template <int PROTO, bool SET, int G, int K, bool DEFER, bool HDRC>
+__device__ __forceinline__ L4Out l4_group(const BatchArgs &b, int fixoff, uint64_t i, uint32_t lane, uint32_t gl)
+{
+    uint8_t *nh = b.base + pkt_off(b, i);
+    const uint32_t caplen = pkt_len(b, i);
+    const uint64_t a = (uint64_t)nh;
+    const uint8_t *c0 = (const uint8_t *)(a & ~15ull);
+    const uint32_t nch = (uint32_t)((((a + caplen + 15) & ~15ull) - (uint64_t)c0) / 16);
+    u32x4 v[K];
+    // nontemporal for Check and for the read-only compute pass of a
+    // two-phase Set
+    constexpr bool NT = UseNT<!SET || DEFER>::value;
+    load_pass<G, K, NT>(c0, nch, 0, gl, v);  // issued before the header loads
+    L4State st;
+    if (SET && DEFER && HDRC && G >= 4)    // two-phase compute pass, grid-stride loop
+        l4_parse_from_chunks<PROTO, SET, G, K>(nh, caplen, fixoff, (uint64_t)c0, lane, v, st);
+    else
+        l4_parse<PROTO, SET>(nh, caplen, fixoff, st);
+    // a lane whose packet needs no sum masks everything (len 0)
+    const uint32_t sum = group_range_sum<G, K, NT>(c0, nch, gl, v, a + st.hl, st.summing ? st.rlen : 0);
+    if (SET && !DEFER && CLK_SET_REGBLK)
+        return l4_result<PROTO, SET, DEFER>(nh, sum, st, gl == 0, [&](uint32_t r) {
+            if (!set_block_store_regs<PROTO, G, K>(nh, st, r, gl, (uint64_t)c0, v))
+                set_field_store<PROTO>(nh, st, r, gl, G, gl == 0);
+        });
+    return l4_result<PROTO, SET, DEFER>(nh, sum, st, gl == 0,
+                                        [&](uint32_t r) { set_field_store<PROTO>(nh, st, r, gl, G, gl == 0); });
+}
+
+// RUNS: packets 0..n-1 in runs of 64 per wave (below); else the grid-stride
+// loop over groups, which also serves the size-class passes (b.perm).
+template <int PROTO, bool SET, int G, int K, bool DEFER, bool RUNS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SET && PROTO == UDP ? CLK_L4_WPE_SET : SET ? 1 : CLK_L4_WPE_CHECK)))
 l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                  uint16_t *out_sum, uint32_t *work)
 {
     const uint32_t lane = threadIdx.x & 63, gl = lane & (G - 1);
+    if (RUNS) {
+        // A wave owns runs of 64 consecutive packets.  Pass p takes packets
+        // 64 run + p (64 / G) + lane / G; each group's writer lane puts the
+        // results in the wave's LDS slots, and after the run one store
+        // instruction per output writes all 64 (lane q: packet 64 run + q).
+        // So every output block (64 B of codes, 256 B of work words, 128 B
+        // of sums) is written whole by one wave: no partial block reaches the
+        // memory controller's read-modify-write, and no block is shared by
+        // the L2s of two XCDs (tools/probes/stash_probe.hip).
+        constexpr uint32_t PPW = 64 / G, R = CLK_L4_RUN < (int)PPW ? PPW : CLK_L4_RUN;
+        __shared__ uint8_t r_code[256];
+        __shared__ uint32_t r_work[SET && DEFER ? 256 : 1];
+        __shared__ uint16_t r_sum[SET ? 256 : 1];
+        const uint32_t wslot = threadIdx.x & ~63u;
+        const uint64_t nruns = (b.n + R - 1) / R;
+        const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
+        for (uint64_t run = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); run < nruns;
+             run += wstride) {
+            const uint64_t i0 = run * R;
+#pragma unroll 1
+            for (uint32_t p = 0; p < R / PPW; p++) {
+                const uint32_t q = p * PPW + lane / G;
+                if (i0 + q < b.n) {
+                    const L4Out o = l4_group<PROTO, SET, G, K, DEFER, false>(b, fixoff, i0 + q, lane, gl);
+                    if (gl == 0) {
+                        r_code[wslot + q] = (uint8_t)o.code;
+                        if (SET && DEFER)
+                            r_work[wslot + q] = o.work;
+                        if (SET)
+                            r_sum[wslot + q] = (uint16_t)o.sum;
+                    }
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint64_t i = i0 + lane;
+            if (lane < R && i < b.n) {
+                out_code[i] = r_code[threadIdx.x];
+                if (SET && DEFER)
+                    work[i] = r_work[threadIdx.x];
+                if (SET && out_sum)
+                    out_sum[i] = r_sum[threadIdx.x];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        return;
+    }
     const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
     const uint64_t jbeg = b.perm ? b.range[0] : 0, jend = b.perm ? b.range[1] : b.n;
     for (uint64_t j = jbeg + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; j < jend; j += groups) {
         const uint64_t i = b.perm ? (uint64_t)b.perm[j] : j;
-        uint8_t *nh = b.base + pkt_off(b, i);
-        const uint32_t caplen = pkt_len(b, i);
-        const uint64_t a = (uint64_t)nh;
-        const uint8_t *c0 = (const uint8_t *)(a & ~15ull);
-        const uint32_t nch = (uint32_t)((((a + caplen + 15) & ~15ull) - (uint64_t)c0) / 16);
-        u32x4 v[K];
-        // nontemporal for Check and for the read-only compute pass of a
-        // two-phase Set
-        constexpr bool NT = UseNT<!SET || DEFER>::value;
-        load_pass<G, K, NT>(c0, nch, 0, gl, v);  // issued before the header loads
-        L4State st;
-        if (SET && DEFER && CLK_HDR_FROM_CHUNKS && G >= 4)    // two-phase compute pass
-            l4_parse_from_chunks<PROTO, SET, G, K>(nh, caplen, fixoff, (uint64_t)c0, lane, v, st);
-        else
-            l4_parse<PROTO, SET>(nh, caplen, fixoff, st);
-        // a lane whose packet needs no sum masks everything (len 0)
-        const uint32_t sum = group_range_sum<G, K, NT>(c0, nch, gl, v, a + st.hl, st.summing ? st.rlen : 0);
-        if (SET && !DEFER && CLK_SET_REGBLK)
-            l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, gl == 0, out_code, out_sum, work, [&](uint32_t r) {
-                if (!set_block_store_regs<PROTO, G, K>(nh, st, r, gl, (uint64_t)c0, v))
-                    set_field_store<PROTO>(nh, st, r, gl, G, gl == 0);
-            });
-        else
-            l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, gl == 0, out_code, out_sum, work, gl, G);
+        const L4Out o = l4_group<PROTO, SET, G, K, DEFER, CLK_HDR_FROM_CHUNKS != 0>(b, fixoff, i, lane, gl);
+        if (gl == 0) {
+            out_code[i] = (uint8_t)o.code;
+            if (SET && DEFER)
+                work[i] = o.work;
+            if (SET && out_sum)
+                out_sum[i] = (uint16_t)o.sum;
+        }
     }
 }
 

@@ -128,6 +128,34 @@ def test_fuzz_parity(torch, ctx, proto, max_total, align):
         compare(torch, ctx, "dec_ttl", arena, n, off=off, length=caplen, max_len=ml, arg=multicast)
 
 
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 130, 257])
+@pytest.mark.parametrize("proto,max_total", [(17, 1600), (6, 1600), (17, 20000), (6, 20000)])
+def test_run_tails(torch, ctx, n, proto, max_total):
+    """The fixed-geometry kernels store their outputs per run of 64 packets
+    (CLK_L4_RUNS): batch sizes around a run boundary, 16 and 64 lanes per
+    packet, Check and Set (fused and two-phase), FIXOFF on and off."""
+    rng = np.random.default_rng(n * 31 + proto + max_total)
+    arena, off, caplen, ml = fuzz.make_batch(rng, n, proto, max_total=max_total, align="any")
+    for op in OPS_L4[proto]:
+        compare(torch, ctx, op, arena, n, off=off, length=caplen, max_len=ml, arg=1)
+    compare(torch, ctx, OPS_L4[proto][1], arena, n, off=off, length=caplen, max_len=ml, arg=0)
+
+
+def test_run_outputs_at_odd_address(torch, ctx):
+    """Verdict bytes written into an output view at an odd address."""
+    rng = np.random.default_rng(3)
+    n = 200
+    arena, off, caplen, ml = fuzz.make_batch(rng, n, 17, max_total=1600, align="any")
+    b = dev_batch(torch, arena, n, off, caplen, max_len=ml)
+    big = torch.full((n + 2,), 0xEE, dtype=torch.uint8, device="cuda:0")
+    ctx.check_udp_header(b, out=big[1:n + 1])
+    ctx.sync()
+    rc, _ = oracle_lib.batch("check_udp", arena.copy(), n, off=off, length=caplen)
+    g = big.cpu().numpy()
+    assert g[0] == 0xEE and g[n + 1] == 0xEE
+    assert np.array_equal(g[1:n + 1], rc)
+
+
 @pytest.mark.parametrize("max_len_hint", [0, 64, 500, 2000, 100000])
 def test_geometry_hint_does_not_change_results(torch, ctx, max_len_hint):
     """Lanes per packet (1/4/16/64, multi-pass) is a speed choice only; a

@@ -112,6 +112,10 @@ VARIANTS = {
     "regblk_fused": ([], {"CLK_SET_MODE": "0"}),
     "two_stream_nt": (["-DCLK_NT_LOADS=1"], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
     "regblk0_fused": (["-DCLK_SET_REGBLK=0"], {"CLK_SET_MODE": "0"}),
+    "runs0": (["-DCLK_L4_RUNS=0"], {}),
+    "cw5": (["-DCLK_L4_WPE_CHECK=5"], {}),
+    "setruns16": (["-DCLK_L4_RUNS_SET_G=16"], {}),
+    "sw4": (["-DCLK_L4_WPE_SET=4"], {}),
 }
 
 
