@@ -6,6 +6,9 @@ pass) and writes
   profiles/<tag>/<workload>_kernel_stats.csv   (rocprofv3 --stats summary)
   profiles/<tag>/<workload>_pmc.json           (per-kernel counters)
   profiles/pmc_<workload>.json                 (what bench.py reads)
+The element duration is the mean over all traced launches (what the
+rocprofv3 --stats summary shows) and, as duration_ms_timed, over the last
+<steps> launches of each kernel: bench.py's timed region, after its warm-up.
 HBM bytes per launch of the element kernel =
   2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
 (FETCH_SIZE is in KiB and reads exactly half the bytes of a wide coalesced
@@ -56,6 +59,7 @@ def short(name):
 def main():
     out, tag, wl = sys.argv[1:4]
     pdir = os.path.join(ROOT, sys.argv[4] if len(sys.argv) > 4 else "profiles", tag)
+    steps = int(sys.argv[5]) if len(sys.argv) > 5 else 0
     os.makedirs(pdir, exist_ok=True)
     stats = find(os.path.join(out, "trace"), "*kernel_stats.csv")
     trace = find(os.path.join(out, "trace"), "*kernel_trace.csv")
@@ -66,7 +70,8 @@ def main():
     if trace:
         for r in rows(trace):
             n = short(r["Kernel_Name"])
-            durs.setdefault(n, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6)
+            durs.setdefault(n, []).append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    durs = {k: [(e - b) * 1e-6 for b, e in sorted(v)] for k, v in durs.items()}     # launch order
     res["trace_ms"] = {k: {"calls": len(v), "mean_ms": statistics.mean(v), "min_ms": min(v)}
                        for k, v in durs.items()}
     counters = {}
@@ -88,6 +93,8 @@ def main():
         if not ks:
             continue
         e = {"kernels": ks, "duration_ms": sum(statistics.mean(durs[k]) for k in ks)}
+        if steps:
+            e["duration_ms_timed"] = sum(statistics.mean(durs[k][-steps:]) for k in ks)
         if "FETCH_SIZE" in counters and "WRITE_SIZE" in counters:
             f = sum(counters["FETCH_SIZE"].get(k, 0.0) for k in ks)
             w = sum(counters["WRITE_SIZE"].get(k, 0.0) for k in ks)

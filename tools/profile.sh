@@ -15,9 +15,9 @@ NOFRAG=--no-frag; [ "${FRAG:-0}" = 1 ] && NOFRAG=
 ARGS="--workload $WL --no-cpu --no-peak --no-c2 --no-c1 $NOFRAG --skip c4,c5 $*"
 # summaries land in gpurun_out/profiles/ (merged back); copy them into profiles/
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- \
-    python3 bench.py --steps 10 --warmup 2 $ARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
+    python3 bench.py --steps 20 --warmup 10 $ARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- \
     python3 bench.py --steps 3 --warmup 1 $ARGS > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
     python3 bench.py --steps 3 --warmup 1 $ARGS > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
-python3 tools/pmc_summary.py "$OUT" "$TAG" "$WL" gpurun_out/profiles
+python3 tools/pmc_summary.py "$OUT" "$TAG" "$WL" gpurun_out/profiles 20
