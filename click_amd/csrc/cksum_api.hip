@@ -238,9 +238,9 @@ template <int PROTO, bool SET, int G>
 void launch_l4_g(clk_ctx *ctx, const clk::BatchArgs &a, unsigned grid, int fixoff, uint8_t *code, uint16_t *sum,
                  uint32_t *work)
 {
-    // runs of 64 packets per wave for packets 0..n-1 (CLK_L4_RUNS), the
-    // grid-stride group loop for a size-class pass
-    constexpr bool RUNS = CLK_L4_RUNS != 0 && (!SET || G >= CLK_L4_RUNS_SET_G);
+    // runs per workgroup for packets 0..n-1 (CLK_L4_RUNS), the grid-stride
+    // group loop for a size-class pass
+    constexpr bool RUNS = CLK_L4_RUNS && (!SET || G >= CLK_L4_RUNS_SET_G);
     if (SET && work && !a.perm)
         hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, K, true, RUNS>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a,
                            fixoff, code, sum, work);
@@ -329,10 +329,11 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
         }
     } else {
         const int g = pick_group(ctx, b);
-        // runs of CLK_L4_RUN packets per wave (CLK_L4_RUNS): a wave per run
-        const uint64_t run = (uint64_t)(CLK_L4_RUN < 64 / g ? 64 / g : CLK_L4_RUN);
-        const bool runs = CLK_L4_RUNS && (!SET || g >= CLK_L4_RUNS_SET_G);
-        const uint64_t threads = runs ? (b->n + run - 1) / run * 64 : b->n * (uint64_t)g;
+        uint64_t threads = b->n * (uint64_t)g;
+        if (CLK_L4_RUNS && (!SET || g >= CLK_L4_RUNS_SET_G)) {   // a workgroup per run
+            const uint64_t run = 256 / g < 64 ? 64 : 256 / g;
+            threads = (b->n + run - 1) / run * BLOCK;
+        }
         launch_l4_dispatch<PROTO, SET>(ctx, args_of(b), grid_for(ctx, threads), fixoff, code, sum, work, g);
     }
     if (work) {

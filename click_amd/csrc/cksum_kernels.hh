@@ -34,10 +34,7 @@
 #define CLK_DIAG_NO_FIELD_STORE 0   // diagnostic builds only (results wrong)
 #endif
 #ifndef CLK_L4_RUNS
-#define CLK_L4_RUNS 1      // l4_kernel: a wave owns runs of CLK_L4_RUN packets and stores their outputs whole
-#endif
-#ifndef CLK_L4_RUN
-#define CLK_L4_RUN 64      // packets per run (at least 64 / G)
+#define CLK_L4_RUNS 1      // l4_kernel: a workgroup owns runs of packets and stores their outputs whole
 #endif
 #ifndef CLK_L4_RUNS_SET_G
 #define CLK_L4_RUNS_SET_G 32   // Set kernels use runs from this G up (C5 -6 %; C3's G = 16 Set +1-2 %: DESIGN.md §6)
@@ -737,7 +734,7 @@ __device__ __forceinline__ L4Out l4_group(const BatchArgs &b, int fixoff, uint64
                                         [&](uint32_t r) { set_field_store<PROTO>(nh, st, r, gl, G, gl == 0); });
 }
 
-// RUNS: packets 0..n-1 in runs of 64 per wave (below); else the grid-stride
+// RUNS: packets 0..n-1 in runs per workgroup (below); else the grid-stride
 // loop over groups, which also serves the size-class passes (b.perm).
 template <int PROTO, bool SET, int G, int K, bool DEFER, bool RUNS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SET && PROTO == UDP ? CLK_L4_WPE_SET : SET ? 1 : CLK_L4_WPE_CHECK)))
@@ -746,52 +743,47 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
 {
     const uint32_t lane = threadIdx.x & 63, gl = lane & (G - 1);
     if (RUNS) {
-        // A wave owns runs of 64 consecutive packets.  Pass p takes packets
-        // 64 run + p (64 / G) + lane / G; each group's writer lane puts the
-        // results in the wave's LDS slots, and after the run one store
-        // instruction per output writes all 64 (lane q: packet 64 run + q).
-        // So every output block (64 B of codes, 256 B of work words, 128 B
-        // of sums) is written whole by one wave: no partial block reaches the
-        // memory controller's read-modify-write, and no block is shared by
-        // the L2s of two XCDs (tools/probes/stash_probe.hip).
-        constexpr uint32_t PPW = 64 / G, R = CLK_L4_RUN < (int)PPW ? PPW : CLK_L4_RUN;
-        __shared__ uint8_t r_code[256];
-        __shared__ uint32_t r_work[SET && DEFER ? 256 : 1];
-        __shared__ uint16_t r_sum[SET ? 256 : 1];
-        const uint32_t wslot = threadIdx.x & ~63u;
-        const uint64_t nruns = (b.n + R - 1) / R;
-        const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
-        for (uint64_t run = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); run < nruns;
-             run += wstride) {
-            const uint64_t i0 = run * R;
+        // A workgroup owns runs of RB consecutive packets (at least 64), 256 / G
+        // per pass, as the grid-stride loop visits them.  The groups' writer
+        // lanes put the results in LDS, and after a workgroup barrier one
+        // store instruction per output and wave writes the run's outputs:
+        // every output block (64 B of codes, 256 B of work words, 128 B of
+        // sums) is written whole by one workgroup, so no partial block
+        // reaches the memory controller's read-modify-write and no block is
+        // shared by the L2s of two XCDs (DESIGN.md §6,
+        // tools/probes/stash_probe.hip).  The two-phase Set parses its
+        // header from loads of its own here (measured faster in runs).
+        constexpr uint32_t PPB = 256 / G, RB = PPB < 64 ? 64 : PPB;
+        __shared__ uint8_t r_code[RB];
+        __shared__ uint32_t r_work[SET && DEFER ? RB : 1];
+        __shared__ uint16_t r_sum[SET ? RB : 1];
+        const uint64_t nruns = (b.n + RB - 1) / RB;
+        for (uint64_t run = blockIdx.x; run < nruns; run += gridDim.x) {       // uniform per workgroup
+            const uint64_t i0 = run * RB;
 #pragma unroll 1
-            for (uint32_t p = 0; p < R / PPW; p++) {
-                const uint32_t q = p * PPW + lane / G;
+            for (uint32_t p = 0; p < RB / PPB; p++) {
+                const uint32_t q = p * PPB + threadIdx.x / G;
                 if (i0 + q < b.n) {
                     const L4Out o = l4_group<PROTO, SET, G, K, DEFER, false>(b, fixoff, i0 + q, lane, gl);
                     if (gl == 0) {
-                        r_code[wslot + q] = (uint8_t)o.code;
+                        r_code[q] = (uint8_t)o.code;
                         if (SET && DEFER)
-                            r_work[wslot + q] = o.work;
+                            r_work[q] = o.work;
                         if (SET)
-                            r_sum[wslot + q] = (uint16_t)o.sum;
+                            r_sum[q] = (uint16_t)o.sum;
                     }
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint64_t i = i0 + lane;
-            if (lane < R && i < b.n) {
+            __syncthreads();
+            const uint64_t i = i0 + threadIdx.x;
+            if (threadIdx.x < RB && i < b.n) {
                 out_code[i] = r_code[threadIdx.x];
                 if (SET && DEFER)
                     work[i] = r_work[threadIdx.x];
                 if (SET && out_sum)
                     out_sum[i] = r_sum[threadIdx.x];
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            __syncthreads();
         }
         return;
     }
