@@ -667,7 +667,7 @@ __device__ __forceinline__ L4Out l4_result(uint8_t *nh, uint32_t sum, L4State &s
     }
     o.code = st.code;
     if (SET && DEFER && st.code != OK)
-        o.work = 0;
+        o.work = st.code;    // bit 31 clear: no field; field_scatter_kernel writes the code
     return o;
 }
 
@@ -677,11 +677,13 @@ __device__ __forceinline__ void l4_finish_with(uint8_t *nh, uint64_t i, uint32_t
 {
     const L4Out o = l4_result<PROTO, SET, DEFER>(nh, sum, st, writer, store);
     if (writer) {
-        out_code[i] = (uint8_t)o.code;
-        if (SET && DEFER)
+        if (SET && DEFER) {          // status and sum follow from the work word (field_scatter_kernel)
             work[i] = o.work;
-        if (SET && out_sum)
-            out_sum[i] = (uint16_t)o.sum;
+        } else {
+            out_code[i] = (uint8_t)o.code;
+            if (SET && out_sum)
+                out_sum[i] = (uint16_t)o.sum;
+        }
     }
 }
 
@@ -754,9 +756,9 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         // tools/probes/stash_probe.hip).  The two-phase Set parses its
         // header from loads of its own here (measured faster in runs).
         constexpr uint32_t PPB = 256 / G, RB = PPB < 64 ? 64 : PPB;
-        __shared__ uint8_t r_code[RB];
+        __shared__ uint8_t r_code[SET && DEFER ? 1 : RB];
         __shared__ uint32_t r_work[SET && DEFER ? RB : 1];
-        __shared__ uint16_t r_sum[SET ? RB : 1];
+        __shared__ uint16_t r_sum[SET && !DEFER ? RB : 1];
         const uint64_t nruns = (b.n + RB - 1) / RB;
         for (uint64_t run = blockIdx.x; run < nruns; run += gridDim.x) {       // uniform per workgroup
             const uint64_t i0 = run * RB;
@@ -766,22 +768,26 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                 if (i0 + q < b.n) {
                     const L4Out o = l4_group<PROTO, SET, G, K, DEFER, false>(b, fixoff, i0 + q, lane, gl);
                     if (gl == 0) {
-                        r_code[q] = (uint8_t)o.code;
-                        if (SET && DEFER)
+                        if (SET && DEFER) {
                             r_work[q] = o.work;
-                        if (SET)
-                            r_sum[q] = (uint16_t)o.sum;
+                        } else {
+                            r_code[q] = (uint8_t)o.code;
+                            if (SET && out_sum)
+                                r_sum[q] = (uint16_t)o.sum;
+                        }
                     }
                 }
             }
             __syncthreads();
             const uint64_t i = i0 + threadIdx.x;
             if (threadIdx.x < RB && i < b.n) {
-                out_code[i] = r_code[threadIdx.x];
-                if (SET && DEFER)
+                if (SET && DEFER) {
                     work[i] = r_work[threadIdx.x];
-                if (SET && out_sum)
-                    out_sum[i] = r_sum[threadIdx.x];
+                } else {
+                    out_code[i] = r_code[threadIdx.x];
+                    if (SET && out_sum)
+                        out_sum[i] = r_sum[threadIdx.x];
+                }
             }
             __syncthreads();
         }
@@ -793,11 +799,13 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         const uint64_t i = b.perm ? (uint64_t)b.perm[j] : j;
         const L4Out o = l4_group<PROTO, SET, G, K, DEFER, CLK_HDR_FROM_CHUNKS != 0>(b, fixoff, i, lane, gl);
         if (gl == 0) {
-            out_code[i] = (uint8_t)o.code;
-            if (SET && DEFER)
+            if (SET && DEFER) {
                 work[i] = o.work;
-            if (SET && out_sum)
-                out_sum[i] = (uint16_t)o.sum;
+            } else {
+                out_code[i] = (uint8_t)o.code;
+                if (SET && out_sum)
+                    out_sum[i] = (uint16_t)o.sum;
+            }
         }
     }
 }
@@ -1519,14 +1527,22 @@ __global__ void __launch_bounds__(256) ip_out_kernel(BatchArgs b, IpOutArgs c, u
 // ---------------------------------------------------------------------------
 template <int FIELD_BASE, bool L4>
 __global__ void __launch_bounds__(256) field_scatter_kernel(BatchArgs b, const uint32_t *work,
-                                                            const uint8_t *status, const uint16_t *sums)
+                                                            const uint8_t *status, const uint16_t *sums,
+                                                            uint8_t *out_code, uint16_t *out_sum)
 {
+    // L4: the compute pass wrote only work[i] (bit 31: the field value, else
+    // the status code); this pass writes the field and, one lane per packet,
+    // the status codes and sums -- 64 consecutive packets per wave, so whole
+    // output blocks
     const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += nthreads) {
         if (L4) {
             const uint32_t w = work[i];
             if (w & 0x80000000u)
                 st_u16(b.base + pkt_off(b, i) + ((w >> 16) & 0xFF) + FIELD_BASE, w & 0xFFFF);
+            out_code[i] = (w & 0x80000000u) ? 0 : (uint8_t)w;
+            if (out_sum)
+                out_sum[i] = (w & 0x80000000u) ? (uint16_t)w : 0;
         } else if (status[i] == 0) {
             st_u16(b.base + pkt_off(b, i) + FIELD_BASE, sums[i]);
         }
