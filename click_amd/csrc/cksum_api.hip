@@ -337,7 +337,7 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
         const int g = pick_group(ctx, b);
         uint64_t threads = b->n * (uint64_t)g;
         if (CLK_L4_RUNS && (!SET || g >= CLK_L4_RUNS_SET_G)) {   // a workgroup per run
-            const uint64_t run = 256 / g < 64 ? 64 : 256 / g;
+            const uint64_t run = 256 / g < 64 ? 64 : 256 / g;        // as l4_kernel's RB
             threads = (b->n + run - 1) / run * BLOCK;
         }
         launch_l4_dispatch<PROTO, SET>(ctx, args_of(b), grid_for(ctx, threads), fixoff, code, sum, work, g);

@@ -30,11 +30,17 @@
 #ifndef CLK_BLOCK_WRITE
 #define CLK_BLOCK_WRITE 0  // tuning knob: fused Set stores rewrite the whole 64 B block (measured slower)
 #endif
+#ifndef CLK_DIAG_NO_WORK_STORE
+#define CLK_DIAG_NO_WORK_STORE 0    // diagnostic builds only (results wrong)
+#endif
 #ifndef CLK_DIAG_NO_FIELD_STORE
 #define CLK_DIAG_NO_FIELD_STORE 0   // diagnostic builds only (results wrong)
 #endif
 #ifndef CLK_L4_RUNS
 #define CLK_L4_RUNS 1      // l4_kernel: a workgroup owns runs of packets and stores their outputs whole
+#endif
+#ifndef CLK_RUNS_HDRC
+#define CLK_RUNS_HDRC 0        // runs: the two-phase Set's header from the chunk registers (measured slower)
 #endif
 #ifndef CLK_L4_RUNS_SET_G
 #define CLK_L4_RUNS_SET_G 32   // Set kernels use runs from this G up (C5 -6 %; C3's G = 16 Set +1-2 %: DESIGN.md §6)
@@ -766,7 +772,7 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             for (uint32_t p = 0; p < RB / PPB; p++) {
                 const uint32_t q = p * PPB + threadIdx.x / G;
                 if (i0 + q < b.n) {
-                    const L4Out o = l4_group<PROTO, SET, G, K, DEFER, false>(b, fixoff, i0 + q, lane, gl);
+                    const L4Out o = l4_group<PROTO, SET, G, K, DEFER, CLK_RUNS_HDRC != 0>(b, fixoff, i0 + q, lane, gl);
                     if (gl == 0) {
                         if (SET && DEFER) {
                             r_work[q] = o.work;
@@ -800,7 +806,8 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         const L4Out o = l4_group<PROTO, SET, G, K, DEFER, CLK_HDR_FROM_CHUNKS != 0>(b, fixoff, i, lane, gl);
         if (gl == 0) {
             if (SET && DEFER) {
-                work[i] = o.work;
+                if (!CLK_DIAG_NO_WORK_STORE || (o.work ^ (uint32_t)b.n) == 0x7F012345u)
+                    work[i] = o.work;
             } else {
                 out_code[i] = (uint8_t)o.code;
                 if (SET && out_sum)

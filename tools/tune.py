@@ -115,8 +115,8 @@ VARIANTS = {
     "runs0": (["-DCLK_L4_RUNS=0"], {}),
     "cw5": (["-DCLK_L4_WPE_CHECK=5"], {}),
     "setruns16": (["-DCLK_L4_RUNS_SET_G=16"], {}),
-    "setruns16sw4": (["-DCLK_L4_RUNS_SET_G=16", "-DCLK_L4_WPE_SET=4"], {}),
     "k16_8": (["-DCLK_K16=8"], {}),
+    "diag_nowork": (["-DCLK_DIAG_NO_WORK_STORE=1"], {}),
     "sw4": (["-DCLK_L4_WPE_SET=4"], {}),
 }
 
