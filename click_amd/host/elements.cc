@@ -281,11 +281,11 @@ int BatchElement::grow_dev(Stage &g, size_t bytes, size_t n)
 
 int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
 {
-    Pending p{data, length, nh_offset, token, -1, 0, 0, 0, anno, 0};
+    Pending p{data, token, 0, length, nh_offset, 0, 0, 0, -1, (uint16_t)anno};
     uint32_t off = 0, len = 0;
     int32_t code = 0;
     if (!span(p, &off, &len, &code)) {
-        p.host_code = code;
+        p.host_code = (int16_t)code;
     } else if (zerocopy_) {
         // the kernel reads the span where it lies (clk_host_register)
         const uint8_t *a = data + off;
@@ -311,10 +311,6 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
         if (!g.zc_host) {                                         // the batch's first staged packet
             g.zc_host = zc_last_;
             g.zc_dev = zc_last_dev_;
-        }
-        if (grow_host(g, 64, g.pend.size() + 1)) {
-            err_ = "out of pinned host memory";
-            return CLK_EINVAL;
         }
         p.slot = (uint64_t)(a - g.zc_host);
         p.span_off = off;
@@ -476,6 +472,8 @@ int BatchElement::complete(Stage &g)
     h_aux8_ = g.h_aux8;
     in_place_ = g.zc;
     size_t k = 0;
+    const bool sums = wants_sums(), pre = has_pre_route_, post = has_post_route_;
+    results_.reserve_more(g.pend.size());
     for (Pending &p : g.pend) {
         int code;
         uint16_t sum = 0;
@@ -483,14 +481,16 @@ int BatchElement::complete(Stage &g)
             code = p.host_code;
         } else {
             code = g.h_codes[k];
-            sum = wants_sums() ? g.h_sums[k] : 0;
+            sum = sums ? g.h_sums[k] : 0;
             k++;
         }
         Result r{p.token, 0, p.length, 0};
-        pre_route(p, results_);
+        if (pre)
+            pre_route(p, results_);
         route(p, code, sum, &r);
         results_.push_back(r);
-        post_route(p, code, results_);
+        if (post)
+            post_route(p, code, results_);
     }
     batches_++;
     packets_ += g.pend.size();
@@ -532,17 +532,7 @@ int BatchElement::flush()
 uint64_t BatchElement::pop_results(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint32_t *aux,
                                    uint64_t cap)
 {
-    uint64_t i = 0;
-    while (i < cap && !results_.empty()) {
-        const Result &r = results_.front();
-        if (tokens) tokens[i] = r.token;
-        if (ports) ports[i] = r.port;
-        if (lengths) lengths[i] = r.length;
-        if (aux) aux[i] = r.aux;
-        results_.pop_front();
-        i++;
-    }
-    return i;       // (the queue's storage is reused once it is empty)
+    return results_.pop(tokens, ports, lengths, aux, cap);   // (storage reused once it is empty)
 }
 
 void BatchElement::write_back(const Pending &p, uint32_t nbytes) const

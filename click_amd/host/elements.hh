@@ -5,7 +5,9 @@
 // and runs the checksum work as one GPU batch per flush() through the C ABI
 // (include/click_amd_cksum.h).  See include/click_amd_elements.h.
 #pragma once
+#include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <map>
 #include <string>
 #include <vector>
@@ -25,31 +27,61 @@ struct Result {
 };
 
 // Routed results in push order: appended by flush(), popped by the caller.
-// A vector with a read index (no per-block allocations as in std::deque);
-// storage is reused once everything has been popped.
+// Struct of arrays with a read index: pops are bulk copies, storage is
+// reused once everything has been popped (no per-block allocations).
 class ResultQueue {
   public:
+    void reserve_more(size_t k)
+    {
+        if (head_ > 4096 && head_ * 2 > tok_.size())      // a caller that never drains: drop the popped prefix
+            compact();
+        const size_t need = tok_.size() + k;
+        if (tok_.capacity() < need) {
+            tok_.reserve(need);
+            port_.reserve(need);
+            len_.reserve(need);
+            aux_.reserve(need);
+        }
+    }
     void push_back(const Result &r)
     {
-        if (head_ > 4096 && head_ * 2 > v_.size()) {     // a caller that never drains: drop the popped prefix
-            v_.erase(v_.begin(), v_.begin() + (long)head_);
-            head_ = 0;
-        }
-        v_.push_back(r);
+        tok_.push_back(r.token);
+        port_.push_back(r.port);
+        len_.push_back(r.length);
+        aux_.push_back(r.aux);
     }
-    bool empty() const { return head_ == v_.size(); }
-    const Result &front() const { return v_[head_]; }
-    void pop_front()
+    bool empty() const { return head_ == tok_.size(); }
+    size_t size() const { return tok_.size() - head_; }
+    uint64_t pop(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap)
     {
-        if (++head_ == v_.size()) {
-            v_.clear();
+        const size_t k = (size_t)std::min<uint64_t>(cap, size());
+        if (tokens) std::memcpy(tokens, tok_.data() + head_, k * sizeof(uint64_t));
+        if (ports) std::memcpy(ports, port_.data() + head_, k * sizeof(int32_t));
+        if (lengths) std::memcpy(lengths, len_.data() + head_, k * sizeof(uint32_t));
+        if (aux) std::memcpy(aux, aux_.data() + head_, k * sizeof(uint32_t));
+        head_ += k;
+        if (head_ == tok_.size()) {
+            tok_.clear();
+            port_.clear();
+            len_.clear();
+            aux_.clear();
             head_ = 0;
         }
+        return k;
     }
-    size_t size() const { return v_.size() - head_; }
 
   private:
-    std::vector<Result> v_;
+    void compact()
+    {
+        tok_.erase(tok_.begin(), tok_.begin() + (long)head_);
+        port_.erase(port_.begin(), port_.begin() + (long)head_);
+        len_.erase(len_.begin(), len_.begin() + (long)head_);
+        aux_.erase(aux_.begin(), aux_.begin() + (long)head_);
+        head_ = 0;
+    }
+    std::vector<uint64_t> tok_;
+    std::vector<int32_t> port_;
+    std::vector<uint32_t> len_, aux_;
     size_t head_ = 0;
 };
 
@@ -84,17 +116,17 @@ class BatchElement {
     size_t pending() const { return st_[cur_].pend.size(); }
 
   protected:
-    struct Pending {
+    struct Pending {         // 48 bytes: staged per packet, read by launch() and flush()
         uint8_t *data;
+        uint64_t token;
+        uint64_t slot;       // staging offset of the span
         uint32_t length;
         int32_t nh_off;
-        uint64_t token;
-        int32_t host_code;   // >= 0: decided on the host (not staged)
-        uint64_t slot;       // staging offset of the span
         uint32_t span_off;   // span start relative to data
         uint32_t span_len;
-        uint32_t anno;       // CLK_ANNO_* bits
         uint32_t index;      // position in the GPU batch (staged packets)
+        int16_t host_code;   // >= 0: decided on the host (not staged)
+        uint16_t anno;       // CLK_ANNO_* bits
     };
     // Bytes the kernel needs, relative to data; return false to decide on the
     // host with *code (routed like a kernel result).
@@ -108,10 +140,12 @@ class BatchElement {
     // upload anno & 0xFF of the staged packets; run() finds it in d_anno_
     virtual bool wants_anno() const { return false; }
     // called by flush() before route(): results() of the packet that precede
-    // its own (IPOutputCombo's clone)
+    // its own (IPOutputCombo's clone); only when has_pre_route_
     virtual void pre_route(Pending &, ResultQueue &) {}
-    // called after route(): results that follow the packet's own (fragments)
+    // called after route(): results that follow the packet's own (fragments);
+    // only when has_post_route_
     virtual void post_route(Pending &, int, ResultQueue &) {}
+    bool has_pre_route_ = false, has_post_route_ = false;
     // after the batch completed, before any packet is routed: nonzero fails
     // the flush (a kernel's internal fault report in the codes)
     virtual int verify(const uint8_t *, size_t) { return 0; }
@@ -368,7 +402,10 @@ class FixIPSrc : public BatchElement {
 // outputs.
 class IPOutputCombo : public BatchElement {
   public:
-    using BatchElement::BatchElement;
+    IPOutputCombo(clk_ctx *ctx, const std::string &name, int noutputs) : BatchElement(ctx, name, noutputs)
+    {
+        has_pre_route_ = true;
+    }
     const char *class_name() const override { return "IPOutputCombo"; }
     int configure(ConfArgs &args, std::string *err) override;
     std::string read_handler(const std::string &h) const override;
@@ -390,7 +427,10 @@ class IPOutputCombo : public BatchElement {
 // HEADROOM; handlers drops, fragments.
 class IPFragmenter : public BatchElement {
   public:
-    using BatchElement::BatchElement;
+    IPFragmenter(clk_ctx *ctx, const std::string &name, int noutputs) : BatchElement(ctx, name, noutputs)
+    {
+        has_post_route_ = true;
+    }
     ~IPFragmenter() override;
     const char *class_name() const override { return "IPFragmenter"; }
     int configure(ConfArgs &args, std::string *err) override;

@@ -2,7 +2,7 @@
 // (diagnostic, not product).  Config 1's 114 B frame, N copies in a host
 // arena; for each element: push_burst of all N into one batch (BATCH >= N, so
 // push() alone is timed), flush() (launch + wait + route), and popping the
-// results.  FixIPSrc (no annotation) and IPGWOptions (no options) decide
+// results; then with 64K batches (push_burst flushes as they fill).  FixIPSrc (no annotation) and IPGWOptions (no options) decide
 // every frame on the host: their time is pure glue bookkeeping.
 // Build: g++ -O2 -std=c++17 -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ tools/probes/glue_probe.cc
 //        -Lclick_amd -lclick_amd_cksum -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,$PWD/click_amd -o tools/probes/glue_probe
@@ -59,10 +59,11 @@ int main(int argc, char **argv)
     std::vector<uint64_t> tok(n + 1);
     std::vector<int32_t> port(n + 1);
     std::vector<uint32_t> len(n + 1);
+    for (uint32_t batch : {n, 65536u})
     for (int zc = 0; zc < 2; zc++)
         for (auto &e : els) {
             char conf[256];
-            snprintf(conf, sizeof conf, "%s%sBATCH %u%s", e[1], e[1][0] ? ", " : "", n, zc ? ", ZEROCOPY true" : "");
+            snprintf(conf, sizeof conf, "%s%sBATCH %u%s", e[1], e[1][0] ? ", " : "", batch, zc ? ", ZEROCOPY true" : "");
             clk_element *el = nullptr;
             if (clk_element_create(ctx, e[0], conf, "x", 2, &el) != CLK_SUCCESS) {
                 fprintf(stderr, "%s: %s\n", e[0], clk_last_error(ctx));
@@ -86,9 +87,9 @@ int main(int argc, char **argv)
                     if (d[k] < best[k])
                         best[k] = d[k];
             }
-            printf("{\"element\": \"%s\", \"zerocopy\": %d, \"n\": %u, \"push_ns\": %.2f, \"flush_ns\": %.2f, "
-                   "\"results_ns\": %.2f}\n",
-                   e[0], zc, n, best[0] / n * 1e9, best[1] / n * 1e9, best[2] / n * 1e9);
+            printf("{\"element\": \"%s\", \"zerocopy\": %d, \"n\": %u, \"batch\": %u, \"push_ns\": %.2f, "
+                   "\"flush_ns\": %.2f, \"results_ns\": %.2f}\n",
+                   e[0], zc, n, batch, best[0] / n * 1e9, best[1] / n * 1e9, best[2] / n * 1e9);
             clk_element_destroy(el);
         }
     clk_host_unregister(ctx, base);
