@@ -462,7 +462,8 @@ def summarize(r, steps, wname):
     }
 
 
-def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24, glue_pkts=1 << 18,
+def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24,
+        glue_pkts=int(os.environ.get("CLK_E2E_GLUE_PKTS", 1 << 21)),
         glue_threads=int(os.environ.get("CLK_E2E_THREADS", 2))):
     """End-to-end rates with the packets in HOST memory (DESIGN.md "E2E").
 
@@ -530,7 +531,8 @@ def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24, glue_pkts=1 
     import numpy as np
     e = Element(ctx, element, ", ".join(x for x in (ELEMENT_CONF.get(element, ""), "BATCH 65536") if x), noutputs=2)
     base = host.data_ptr()
-    ptrs = (np.arange(glue_pkts, dtype=np.uint64) * np.uint64(stride) + np.uint64(base))
+    slots = np.arange(glue_pkts, dtype=np.uint64) % np.uint64(2 * chunk_pkts)    # the host buffer's packets, reused
+    ptrs = slots * np.uint64(stride) + np.uint64(base)
     lens = np.full(glue_pkts, L, np.uint32)
     nhs = np.zeros(glue_pkts, np.int32)
     e.push_burst(ptrs, lens, nhs, first_token=0)     # warm-up: both staging buffers allocated
@@ -550,7 +552,7 @@ def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24, glue_pkts=1 
     hostnp = raw[(-raw.ctypes.data) % 4096:][:host.numel()]
     hostnp[:] = host.numpy()
     dbase = ctx.host_register(hostnp)
-    zptrs = (np.arange(glue_pkts, dtype=np.uint64) * np.uint64(stride) + np.uint64(hostnp.ctypes.data))
+    zptrs = slots * np.uint64(stride) + np.uint64(hostnp.ctypes.data)
     try:
         zb = click_amd.Batch(dbase, chunk_pkts * 2, stride=stride, fixed_len=L)
         st = torch.empty(chunk_pkts * 2, dtype=torch.uint8, device="cuda")
