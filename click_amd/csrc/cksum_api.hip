@@ -224,7 +224,10 @@ int max_class(const clk_batch *b)
 template <int G>
 void launch_range(clk_ctx *ctx, const clk::BatchArgs &a, unsigned grid, uint16_t *out)
 {
-    hipLaunchKernelGGL((clk::range_kernel<G, K>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a, out);
+    if (CLK_L4_RUNS && !a.perm)      // runs per workgroup, as l4_kernel
+        hipLaunchKernelGGL((clk::range_kernel<G, k_for(G), true>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a, out);
+    else
+        hipLaunchKernelGGL((clk::range_kernel<G, k_for(G), false>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a, out);
 }
 
 void launch_range_dispatch(clk_ctx *ctx, const clk::BatchArgs &a, unsigned grid, uint16_t *out, int g)
@@ -532,7 +535,12 @@ int clk_in_cksum(clk_ctx *ctx, const clk_batch *b, uint16_t *out_sum)
         }
     } else {
         const int g = pick_group(ctx, b);
-        launch_range_dispatch(ctx, args_of(b), grid_for(ctx, b->n * (uint64_t)g), out_sum, g);
+        uint64_t threads = b->n * (uint64_t)g;
+        if (CLK_L4_RUNS) {                                        // a workgroup per run
+            const uint64_t run = 256 / g < 64 ? 64 : 256 / g;
+            threads = (b->n + run - 1) / run * BLOCK;
+        }
+        launch_range_dispatch(ctx, args_of(b), grid_for(ctx, threads), out_sum, g);
     }
     return check_launch(ctx, "clk_in_cksum");
 }

@@ -246,24 +246,54 @@ __device__ __forceinline__ uint32_t group_range_sum(const uint8_t *c0, uint32_t 
 }
 
 // clk_in_cksum: click_in_cksum(base+off_i, len_i) (lib/in_cksum.c:20-51).
-template <int G, int K>
+// RUNS (packets 0..n-1): a workgroup owns max(64, 256/G) consecutive
+// packets and writes their sums whole after one barrier, as l4_kernel does;
+// nontemporal loads (once-read stream).  Else the grid-stride loop, which
+// also serves the size-class passes (b.perm).
+template <int G, int K, bool RUNS>
 __global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_sum)
 {
     const uint32_t lane = threadIdx.x & 63, gl = lane & (G - 1);
-    const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
-    const uint64_t jbeg = b.perm ? b.range[0] : 0, jend = b.perm ? b.range[1] : b.n;
-    for (uint64_t j = jbeg + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; j < jend; j += groups) {
-        const uint64_t i = b.perm ? (uint64_t)b.perm[j] : j;
+    constexpr bool NT = UseNT<true>::value;
+    auto one = [&](uint64_t i) -> uint32_t {
         const uint8_t *p = b.base + pkt_off(b, i);
         const int len = (int)pkt_len(b, i);
         const uint64_t s = (uint64_t)p;
         const uint8_t *c0 = (const uint8_t *)(s & ~15ull);
         const uint32_t nch = len > 0 ? (uint32_t)(((s + (uint64_t)len + 15) & ~15ull) - (uint64_t)c0) / 16 : 0;
         u32x4 v[K];
-        load_pass<G, K>(c0, nch, 0, gl, v);
-        const uint32_t sum = group_range_sum<G, K>(c0, nch, gl, v, s, len);
+        load_pass<G, K, NT>(c0, nch, 0, gl, v);
+        return in_cksum_fold(group_range_sum<G, K, NT>(c0, nch, gl, v, s, len));
+    };
+    if (RUNS) {
+        constexpr uint32_t PPB = 256 / G, RB = PPB < 64 ? 64 : PPB;
+        __shared__ uint16_t r_sum[RB];
+        const uint64_t nruns = (b.n + RB - 1) / RB;
+        for (uint64_t run = blockIdx.x; run < nruns; run += gridDim.x) {       // uniform per workgroup
+            const uint64_t i0 = run * RB;
+#pragma unroll 1
+            for (uint32_t p = 0; p < RB / PPB; p++) {
+                const uint32_t q = p * PPB + threadIdx.x / G;
+                if (i0 + q < b.n) {
+                    const uint32_t r = one(i0 + q);
+                    if (gl == 0)
+                        r_sum[q] = (uint16_t)r;
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x < RB && i0 + threadIdx.x < b.n)
+                out_sum[i0 + threadIdx.x] = r_sum[threadIdx.x];
+            __syncthreads();
+        }
+        return;
+    }
+    const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
+    const uint64_t jbeg = b.perm ? b.range[0] : 0, jend = b.perm ? b.range[1] : b.n;
+    for (uint64_t j = jbeg + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; j < jend; j += groups) {
+        const uint64_t i = b.perm ? (uint64_t)b.perm[j] : j;
+        const uint32_t r = one(i);
         if (gl == 0)
-            out_sum[i] = (uint16_t)in_cksum_fold(sum);
+            out_sum[i] = (uint16_t)r;
     }
 }
 

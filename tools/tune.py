@@ -171,6 +171,7 @@ def main():
     base_ctx.gen_packets(b, proto=w["proto"])
     base_ctx.set_ip_checksum(b, want_sums=False)
     status = torch.empty(n, dtype=torch.uint8, device="cuda")
+    sums16 = torch.empty(n, dtype=torch.uint16, device="cuda")
     bench.run_element(base_ctx, "SetTCPChecksum" if w["proto"] == 6 else "SetUDPChecksum", b, status)
     ctxs = {}
     for nm in names:
@@ -191,6 +192,7 @@ def main():
                 "CheckUDPHeader": lambda c: c.check_udp_header(b, out=status),
                 "CheckTCPHeader": lambda c: c.check_tcp_header(b, out=status),
                 "CheckIPHeader": lambda c: c.check_ip_header(b, out=status),
+                "InCksum": lambda c: c.in_cksum(b, out=sums16),
                 "IPFragmenter": lambda c: frag(c)}
     if os.environ.get("TUNE_ELEMENT") == "IPFragmenter":       # C3 to MTU 576; headers restored per call
         hdr = arena.view(n, w["stride"])[:, :12]
@@ -225,6 +227,8 @@ def main():
             times[nm].append(s.elapsed_time(e) / args.launches)
     if element == "IPFragmenter":
         alg = 1924 * n
+    elif element == "InCksum":
+        alg = (w["L"] + 2) * n
     else:
         alg = bench.ALG[element](w["L"]) * n if args.workload != "c4" else sum_l + (bench.ALG[element](0) + 12) * n
     out = {nm: {"median_ms": round(statistics.median(t), 4), "min_ms": round(min(t), 4),
