@@ -250,12 +250,8 @@ __device__ __forceinline__ uint32_t group_range_sum(const uint8_t *c0, uint32_t 
 // packets and writes their sums whole after one barrier, as l4_kernel does;
 // nontemporal loads (once-read stream).  Else the grid-stride loop, which
 // also serves the size-class passes (b.perm).
-#ifndef CLK_RANGE_WPE_MAX
-#define CLK_RANGE_WPE_MAX 8
-#endif
 template <int G, int K, bool RUNS>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, CLK_RANGE_WPE_MAX)))
-range_kernel(BatchArgs b, uint16_t *out_sum)
+__global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_sum)
 {
     const uint32_t lane = threadIdx.x & 63, gl = lane & (G - 1);
     constexpr bool NT = UseNT<true>::value;

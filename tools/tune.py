@@ -117,9 +117,6 @@ VARIANTS = {
     "setruns16": (["-DCLK_L4_RUNS_SET_G=16"], {}),
     "k16_8": (["-DCLK_K16=8"], {}),
     "diag_nowork": (["-DCLK_DIAG_NO_WORK_STORE=1"], {}),
-    "rw5": (["-DCLK_RANGE_WPE_MAX=5"], {}),
-    "rw6": (["-DCLK_RANGE_WPE_MAX=6"], {}),
-    "rw4": (["-DCLK_RANGE_WPE_MAX=4"], {}),
     "sw4": (["-DCLK_L4_WPE_SET=4"], {}),
 }
 
