@@ -193,11 +193,28 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, pa
             ctx.gen_corrupt(b, **corrupt)             # flip the same bits back (untimed)
         dig.append(expect_drops)
         wall, kernel_ms, dig = shard.reduce_results(torch, dist, coll_dev, wall, kernel_ms, dig)
+        gather = None
+        if dist is not None and sums is not None:
+            # SURVEY §8(e) (2), untimed for the metric: every rank's checksums
+            # to rank 0 over the communicator, checked against the digest
+            try:
+                dist.barrier()
+                torch.cuda.synchronize()
+                tg = time.perf_counter()
+                allsums = shard.gather_results(torch, dist, coll_dev, sums)
+                torch.cuda.synchronize()
+                g_ms = (time.perf_counter() - tg) * 1e3
+                gather = {"bytes_per_rank": 2 * n, "ms": round(g_ms, 3),
+                          "GBs_into_root": round(2 * n * world / (g_ms * 1e-3) / 1e9, 1)}
+                if allsums is not None:
+                    gather["matches_digest"] = int(allsums.to(torch.int64).sum()) == dig[2]
+            except Exception as ex:             # reported, not fatal
+                gather = {"error": repr(ex)}
         out[e] = dict(wall=wall, kernel_ms=kernel_ms, kernel_ms_min=min(kms), n=n, ck_bytes=ck_bytes,
                       alg_bytes=alg[e], w=w, element=e, ok_total=dig[0], n_total=dig[1],
                       digest={"ok": dig[0], "packets": dig[1], "sum16": dig[2], "xor16": dig[3],
                               "drops": dig[1] - dig[0], "expected_drops": dig[4],
-                              "drops_exact": dig[1] - dig[0] == dig[4]})
+                              "drops_exact": dig[1] - dig[0] == dig[4]}, gather=gather)
         del sums
     del arena, status, b, l4sums
     torch.cuda.empty_cache()
@@ -459,6 +476,7 @@ def summarize(r, steps, wname):
                      "kernel_ms": round(r["kernel_ms"], 4), "kernel_ms_min": round(r["kernel_ms_min"], 4),
                      "alg_bytes_per_launch": r["alg_bytes"], "traffic_source": tsrc},
         "verify": r["digest"],
+        **({"gather_to_rank0": r["gather"]} if r.get("gather") else {}),
     }
 
 

@@ -64,3 +64,20 @@ def reduce_results(torch, dist, device, wall_s, kernel_ms, dig):
         xr ^= int(g.item())
     d = [int(v) for v in d.tolist()]
     return float(t[0]), float(t[1]), d[:3] + [xr] + d[3:]
+
+
+def gather_results(torch, dist, device, values, root=0):
+    """SURVEY §8(e) collective (2): every rank's per-packet results (the u16
+    checksums a Set wrote) to `root`, in rank order -- the shards are
+    contiguous global index ranges, so the concatenation is the whole
+    batch's result array.  One all_gather over the communicator (RCCL over
+    xGMI for the nccl backend; gloo on the CPU); equal shard sizes.
+    Returns the concatenated tensor on `root`, None elsewhere."""
+    if dist is None:
+        return values
+    # as bytes: neither RCCL nor gloo carries uint16
+    src = values.to(device).contiguous().view(torch.uint8)
+    parts = [torch.empty_like(src) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, src)
+    return torch.cat(parts).view(values.dtype) if dist.get_rank() == root else None
+

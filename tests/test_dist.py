@@ -45,7 +45,8 @@ def worker(rank, world, port, q):
     codes, sums = run_shard(lo, hi)
     dig = shard.digest(torch, codes, sums)
     wall, kms, total = shard.reduce_results(torch, dist, "cpu", 1.0 + rank, 2.0 * (rank + 1), dig)
-    q.put((rank, lo, hi, wall, kms, total))
+    allsums = shard.gather_results(torch, dist, "cpu", sums.to(torch.uint16))
+    q.put((rank, lo, hi, wall, kms, total, None if allsums is None else allsums.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -71,6 +72,9 @@ def test_sharded_digest_matches_single_process():
     single = shard.digest(torch, codes, sums)
     assert out[0][5] == single and out[1][5] == single
     assert single[0] == N_TOTAL
+    # the gathered checksums on rank 0 are the whole batch's, in packet order
+    assert out[1][6] is None
+    assert out[0][6].dtype == np.uint16 and np.array_equal(out[0][6].astype(np.int64), sums.numpy())
 
 
 def test_shard_by_bytes_balances_imix():

@@ -135,3 +135,7 @@ def test_bench_two_ranks_match_one(torch):
         assert two["elements"][e]["verify"]["packets"] == 2 * n
     chk = two["elements"]["CheckUDPHeader"]["verify"]
     assert chk["drops_exact"] and chk["drops"] > 0
+    # the Set's checksums gathered to rank 0 agree with the reduced digest
+    g = two["elements"]["SetUDPChecksum"]["gather_to_rank0"]
+    assert g.get("matches_digest") is True, g
+    assert "gather_to_rank0" not in one["elements"]["SetUDPChecksum"]
