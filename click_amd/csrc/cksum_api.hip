@@ -22,6 +22,10 @@ struct clk_ctx {
     int max_blocks;    // grid cap (tuning: CLK_MAX_BLOCKS)
     int force_group;   // lanes per packet override (tuning: CLK_FORCE_GROUP)
     int set_mode;      // -1 auto; 0: Set kernels store the field; 1: two-phase (CLK_SET_MODE)
+    int diag_phase;    // diagnostics only (CLK_DIAG_SET_PHASE): two-phase Set runs 1 its compute pass
+                       // alone, 2 its scatter alone (over the previous call's work words: the
+                       // first call runs both); 0 both
+    bool diag_primed;
     uint64_t bin_min;  // variable-length batches of >= bin_min packets run by size class (CLK_BIN_MIN)
     int bin_grid;      // grid cap of a size-class pass (CLK_BIN_GRID)
     int varlen;        // variable-length batches: 2 the packet-stream kernel, 1 the
@@ -302,7 +306,9 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
         if (two)
             work = (uint32_t *)ctx->scratch;
     }
-    if (bins && ctx->varlen == 2) {
+    if (work && ctx->diag_phase == 2 && ctx->diag_primed) {
+        // diagnostics: scatter only
+    } else if (bins && ctx->varlen == 2) {
         constexpr int KV = CLK_SKV;
         uint64_t blocks = (b->n + 255) / 256;            // 4 waves x 64 packets per block
         if (blocks > (uint64_t)ctx->max_blocks)
@@ -345,7 +351,9 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
         }
         launch_l4_dispatch<PROTO, SET>(ctx, args_of(b), grid_for(ctx, threads), fixoff, code, sum, work, g);
     }
-    if (work) {
+    if (work)
+        ctx->diag_primed = true;
+    if (work && ctx->diag_phase != 1) {
         constexpr int FIELD = PROTO == clk::UDP ? 6 : 16;
         hipLaunchKernelGGL((clk::field_scatter_kernel<FIELD, true>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
                            ctx->cur, args_of(b), (const uint32_t *)work, (const uint8_t *)nullptr,
@@ -414,6 +422,10 @@ int clk_ctx_create(int device, clk_ctx **out)
     c->set_mode = -1;
     if (const char *sm = std::getenv("CLK_SET_MODE"))
         c->set_mode = std::atoi(sm) == 1 ? 1 : 0;
+    c->diag_phase = 0;
+    c->diag_primed = false;
+    if (const char *dp = std::getenv("CLK_DIAG_SET_PHASE"))
+        c->diag_phase = std::atoi(dp);
     c->bin_min = 65536;
     if (const char *bm = std::getenv("CLK_BIN_MIN"))
         c->bin_min = (uint64_t)std::strtoull(bm, nullptr, 10);

@@ -43,7 +43,7 @@
 #define CLK_RUNS_HDRC 0        // runs: the two-phase Set's header from the chunk registers (measured slower)
 #endif
 #ifndef CLK_L4_RUNS_SET_G
-#define CLK_L4_RUNS_SET_G 32   // Set kernels use runs from this G up (C5 -6 %; C3's G = 16 Set +1-2 %: DESIGN.md §6)
+#define CLK_L4_RUNS_SET_G 16   // Set kernels use runs from this G up (C5 -6 %; C3 -5 % with nontemporal scatter stores: DESIGN.md §6)
 #endif
 
 namespace clk {
@@ -93,6 +93,28 @@ constexpr uint32_t TTL_EXPIRED = 1, TTL_UNCHANGED = 2;
 // (setipchecksum.cc:74-95), one lane per packet.
 // ---------------------------------------------------------------------------
 enum IpMode { IP_CHECK = 0, IP_CHECK_NOCKSUM = 1, IP_SET = 2 };
+
+// Field stores of the one-lane-per-packet rewriting kernels (SetIPChecksum,
+// DecIPTTL).  CLK_FIELD_NT: nontemporal, so the partial-block write reaches
+// HBM inside the kernel instead of lingering dirty in the caches until the
+// next kernel's reads evict it.
+#ifndef CLK_FIELD_NT
+#define CLK_FIELD_NT 1     // C2 SetIPChecksum 0.4065 vs 0.4116 ms, DecIPTTL 0.4083 vs 0.4122
+#endif
+__device__ __forceinline__ void field_st_u16(uint8_t *p, uint32_t v)
+{
+    if (CLK_FIELD_NT && ((uint64_t)p & 1) == 0)
+        __builtin_nontemporal_store((uint16_t)v, (__attribute__((address_space(1))) uint16_t *)p);
+    else
+        st_u16(p, v);
+}
+__device__ __forceinline__ void field_st_u32(uint8_t *p, uint32_t v)    // 4-byte aligned p
+{
+    if (CLK_FIELD_NT)
+        __builtin_nontemporal_store(v, (__attribute__((address_space(1))) uint32_t *)p);
+    else
+        *(__attribute__((address_space(1))) uint32_t *)p = v;
+}
 
 template <int MODE, bool DEFER>
 __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t offset,
@@ -153,7 +175,7 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
                     stored = in_cksum_fold(sum);       // setipchecksum.cc:86
 #if !CLK_DIAG_NO_FIELD_STORE
                     if (!DEFER)                        // else field_scatter_kernel writes it
-                        st_u16(ip + 10, stored);
+                        field_st_u16(ip + 10, stored);
 #endif
                 }
             } else {
@@ -671,6 +693,46 @@ __device__ __forceinline__ bool set_block_store_stash(uint8_t *nh, const L4State
     return true;
 }
 
+// The same, patching the stash in LDS instead of storing: returns the
+// block's address | its first stash chunk (0: not available), and the
+// packet-stream kernel stores the patched blocks coalesced
+// (CLK_STASH_COALESCE).
+#ifndef CLK_STASH_COALESCE
+#define CLK_STASH_COALESCE 0
+#endif
+#ifndef CLK_STASH_NT
+#define CLK_STASH_NT 0
+#endif
+template <int PROTO, int HC>
+__device__ __forceinline__ uint64_t set_block_patch_stash(uint8_t *nh, const L4State &st, uint32_t r, uint64_t c0,
+                                                          u32x4 (&hs)[HC])
+{
+    constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
+    const uint64_t a = (uint64_t)nh, fa = a + st.hl + FIELD, xa = a + st.hl + 12;
+    const uint64_t blk = fa & ~63ull;
+    if (!(blk >= a && blk + 64 <= a + st.caplen && fa + 1 < blk + 64))
+        return 0;
+    const uint32_t q0 = (uint32_t)(blk - c0) >> 4;
+    if (q0 + 4 > (uint32_t)HC)
+        return 0;
+    const bool fix_in = st.fix && xa >= blk && xa < blk + 64;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; q++) {
+        const uint64_t ca = blk + 16ull * q;
+        if (fa - ca < 16 || fa + 1 - ca < 16 || (fix_in && xa - ca < 16)) {
+            u32x4 w = hs[q0 + q];
+            patch_byte(w, ca, fa, r);
+            patch_byte(w, ca, fa + 1, r >> 8);
+            if (fix_in)
+                patch_byte(w, ca, xa, st.new_b12);
+            hs[q0 + q] = w;
+        }
+    }
+    if (st.fix && !fix_in)
+        nh[st.hl + 12] = (uint8_t)st.new_b12;
+    return blk | q0;
+}
+
 // A packet's outputs: status code, two-phase work word, Set checksum.
 struct L4Out {
     uint32_t code, work, sum;
@@ -737,7 +799,7 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
 // (same addresses across the group: one request per wave instruction), so
 // one memory round trip serves the parse and the sum.
 #ifndef CLK_L4_WPE_SET
-#define CLK_L4_WPE_SET 5     // UDP Set l4_kernels: 5 waves/SIMD (C3 -4 %); TCP Set keeps 4 (C5 +0.6 % at 5)
+#define CLK_L4_WPE_SET 4     // UDP Set l4_kernels: 4 waves/SIMD, as the Check run loop (C3 Set 4.60 vs 4.65 ms at 5)
 #endif
 #ifndef CLK_L4_WPE_CHECK
 #define CLK_L4_WPE_CHECK 4   // 4 waves/SIMD: the run loop spills at 5 (C3 Check 4.14 vs 3.81 ms)
@@ -1036,7 +1098,7 @@ __device__ __forceinline__ uint32_t chunk_outside(const u32x4 V, uint64_t ca, ui
 template <int PROTO, bool SET, bool DEFER, int KV, bool PF, bool MARKS>
 __global__ void __launch_bounds__(256)
 #if CLK_SWPE
-__attribute__((amdgpu_waves_per_eu(SET && CLK_SET_REGBLK && CLK_SWPE > 6 ? 6 : PROTO == TCP && CLK_SWPE > 7 ? 7 : CLK_SWPE)))
+__attribute__((amdgpu_waves_per_eu(SET && !DEFER && CLK_SET_REGBLK && CLK_SWPE > 6 ? 6 : PROTO == TCP && CLK_SWPE > 7 ? 7 : CLK_SWPE)))
 #endif
 l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                         uint16_t *out_sum, uint32_t *work)
@@ -1045,9 +1107,11 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
     // stashed head chunks: every header dword when (nh&~3) - c0 + 4*HDR_DW <= 16*HC
     // (always for HC = 4 / 3; for 16 B-aligned packets with 3 / 2), else
     // the parse loads the missing dwords itself
-    // A Set stashes 4 (the field's 64 B block, stored whole from the stash).
+    // A fused Set stashes 4 (the field's 64 B block, stored whole from the
+    // stash); the two-phase compute pass stores nothing and needs no more.
     constexpr int HC0 = PROTO == TCP ? 3 + CLK_SHC_EXTRA : 2 + CLK_SHC_EXTRA;
-    constexpr int HC = SET && CLK_SET_REGBLK && HC0 < 4 ? 4 : HC0;
+    constexpr int HC = SET && !DEFER && CLK_SET_REGBLK && HC0 < 4 ? 4 : HC0;
+    constexpr bool COAL = SET && !DEFER && CLK_SET_REGBLK && CLK_STASH_COALESCE;
     __shared__ u32x4 head[4][64][HC];
     __shared__ u32x4 tail[4][64];
     __shared__ u32x4 pk[4][64];       // {c0 lo, c0 hi, chunk start, nch | odd << 31}
@@ -1230,6 +1294,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint64_t blk_q0 = 0;         // COAL: the patched block's address | its first stash chunk
         if (live) {
             const uint32_t *hw = (const uint32_t *)&head[wv][lane][0];
             const uint32_t q0 = (uint32_t)((a & ~3ull) - c0) >> 2;   // first header dword in the stash
@@ -1261,13 +1326,42 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                     sum = lane_range_sum(s, rlen);
                 }
             }
-            if (SET && !DEFER && CLK_SET_REGBLK)
+            if (COAL)
+                l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work, [&](uint32_t r) {
+                    blk_q0 = set_block_patch_stash<PROTO, HC>(nh, st, r, c0, head[wv][lane]);
+                    if (!blk_q0)
+                        set_field_store<PROTO>(nh, st, r, 0, 1, true);
+                });
+            else if (SET && !DEFER && CLK_SET_REGBLK)
                 l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work, [&](uint32_t r) {
                     if (!set_block_store_stash<PROTO, HC>(nh, st, r, c0, head[wv][lane]))
                         set_field_store<PROTO>(nh, st, r, 0, 1, true);
                 });
             else
                 l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work);
+        }
+        if (COAL) {
+            // the patched blocks leave by 4 store instructions, each writing
+            // 16 whole blocks: lanes 4p'..4p'+3 store quarters 0..3 of packet
+            // 16 s + p' (a full 64 B write per 4 lanes)
+            pk[wv][lane] = u32x4{(uint32_t)blk_q0, (uint32_t)(blk_q0 >> 32), 0, 0};
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (uint32_t s4 = 0; s4 < 4; s4++) {
+                const uint32_t p = 16 * s4 + (lane >> 2), q = lane & 3;
+                const u32x4 P = pk[wv][p];
+                const uint64_t bq = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
+                if (bq) {
+                    const uint64_t ca = (bq & ~63ull) + 16ull * q;
+                    const u32x4 w = head[wv][p][(bq & 63) + q];
+                    if (CLK_STASH_NT)
+                        __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x4 *)ca);
+                    else
+                        *(__attribute__((address_space(1))) u32x4 *)ca = w;
+                }
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -1296,10 +1390,10 @@ __global__ void __launch_bounds__(256) dec_ttl_kernel(BatchArgs b, int multicast
                     const uint32_t s = (~(uint32_t)bswap16(w >> 16) & 0xFFFF) + 0xFEFF;
                     stored = ~(uint32_t)bswap16((s + (s >> 16)) & 0xFFFF) & 0xFFFF;
                     if (((uint64_t)ip & 3) == 0) {
-                        *(uint32_t *)(ip + 8) = (ttl - 1) | (w & 0xFF00) | (stored << 16);
+                        field_st_u32(ip + 8, (ttl - 1) | (w & 0xFF00) | (stored << 16));
                     } else {
                         ip[8] = (uint8_t)(ttl - 1);
-                        st_u16(ip + 10, stored);
+                        field_st_u16(ip + 10, stored);
                     }
                     code = OK;
                 }
@@ -1562,6 +1656,22 @@ __global__ void __launch_bounds__(256) ip_out_kernel(BatchArgs b, IpOutArgs c, u
 // FIELD_BASE: 10 for ip_sum (work = 0x80000000 | value), or the transport
 // field offset (6 / 16) added to the hl packed in work bits 16..23.
 // ---------------------------------------------------------------------------
+#ifndef CLK_SCATTER_ST
+#define CLK_SCATTER_ST 1   // field stores: 0 plain, 1 nontemporal (default), 2 sc0 sc1, 3 sc0 sc1 nt
+#endif
+__device__ __forceinline__ void scatter_st_u16(uint8_t *p, uint32_t v)
+{
+    if (CLK_SCATTER_ST == 0 || ((uint64_t)p & 1)) {
+        st_u16(p, v);
+    } else if (CLK_SCATTER_ST == 1) {
+        __builtin_nontemporal_store((uint16_t)v, (__attribute__((address_space(1))) uint16_t *)p);
+    } else if (CLK_SCATTER_ST == 2) {
+        asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"((uint64_t)p), "v"(v) : "memory");
+    } else {
+        asm volatile("global_store_short %0, %1, off sc0 sc1 nt" ::"v"((uint64_t)p), "v"(v) : "memory");
+    }
+}
+
 template <int FIELD_BASE, bool L4>
 __global__ void __launch_bounds__(256) field_scatter_kernel(BatchArgs b, const uint32_t *work,
                                                             const uint8_t *status, const uint16_t *sums,
@@ -1576,12 +1686,12 @@ __global__ void __launch_bounds__(256) field_scatter_kernel(BatchArgs b, const u
         if (L4) {
             const uint32_t w = work[i];
             if (w & 0x80000000u)
-                st_u16(b.base + pkt_off(b, i) + ((w >> 16) & 0xFF) + FIELD_BASE, w & 0xFFFF);
+                scatter_st_u16(b.base + pkt_off(b, i) + ((w >> 16) & 0xFF) + FIELD_BASE, w & 0xFFFF);
             out_code[i] = (w & 0x80000000u) ? 0 : (uint8_t)w;
             if (out_sum)
                 out_sum[i] = (w & 0x80000000u) ? (uint16_t)w : 0;
         } else if (status[i] == 0) {
-            st_u16(b.base + pkt_off(b, i) + FIELD_BASE, sums[i]);
+            scatter_st_u16(b.base + pkt_off(b, i) + FIELD_BASE, sums[i]);
         }
     }
 }

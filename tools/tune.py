@@ -118,6 +118,18 @@ VARIANTS = {
     "k16_8": (["-DCLK_K16=8"], {}),
     "diag_nowork": (["-DCLK_DIAG_NO_WORK_STORE=1"], {}),
     "sw4": (["-DCLK_L4_WPE_SET=4"], {}),
+    "setruns16sw4": (["-DCLK_L4_RUNS_SET_G=16", "-DCLK_L4_WPE_SET=4"], {}),
+    "scnt": (["-DCLK_SCATTER_ST=1"], {}),
+    "scst0": (["-DCLK_SCATTER_ST=0"], {}),
+    "fieldnt": (["-DCLK_FIELD_NT=1"], {}),
+    "scoal": (["-DCLK_STASH_COALESCE=1"], {}),
+    "scoalnt": (["-DCLK_STASH_COALESCE=1", "-DCLK_STASH_NT=1"], {}),
+    "r32": (["-DCLK_L4_RUNS_SET_G=32"], {}),
+    "two_stream_scst0": (["-DCLK_SCATTER_ST=0"], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
+    "scsc": (["-DCLK_SCATTER_ST=2"], {}),
+    "scscnt": (["-DCLK_SCATTER_ST=3"], {}),
+    "r16scnt": (["-DCLK_L4_RUNS_SET_G=16", "-DCLK_SCATTER_ST=1"], {}),
+    "r16scsc": (["-DCLK_L4_RUNS_SET_G=16", "-DCLK_SCATTER_ST=2"], {}),
 }
 
 
@@ -192,6 +204,7 @@ def main():
                 "CheckUDPHeader": lambda c: c.check_udp_header(b, out=status),
                 "CheckTCPHeader": lambda c: c.check_tcp_header(b, out=status),
                 "CheckIPHeader": lambda c: c.check_ip_header(b, out=status),
+                "DecIPTTL": lambda c: c.dec_ip_ttl(b, status=status, want_sums=False),
                 "InCksum": lambda c: c.in_cksum(b, out=sums16),
                 "IPFragmenter": lambda c: frag(c)}
     if os.environ.get("TUNE_ELEMENT") == "IPFragmenter":       # C3 to MTU 576; headers restored per call
