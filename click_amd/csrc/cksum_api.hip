@@ -355,9 +355,13 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
         ctx->diag_primed = true;
     if (work && ctx->diag_phase != 1) {
         constexpr int FIELD = PROTO == clk::UDP ? 6 : 16;
-        hipLaunchKernelGGL((clk::field_scatter_kernel<FIELD, true>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
-                           ctx->cur, args_of(b), (const uint32_t *)work, (const uint8_t *)nullptr,
-                           (const uint16_t *)nullptr, code, sum);
+        if (CLK_SCATTER_BLOCK)
+            hipLaunchKernelGGL((clk::field_scatter_block_kernel<FIELD>), dim3(grid_for(ctx, 4 * b->n)), dim3(BLOCK), 0,
+                               ctx->cur, args_of(b), (const uint32_t *)work, code, sum);
+        else
+            hipLaunchKernelGGL((clk::field_scatter_kernel<FIELD, true>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
+                               ctx->cur, args_of(b), (const uint32_t *)work, (const uint8_t *)nullptr,
+                               (const uint16_t *)nullptr, code, sum);
     }
     return check_launch(ctx, fn);
 }

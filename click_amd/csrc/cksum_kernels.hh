@@ -698,10 +698,10 @@ __device__ __forceinline__ bool set_block_store_stash(uint8_t *nh, const L4State
 // packet-stream kernel stores the patched blocks coalesced
 // (CLK_STASH_COALESCE).
 #ifndef CLK_STASH_COALESCE
-#define CLK_STASH_COALESCE 0
+#define CLK_STASH_COALESCE 1   // C4 Set 6.10 ms with nontemporal stores, 6.72 plain, 6.65 per-lane blocks
 #endif
 #ifndef CLK_STASH_NT
-#define CLK_STASH_NT 0
+#define CLK_STASH_NT 1         // full 64 B nontemporal writes: no read-modify-write, nothing left dirty
 #endif
 template <int PROTO, int HC>
 __device__ __forceinline__ uint64_t set_block_patch_stash(uint8_t *nh, const L4State &st, uint32_t r, uint64_t c0,
@@ -1669,6 +1669,42 @@ __device__ __forceinline__ void scatter_st_u16(uint8_t *p, uint32_t v)
         asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"((uint64_t)p), "v"(v) : "memory");
     } else {
         asm volatile("global_store_short %0, %1, off sc0 sc1 nt" ::"v"((uint64_t)p), "v"(v) : "memory");
+    }
+}
+
+// CLK_SCATTER_BLOCK (tuning): 4 lanes per packet read the field's 64 B
+// block, patch it and store it whole, nontemporal -- one full-block write
+// per field instead of a read-modify-write at the memory controller.
+#ifndef CLK_SCATTER_BLOCK
+#define CLK_SCATTER_BLOCK 0
+#endif
+template <int FIELD>
+__global__ void __launch_bounds__(256) field_scatter_block_kernel(BatchArgs b, const uint32_t *work,
+                                                                  uint8_t *out_code, uint16_t *out_sum)
+{
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < 4 * b.n; j += nthreads) {
+        const uint64_t i = j >> 2;
+        const uint32_t q = (uint32_t)j & 3;
+        const uint32_t w = work[i];
+        if (w & 0x80000000u) {
+            uint8_t *nh = b.base + pkt_off(b, i);
+            const uint64_t a = (uint64_t)nh, fa = a + ((w >> 16) & 0xFF) + FIELD, blk = fa & ~63ull;
+            if (blk >= a && blk + 64 <= a + pkt_len(b, i) && fa + 1 < blk + 64) {
+                const uint64_t ca = blk + 16ull * q;
+                u32x4 v = gload16(ca);
+                patch_byte(v, ca, fa, w);
+                patch_byte(v, ca, fa + 1, w >> 8);
+                __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *)ca);
+            } else if (q == 0) {
+                scatter_st_u16(nh + ((w >> 16) & 0xFF) + FIELD, w & 0xFFFF);
+            }
+        }
+        if (q == 0) {
+            out_code[i] = (w & 0x80000000u) ? 0 : (uint8_t)w;
+            if (out_sum)
+                out_sum[i] = (w & 0x80000000u) ? (uint16_t)w : 0;
+        }
     }
 }
 

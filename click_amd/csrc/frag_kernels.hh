@@ -235,6 +235,12 @@ __device__ __forceinline__ u32x4 load16_guarded(uint64_t p, uint64_t hi)
 #ifndef CLK_FRAG_UA
 #define CLK_FRAG_UA 1
 #endif
+#ifndef CLK_FRAG_HDR16
+#define CLK_FRAG_HDR16 1    // prologue: the rewritten first-fragment header as one 16 B store
+#endif
+#ifndef CLK_FRAG_HDR_NT
+#define CLK_FRAG_HDR_NT 0   // ... nontemporal (tuning knob)
+#endif
 #ifndef CLK_FRAG_NT_STORE
 #define CLK_FRAG_NT_STORE 0
 #endif
@@ -432,10 +438,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
                     for (int d = 0; d < 5; d++)
                         sum += (h[d] & 0xFFFF) + (h[d] >> 16);
                     const uint32_t ck = in_cksum_fold(sum);
-                    st_u16(ip + 2, h[0] >> 16);
-                    st_u16(ip + 4, h[1] & 0xFFFF);
-                    st_u16(ip + 6, h[1] >> 16);
-                    st_u16(ip + 10, ck);
+                    if (CLK_FRAG_HDR16 && ((uint64_t)ip & 3) == 0) {
+                        // one 16 B store of bytes [0, 16) (ip_src rewritten
+                        // unchanged): one partial-block write instead of four
+                        const u32x4 w = {h[0], h[1], h[2] | (ck << 16), h[3]};
+                        typedef __attribute__((address_space(1))) u32x4_a4 g4;
+                        if (CLK_FRAG_HDR_NT)
+                            __builtin_nontemporal_store(w, (g4 *)ip);
+                        else
+                            *(g4 *)ip = w;
+                    } else {
+                        st_u16(ip + 2, h[0] >> 16);
+                        st_u16(ip + 4, h[1] & 0xFFFF);
+                        st_u16(ip + 6, h[1] >> 16);
+                        st_u16(ip + 10, ck);
+                    }
                 }
             }
             tn += vn[k];

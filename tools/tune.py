@@ -123,6 +123,9 @@ VARIANTS = {
     "scst0": (["-DCLK_SCATTER_ST=0"], {}),
     "fieldnt": (["-DCLK_FIELD_NT=1"], {}),
     "scoal": (["-DCLK_STASH_COALESCE=1"], {}),
+    "fh4": (["-DCLK_FRAG_HDR16=0"], {}),
+    "scblk": (["-DCLK_SCATTER_BLOCK=1"], {}),
+    "fhnt": (["-DCLK_FRAG_HDR_NT=1"], {}),
     "scoalnt": (["-DCLK_STASH_COALESCE=1", "-DCLK_STASH_NT=1"], {}),
     "r32": (["-DCLK_L4_RUNS_SET_G=32"], {}),
     "two_stream_scst0": (["-DCLK_SCATTER_ST=0"], {"CLK_SET_MODE": "1", "CLK_VARLEN": "2"}),
