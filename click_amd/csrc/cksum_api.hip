@@ -139,7 +139,10 @@ constexpr int k_for(int G) { return G == 16 ? CLK_K16 : K; }
 #define CLK_VU 1           // sub-passes whose loads are issued together
 #endif
 #ifndef CLK_SKV
-#define CLK_SKV 2          // chunks per lane per pass of the packet-stream kernel
+#define CLK_SKV 2          // chunks per lane per pass of the packet-stream kernel (Set)
+#endif
+#ifndef CLK_SKV_CHECK
+#define CLK_SKV_CHECK 3    // ... Check, at CLK_SWPE_CHECK waves per SIMD (C4 Check 4.01 vs 4.08 ms with 2 at 8)
 #endif
 #ifndef CLK_SPF
 #define CLK_SPF 0          // packet-stream kernel: prefetch the next pass (tuning knob)
@@ -309,7 +312,7 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
     if (work && ctx->diag_phase == 2 && ctx->diag_primed) {
         // diagnostics: scatter only
     } else if (bins && ctx->varlen == 2) {
-        constexpr int KV = CLK_SKV;
+        constexpr int KV = SET ? CLK_SKV : CLK_SKV_CHECK;
         uint64_t blocks = (b->n + 255) / 256;            // 4 waves x 64 packets per block
         if (blocks > (uint64_t)ctx->max_blocks)
             blocks = (uint64_t)ctx->max_blocks;

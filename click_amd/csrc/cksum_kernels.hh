@@ -27,6 +27,9 @@
 #ifndef CLK_SWPE
 #define CLK_SWPE 8         // packet-stream kernel: request this many waves per SIMD (TCP: at most 7, its 3 stashed head chunks)
 #endif
+#ifndef CLK_SWPE_CHECK
+#define CLK_SWPE_CHECK 6   // ... the Check kernels, with 3 chunks per lane per pass (CLK_SKV_CHECK)
+#endif
 #ifndef CLK_BLOCK_WRITE
 #define CLK_BLOCK_WRITE 0  // tuning knob: fused Set stores rewrite the whole 64 B block (measured slower)
 #endif
@@ -801,6 +804,9 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
 #ifndef CLK_L4_WPE_SET
 #define CLK_L4_WPE_SET 4     // UDP Set l4_kernels: 4 waves/SIMD, as the Check run loop (C3 Set 4.60 vs 4.65 ms at 5)
 #endif
+#ifndef CLK_SET_OCC_PAD
+#define CLK_SET_OCC_PAD 28672   // two-phase compute pass (runs): LDS caps it at 5 waves/SIMD (C3 3.75 vs 3.83 ms at 6)
+#endif
 #ifndef CLK_L4_WPE_CHECK
 #define CLK_L4_WPE_CHECK 4   // 4 waves/SIMD: the run loop spills at 5 (C3 Check 4.14 vs 3.81 ms)
 #endif
@@ -854,6 +860,12 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         // tools/probes/stash_probe.hip).  The two-phase Set parses its
         // header from loads of its own here (measured faster in runs).
         constexpr uint32_t PPB = 256 / G, RB = PPB < 64 ? 64 : PPB;
+#if CLK_SET_OCC_PAD
+        // tuning: LDS padding caps the two-phase compute pass's occupancy
+        __shared__ uint8_t occ_pad[SET && DEFER ? CLK_SET_OCC_PAD : 1];
+        if (b.n == ~0ull)
+            occ_pad[threadIdx.x] = 1;
+#endif
         __shared__ uint8_t r_code[SET && DEFER ? 1 : RB];
         __shared__ uint32_t r_work[SET && DEFER ? RB : 1];
         __shared__ uint16_t r_sum[SET && !DEFER ? RB : 1];
@@ -1098,7 +1110,7 @@ __device__ __forceinline__ uint32_t chunk_outside(const u32x4 V, uint64_t ca, ui
 template <int PROTO, bool SET, bool DEFER, int KV, bool PF, bool MARKS>
 __global__ void __launch_bounds__(256)
 #if CLK_SWPE
-__attribute__((amdgpu_waves_per_eu(SET && !DEFER && CLK_SET_REGBLK && CLK_SWPE > 6 ? 6 : PROTO == TCP && CLK_SWPE > 7 ? 7 : CLK_SWPE)))
+__attribute__((amdgpu_waves_per_eu(!SET ? CLK_SWPE_CHECK : SET && !DEFER && CLK_SET_REGBLK && CLK_SWPE > 6 ? 6 : PROTO == TCP && CLK_SWPE > 7 ? 7 : CLK_SWPE)))
 #endif
 l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                                                         uint16_t *out_sum, uint32_t *work)

@@ -125,6 +125,13 @@ VARIANTS = {
     "scoal": (["-DCLK_STASH_COALESCE=1"], {}),
     "fh4": (["-DCLK_FRAG_HDR16=0"], {}),
     "scblk": (["-DCLK_SCATTER_BLOCK=1"], {}),
+    "occ5": (["-DCLK_SET_OCC_PAD=28672"], {}),
+    "occ6": (["-DCLK_SET_OCC_PAD=0"], {}),
+    "skv4w5": (["-DCLK_SKV=4", "-DCLK_SWPE=5"], {}),
+    "skv4w6": (["-DCLK_SKV=4", "-DCLK_SWPE=6"], {}),
+    "skv3w6": (["-DCLK_SKV=3", "-DCLK_SWPE=6"], {}),
+    "skv8w4": (["-DCLK_SKV=8", "-DCLK_SWPE=4"], {}),
+    "occ4": (["-DCLK_SET_OCC_PAD=36864"], {}),
     "fhnt": (["-DCLK_FRAG_HDR_NT=1"], {}),
     "scoalnt": (["-DCLK_STASH_COALESCE=1", "-DCLK_STASH_NT=1"], {}),
     "r32": (["-DCLK_L4_RUNS_SET_G=32"], {}),
