@@ -574,7 +574,7 @@ int clk_check_ip_header(clk_ctx *ctx, const clk_batch *b, const clk_ip_check_cfg
         return fail(ctx, CLK_EINVAL, "clk_check_ip_header: null address list");
     if (b->n == 0) return CLK_SUCCESS;
     if (!out_verdict) return fail(ctx, CLK_EINVAL, "clk_check_ip_header: null output");
-    const unsigned grid = grid_for(ctx, b->n);
+    const unsigned grid = grid_for(ctx, (CLK_IPH_PAIR ? 2 : 1) * b->n);
     if (cfg->checksum)
         hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
                            args_of(b), cfg->offset, cfg->badsrc, cfg->nbadsrc, cfg->gooddst, cfg->ngooddst,

@@ -34,6 +34,9 @@ VARIANTS = {
     "fusednt": (["-DCLK_NT_LOADS=1"], {"CLK_SET_MODE": "0"}),
     "two": ([], {"CLK_SET_MODE": "1"}),
     "mb8k": ([], {"CLK_MAX_BLOCKS": "8192"}),
+    "mb16k": ([], {"CLK_MAX_BLOCKS": "16384"}),
+    "mb32k": ([], {"CLK_MAX_BLOCKS": "32768"}),
+    "iphpair": (["-DCLK_IPH_PAIR=1"], {}),
     "mb64k": ([], {"CLK_MAX_BLOCKS": "65536"}),
     "mb1m": ([], {"CLK_MAX_BLOCKS": "1048576"}),
     "diag_nofield": (["-DCLK_DIAG_NO_FIELD_STORE=1"], {}),
