@@ -27,6 +27,9 @@
 #ifndef CLK_SWPE
 #define CLK_SWPE 8         // packet-stream kernel: request this many waves per SIMD (TCP: at most 7, its 3 stashed head chunks)
 #endif
+#ifndef CLK_STREAM_NT_CHECK
+#define CLK_STREAM_NT_CHECK 0   // packet-stream Check: nontemporal chunk loads (tuning knob)
+#endif
 #ifndef CLK_SWPE_CHECK
 #define CLK_SWPE_CHECK 6   // ... the Check kernels, with 3 chunks per lane per pass (CLK_SKV_CHECK)
 #endif
@@ -1253,7 +1256,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                 const uint32_t r = c - P[2];
                 inf[k] = r | (r == (P[3] & 0x7FFFFFFFu) - 1 ? 1u << 30 : 0u) | (P[3] & 0x80000000u);
                 const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
-                if (UseNT<false>::value)
+                if (UseNT<CLK_STREAM_NT_CHECK && !SET>::value)
                     v[k] = c < total ? __builtin_nontemporal_load((const u32x4 *)(cf + 16ull * (c - P[2])))
                                      : u32x4{0, 0, 0, 0};
                 else

@@ -37,6 +37,9 @@ VARIANTS = {
     "mb16k": ([], {"CLK_MAX_BLOCKS": "16384"}),
     "mb32k": ([], {"CLK_MAX_BLOCKS": "32768"}),
     "iphpair": (["-DCLK_IPH_PAIR=1"], {}),
+    "sntc": (["-DCLK_STREAM_NT_CHECK=1"], {}),
+    "ck3w7": (["-DCLK_SKV_CHECK=3", "-DCLK_SWPE_CHECK=7"], {}),
+    "ck3w5": (["-DCLK_SKV_CHECK=3", "-DCLK_SWPE_CHECK=5"], {}),
     "mb64k": ([], {"CLK_MAX_BLOCKS": "65536"}),
     "mb1m": ([], {"CLK_MAX_BLOCKS": "1048576"}),
     "diag_nofield": (["-DCLK_DIAG_NO_FIELD_STORE=1"], {}),
