@@ -143,6 +143,8 @@ def make_batch(rng, n, proto, max_total=1600, opt_frac=0.2, mutate_frac=0.5, tin
                 pos += int(rng.integers(0, 16))
             elif align == "even":
                 pos += 2 * int(rng.integers(0, 8))
+            elif align == 64:                  # 64 B-aligned packet starts (the benches' layouts)
+                pos = (pos + 63) // 64 * 64
             off[i] = pos
             pos += len(p) + int(rng.integers(0, 24))
         size = pos + 64

@@ -335,6 +335,29 @@ def test_set_modes_bit_exact(torch, mode, monkeypatch):
     c.close()
 
 
+@pytest.mark.parametrize("mode", ["0", "1"])
+def test_stream_set_modes_bit_exact(torch, mode, monkeypatch):
+    """The packet-stream kernel's Sets: fused (mode 0: the patched 64 B
+    blocks stored coalesced from the LDS stash, or the field alone when its
+    block is not the packet's) and two-phase (mode 1: the compute pass
+    stashes fewer chunks, then the nontemporal scatter), any alignment,
+    FIXOFF on and off."""
+    import click_amd
+    monkeypatch.setenv("CLK_SET_MODE", mode)
+    monkeypatch.setenv("CLK_BIN_MIN", "1")
+    monkeypatch.setenv("CLK_VARLEN", "2")
+    c = click_amd.Context(0)
+    rng = np.random.default_rng(57 + int(mode))
+    for proto, mt in ((17, 1600), (6, 1600), (17, 200), (6, 9000)):
+        for align in ("any", 64):
+            arena, off, caplen, ml = fuzz.make_batch(rng, 1500, proto, max_total=mt, align=align)
+            op = OPS_L4[proto][1]
+            compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=1)
+            if proto == 6:
+                compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=0)
+    c.close()
+
+
 @pytest.mark.parametrize("bin_min,varlen", [("1", "2"), ("1", "1"), ("1", "0"), ("100000000", "1")])
 def test_size_class_partition_bit_exact(torch, bin_min, varlen, monkeypatch):
     """Variable-length batches run by the packet-stream kernel (varlen 2),
