@@ -830,6 +830,9 @@ __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum,
 #ifndef CLK_SET_OCC_PAD
 #define CLK_SET_OCC_PAD 28672   // two-phase compute pass (runs): LDS caps it at 5 waves/SIMD (C3 3.75 vs 3.83 ms at 6)
 #endif
+#ifndef CLK_SET_OCC_PAD64
+#define CLK_SET_OCC_PAD64 28672 // ... for 64-lane groups (C5)
+#endif
 #ifndef CLK_L4_WPE_CHECK
 #define CLK_L4_WPE_CHECK 4   // 4 waves/SIMD: the run loop spills at 5 (C3 Check 4.14 vs 3.81 ms)
 #endif
@@ -885,7 +888,7 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         constexpr uint32_t PPB = 256 / G, RB = PPB < 64 ? 64 : PPB;
 #if CLK_SET_OCC_PAD
         // tuning: LDS padding caps the two-phase compute pass's occupancy
-        __shared__ uint8_t occ_pad[SET && DEFER ? CLK_SET_OCC_PAD : 1];
+        __shared__ uint8_t occ_pad[SET && DEFER ? (G == 64 ? CLK_SET_OCC_PAD64 : CLK_SET_OCC_PAD) : 1];
         if (b.n == ~0ull)
             occ_pad[threadIdx.x] = 1;
 #endif

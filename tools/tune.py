@@ -138,6 +138,8 @@ VARIANTS = {
     "skv3w6": (["-DCLK_SKV=3", "-DCLK_SWPE=6"], {}),
     "skv8w4": (["-DCLK_SKV=8", "-DCLK_SWPE=4"], {}),
     "occ4": (["-DCLK_SET_OCC_PAD=36864"], {}),
+    "occ64_4": (["-DCLK_SET_OCC_PAD64=36864"], {}),
+    "occ64_3": (["-DCLK_SET_OCC_PAD64=49152"], {}),
     "fhnt": (["-DCLK_FRAG_HDR_NT=1"], {}),
     "scoalnt": (["-DCLK_STASH_COALESCE=1", "-DCLK_STASH_NT=1"], {}),
     "r32": (["-DCLK_L4_RUNS_SET_G=32"], {}),
