@@ -22,6 +22,8 @@ struct clk_ctx {
     int max_blocks;    // grid cap (tuning: CLK_MAX_BLOCKS)
     int force_group;   // lanes per packet override (tuning: CLK_FORCE_GROUP)
     int set_mode;      // -1 auto; 0: Set kernels store the field; 1: two-phase (CLK_SET_MODE)
+    int scatter_blocks; // grid cap of field_scatter_kernel (CLK_SCATTER_BLOCKS): fewer, longer-lived
+                        // waves (C3 scatter 0.57 vs 0.67 ms at 16K vs 64K blocks)
     int diag_phase;    // diagnostics only (CLK_DIAG_SET_PHASE): two-phase Set runs 1 its compute pass
                        // alone, 2 its scatter alone (over the previous call's work words: the
                        // first call runs both); 0 both
@@ -362,7 +364,8 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
             hipLaunchKernelGGL((clk::field_scatter_block_kernel<FIELD>), dim3(grid_for(ctx, 4 * b->n)), dim3(BLOCK), 0,
                                ctx->cur, args_of(b), (const uint32_t *)work, code, sum);
         else
-            hipLaunchKernelGGL((clk::field_scatter_kernel<FIELD, true>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
+            hipLaunchKernelGGL((clk::field_scatter_kernel<FIELD, true>),
+                               dim3(std::min<unsigned>(grid_for(ctx, b->n), (unsigned)ctx->scatter_blocks)), dim3(BLOCK), 0,
                                ctx->cur, args_of(b), (const uint32_t *)work, (const uint8_t *)nullptr,
                                (const uint16_t *)nullptr, code, sum);
     }
@@ -429,6 +432,12 @@ int clk_ctx_create(int device, clk_ctx **out)
     c->set_mode = -1;
     if (const char *sm = std::getenv("CLK_SET_MODE"))
         c->set_mode = std::atoi(sm) == 1 ? 1 : 0;
+    c->scatter_blocks = 16384;
+    if (const char *sb = std::getenv("CLK_SCATTER_BLOCKS")) {
+        const int v = std::atoi(sb);
+        if (v > 0)
+            c->scatter_blocks = v;
+    }
     c->diag_phase = 0;
     c->diag_primed = false;
     if (const char *dp = std::getenv("CLK_DIAG_SET_PHASE"))

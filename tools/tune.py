@@ -35,6 +35,9 @@ VARIANTS = {
     "two": ([], {"CLK_SET_MODE": "1"}),
     "mb8k": ([], {"CLK_MAX_BLOCKS": "8192"}),
     "mb16k": ([], {"CLK_MAX_BLOCKS": "16384"}),
+    "sb8k": ([], {"CLK_SCATTER_BLOCKS": "8192"}),
+    "sb64k": ([], {"CLK_SCATTER_BLOCKS": "65536"}),
+    "sb4k": ([], {"CLK_SCATTER_BLOCKS": "4096"}),
     "mb32k": ([], {"CLK_MAX_BLOCKS": "32768"}),
     "iphpair": (["-DCLK_IPH_PAIR=1"], {}),
     "sntc": (["-DCLK_STREAM_NT_CHECK=1"], {}),
@@ -206,7 +209,8 @@ def main():
     ctxs = {}
     for nm in names:
         _, env = VARIANTS[nm]
-        saved = {k: os.environ.get(k) for k in ("CLK_MAX_BLOCKS", "CLK_FORCE_GROUP", "CLK_SET_MODE", "CLK_VARLEN")}
+        saved = {k: os.environ.get(k) for k in ("CLK_MAX_BLOCKS", "CLK_FORCE_GROUP", "CLK_SET_MODE", "CLK_VARLEN",
+                                                "CLK_SCATTER_BLOCKS")}
         for k in saved:
             os.environ.pop(k, None)
         os.environ.update(env)
