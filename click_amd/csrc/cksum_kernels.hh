@@ -1716,6 +1716,9 @@ __device__ __forceinline__ void scatter_st_u16(uint8_t *p, uint32_t v)
 #ifndef CLK_SCATTER_BLOCK
 #define CLK_SCATTER_BLOCK 0
 #endif
+#ifndef CLK_SCATTER_UNROLL
+#define CLK_SCATTER_UNROLL 1
+#endif
 template <int FIELD>
 __global__ void __launch_bounds__(256) field_scatter_block_kernel(BatchArgs b, const uint32_t *work,
                                                                   uint8_t *out_code, uint16_t *out_sum)
@@ -1756,6 +1759,27 @@ __global__ void __launch_bounds__(256) field_scatter_kernel(BatchArgs b, const u
     // the status codes and sums -- 64 consecutive packets per wave, so whole
     // output blocks
     const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    if (L4 && CLK_SCATTER_UNROLL > 1) {     // tuning: U work words loaded before the stores
+        constexpr int U = CLK_SCATTER_UNROLL;
+        for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < b.n; i0 += U * nthreads) {
+            uint32_t w[U];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                w[u] = i0 + u * nthreads < b.n ? work[i0 + u * nthreads] : 0u;
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t i = i0 + u * nthreads;
+                if (i < b.n) {
+                    if (w[u] & 0x80000000u)
+                        scatter_st_u16(b.base + pkt_off(b, i) + ((w[u] >> 16) & 0xFF) + FIELD_BASE, w[u] & 0xFFFF);
+                    out_code[i] = (w[u] & 0x80000000u) ? 0 : (uint8_t)w[u];
+                    if (out_sum)
+                        out_sum[i] = (w[u] & 0x80000000u) ? (uint16_t)w[u] : 0;
+                }
+            }
+        }
+        return;
+    }
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += nthreads) {
         if (L4) {
             const uint32_t w = work[i];

@@ -36,6 +36,8 @@ VARIANTS = {
     "mb8k": ([], {"CLK_MAX_BLOCKS": "8192"}),
     "mb16k": ([], {"CLK_MAX_BLOCKS": "16384"}),
     "sb8k": ([], {"CLK_SCATTER_BLOCKS": "8192"}),
+    "scu4": (["-DCLK_SCATTER_UNROLL=4"], {}),
+    "scu4sb4k": (["-DCLK_SCATTER_UNROLL=4"], {"CLK_SCATTER_BLOCKS": "4096"}),
     "sb64k": ([], {"CLK_SCATTER_BLOCKS": "65536"}),
     "sb4k": ([], {"CLK_SCATTER_BLOCKS": "4096"}),
     "mb32k": ([], {"CLK_MAX_BLOCKS": "32768"}),
