@@ -880,6 +880,9 @@ def main():
                        "parallelism": "dp%d (disjoint packet shards, no data-path collective)" % world},
             "roofline": hs["roofline"],
             "verify": hs["verify"],
+            # the library reads no environment variable; bench-side CLK_* test
+            # switches present in this run are recorded here
+            "clk_env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("CLK_")},
             "elements": {e: summarize(r, args.steps, args.workload) for e, r in main_res.items()},
         }
         if c2:

@@ -173,6 +173,14 @@ class Context:
     def reserve(self, max_packets):
         self._check(self.lib.clk_ctx_reserve(self.h, int(max_packets)))
 
+    def tune(self, **knobs):
+        """Speed-only tuning (clk_ctx_tune): max_blocks, scatter_blocks,
+        set_mode (-1 auto, 0 fused, 1 two-phase), stream_min, group.  No
+        setting changes a result."""
+        for k, v in knobs.items():
+            self._check(self.lib.clk_ctx_tune(self.h, _abi.TUNE[k], int(v)))
+        return self
+
     # -- helpers ---------------------------------------------------------------
     def _out(self, n, dtype):
         return self._torch.empty(max(n, 1), dtype=dtype, device="cuda:%d" % self.device)

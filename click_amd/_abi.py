@@ -34,6 +34,8 @@ CLK_TTL_EXPIRED = 1
 CLK_TTL_UNCHANGED = 2
 CLK_GWOPT_OK = 0
 CLK_GWOPT_ERROR = 1
+# clk_tune_knob
+TUNE = {"max_blocks": 1, "scatter_blocks": 2, "set_mode": 3, "stream_min": 4, "group": 5}
 
 
 class clk_batch(ctypes.Structure):
@@ -121,6 +123,7 @@ SIGNATURES = {
     "clk_ctx_sync": (ctypes.c_int, [_P]),
     "clk_ctx_device": (ctypes.c_int, [_P]),
     "clk_ctx_reserve": (ctypes.c_int, [_P, ctypes.c_uint64]),
+    "clk_ctx_tune": (ctypes.c_int, [_P, ctypes.c_int, ctypes.c_int64]),
     "clk_last_error": (ctypes.c_char_p, [_P]),
     "clk_in_cksum": (ctypes.c_int, [_P, _BP, _P]),
     "clk_check_ip_header": (ctypes.c_int, [_P, _BP, ctypes.POINTER(clk_ip_check_cfg), _P]),

@@ -19,20 +19,15 @@ struct clk_ctx {
     int device;
     hipStream_t own;
     hipStream_t cur;
-    int max_blocks;    // grid cap (tuning: CLK_MAX_BLOCKS)
-    int force_group;   // lanes per packet override (tuning: CLK_FORCE_GROUP)
-    int set_mode;      // -1 auto; 0: Set kernels store the field; 1: two-phase (CLK_SET_MODE)
-    int scatter_blocks; // grid cap of field_scatter_kernel (CLK_SCATTER_BLOCKS): fewer, longer-lived
-                        // waves (C3 scatter 0.57 vs 0.67 ms at 16K vs 64K blocks)
-    int diag_phase;    // diagnostics only (CLK_DIAG_SET_PHASE): two-phase Set runs 1 its compute pass
-                       // alone, 2 its scatter alone (over the previous call's work words: the
-                       // first call runs both); 0 both
-    bool diag_primed;
-    uint64_t bin_min;  // variable-length batches of >= bin_min packets run by size class (CLK_BIN_MIN)
-    int bin_grid;      // grid cap of a size-class pass (CLK_BIN_GRID)
-    int varlen;        // variable-length batches: 2 the packet-stream kernel, 1 the
-                       // wave-cooperative range kernel, 0 the size-class partition (CLK_VARLEN)
-    void *scratch;     // two-phase work array (grown on demand)
+    // speed-only tuning (clk_ctx_tune; never read from the environment):
+    // every setting gives bit-identical results
+    int max_blocks;      // grid cap
+    int force_group;     // lanes per packet of the fixed-geometry kernels (0: by max_len)
+    int set_mode;        // -1 auto; 0: Set kernels store the field; 1: two-phase
+    int scatter_blocks;  // grid cap of field_scatter_kernel: fewer, longer-lived waves
+                         // (C3 scatter 0.57 vs 0.67 ms at 16K vs 64K blocks)
+    uint64_t stream_min; // len[] batches of >= stream_min packets run by the packet-stream kernel
+    void *scratch;       // two-phase work array (grown on demand)
     size_t scratch_bytes;
     uint32_t *dev_flags;   // device word kernels report internal faults in (fragmenter look-back timeout)
     bool check_flags;      // a launch since the last clk_ctx_sync may have set dev_flags
@@ -118,8 +113,6 @@ clk::BatchArgs args_of(const clk_batch *b)
     a.len = b->len;
     a.fixed_len = b->fixed_len;
     a.n = b->n;
-    a.perm = nullptr;
-    a.range = nullptr;
     return a;
 }
 
@@ -134,23 +127,11 @@ constexpr int K = CLK_K;   // 16-byte chunk loads in flight per lane per pass
 // l4_kernel's loads per lane and pass at G lanes per packet.  pick_group
 // sizes G by K; a G = 16 packet past 16 * CLK_K16 chunks takes two passes.
 constexpr int k_for(int G) { return G == 16 ? CLK_K16 : K; }
-#ifndef CLK_KV
-#define CLK_KV 2           // chunks per lane per sub-pass of the variable-length kernel
-#endif
-#ifndef CLK_VU
-#define CLK_VU 1           // sub-passes whose loads are issued together
-#endif
 #ifndef CLK_SKV
 #define CLK_SKV 2          // chunks per lane per pass of the packet-stream kernel (Set)
 #endif
 #ifndef CLK_SKV_CHECK
 #define CLK_SKV_CHECK 3    // ... Check, at CLK_SWPE_CHECK waves per SIMD (C4 Check 4.01 vs 4.08 ms with 2 at 8)
-#endif
-#ifndef CLK_SPF
-#define CLK_SPF 0          // packet-stream kernel: prefetch the next pass (tuning knob)
-#endif
-#ifndef CLK_SMARK
-#define CLK_SMARK 0        // packet-stream kernel: chunk->packet by marks + wave max-scan (tuning knob)
 #endif
 
 // Lanes per packet: the fewest (of 1, 4, 16, 64) whose K-deep pass covers
@@ -177,63 +158,18 @@ unsigned grid_for(const clk_ctx *ctx, uint64_t threads)
     return g ? (unsigned)g : 1u;
 }
 
-// Scratch layout for n packets: [work u32 x n][perm u32 x n][counts u32 x
-// NCLASS x nblocks][range u64 x 2 x NCLASS].
-struct ScratchLayout {
-    size_t work, perm, counts, range, bytes;
-    uint32_t nblocks;
-};
-ScratchLayout scratch_layout(uint64_t n)
-{
-    ScratchLayout L;
-    L.nblocks = (uint32_t)((n + clk::BIN_TILE - 1) / clk::BIN_TILE);
-    L.work = 0;
-    L.perm = (n * 4 + 255) & ~size_t(255);
-    L.counts = L.perm + ((n * 4 + 255) & ~size_t(255));
-    L.range = L.counts + (((size_t)clk::NCLASS * L.nblocks * 4 + 255) & ~size_t(255));
-    L.bytes = L.range + 2 * clk::NCLASS * 8;
-    return L;
-}
+// Scratch for n packets: the two-phase Set's work words (u32 x n).
+size_t work_bytes(uint64_t n) { return (n * 4 + 255) & ~size_t(255); }
 
-// Host mirror of clk::size_class (lanes per packet G = 1 << class).
-int size_class_host(uint32_t len)
+bool use_stream(const clk_ctx *ctx, const clk_batch *b)
 {
-    const uint64_t nch = (uint64_t)len / 16 + 2;
-    int c = 0;
-    while (c < clk::NCLASS - 1 && nch > ((uint64_t)K << c))
-        c++;
-    return c;
-}
-
-bool use_bins(const clk_ctx *ctx, const clk_batch *b)
-{
-    return b->len && !ctx->force_group && b->n >= ctx->bin_min && b->n < (1ull << 32);
-}
-
-// Partition the batch by size class into the scratch (count, scan, scatter).
-int bin_batch(clk_ctx *ctx, const clk_batch *b, const ScratchLayout &L)
-{
-    uint8_t *sc = (uint8_t *)ctx->scratch;
-    uint32_t *counts = (uint32_t *)(sc + L.counts);
-    hipLaunchKernelGGL((clk::bin_count_kernel<K>), dim3(L.nblocks), dim3(BLOCK), 0, ctx->cur, b->len, b->n, counts,
-                       L.nblocks);
-    hipLaunchKernelGGL(clk::bin_scan_kernel, dim3(1), dim3(1024), 0, ctx->cur, counts, L.nblocks,
-                       (uint64_t *)(sc + L.range), b->n);
-    hipLaunchKernelGGL((clk::bin_scatter_kernel<K>), dim3(L.nblocks), dim3(BLOCK), 0, ctx->cur, b->len, b->n,
-                       (const uint32_t *)counts, L.nblocks, (uint32_t *)(sc + L.perm));
-    return CLK_SUCCESS;
-}
-
-// Classes that can be non-empty: 0 .. class of max_len (all when unknown).
-int max_class(const clk_batch *b)
-{
-    return b->max_len ? size_class_host(b->max_len) : clk::NCLASS - 1;
+    return b->len && !ctx->force_group && b->n >= ctx->stream_min;
 }
 
 template <int G>
 void launch_range(clk_ctx *ctx, const clk::BatchArgs &a, unsigned grid, uint16_t *out)
 {
-    if (CLK_L4_RUNS && !a.perm)      // runs per workgroup, as l4_kernel
+    if (CLK_L4_RUNS)                 // runs per workgroup, as l4_kernel
         hipLaunchKernelGGL((clk::range_kernel<G, k_for(G), true>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a, out);
     else
         hipLaunchKernelGGL((clk::range_kernel<G, k_for(G), false>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a, out);
@@ -256,20 +192,14 @@ template <int PROTO, bool SET, int G>
 void launch_l4_g(clk_ctx *ctx, const clk::BatchArgs &a, unsigned grid, int fixoff, uint8_t *code, uint16_t *sum,
                  uint32_t *work)
 {
-    // runs per workgroup for packets 0..n-1 (CLK_L4_RUNS), the grid-stride
-    // group loop for a size-class pass
+    // runs per workgroup (CLK_L4_RUNS) for Check and for Sets from
+    // CLK_L4_RUNS_SET_G lanes per packet, else the grid-stride group loop
     constexpr bool RUNS = CLK_L4_RUNS && (!SET || G >= CLK_L4_RUNS_SET_G);
-    if (SET && work && !a.perm)
+    if (SET && work)
         hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, k_for(G), true, RUNS>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a,
                            fixoff, code, sum, work);
-    else if (SET && work)
-        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, k_for(G), true, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a,
-                           fixoff, code, sum, work);
-    else if (!a.perm)
-        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, k_for(G), false, RUNS>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a,
-                           fixoff, code, sum, work);
     else
-        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, k_for(G), false, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a,
+        hipLaunchKernelGGL((clk::l4_kernel<PROTO, SET, G, k_for(G), false, RUNS>), dim3(grid), dim3(BLOCK), 0, ctx->cur, a,
                            fixoff, code, sum, work);
 }
 
@@ -298,55 +228,27 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
     if (b->n == 0) return CLK_SUCCESS;
     if (!code) return fail(ctx, CLK_EINVAL, "%s: null output", fn);
     uint32_t *work = nullptr;
-    const bool bins = use_bins(ctx, b);
-    const bool stream = bins && ctx->varlen == 2;
-    // auto (-1): two-phase for the fixed-geometry and size-class Set
-    // kernels (a read-only compute pass, then field_scatter_kernel), fused
-    // for the packet-stream kernel (phase C stores the field's 64 B block
-    // from its LDS stash); DESIGN.md §6
+    const bool stream = use_stream(ctx, b);
+    // auto (-1): two-phase for the fixed-geometry Set kernels (a read-only
+    // compute pass, then field_scatter_kernel), fused for the packet-stream
+    // kernel (phase C stores the field's 64 B block from its LDS stash);
+    // DESIGN.md §6
     const bool two = SET && (ctx->set_mode == 1 || (ctx->set_mode < 0 && !stream));
-    const ScratchLayout L = scratch_layout(b->n);
-    if (two || bins) {
-        if ((r = ensure_scratch(ctx, L.bytes))) return r;
-        if (two)
-            work = (uint32_t *)ctx->scratch;
+    if (two) {
+        if ((r = ensure_scratch(ctx, work_bytes(b->n)))) return r;
+        work = (uint32_t *)ctx->scratch;
     }
-    if (work && ctx->diag_phase == 2 && ctx->diag_primed) {
-        // diagnostics: scatter only
-    } else if (bins && ctx->varlen == 2) {
+    if (stream) {
         constexpr int KV = SET ? CLK_SKV : CLK_SKV_CHECK;
         uint64_t blocks = (b->n + 255) / 256;            // 4 waves x 64 packets per block
         if (blocks > (uint64_t)ctx->max_blocks)
             blocks = (uint64_t)ctx->max_blocks;
         if (work)
-            hipLaunchKernelGGL((clk::l4_stream_kernel<PROTO, SET, true, KV, CLK_SPF != 0, CLK_SMARK != 0>), dim3((unsigned)blocks), dim3(BLOCK), 0,
+            hipLaunchKernelGGL((clk::l4_stream_kernel<PROTO, SET, true, KV>), dim3((unsigned)blocks), dim3(BLOCK), 0,
                                ctx->cur, args_of(b), fixoff, code, sum, work);
         else
-            hipLaunchKernelGGL((clk::l4_stream_kernel<PROTO, SET, false, KV, CLK_SPF != 0, CLK_SMARK != 0>), dim3((unsigned)blocks), dim3(BLOCK),
-                               0, ctx->cur, args_of(b), fixoff, code, sum, work);
-    } else if (bins && ctx->varlen) {
-        constexpr int KV = CLK_KV, VU = CLK_VU;
-        uint64_t blocks = (b->n + 255) / 256;            // 4 waves x 64 packets per block
-        if (blocks > (uint64_t)ctx->max_blocks)
-            blocks = (uint64_t)ctx->max_blocks;
-        if (work)
-            hipLaunchKernelGGL((clk::l4_varlen_kernel<PROTO, SET, true, KV, VU>), dim3((unsigned)blocks), dim3(BLOCK), 0,
+            hipLaunchKernelGGL((clk::l4_stream_kernel<PROTO, SET, false, KV>), dim3((unsigned)blocks), dim3(BLOCK), 0,
                                ctx->cur, args_of(b), fixoff, code, sum, work);
-        else
-            hipLaunchKernelGGL((clk::l4_varlen_kernel<PROTO, SET, false, KV, VU>), dim3((unsigned)blocks), dim3(BLOCK),
-                               0, ctx->cur, args_of(b), fixoff, code, sum, work);
-    } else if (bins) {
-        bin_batch(ctx, b, L);
-        clk::BatchArgs a = args_of(b);
-        a.perm = (const uint32_t *)((uint8_t *)ctx->scratch + L.perm);
-        for (int c = 0; c <= max_class(b); c++) {
-            a.range = (const uint64_t *)((uint8_t *)ctx->scratch + L.range) + 2 * c;
-            const int g = 1 << c;
-            uint64_t blocks = (b->n * (uint64_t)g + BLOCK - 1) / BLOCK;
-            if (blocks > (uint64_t)ctx->bin_grid)
-                blocks = (uint64_t)ctx->bin_grid;
-            launch_l4_dispatch<PROTO, SET>(ctx, a, (unsigned)blocks, fixoff, code, sum, work, g);
-        }
     } else {
         const int g = pick_group(ctx, b);
         uint64_t threads = b->n * (uint64_t)g;
@@ -356,18 +258,11 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
         }
         launch_l4_dispatch<PROTO, SET>(ctx, args_of(b), grid_for(ctx, threads), fixoff, code, sum, work, g);
     }
-    if (work)
-        ctx->diag_primed = true;
-    if (work && ctx->diag_phase != 1) {
+    if (work) {
         constexpr int FIELD = PROTO == clk::UDP ? 6 : 16;
-        if (CLK_SCATTER_BLOCK)
-            hipLaunchKernelGGL((clk::field_scatter_block_kernel<FIELD>), dim3(grid_for(ctx, 4 * b->n)), dim3(BLOCK), 0,
-                               ctx->cur, args_of(b), (const uint32_t *)work, code, sum);
-        else
-            hipLaunchKernelGGL((clk::field_scatter_kernel<FIELD, true>),
-                               dim3(std::min<unsigned>(grid_for(ctx, b->n), (unsigned)ctx->scatter_blocks)), dim3(BLOCK), 0,
-                               ctx->cur, args_of(b), (const uint32_t *)work, (const uint8_t *)nullptr,
-                               (const uint16_t *)nullptr, code, sum);
+        hipLaunchKernelGGL((clk::field_scatter_kernel<FIELD>),
+                           dim3(std::min<unsigned>(grid_for(ctx, b->n), (unsigned)ctx->scatter_blocks)), dim3(BLOCK), 0,
+                           ctx->cur, args_of(b), (const uint32_t *)work, code, sum);
     }
     return check_launch(ctx, fn);
 }
@@ -422,46 +317,12 @@ int clk_ctx_create(int device, clk_ctx **out)
     c->device = device;
     c->err[0] = 0;
     c->max_blocks = 262144;
-    if (const char *mb = std::getenv("CLK_MAX_BLOCKS")) {
-        int v = std::atoi(mb);
-        if (v > 0)
-            c->max_blocks = v;
-    }
     c->scratch = nullptr;
     c->scratch_bytes = 0;
     c->set_mode = -1;
-    if (const char *sm = std::getenv("CLK_SET_MODE"))
-        c->set_mode = std::atoi(sm) == 1 ? 1 : 0;
     c->scatter_blocks = 16384;
-    if (const char *sb = std::getenv("CLK_SCATTER_BLOCKS")) {
-        const int v = std::atoi(sb);
-        if (v > 0)
-            c->scatter_blocks = v;
-    }
-    c->diag_phase = 0;
-    c->diag_primed = false;
-    if (const char *dp = std::getenv("CLK_DIAG_SET_PHASE"))
-        c->diag_phase = std::atoi(dp);
-    c->bin_min = 65536;
-    if (const char *bm = std::getenv("CLK_BIN_MIN"))
-        c->bin_min = (uint64_t)std::strtoull(bm, nullptr, 10);
-    c->bin_grid = 16384;
-    if (const char *bg = std::getenv("CLK_BIN_GRID")) {
-        int v = std::atoi(bg);
-        if (v > 0)
-            c->bin_grid = v;
-    }
-    c->varlen = 2;
-    if (const char *vl = std::getenv("CLK_VARLEN")) {
-        const int v = std::atoi(vl);
-        c->varlen = v >= 0 && v <= 2 ? v : 2;
-    }
+    c->stream_min = 65536;
     c->force_group = 0;
-    if (const char *fg = std::getenv("CLK_FORCE_GROUP")) {
-        int v = std::atoi(fg);
-        if (v == 1 || v == 2 || v == 4 || v == 8 || v == 16 || v == 32 || v == 64)
-            c->force_group = v;
-    }
     e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete c;
@@ -510,7 +371,39 @@ int clk_ctx_reserve(clk_ctx *ctx, uint64_t max_packets)
 {
     int r = enter(ctx);
     if (r) return r;
-    return ensure_scratch(ctx, scratch_layout(max_packets).bytes);
+    return ensure_scratch(ctx, work_bytes(max_packets));
+}
+
+int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value)
+{
+    if (!ctx)
+        return fail(nullptr, CLK_EINVAL, "null context");
+    switch (knob) {
+    case CLK_TUNE_MAX_BLOCKS:
+        if (value < 1 || value > (1 << 30)) break;
+        ctx->max_blocks = (int)value;
+        return CLK_SUCCESS;
+    case CLK_TUNE_SCATTER_BLOCKS:
+        if (value < 1 || value > (1 << 30)) break;
+        ctx->scatter_blocks = (int)value;
+        return CLK_SUCCESS;
+    case CLK_TUNE_SET_MODE:
+        if (value < -1 || value > 1) break;
+        ctx->set_mode = (int)value;
+        return CLK_SUCCESS;
+    case CLK_TUNE_STREAM_MIN:
+        if (value < 1) break;
+        ctx->stream_min = (uint64_t)value;
+        return CLK_SUCCESS;
+    case CLK_TUNE_GROUP:
+        if (!(value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16 || value == 32 ||
+              value == 64)) break;
+        ctx->force_group = (int)value;
+        return CLK_SUCCESS;
+    default:
+        return fail(ctx, CLK_EINVAL, "clk_ctx_tune: unknown knob %d", knob);
+    }
+    return fail(ctx, CLK_EINVAL, "clk_ctx_tune: knob %d: bad value %lld", knob, (long long)value);
 }
 
 int clk_ctx_sync(clk_ctx *ctx)
@@ -548,28 +441,13 @@ int clk_in_cksum(clk_ctx *ctx, const clk_batch *b, uint16_t *out_sum)
     if ((r = check_batch(ctx, b, "clk_in_cksum"))) return r;
     if (b->n == 0) return CLK_SUCCESS;
     if (!out_sum) return fail(ctx, CLK_EINVAL, "clk_in_cksum: null output");
-    if (use_bins(ctx, b)) {
-        const ScratchLayout L = scratch_layout(b->n);
-        if ((r = ensure_scratch(ctx, L.bytes))) return r;
-        bin_batch(ctx, b, L);
-        clk::BatchArgs a = args_of(b);
-        a.perm = (const uint32_t *)((uint8_t *)ctx->scratch + L.perm);
-        for (int c = 0; c <= max_class(b); c++) {
-            a.range = (const uint64_t *)((uint8_t *)ctx->scratch + L.range) + 2 * c;
-            uint64_t blocks = (b->n * (uint64_t)(1 << c) + BLOCK - 1) / BLOCK;
-            if (blocks > (uint64_t)ctx->bin_grid)
-                blocks = (uint64_t)ctx->bin_grid;
-            launch_range_dispatch(ctx, a, (unsigned)blocks, out_sum, 1 << c);
-        }
-    } else {
-        const int g = pick_group(ctx, b);
-        uint64_t threads = b->n * (uint64_t)g;
-        if (CLK_L4_RUNS) {                                        // a workgroup per run
-            const uint64_t run = 256 / g < 64 ? 64 : 256 / g;
-            threads = (b->n + run - 1) / run * BLOCK;
-        }
-        launch_range_dispatch(ctx, args_of(b), grid_for(ctx, threads), out_sum, g);
+    const int g = pick_group(ctx, b);
+    uint64_t threads = b->n * (uint64_t)g;
+    if (CLK_L4_RUNS) {                                        // a workgroup per run
+        const uint64_t run = 256 / g < 64 ? 64 : 256 / g;
+        threads = (b->n + run - 1) / run * BLOCK;
     }
+    launch_range_dispatch(ctx, args_of(b), grid_for(ctx, threads), out_sum, g);
     return check_launch(ctx, "clk_in_cksum");
 }
 
@@ -585,11 +463,11 @@ int clk_check_ip_header(clk_ctx *ctx, const clk_batch *b, const clk_ip_check_cfg
     if (!out_verdict) return fail(ctx, CLK_EINVAL, "clk_check_ip_header: null output");
     const unsigned grid = grid_for(ctx, (CLK_IPH_PAIR ? 2 : 1) * b->n);
     if (cfg->checksum)
-        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
+        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
                            args_of(b), cfg->offset, cfg->badsrc, cfg->nbadsrc, cfg->gooddst, cfg->ngooddst,
                            out_verdict, (uint16_t *)nullptr);
     else
-        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK_NOCKSUM, false>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
+        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_CHECK_NOCKSUM>), dim3(grid), dim3(BLOCK), 0, ctx->cur,
                            args_of(b), cfg->offset, cfg->badsrc, cfg->nbadsrc, cfg->gooddst, cfg->ngooddst,
                            out_verdict, (uint16_t *)nullptr);
     return check_launch(ctx, "clk_check_ip_header");
@@ -602,23 +480,9 @@ int clk_set_ip_checksum(clk_ctx *ctx, const clk_batch *b, uint8_t *out_status, u
     if ((r = check_batch(ctx, b, "clk_set_ip_checksum"))) return r;
     if (b->n == 0) return CLK_SUCCESS;
     if (!out_status) return fail(ctx, CLK_EINVAL, "clk_set_ip_checksum: null output");
-    if (ctx->set_mode == 1) {                // auto: fused for SetIPChecksum
-        uint16_t *sums = out_sum;
-        if (!sums) {
-            if ((r = ensure_scratch(ctx, b->n * sizeof(uint16_t)))) return r;
-            sums = (uint16_t *)ctx->scratch;
-        }
-        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_SET, true>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
-                           ctx->cur, args_of(b), 0u, (const uint32_t *)nullptr, 0u, (const uint32_t *)nullptr, 0u,
-                           out_status, sums);
-        hipLaunchKernelGGL((clk::field_scatter_kernel<10, false>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
-                           ctx->cur, args_of(b), (const uint32_t *)nullptr, (const uint8_t *)out_status,
-                           (const uint16_t *)sums, (uint8_t *)nullptr, (uint16_t *)nullptr);
-    } else {
-        hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_SET, false>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0,
-                           ctx->cur, args_of(b), 0u, (const uint32_t *)nullptr, 0u, (const uint32_t *)nullptr, 0u,
-                           out_status, out_sum);
-    }
+    hipLaunchKernelGGL((clk::ip_header_kernel<clk::IP_SET>), dim3(grid_for(ctx, b->n)), dim3(BLOCK), 0, ctx->cur,
+                       args_of(b), 0u, (const uint32_t *)nullptr, 0u, (const uint32_t *)nullptr, 0u, out_status,
+                       out_sum);
     return check_launch(ctx, "clk_set_ip_checksum");
 }
 

@@ -21,9 +21,6 @@
 #ifndef CLK_NT_STORES
 #define CLK_NT_STORES 0    // tuning knob: nontemporal checksum-field stores
 #endif
-#ifndef CLK_SHC_EXTRA
-#define CLK_SHC_EXTRA 0    // packet-stream kernel: head chunks stashed beyond the aligned-header minimum
-#endif
 #ifndef CLK_SWPE
 #define CLK_SWPE 8         // packet-stream kernel: request this many waves per SIMD (TCP: at most 7, its 3 stashed head chunks)
 #endif
@@ -33,20 +30,8 @@
 #ifndef CLK_SWPE_CHECK
 #define CLK_SWPE_CHECK 6   // ... the Check kernels, with 3 chunks per lane per pass (CLK_SKV_CHECK)
 #endif
-#ifndef CLK_BLOCK_WRITE
-#define CLK_BLOCK_WRITE 0  // tuning knob: fused Set stores rewrite the whole 64 B block (measured slower)
-#endif
-#ifndef CLK_DIAG_NO_WORK_STORE
-#define CLK_DIAG_NO_WORK_STORE 0    // diagnostic builds only (results wrong)
-#endif
-#ifndef CLK_DIAG_NO_FIELD_STORE
-#define CLK_DIAG_NO_FIELD_STORE 0   // diagnostic builds only (results wrong)
-#endif
 #ifndef CLK_L4_RUNS
 #define CLK_L4_RUNS 1      // l4_kernel: a workgroup owns runs of packets and stores their outputs whole
-#endif
-#ifndef CLK_RUNS_HDRC
-#define CLK_RUNS_HDRC 0        // runs: the two-phase Set's header from the chunk registers (measured slower)
 #endif
 #ifndef CLK_L4_RUNS_SET_G
 #define CLK_L4_RUNS_SET_G 16   // Set kernels use runs from this G up (C5 -6 %; C3 -5 % with nontemporal scatter stores: DESIGN.md §6)
@@ -69,10 +54,6 @@ struct BatchArgs {
     const uint32_t *len;
     uint32_t fixed_len;
     uint64_t n;
-    // size-class pass (bin_* kernels below): packets perm[j] for j in
-    // [range[0], range[1]); perm == nullptr: packets 0..n-1
-    const uint32_t *perm;
-    const uint64_t *range;
 };
 
 __device__ __forceinline__ uint64_t pkt_off(const BatchArgs &b, uint64_t i)
@@ -125,7 +106,7 @@ __device__ __forceinline__ void field_st_u32(uint8_t *p, uint32_t v)    // 4-byt
 #ifndef CLK_IPH_PAIR
 #define CLK_IPH_PAIR 1   // C2 CheckIPHeader 0.168 vs 0.182 ms with one lane per packet
 #endif
-template <int MODE, bool DEFER>
+template <int MODE>
 __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t offset,
                                                         const uint32_t *badsrc, uint32_t nbadsrc,
                                                         const uint32_t *gooddst, uint32_t ngooddst,
@@ -198,10 +179,7 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
                     }
                     sum -= h[2] >> 16;                 // ip_sum = 0 (setipchecksum.cc:85)
                     stored = in_cksum_fold(sum);       // setipchecksum.cc:86
-#if !CLK_DIAG_NO_FIELD_STORE
-                    if (!DEFER)                        // else field_scatter_kernel writes it
-                        field_st_u16(ip + 10, stored);
-#endif
+                    field_st_u16(ip + 10, stored);
                 }
             } else {
                 const uint32_t len = bswap16(h[0] >> 16);
@@ -297,7 +275,7 @@ __device__ __forceinline__ uint32_t group_range_sum(const uint8_t *c0, uint32_t 
 // RUNS (packets 0..n-1): a workgroup owns max(64, 256/G) consecutive
 // packets and writes their sums whole after one barrier, as l4_kernel does;
 // nontemporal loads (once-read stream).  Else the grid-stride loop, which
-// also serves the size-class passes (b.perm).
+// for the multi-pass geometry hint paths.
 template <int G, int K, bool RUNS>
 __global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_sum)
 {
@@ -336,9 +314,7 @@ __global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_s
         return;
     }
     const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
-    const uint64_t jbeg = b.perm ? b.range[0] : 0, jend = b.perm ? b.range[1] : b.n;
-    for (uint64_t j = jbeg + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; j < jend; j += groups) {
-        const uint64_t i = b.perm ? (uint64_t)b.perm[j] : j;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; i < b.n; i += groups) {
         const uint32_t r = one(i);
         if (gl == 0)
             out_sum[i] = (uint16_t)r;
@@ -598,36 +574,16 @@ __device__ __forceinline__ void patch_byte(u32x4 &v, uint64_t va, uint64_t at, u
     }
 }
 
-// Fused Set stores.  HBM rewrites a partially written 64 B block by
-// read-modify-write: alone, one 2 B store per 1536 B slot runs at 21.6 G
-// stores/s and a full 64 B block at 39 G/s (tools/probes/write_probe.hip).
-// With CLK_BLOCK_WRITE, when the 64 B-aligned block holding the field lies
-// inside this packet, the lanes re-read it, patch the field (and the FIXOFF
-// byte when it falls in the block) and store the whole block; lane `gl` of
-// `ng` takes quarters gl, gl+ng, ...  Inside the streaming kernels this
-// measured slower (C3 5.19 vs 4.94 ms, C4 7.11 vs 6.64 ms), so by default
-// the writer lane stores the bytes alone.
+// Fused Set store of the field bytes alone (and FIXOFF's th_off byte) by the
+// writer lane, when the field's 64 B block cannot be stored whole.  (HBM
+// rewrites a partially written 64 B block by read-modify-write: alone, one
+// 2 B store per 1536 B slot runs at 21.6 G stores/s and a full 64 B block at
+// 39 G/s, tools/probes/write_probe.hip.)
 template <int PROTO>
-__device__ __forceinline__ void set_field_store(uint8_t *nh, const L4State &st, uint32_t r, uint32_t gl,
-                                                uint32_t ng, bool writer)
+__device__ __forceinline__ void set_field_store(uint8_t *nh, const L4State &st, uint32_t r, bool writer)
 {
     constexpr uint32_t FIELD = PROTO == UDP ? 6 : 16;
-    const uint64_t a = (uint64_t)nh, fa = a + st.hl + FIELD, xa = a + st.hl + 12;
-    const uint64_t blk = fa & ~63ull;
-    if (CLK_BLOCK_WRITE && blk >= a && blk + 64 <= a + st.caplen) {
-        const bool fix_in = st.fix && (xa - blk) < 64;
-        for (uint32_t q = gl; q < 4; q += ng) {
-            const uint64_t qa = blk + 16 * q;
-            u32x4 v = gload16(qa);
-            patch_byte(v, qa, fa, r);
-            patch_byte(v, qa, fa + 1, r >> 8);
-            if (fix_in)
-                patch_byte(v, qa, xa, st.new_b12);
-            *(__attribute__((address_space(1))) u32x4 *)qa = v;
-        }
-        if (writer && st.fix && !fix_in)
-            nh[st.hl + 12] = (uint8_t)st.new_b12;
-    } else if (writer) {
+    if (writer) {
         if (st.fix)
             nh[st.hl + 12] = (uint8_t)st.new_b12;
         st_u16(nh + st.hl + FIELD, r);
@@ -776,7 +732,6 @@ __device__ __forceinline__ L4Out l4_result(uint8_t *nh, uint32_t sum, L4State &s
         const uint32_t r = PROTO == ICMP ? csum : pseudohdr_ph(csum, st.ph);
         if (SET) {
             o.sum = r;
-#if !CLK_DIAG_NO_FIELD_STORE
             if (DEFER) {         // the field is written by field_scatter_kernel
                 if (writer && st.fix)
                     nh[st.hl + 12] = (uint8_t)st.new_b12;
@@ -784,7 +739,6 @@ __device__ __forceinline__ L4Out l4_result(uint8_t *nh, uint32_t sum, L4State &s
             } else {
                 store(r);
             }
-#endif
         } else if (r != 0) {
             st.code = L4_BAD_CHECKSUM;
         }
@@ -813,11 +767,10 @@ __device__ __forceinline__ void l4_finish_with(uint8_t *nh, uint64_t i, uint32_t
 
 template <int PROTO, bool SET, bool DEFER>
 __device__ __forceinline__ void l4_finish(uint8_t *nh, uint64_t i, uint32_t sum, L4State &st, bool writer,
-                                          uint8_t *out_code, uint16_t *out_sum, uint32_t *work,
-                                          uint32_t gl = 0, uint32_t ng = 1)
+                                          uint8_t *out_code, uint16_t *out_sum, uint32_t *work)
 {
     l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, writer, out_code, out_sum, work,
-                                      [&](uint32_t r) { set_field_store<PROTO>(nh, st, r, gl, ng, writer); });
+                                      [&](uint32_t r) { set_field_store<PROTO>(nh, st, r, writer); });
 }
 
 // Fixed geometry: G lanes per packet.  Every lane of a group issues the
@@ -860,14 +813,14 @@ __device__ __forceinline__ L4Out l4_group(const BatchArgs &b, int fixoff, uint64
     if (SET && !DEFER && CLK_SET_REGBLK)
         return l4_result<PROTO, SET, DEFER>(nh, sum, st, gl == 0, [&](uint32_t r) {
             if (!set_block_store_regs<PROTO, G, K>(nh, st, r, gl, (uint64_t)c0, v))
-                set_field_store<PROTO>(nh, st, r, gl, G, gl == 0);
+                set_field_store<PROTO>(nh, st, r, gl == 0);
         });
     return l4_result<PROTO, SET, DEFER>(nh, sum, st, gl == 0,
-                                        [&](uint32_t r) { set_field_store<PROTO>(nh, st, r, gl, G, gl == 0); });
+                                        [&](uint32_t r) { set_field_store<PROTO>(nh, st, r, gl == 0); });
 }
 
 // RUNS: packets 0..n-1 in runs per workgroup (below); else the grid-stride
-// loop over groups, which also serves the size-class passes (b.perm).
+// loop over groups (the two-phase Set's compute pass for G < CLK_L4_RUNS_SET_G).
 template <int PROTO, bool SET, int G, int K, bool DEFER, bool RUNS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SET && PROTO == UDP ? CLK_L4_WPE_SET : SET ? 1 : CLK_L4_WPE_CHECK)))
 l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
@@ -902,7 +855,7 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             for (uint32_t p = 0; p < RB / PPB; p++) {
                 const uint32_t q = p * PPB + threadIdx.x / G;
                 if (i0 + q < b.n) {
-                    const L4Out o = l4_group<PROTO, SET, G, K, DEFER, CLK_RUNS_HDRC != 0>(b, fixoff, i0 + q, lane, gl);
+                    const L4Out o = l4_group<PROTO, SET, G, K, DEFER, false>(b, fixoff, i0 + q, lane, gl);
                     if (gl == 0) {
                         if (SET && DEFER) {
                             r_work[q] = o.work;
@@ -930,158 +883,17 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         return;
     }
     const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
-    const uint64_t jbeg = b.perm ? b.range[0] : 0, jend = b.perm ? b.range[1] : b.n;
-    for (uint64_t j = jbeg + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; j < jend; j += groups) {
-        const uint64_t i = b.perm ? (uint64_t)b.perm[j] : j;
+    for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; i < b.n; i += groups) {
         const L4Out o = l4_group<PROTO, SET, G, K, DEFER, CLK_HDR_FROM_CHUNKS != 0>(b, fixoff, i, lane, gl);
         if (gl == 0) {
             if (SET && DEFER) {
-                if (!CLK_DIAG_NO_WORK_STORE || (o.work ^ (uint32_t)b.n) == 0x7F012345u)
-                    work[i] = o.work;
+                work[i] = o.work;
             } else {
                 out_code[i] = (uint8_t)o.code;
                 if (SET && out_sum)
                     out_sum[i] = (uint16_t)o.sum;
             }
         }
-    }
-}
-
-// Variable lengths (IMIX): a wave takes 64 consecutive packets.
-//   Phase A: one lane per packet parses its header and publishes, in LDS,
-//            its summed range as 16-byte chunks: first chunk address, chunk
-//            offset in the wave's concatenated chunk list (exclusive scan),
-//            range start within the first chunk, range length.
-//   Phase B: the wave walks the concatenated chunk list in passes of VU
-//            sub-passes of KV chunks per lane, each lane a contiguous run
-//            (lane l of sub-pass u owns chunks u*64*KV + l*KV + [0, KV));
-//            all VU*KV loads are issued before any is summed.  The lane finds its first
-//            chunk's packet by binary search, steps forward at packet
-//            boundaries, sums in registers and adds the partial into the
-//            packet's LDS accumulator only when the packet changes (u32
-//            adds, exact mod 2^32).  A pass reads 64*KV*16 contiguous bytes
-//            of a packed arena.
-//   Phase C: each lane finishes its packet from its accumulator.
-// No workgroup barriers: every LDS word is private to one wave.
-template <int PROTO, bool SET, bool DEFER, int KV, int VU>
-__global__ void __launch_bounds__(256) l4_varlen_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
-                                                        uint16_t *out_sum, uint32_t *work)
-{
-    __shared__ u32x4 pk[4][64];       // {cfirst lo, cfirst hi, chunk start, rlen | (s & 15) << 24}
-    __shared__ uint32_t cst[4][68];   // chunk starts; cst[64] = total, padded
-    __shared__ uint32_t acc[4][64];
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t nruns = (b.n + 63) / 64;
-    const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
-    for (uint64_t run = (uint64_t)blockIdx.x * (blockDim.x / 64) + wv; run < nruns; run += wstride) {
-        const uint64_t i = run * 64 + lane;
-        const bool live = i < b.n;
-        uint8_t *nh = b.base;
-        L4State st;
-        st.summing = false;
-        st.code = OK;
-        st.rlen = 0;
-        st.hl = 0;
-        if (live) {
-            nh = b.base + pkt_off(b, i);
-            l4_parse<PROTO, SET>(nh, pkt_len(b, i), fixoff, st);
-        }
-        const int rlen = st.summing ? st.rlen : 0;
-        const uint64_t s = (uint64_t)nh + st.hl;
-        const uint64_t cfirst = s & ~15ull;
-        const uint32_t nchunks = rlen > 0 ? (uint32_t)((((s + (uint64_t)rlen + 15) & ~15ull) - cfirst) >> 4) : 0u;
-        uint32_t incl = nchunks;                             // wave-inclusive scan
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t t = __shfl_up(incl, d, 64);
-            if ((int)lane >= d)
-                incl += t;
-        }
-        const uint32_t total = __shfl(incl, 63, 64);
-        const uint32_t rl = rlen > 0 ? (uint32_t)rlen : 0u;   // L4 ranges are < 2^16 bytes
-        pk[wv][lane] = u32x4{(uint32_t)cfirst, (uint32_t)(cfirst >> 32), incl - nchunks,
-                             rl | ((uint32_t)(s & 15) << 24)};
-        cst[wv][lane] = incl - nchunks;
-        if (lane == 63)
-            cst[wv][64] = total;
-        acc[wv][lane] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t cb = 0; cb < total; cb += 64 * KV * VU) {     // wave-uniform
-            u32x4 v[VU * KV];
-            u32x4 Pk[VU * KV];
-            uint32_t jk[VU * KV];
-#pragma unroll
-            for (int u = 0; u < VU; u++) {
-                const uint32_t c0 = cb + 64 * KV * u + lane * KV;
-                // last packet whose chunk start <= c0
-                uint32_t j = 0;
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1)
-                    if (j + step < 64 && cst[wv][j + step] <= c0)
-                        j += step;
-                uint32_t nxt = cst[wv][j + 1];
-                u32x4 P = pk[wv][j];
-#pragma unroll
-                for (int k = 0; k < KV; k++) {
-                    const uint32_t c = c0 + k;
-                    if (c < total && c >= nxt) {
-                        do {                                       // skip to the chunk's packet
-                            j++;
-                            nxt = cst[wv][j + 1];
-                        } while (c >= nxt);
-                        P = pk[wv][j];
-                    }
-                    jk[u * KV + k] = j;
-                    Pk[u * KV + k] = P;
-                    const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
-                    v[u * KV + k] = c < total ? gload16(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < VU; u++) {
-                const uint32_t c0 = cb + 64 * KV * u + lane * KV;
-                uint32_t cur = jk[u * KV], part = 0;
-#pragma unroll
-                for (int k = 0; k < KV; k++) {
-                    const uint32_t c = c0 + k;
-                    if (c >= total)
-                        break;
-                    if (jk[u * KV + k] != cur) {
-                        atomicAdd(&acc[wv][cur], part);
-                        part = 0;
-                        cur = jk[u * KV + k];
-                    }
-                    const u32x4 Q = Pk[u * KV + k];
-                    const u32x4 V = v[u * KV + k];
-                    const int rlj = (int)(Q[3] & 0xFFFFFF);
-                    const uint32_t s15 = Q[3] >> 24;
-                    const uint32_t sel = (s15 & 1) ? 0x02030001u : 0x03020100u;   // odd start: swap bytes
-                    const int rel = (int)(16 * (c - Q[2])) - (int)s15;          // chunk start - range start
-                    if (rel >= 0 && rel + 16 <= rlj) {
-#pragma unroll
-                        for (int q = 0; q < 4; q++)
-                            part = dot_words(__builtin_amdgcn_perm(V[q], V[q], sel), part);
-                    } else {
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            const uint32_t dm = V[q] & lowmask(rlj - rel - 4 * q) & ~lowmask(-rel - 4 * q);
-                            part = dot_words(__builtin_amdgcn_perm(dm, dm, sel), part);
-                        }
-                    }
-                }
-                if (c0 < total)
-                    atomicAdd(&acc[wv][cur], part);
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t sum = acc[wv][lane];
-        if (live)
-            l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work);
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -1133,7 +945,7 @@ __device__ __forceinline__ uint32_t chunk_outside(const u32x4 V, uint64_t ca, ui
 //            bytes) is re-summed from global memory by its lane.
 // The sum mod 2^32 is order-free (cksum_device.hh), so whole-chunk sums
 // minus the excluded bytes equal the reference's word sum exactly.
-template <int PROTO, bool SET, bool DEFER, int KV, bool PF, bool MARKS>
+template <int PROTO, bool SET, bool DEFER, int KV>
 __global__ void __launch_bounds__(256)
 #if CLK_SWPE
 __attribute__((amdgpu_waves_per_eu(!SET ? CLK_SWPE_CHECK : SET && !DEFER && CLK_SET_REGBLK && CLK_SWPE > 6 ? 6 : PROTO == TCP && CLK_SWPE > 7 ? 7 : CLK_SWPE)))
@@ -1147,7 +959,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
     // the parse loads the missing dwords itself
     // A fused Set stashes 4 (the field's 64 B block, stored whole from the
     // stash); the two-phase compute pass stores nothing and needs no more.
-    constexpr int HC0 = PROTO == TCP ? 3 + CLK_SHC_EXTRA : 2 + CLK_SHC_EXTRA;
+    constexpr int HC0 = PROTO == TCP ? 3 : 2;
     constexpr int HC = SET && !DEFER && CLK_SET_REGBLK && HC0 < 4 ? 4 : HC0;
     constexpr bool COAL = SET && !DEFER && CLK_SET_REGBLK && CLK_STASH_COALESCE;
     __shared__ u32x4 head[4][64][HC];
@@ -1155,7 +967,6 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
     __shared__ u32x4 pk[4][64];       // {c0 lo, c0 hi, chunk start, nch | odd << 31}
     __shared__ uint32_t cst[4][68];   // chunk starts; cst[64] = total
     __shared__ uint32_t acc[4][64];
-    __shared__ uint32_t mark[4][MARKS ? 64 * KV : 1];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t nruns = (b.n + 63) / 64;
     const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
@@ -1189,68 +1000,27 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // issue: find the packets of this lane's KV chunks at cb and load them
-        uint32_t carry = 0;          // MARKS: 1 + the packet of the chunk before this pass (wave-uniform)
         // per chunk the consumer needs its packet (jk) and inf = its index r in
         // the packet | last chunk << 30 | odd packet << 31 (2 VGPRs per chunk
         // rather than the packet's 4-word record: KV = 4 fits 8 waves)
         auto issue = [&](uint32_t cb, u32x4 (&v)[KV], uint32_t (&jk)[KV], uint32_t (&inf)[KV]) {
             const uint32_t cl = cb + lane * KV;
-            if (MARKS) {
-                // each packet marks its first chunk in the pass window, a
-                // wave max-scan carries the packet index to every chunk:
-                // no dependent LDS chain
+            uint32_t j = 0;                                    // last packet whose chunk start <= cl
 #pragma unroll
-                for (int k = 0; k < KV; k++)
-                    mark[wv][lane * KV + k] = 0;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const uint32_t my_start = incl - nch;
-                if (nch && my_start >= cb && my_start - cb < 64u * KV)
-                    mark[wv][my_start - cb] = lane + 1;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                uint32_t m[KV], lm = 0;
+            for (int step = 32; step >= 1; step >>= 1)
+                if (cst[wv][j + step] <= cl)
+                    j += step;
+            uint32_t nxt = cst[wv][j + 1];
 #pragma unroll
-                for (int k = 0; k < KV; k++) {
-                    m[k] = mark[wv][lane * KV + k];
-                    lm = m[k] > lm ? m[k] : lm;
+            for (int k = 0; k < KV; k++) {
+                const uint32_t c = cl + k;
+                if (c < total && c >= nxt) {
+                    do {
+                        j++;
+                        nxt = cst[wv][j + 1];
+                    } while (c >= nxt);
                 }
-                uint32_t x = lm;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t t = __shfl_up(x, d, 64);
-                    if ((int)lane >= d)
-                        x = t > x ? t : x;
-                }
-                uint32_t run = __shfl_up(x, 1, 64);
-                run = lane == 0 ? carry : (run > carry ? run : carry);
-                const uint32_t last = __shfl(x, 63, 64);
-                carry = last > carry ? last : carry;
-#pragma unroll
-                for (int k = 0; k < KV; k++) {
-                    run = m[k] > run ? m[k] : run;
-                    jk[k] = run ? run - 1 : 0;
-                }
-            } else {
-                uint32_t j = 0;                                    // last packet whose chunk start <= cl
-#pragma unroll
-                for (int step = 32; step >= 1; step >>= 1)
-                    if (cst[wv][j + step] <= cl)
-                        j += step;
-                uint32_t nxt = cst[wv][j + 1];
-#pragma unroll
-                for (int k = 0; k < KV; k++) {
-                    const uint32_t c = cl + k;
-                    if (c < total && c >= nxt) {
-                        do {
-                            j++;
-                            nxt = cst[wv][j + 1];
-                        } while (c >= nxt);
-                    }
-                    jk[k] = j;
-                }
+                jk[k] = j;
             }
 #pragma unroll
             for (int k = 0; k < KV; k++) {
@@ -1300,34 +1070,11 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             if (cl < total)
                 atomicAdd(&acc[wv][cur], part);
         };
-        if (PF) {                 // the next pass's loads are in flight while this pass is summed
+        for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
             u32x4 v[KV];
             uint32_t jk[KV], inf[KV];
-            if (total)
-                issue(0, v, jk, inf);
-            for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
-                u32x4 v2[KV];
-                uint32_t j2[KV], i2[KV];
-                const bool more = cb + 64 * KV < total;
-                if (more)
-                    issue(cb + 64 * KV, v2, j2, i2);
-                consume(cb, v, jk, inf);
-                if (more) {
-#pragma unroll
-                    for (int k = 0; k < KV; k++) {
-                        v[k] = v2[k];
-                        jk[k] = j2[k];
-                        inf[k] = i2[k];
-                    }
-                }
-            }
-        } else {
-            for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
-                u32x4 v[KV];
-                uint32_t jk[KV], inf[KV];
-                issue(cb, v, jk, inf);
-                consume(cb, v, jk, inf);
-            }
+            issue(cb, v, jk, inf);
+            consume(cb, v, jk, inf);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1368,12 +1115,12 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                 l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work, [&](uint32_t r) {
                     blk_q0 = set_block_patch_stash<PROTO, HC>(nh, st, r, c0, head[wv][lane]);
                     if (!blk_q0)
-                        set_field_store<PROTO>(nh, st, r, 0, 1, true);
+                        set_field_store<PROTO>(nh, st, r, true);
                 });
             else if (SET && !DEFER && CLK_SET_REGBLK)
                 l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work, [&](uint32_t r) {
                     if (!set_block_store_stash<PROTO, HC>(nh, st, r, c0, head[wv][lane]))
-                        set_field_store<PROTO>(nh, st, r, 0, 1, true);
+                        set_field_store<PROTO>(nh, st, r, true);
                 });
             else
                 l4_finish<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work);
@@ -1688,230 +1435,37 @@ __global__ void __launch_bounds__(256) ip_out_kernel(BatchArgs b, IpOutArgs c, u
 // ---------------------------------------------------------------------------
 // Deferred Set stores.  Writing the 2-byte checksum field into the packet
 // while the same kernel streams packet bytes in costs far more than its
-// bytes (DESIGN.md "Set stores"); the two-phase Set computes in a read-only
-// pass (field value + transport offset into work[]) and this pass scatters
-// the fields: base + off_i + field_at(work) <- value for work bit 31.
-// FIELD_BASE: 10 for ip_sum (work = 0x80000000 | value), or the transport
-// field offset (6 / 16) added to the hl packed in work bits 16..23.
+// bytes (DESIGN.md "Why Set is slower"); the two-phase Set computes in a
+// read-only pass (field value + transport offset into work[]) and this pass
+// scatters the fields: base + off_i + hl + FIELD <- value for work bit 31
+// (hl in work bits 16..23).  Nontemporal stores, so the partial-block write
+// reaches HBM inside this kernel instead of lingering dirty in the caches
+// until the next kernel's reads evict it.
 // ---------------------------------------------------------------------------
-#ifndef CLK_SCATTER_ST
-#define CLK_SCATTER_ST 1   // field stores: 0 plain, 1 nontemporal (default), 2 sc0 sc1, 3 sc0 sc1 nt
-#endif
 __device__ __forceinline__ void scatter_st_u16(uint8_t *p, uint32_t v)
 {
-    if (CLK_SCATTER_ST == 0 || ((uint64_t)p & 1)) {
+    if ((uint64_t)p & 1)
         st_u16(p, v);
-    } else if (CLK_SCATTER_ST == 1) {
+    else
         __builtin_nontemporal_store((uint16_t)v, (__attribute__((address_space(1))) uint16_t *)p);
-    } else if (CLK_SCATTER_ST == 2) {
-        asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"((uint64_t)p), "v"(v) : "memory");
-    } else {
-        asm volatile("global_store_short %0, %1, off sc0 sc1 nt" ::"v"((uint64_t)p), "v"(v) : "memory");
-    }
 }
 
-// CLK_SCATTER_BLOCK (tuning): 4 lanes per packet read the field's 64 B
-// block, patch it and store it whole, nontemporal -- one full-block write
-// per field instead of a read-modify-write at the memory controller.
-#ifndef CLK_SCATTER_BLOCK
-#define CLK_SCATTER_BLOCK 0
-#endif
-#ifndef CLK_SCATTER_UNROLL
-#define CLK_SCATTER_UNROLL 1
-#endif
 template <int FIELD>
-__global__ void __launch_bounds__(256) field_scatter_block_kernel(BatchArgs b, const uint32_t *work,
-                                                                  uint8_t *out_code, uint16_t *out_sum)
+__global__ void __launch_bounds__(256) field_scatter_kernel(BatchArgs b, const uint32_t *work, uint8_t *out_code,
+                                                            uint16_t *out_sum)
 {
-    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < 4 * b.n; j += nthreads) {
-        const uint64_t i = j >> 2;
-        const uint32_t q = (uint32_t)j & 3;
-        const uint32_t w = work[i];
-        if (w & 0x80000000u) {
-            uint8_t *nh = b.base + pkt_off(b, i);
-            const uint64_t a = (uint64_t)nh, fa = a + ((w >> 16) & 0xFF) + FIELD, blk = fa & ~63ull;
-            if (blk >= a && blk + 64 <= a + pkt_len(b, i) && fa + 1 < blk + 64) {
-                const uint64_t ca = blk + 16ull * q;
-                u32x4 v = gload16(ca);
-                patch_byte(v, ca, fa, w);
-                patch_byte(v, ca, fa + 1, w >> 8);
-                __builtin_nontemporal_store(v, (__attribute__((address_space(1))) u32x4 *)ca);
-            } else if (q == 0) {
-                scatter_st_u16(nh + ((w >> 16) & 0xFF) + FIELD, w & 0xFFFF);
-            }
-        }
-        if (q == 0) {
-            out_code[i] = (w & 0x80000000u) ? 0 : (uint8_t)w;
-            if (out_sum)
-                out_sum[i] = (w & 0x80000000u) ? (uint16_t)w : 0;
-        }
-    }
-}
-
-template <int FIELD_BASE, bool L4>
-__global__ void __launch_bounds__(256) field_scatter_kernel(BatchArgs b, const uint32_t *work,
-                                                            const uint8_t *status, const uint16_t *sums,
-                                                            uint8_t *out_code, uint16_t *out_sum)
-{
-    // L4: the compute pass wrote only work[i] (bit 31: the field value, else
-    // the status code); this pass writes the field and, one lane per packet,
-    // the status codes and sums -- 64 consecutive packets per wave, so whole
+    // the compute pass wrote only work[i] (bit 31: the field value, else the
+    // status code); this pass writes the field and, one lane per packet, the
+    // status codes and sums -- 64 consecutive packets per wave, so whole
     // output blocks
     const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
-    if (L4 && CLK_SCATTER_UNROLL > 1) {     // tuning: U work words loaded before the stores
-        constexpr int U = CLK_SCATTER_UNROLL;
-        for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < b.n; i0 += U * nthreads) {
-            uint32_t w[U];
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                w[u] = i0 + u * nthreads < b.n ? work[i0 + u * nthreads] : 0u;
-#pragma unroll
-            for (int u = 0; u < U; u++) {
-                const uint64_t i = i0 + u * nthreads;
-                if (i < b.n) {
-                    if (w[u] & 0x80000000u)
-                        scatter_st_u16(b.base + pkt_off(b, i) + ((w[u] >> 16) & 0xFF) + FIELD_BASE, w[u] & 0xFFFF);
-                    out_code[i] = (w[u] & 0x80000000u) ? 0 : (uint8_t)w[u];
-                    if (out_sum)
-                        out_sum[i] = (w[u] & 0x80000000u) ? (uint16_t)w[u] : 0;
-                }
-            }
-        }
-        return;
-    }
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < b.n; i += nthreads) {
-        if (L4) {
-            const uint32_t w = work[i];
-            if (w & 0x80000000u)
-                scatter_st_u16(b.base + pkt_off(b, i) + ((w >> 16) & 0xFF) + FIELD_BASE, w & 0xFFFF);
-            out_code[i] = (w & 0x80000000u) ? 0 : (uint8_t)w;
-            if (out_sum)
-                out_sum[i] = (w & 0x80000000u) ? (uint16_t)w : 0;
-        } else if (status[i] == 0) {
-            scatter_st_u16(b.base + pkt_off(b, i) + FIELD_BASE, sums[i]);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// Size classes for variable-length batches (IMIX).  One geometry cannot fit
-// 64 B and 1500 B packets at once (a 16-lane group on a 64 B packet idles
-// 12 lanes; a lane per 1500 B packet serialises 12 passes), so a stable
-// partition by size class -- count, scan, scatter of packet indices -- lets
-// each class run with its own lanes-per-packet G = 1 << class.
-// ---------------------------------------------------------------------------
-constexpr int NCLASS = 7;                       // G = 1, 2, 4, ..., 64
-constexpr uint32_t BIN_TILE = 4096;             // packets per block in the bin kernels
-
-template <int K>
-__device__ __forceinline__ uint32_t size_class(uint32_t len)
-{
-    const uint32_t nch = len / 16 + 2;          // chunks of a range at the worst alignment
-    uint32_t c = 0;
-    while (c < NCLASS - 1 && nch > (uint32_t)K << c)
-        c++;
-    return c;
-}
-
-template <int K>
-__global__ void __launch_bounds__(256) bin_count_kernel(const uint32_t *len, uint64_t n, uint32_t *counts,
-                                                        uint32_t nblocks)
-{
-    __shared__ uint32_t h[NCLASS];
-    if (threadIdx.x < NCLASS)
-        h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint64_t lo = (uint64_t)blockIdx.x * BIN_TILE;
-    const uint64_t hi = lo + BIN_TILE < n ? lo + BIN_TILE : n;
-    for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x)
-        atomicAdd(&h[size_class<K>(len[i])], 1u);
-    __syncthreads();
-    if (threadIdx.x < NCLASS)
-        counts[threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
-}
-
-// One block: exclusive scan of counts in class-major order (in place), and
-// the class ranges range[2c], range[2c+1] = [start, end) into perm.
-__global__ void __launch_bounds__(1024) bin_scan_kernel(uint32_t *counts, uint32_t nblocks, uint64_t *range,
-                                                        uint64_t n)
-{
-    __shared__ uint64_t part[1024];
-    __shared__ uint64_t cstart[NCLASS];
-    const uint64_t total = (uint64_t)NCLASS * nblocks;
-    const uint64_t per = (total + blockDim.x - 1) / blockDim.x;
-    const uint64_t lo = threadIdx.x * per < total ? threadIdx.x * per : total;
-    const uint64_t hi = lo + per < total ? lo + per : total;
-    uint64_t s = 0;
-    for (uint64_t k = lo; k < hi; k++)
-        s += counts[k];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t run = 0;
-        for (uint32_t t = 0; t < blockDim.x; t++) {
-            const uint64_t v = part[t];
-            part[t] = run;
-            run += v;
-        }
-    }
-    __syncthreads();
-    uint64_t run = part[threadIdx.x];
-    for (uint64_t k = lo; k < hi; k++) {
-        const uint32_t v = counts[k];
-        counts[k] = (uint32_t)run;
-        if (k % nblocks == 0)
-            cstart[k / nblocks] = run;                  // first block of class k / nblocks
-        run += v;
-    }
-    __syncthreads();
-    if (threadIdx.x < NCLASS) {
-        const uint32_t c = threadIdx.x;
-        range[2 * c] = cstart[c];
-        range[2 * c + 1] = c + 1 < NCLASS ? cstart[c + 1] : n;
-    }
-}
-
-// Stable scatter: block b writes the indices of its tile, class by class, in
-// packet order, at the offsets bin_scan_kernel produced.
-template <int K>
-__global__ void __launch_bounds__(256) bin_scatter_kernel(const uint32_t *len, uint64_t n, const uint32_t *offsets,
-                                                          uint32_t nblocks, uint32_t *perm)
-{
-    __shared__ uint32_t base[NCLASS];
-    __shared__ uint32_t wave_cnt[4][NCLASS];
-    if (threadIdx.x < NCLASS)
-        base[threadIdx.x] = offsets[threadIdx.x * nblocks + blockIdx.x];
-    __syncthreads();
-    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t lo = (uint64_t)blockIdx.x * BIN_TILE;
-    const uint64_t hi = lo + BIN_TILE < n ? lo + BIN_TILE : n;
-    for (uint64_t s0 = lo; s0 < hi; s0 += blockDim.x) {
-        const uint64_t i = s0 + threadIdx.x;
-        const bool live = i < hi;
-        const uint32_t c = live ? size_class<K>(len[i]) : NCLASS;
-        uint32_t rank = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < NCLASS; k++) {
-            const uint64_t m = __ballot(c == k);
-            if (c == k)
-                rank = __popcll(m & ((1ull << lane) - 1));
-            if (lane == 0)
-                wave_cnt[wv][k] = (uint32_t)__popcll(m);
-        }
-        __syncthreads();
-        if (live) {
-            uint32_t before = 0;
-            for (uint32_t w = 0; w < wv; w++)
-                before += wave_cnt[w][c];
-            perm[base[c] + before + rank] = (uint32_t)i;
-        }
-        __syncthreads();
-        if (threadIdx.x < NCLASS) {
-            const uint32_t k = threadIdx.x;
-            base[k] += wave_cnt[0][k] + wave_cnt[1][k] + wave_cnt[2][k] + wave_cnt[3][k];
-        }
-        __syncthreads();
+        const uint32_t w = work[i];
+        if (w & 0x80000000u)
+            scatter_st_u16(b.base + pkt_off(b, i) + ((w >> 16) & 0xFF) + FIELD, w & 0xFFFF);
+        out_code[i] = (w & 0x80000000u) ? 0 : (uint8_t)w;
+        if (out_sum)
+            out_sum[i] = (w & 0x80000000u) ? (uint16_t)w : 0;
     }
 }
 

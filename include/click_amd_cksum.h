@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CLK_ABI_VERSION 4
+#define CLK_ABI_VERSION 5
 
 /* ---- return codes -------------------------------------------------------- */
 #define CLK_SUCCESS 0
@@ -94,11 +94,24 @@ void *clk_ctx_own_stream(clk_ctx *ctx);
 int clk_ctx_sync(clk_ctx *ctx);
 int clk_ctx_device(clk_ctx *ctx);
 /* Pre-size the context's device scratch for batches of up to max_packets
- * (about 8 bytes per packet: the two-phase UDP/TCP Set's work array and the
- * size-class partition of variable-length batches); without it the first
- * larger batch allocates synchronously.  After a reserve, batched
+ * (4 bytes per packet: the two-phase UDP/TCP Set's work array); without it
+ * the first larger batch allocates synchronously.  After a reserve, batched
  * calls of that size allocate nothing (safe inside hipGraph capture). */
 int clk_ctx_reserve(clk_ctx *ctx, uint64_t max_packets);
+/* Speed-only tuning of one context (tools/tune.py; defaults are the measured
+ * best).  No setting changes any result: every kernel choice
+ * they select is bit-exact against the reference.  Nothing is read from the
+ * environment.  CLK_EINVAL for an unknown knob or an out-of-range value.   */
+enum clk_tune_knob {
+    CLK_TUNE_MAX_BLOCKS = 1,          /* grid cap of every launch (default 262144)       */
+    CLK_TUNE_SCATTER_BLOCKS = 2,      /* grid cap of the two-phase Set's scatter (16384) */
+    CLK_TUNE_SET_MODE = 3,            /* -1 auto, 0 fused Set, 1 two-phase Set           */
+    CLK_TUNE_STREAM_MIN = 4,          /* len[] batches of >= this many packets run by the
+                                         packet-stream kernel (65536)                     */
+    CLK_TUNE_GROUP = 5                /* lanes per packet of the fixed-geometry kernels:
+                                         0 (by max_len), 1, 2, 4, ..., 64                 */
+};
+int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value);
 /* Last error text for `ctx` (or for the calling thread when ctx == NULL). */
 const char *clk_last_error(clk_ctx *ctx);
 int clk_abi_version(void);
@@ -120,10 +133,10 @@ typedef struct clk_batch {
     const uint32_t *len;
     uint32_t fixed_len;
     uint32_t max_len;   /* optional upper bound on len_i (0 = unknown).  With
-                           len != NULL, large batches are partitioned by
-                           size class on the device and each class runs with
-                           its own lanes-per-packet; smaller ones use one
-                           geometry picked from max_len                      */
+                           len != NULL, large batches run by the packet-stream
+                           kernel (whole-chunk sums, lengths free per packet);
+                           smaller ones in one lanes-per-packet geometry
+                           picked from max_len                               */
     uint64_t n;
 } clk_batch;
 

@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
         assert name in _abi.SIGNATURES, "ctypes binding lacks " + name
-    assert lib.clk_abi_version() == 4
+    assert lib.clk_abi_version() == 5
 
 
 def test_codes_agree_with_header_and_oracle():

@@ -315,13 +315,12 @@ def test_dec_ttl_full_size(torch, ctx):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
-def test_set_modes_bit_exact(torch, mode, monkeypatch):
+@pytest.mark.parametrize("mode", [0, 1])
+def test_set_modes_bit_exact(torch, mode):
     """Fused (mode 0) and two-phase (mode 1, compute then scatter) Set
     kernels give identical results on fuzzed batches."""
     import click_amd
-    monkeypatch.setenv("CLK_SET_MODE", mode)
-    c = click_amd.Context(0)
+    c = click_amd.Context(0).tune(set_mode=mode)
     rng = np.random.default_rng(31)
     for proto in (17, 6):
         arena, off, caplen, ml = fuzz.make_batch(rng, 1500, proto, max_total=1600)
@@ -335,18 +334,15 @@ def test_set_modes_bit_exact(torch, mode, monkeypatch):
     c.close()
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
-def test_stream_set_modes_bit_exact(torch, mode, monkeypatch):
+@pytest.mark.parametrize("mode", [0, 1])
+def test_stream_set_modes_bit_exact(torch, mode):
     """The packet-stream kernel's Sets: fused (mode 0: the patched 64 B
     blocks stored coalesced from the LDS stash, or the field alone when its
     block is not the packet's) and two-phase (mode 1: the compute pass
     stashes fewer chunks, then the nontemporal scatter), any alignment,
     FIXOFF on and off."""
     import click_amd
-    monkeypatch.setenv("CLK_SET_MODE", mode)
-    monkeypatch.setenv("CLK_BIN_MIN", "1")
-    monkeypatch.setenv("CLK_VARLEN", "2")
-    c = click_amd.Context(0)
+    c = click_amd.Context(0).tune(set_mode=mode, stream_min=1)
     rng = np.random.default_rng(57 + int(mode))
     for proto, mt in ((17, 1600), (6, 1600), (17, 200), (6, 9000)):
         for align in ("any", 64):
@@ -358,23 +354,20 @@ def test_stream_set_modes_bit_exact(torch, mode, monkeypatch):
     c.close()
 
 
-@pytest.mark.parametrize("bin_min,varlen", [("1", "2"), ("1", "1"), ("1", "0"), ("100000000", "1")])
-def test_size_class_partition_bit_exact(torch, bin_min, varlen, monkeypatch):
-    """Variable-length batches run by the packet-stream kernel (varlen 2),
-    the wave-cooperative range kernel (varlen 1), by size class
-    (count/scan/scatter of packet indices, one lanes-per-packet geometry per
-    class; varlen 0), or in one geometry: all identical and oracle-exact."""
+@pytest.mark.parametrize("stream_min,group", [(1, 0), (100000000, 0), (100000000, 4), (100000000, 64)])
+def test_variable_length_paths_bit_exact(torch, stream_min, group):
+    """Variable-length batches run by the packet-stream kernel (stream_min
+    1) or in one lanes-per-packet geometry (by max_len, or forced): all
+    identical and oracle-exact."""
     import click_amd
-    monkeypatch.setenv("CLK_BIN_MIN", bin_min)
-    monkeypatch.setenv("CLK_VARLEN", varlen)
-    c = click_amd.Context(0)
+    c = click_amd.Context(0).tune(stream_min=stream_min, group=group)
     rng = np.random.default_rng(41)
     for proto, mt in ((17, 1600), (6, 9000), (17, 200), (1, 1600)):
         arena, off, caplen, ml = fuzz.make_batch(rng, 2000, proto, max_total=mt)
         for op in ("in_cksum",) + OPS_L4[proto]:
             compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=1)
             compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=0, arg=1)
-    # IMIX-like sizes across many bin tiles (BIN_TILE = 4096 packets)
+    # IMIX-like sizes, packed at 64 B-aligned offsets
     n = 20000
     L = rng.choice(np.array([64, 576, 1500], np.uint32), n, p=[7 / 12, 4 / 12, 1 / 12]).astype(np.uint32)
     slot = (L + 63) // 64 * 64
@@ -387,4 +380,13 @@ def test_size_class_partition_bit_exact(torch, bin_min, varlen, monkeypatch):
     for op in ("set_udp", "check_udp", "in_cksum"):
         compare(torch, c, op, arena, n, off=off, length=L, max_len=1500)
         oracle_lib.batch(op, arena, n, off=off, length=L)
+    c.close()
+
+
+def test_tune_rejects_bad_values(torch):
+    import click_amd
+    c = click_amd.Context(0)
+    for k, v in (("group", 3), ("set_mode", 2), ("max_blocks", 0), ("stream_min", 0)):
+        with pytest.raises(click_amd.ClickAmdError):
+            c.tune(**{k: v})
     c.close()

@@ -24,18 +24,16 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# element -> kernels one call launches (two-phase Set = compute + scatter)
-# (fixed-geometry l4_kernel or the variable-length l4_varlen_kernel)
+# element -> kernels one call launches (two-phase Set = compute + scatter;
+# fixed-geometry l4_kernel or the variable-length l4_stream_kernel)
 ELEMENT_KERNELS = {
-    "CheckUDPHeader": ["l4_kernel<17, false", "l4_varlen_kernel<17, false", "l4_stream_kernel<17, false"],
-    "SetUDPChecksum": ["l4_kernel<17, true", "l4_varlen_kernel<17, true", "l4_stream_kernel<17, true",
-                       "field_scatter_kernel<6, true"],
-    "CheckTCPHeader": ["l4_kernel<6, false", "l4_varlen_kernel<6, false", "l4_stream_kernel<6, false"],
-    "SetTCPChecksum": ["l4_kernel<6, true", "l4_varlen_kernel<6, true", "l4_stream_kernel<6, true",
-                       "field_scatter_kernel<16, true"],
-    "CheckICMPHeader": ["l4_kernel<1, false", "l4_varlen_kernel<1, false", "l4_stream_kernel<1, false"],
+    "CheckUDPHeader": ["l4_kernel<17, false", "l4_stream_kernel<17, false"],
+    "SetUDPChecksum": ["l4_kernel<17, true", "l4_stream_kernel<17, true", "field_scatter_kernel<6>"],
+    "CheckTCPHeader": ["l4_kernel<6, false", "l4_stream_kernel<6, false"],
+    "SetTCPChecksum": ["l4_kernel<6, true", "l4_stream_kernel<6, true", "field_scatter_kernel<16>"],
+    "CheckICMPHeader": ["l4_kernel<1, false", "l4_stream_kernel<1, false"],
     "CheckIPHeader": ["ip_header_kernel<0"],
-    "SetIPChecksum": ["ip_header_kernel<2", "field_scatter_kernel<10"],
+    "SetIPChecksum": ["ip_header_kernel<2"],
     "DecIPTTL": ["dec_ttl_kernel"],
     "IPOutputCombo": ["ip_out_kernel<2"],
     "IPFragmenter": ["frag_plan_kernel", "frag_scan_kernel", "frag_write_kernel"],   # one launch (frag_write_kernel<true>) or three
