@@ -72,9 +72,10 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def imix_layout(torch, n, seed, first_idx):
-    """Packet sizes 64/576/1500 with P = 7/12, 4/12, 1/12 by hash; packed at
-    64 B-aligned offsets.  Returns (off int64, len int32, arena bytes, sum L)."""
+def imix_lengths(n, seed, first_idx):
+    """C4 packet lengths 64/576/1500 with P = 7/12, 4/12, 1/12, by a hash of
+    the global packet index (the same hash as oracle/cksum_oracle.c
+    imix_len)."""
     import numpy as np
     i = np.arange(first_idx, first_idx + n, dtype=np.uint64)
     with np.errstate(over="ignore"):
@@ -83,12 +84,73 @@ def imix_layout(torch, n, seed, first_idx):
         x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         x = x ^ (x >> np.uint64(31))
     r = (x % np.uint64(12)).astype(np.int64)
-    L = np.where(r < 7, 64, np.where(r < 11, 576, 1500)).astype(np.int64)
+    return np.where(r < 7, 64, np.where(r < 11, 576, 1500)).astype(np.int64)
+
+
+def imix_layout(torch, n, seed, first_idx):
+    """C4 packets [first_idx, first_idx + n) packed at 64 B-aligned offsets.
+    Returns (off int64, len int32, arena bytes, sum L)."""
+    import numpy as np
+    L = imix_lengths(n, seed, first_idx)
     slot = (L + 63) // 64 * 64
     off = np.zeros(n, np.int64)
     np.cumsum(slot[:-1], out=off[1:])
     total = int(off[-1] + slot[-1])
     return (torch.from_numpy(off).cuda(), torch.from_numpy(L.astype(np.int32)).cuda(), total, int(L.sum()))
+
+
+# Host-oracle verification of every timed element (SURVEY §8(e)(1)):
+# nanoseconds of one host thread per packet byte for oracle_digest (gen +
+# the Set and Check passes), used to size the verified range to the budget
+ORACLE_NS_PER_BYTE = 1.3
+VERIFY_BUDGET_S = float(os.environ.get("CLK_VERIFY_BUDGET_S", 20))     # bench-side: per workload and rank
+
+
+class OracleVerify:
+    """The oracle's digest (tests/oracle_lib.digest over oracle/cksum_oracle.c
+    oracle_digest) of exactly this rank's work -- global packets
+    [first, first + m), m = n or the prefix that fits VERIFY_BUDGET_S on
+    `threads` host threads -- run in a background thread (ctypes releases
+    the GIL) while the GPU measures; joined before any host timing."""
+
+    def __init__(self, wname, elements, first, n, ttl_runs, threads):
+        import threading
+        w = WORKLOADS[wname]
+        mean_len = 354.33 if wname == "c4" else w["L"]
+        fit = int(VERIFY_BUDGET_S * 1e9 * threads / (ORACLE_NS_PER_BYTE * (mean_len + 64)))
+        self.m = min(n, max(fit, 1 << 16))
+        self.first, self.elements, self.result, self.error = first, elements, None, None
+        self.secs = None
+        kw = dict(elements=list(elements), proto=w["proto"], first_idx=first, n=self.m, fixed_len=w["L"],
+                  imix=wname == "c4", corrupt_seed=CORRUPT_SEED, corrupt_log2=CORRUPT_LOG2, ip_span=(12, 20),
+                  ttl_runs=ttl_runs, my_ip=0x18041A12, mtu=1500, threads=threads)
+
+        def run():
+            try:
+                from tests import oracle_lib
+                t0 = time.perf_counter()
+                self.result = oracle_lib.digest(**kw)
+                self.secs = time.perf_counter() - t0
+            except Exception as e:            # reported in the record
+                self.error = repr(e)
+        self.t = threading.Thread(target=run, daemon=True)
+        self.t.start()
+
+    def join(self):
+        self.t.join()
+        return self.result
+
+
+def verify_threads(world):
+    """Host threads for the oracle digest of one rank: the CPUs this process
+    may use (cgroup quota), shared by the node's ranks, one left for the
+    rank's launching thread."""
+    topo = host_topology()
+    ncpu = len(topo["cpus"])
+    if topo["quota"]:
+        ncpu = min(ncpu, max(1, int(topo["quota"])))
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", world))
+    return max(1, ncpu // max(1, local) - 1)
 
 
 def run_element(ctx, name, b, status):
@@ -112,30 +174,40 @@ def run_element(ctx, name, b, status):
         raise ValueError(name)
 
 
-def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, packets=None, coll_dev="cuda"):
+def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, packets=None, coll_dev="cuda",
+            verify=True):
     """Generate the shard in HBM, make every checksum valid (untimed), then
     time each of the workload's elements: warmup + `steps` launches between
     barriers + synchronize; HIP events on the launch stream give the kernel
     time.  Check elements run over a batch with 1 in 1024 packets corrupted
     (one flipped bit), so the drop path is inside the timed
     region; the corruption is undone before the next element.
+    Shards: contiguous global packet ranges; C4's are byte-balanced
+    (shard.balanced_cuts).  verify: the host oracle's digest of this rank's
+    packets (OracleVerify) is compared with the GPU's after the reduction.
     Returns {element: result}."""
     import click_amd
     from click_amd import shard
     w = dict(WORKLOADS[wname])
     n = packets or w["n"]
-    first, _ = shard.shard_range(rank, world, n * world)   # this rank's global packet indices
     if wname == "c4":
+        first = 0
+        if dist is not None:       # byte-balanced shards of the world * n packet batch
+            first, hi = shard.balanced_cuts(torch, dist, coll_dev, rank * n, imix_lengths(n, seed, rank * n))
+            n = hi - first
         off, ln, total, sum_l = imix_layout(torch, n, seed, first)
         arena = torch.empty(total, dtype=torch.uint8, device="cuda")
         b = click_amd.Batch(arena, n, off=off, length=ln, max_len=1500)
         ck_bytes = sum_l
         alg = {e: (sum_l + (ALG[e](0)) * n + 12 * n) for e in w["elements"]}   # + descriptor (off u64, len u32)
     else:
+        first, _ = shard.shard_range(rank, world, n * world)   # this rank's global packet indices
         arena = torch.empty(n * w["stride"], dtype=torch.uint8, device="cuda")
         b = click_amd.Batch(arena, n, stride=w["stride"], fixed_len=w["L"])
         ck_bytes = w["ck"] * n
         alg = {e: ALG[e](w["L"]) * n for e in w["elements"]}
+    shards = shard.all_gather_ints(torch, dist, coll_dev, [first, n, ck_bytes])   # [first, packets, bytes] per rank
+    ver = OracleVerify(wname, w["elements"], first, n, warmup + steps, verify_threads(world)) if verify else None
     status = torch.empty(n, dtype=torch.uint8, device="cuda")
     ctx.reserve(n)
     ctx.gen_packets(b, proto=w["proto"], seed=seed, first_idx=first)
@@ -188,15 +260,20 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, pa
             {"SetUDPChecksum": ctx.set_udp_checksum, "SetTCPChecksum": ctx.set_tcp_checksum,
              "SetIPChecksum": ctx.set_ip_checksum}[e](b, status=status, sums=sums)
         torch.cuda.synchronize()
-        dig = shard.digest(torch, status, sums)
+        dig = shard.digest(torch, status, sums, first)
+        # the same digest over the oracle-verified prefix of the shard
+        m = ver.m if ver else 0
+        sub = shard.digest(torch, status[:m], None if sums is None else sums[:m], first) if ver else None
         if corrupt:
             ctx.gen_corrupt(b, **corrupt)             # flip the same bits back (untimed)
-        dig.append(expect_drops)
-        wall, kernel_ms, dig = shard.reduce_results(torch, dist, coll_dev, wall, kernel_ms, dig)
+        wall, kernel_ms, dig, (expect_drops,), per_rank = shard.reduce_results(
+            torch, dist, coll_dev, wall, kernel_ms, dig, [expect_drops])
+        if sub is not None:
+            _, _, sub, _, _ = shard.reduce_results(torch, dist, coll_dev, 0.0, 0.0, sub)
         gather = None
         if dist is not None and sums is not None:
             # SURVEY §8(e) (2), untimed for the metric: every rank's checksums
-            # to rank 0 over the communicator, checked against the digest
+            # to rank 0 only (grouped send/recv), checked against the digest
             try:
                 dist.barrier()
                 torch.cuda.synchronize()
@@ -204,21 +281,45 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, pa
                 allsums = shard.gather_results(torch, dist, coll_dev, sums)
                 torch.cuda.synchronize()
                 g_ms = (time.perf_counter() - tg) * 1e3
-                gather = {"bytes_per_rank": 2 * n, "ms": round(g_ms, 3),
-                          "GBs_into_root": round(2 * n * world / (g_ms * 1e-3) / 1e9, 1)}
+                gather = {"bytes_into_root": 2 * (dig["packets"] - n), "ms": round(g_ms, 3),
+                          "GBs_into_root": round(2 * (dig["packets"] - n) / (g_ms * 1e-3) / 1e9, 1),
+                          "on_root_only": (allsums is not None) == (rank == 0)}
                 if allsums is not None:
-                    gather["matches_digest"] = int(allsums.to(torch.int64).sum()) == dig[2]
+                    gather["matches_digest"] = (int(allsums.to(torch.int64).sum()) == dig["sum16"]
+                                                and int(allsums.numel()) == dig["packets"])
             except Exception as ex:             # reported, not fatal
                 gather = {"error": repr(ex)}
         out[e] = dict(wall=wall, kernel_ms=kernel_ms, kernel_ms_min=min(kms), n=n, ck_bytes=ck_bytes,
-                      alg_bytes=alg[e], w=w, element=e, ok_total=dig[0], n_total=dig[1],
-                      digest={"ok": dig[0], "packets": dig[1], "sum16": dig[2], "xor16": dig[3],
-                              "drops": dig[1] - dig[0], "expected_drops": dig[4],
-                              "drops_exact": dig[1] - dig[0] == dig[4]}, gather=gather)
+                      alg_bytes=alg[e], w=w, element=e, ok_total=dig["ok"], n_total=dig["packets"],
+                      per_rank=per_rank, sub=sub, shards=shards,
+                      digest=dict(dig, drops=dig["packets"] - dig["ok"], expected_drops=expect_drops,
+                                  drops_exact=dig["packets"] - dig["ok"] == expect_drops),
+                      gather=gather)
         del sums
     del arena, status, b, l4sums
     torch.cuda.empty_cache()
+    if ver:
+        res = ver.join()
+        for e, r in out.items():
+            o = oracle_check(torch, dist, coll_dev, ver, res, e, r["sub"])
+            if "verified_packets" in o:
+                o["full_batch"] = o["verified_packets"] == r["digest"]["packets"]
+            r["digest"]["oracle"] = o
     return out
+
+
+def oracle_check(torch, dist, coll_dev, ver, res, e, sub):
+    """Reduce this rank's oracle digest of element e over ranks (every rank
+    joins the same collectives, with an error flag) and compare it field by
+    field with the GPU's digest of the same packets."""
+    from click_amd import shard
+    err = 1 if res is None else 0
+    od = {f: 0 if err else res[e][f] for f in shard.DIGEST_FIELDS}
+    _, _, od, (m_all, errs), _ = shard.reduce_results(torch, dist, coll_dev, 0.0, 0.0, od, [ver.m, err])
+    if errs:
+        return {"error": ver.error or "oracle digest failed on %d rank(s)" % errs}
+    return {"oracle_match": od == sub, "verified_packets": m_all, "host_digest": od,
+            "oracle_s_rank0": round(ver.secs or 0, 2)}
 
 
 CORRUPT_SEED, CORRUPT_LOG2 = 0xBAD, 10
@@ -284,8 +385,10 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
     kernel_ms = sum(kms) / len(kms)
     totals = [int(x) for x in r["totals"].cpu()]
     ok = int((port == 2).sum()) if totals == [2 * n, 976 * n] else 0
-    dig = [ok, n, totals[0], 0]
-    _, kernel_ms, dig = shard.reduce_results(torch, dist, coll_dev, 0.0, kernel_ms, dig)
+    dig = dict.fromkeys(shard.DIGEST_FIELDS, 0)
+    dig.update(ok=ok, packets=n)
+    _, kernel_ms, dig, (nfrag,), _ = shard.reduce_results(torch, dist, coll_dev, 0.0, kernel_ms, dig, [totals[0]])
+    dig = [dig["ok"], dig["packets"], nfrag]
     del arena, out, saved, port, first_len, frag_first
     torch.cuda.empty_cache()
     alg = (20 + 928 + 968 + 8) * n
@@ -476,6 +579,9 @@ def summarize(r, steps, wname):
                      "kernel_ms": round(r["kernel_ms"], 4), "kernel_ms_min": round(r["kernel_ms_min"], 4),
                      "alg_bytes_per_launch": r["alg_bytes"], "traffic_source": tsrc},
         "verify": r["digest"],
+        **({"per_rank": [{"wall_ms": round(w_ * 1e3, 3), "kernel_ms": round(k_, 4), "first": sh[0], "packets": sh[1],
+                          "bytes": sh[2]} for (w_, k_), sh in zip(r["per_rank"], r["shards"])]}
+           if len(r["per_rank"]) > 1 else {}),
         **({"gather_to_rank0": r["gather"]} if r.get("gather") else {}),
     }
 
@@ -801,6 +907,8 @@ def main():
     ap.add_argument("--no-frag", action="store_true", help="skip the IPFragmenter measurement (C3)")
     ap.add_argument("--skip", default="", help="comma list of side configurations to skip: c4,c5")
     ap.add_argument("--e2e", action="store_true", help="measure the host-resident end-to-end rates instead")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the host-oracle digest of each element's results (SURVEY §8(e)(1))")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -845,7 +953,7 @@ def main():
         return
     pk = args.packets or None
     meas = lambda wl: measure(torch, ctx, dist, rank, world, wl, args.steps, args.warmup, packets=pk,
-                              coll_dev=coll_dev)
+                              coll_dev=coll_dev, verify=not args.no_verify)
     main_res = meas(args.workload)
     c2 = None
     if args.workload != "c2" and not args.no_c2:

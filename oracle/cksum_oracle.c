@@ -758,8 +758,12 @@ void oracle_gen_packet(uint8_t *pkt, uint32_t length, int proto, uint64_t seed, 
     uint8_t hdr[40];
     for (uint32_t i = 0; i < length; i += 8) {
         uint64_t h = gen_word(seed, idx, i >> 3);
-        for (uint32_t k = 0; k < 8 && i + k < length; k++)
-            pkt[i + k] = (uint8_t)(h >> (8 * k));
+        if (i + 8 <= length) {
+            memcpy(pkt + i, &h, 8);              /* little-endian host: bytes h >> 8k */
+        } else {
+            for (uint32_t k = 0; i + k < length; k++)
+                pkt[i + k] = (uint8_t)(h >> (8 * k));
+        }
     }
     /* header words use counters past the payload's (w = 0x1FFF, 0x1FFE) */
     uint64_t a = gen_word(seed, idx, 0x1FFF), b = gen_word(seed, idx, 0x1FFE);
@@ -1024,4 +1028,153 @@ int oracle_cpu_baseline(const struct oracle_cb_cfg *cfg, const int *cpus, int nt
     free(a);
     free(th);
     return err ? -2 : 0;
+}
+
+/* ---- bench.py self-verification -------------------------
+ * The oracle's digest of exactly the work one rank of bench.py did, computed
+ * packet by packet from the global packet index, so a full-size GPU result
+ * is checked without holding the batch in host memory.  Per packet g in
+ * [first_idx, first_idx + n): generate it (oracle_gen_packet; C4: length
+ * imix_len(seed, g)), SetIPChecksum, then the L4 Set of `proto` (the bench's
+ * untimed preparation; their results are the Set elements' results, since a
+ * Set zeroes its field before summing).  Check legs: the packet with the
+ * bench's corruption applied (corrupt_kernel's pick and bit), then the
+ * element.  DecIPTTL / IPOutputCombo legs: TTL 255 + SetIPChecksum, then
+ * ttl_runs passes of the element; the last pass's code.
+ * Digest per leg: ok (code 0), packets, sum16 = sum of checksums, xor16,
+ * wsum16 = sum of checksum * w(g), wcode = sum of code * w(g), with
+ * w(g) = (g * 40503) mod 2^16 (position-weighted: a permutation of results
+ * changes it).  Threads take contiguous index ranges. */
+/* corrupt_kernel (click_amd/csrc/cksum_kernels.hh) on one packet of global
+ * index g: picked when the low rate_log2 bits of h are zero; flips bit
+ * (h >> 8) & 7 of byte lo + (h >> 20) % (hi' - lo).  Flipping twice
+ * restores it.  Returns 1 when a bit was flipped. */
+static int corrupt_one(uint8_t *p, uint32_t len, uint64_t seed, uint64_t g, uint32_t rate_log2,
+                       uint32_t lo_arg, uint32_t hi_arg)
+{
+    const uint64_t h = oracle_splitmix64(seed ^ (g * 0xD1B54A32D192ED03ull));
+    const uint64_t mask = rate_log2 >= 64 ? ~0ull : ((1ull << rate_log2) - 1);
+    if ((h & mask) != 0)
+        return 0;
+    const uint32_t lo = lo_arg != ~0u ? lo_arg : (len > 40 ? 40 : (len > 20 ? 20 : 0));
+    const uint32_t hi = hi_arg && hi_arg < len ? hi_arg : len;
+    if (hi <= lo)
+        return 0;
+    const uint32_t pos = lo + (uint32_t)((h >> 20) % (uint64_t)(hi - lo));
+    p[pos] ^= (uint8_t)(1u << ((h >> 8) & 7));
+    return 1;
+}
+
+struct dg_thread {
+    const struct oracle_digest_cfg *cfg;
+    uint64_t lo, hi;
+    struct oracle_digest_leg leg[ORACLE_DG_NLEGS];
+    int err;
+};
+
+static void dg_add(struct oracle_digest_leg *l, uint64_t g, int code, uint16_t sum)
+{
+    const uint64_t w = (g * 40503u) & 0xFFFF;
+    l->packets++;
+    l->ok += code == 0;
+    l->sum16 += sum;
+    l->xor16 ^= sum;
+    l->wsum16 += (uint64_t)sum * w;
+    l->wcode += (uint64_t)(uint8_t)code * w;
+}
+
+static void *dg_run(void *vp)
+{
+    struct dg_thread *a = (struct dg_thread *)vp;
+    const struct oracle_digest_cfg *c = a->cfg;
+    uint8_t *buf = 0;
+    if (posix_memalign((void **)&buf, 64, 65536 + 64)) {
+        a->err = 1;
+        return 0;
+    }
+    const int set_l4 = c->proto == 6 ? ORACLE_OP_SET_TCP : ORACLE_OP_SET_UDP;
+    const int check_l4 = c->proto == 6 ? ORACLE_OP_CHECK_TCP : ORACLE_OP_CHECK_UDP;
+    for (uint64_t g = a->lo; g < a->hi; g++) {
+        const uint32_t L = c->imix ? (uint32_t)imix_len(c->seed, g) : c->fixed_len;
+        if (L > 65536) { a->err = 1; break; }
+        oracle_gen_packet(buf, L, c->proto, c->seed, g);
+        uint16_t s_ip = 0, s_l4 = 0;
+        const int r_ip = run_one(ORACLE_OP_SET_IP, buf, L, 0, &s_ip);
+        const int r_l4 = run_one(set_l4, buf, L, 0, &s_l4);
+        if (c->legs & (1u << ORACLE_DG_SET_IP))
+            dg_add(&a->leg[ORACLE_DG_SET_IP], g, r_ip, s_ip);
+        if (c->legs & (1u << ORACLE_DG_SET_L4))
+            dg_add(&a->leg[ORACLE_DG_SET_L4], g, r_l4, s_l4);
+        uint16_t z;
+        if (c->legs & (1u << ORACLE_DG_CHECK_L4)) {
+            const int f = corrupt_one(buf, L, c->corrupt_seed, g, c->corrupt_log2, ~0u, 0);
+            dg_add(&a->leg[ORACLE_DG_CHECK_L4], g, run_one(check_l4, buf, L, 1, &z), 0);
+            if (f)
+                corrupt_one(buf, L, c->corrupt_seed, g, c->corrupt_log2, ~0u, 0);
+        }
+        if (c->legs & (1u << ORACLE_DG_CHECK_IP)) {
+            const int f = corrupt_one(buf, L, c->corrupt_seed, g, c->corrupt_log2, c->ip_lo, c->ip_hi);
+            dg_add(&a->leg[ORACLE_DG_CHECK_IP], g, run_one(ORACLE_OP_CHECK_IP, buf, L, 1, &z), 0);
+            if (f)
+                corrupt_one(buf, L, c->corrupt_seed, g, c->corrupt_log2, c->ip_lo, c->ip_hi);
+        }
+        if (c->legs & (1u << ORACLE_DG_DEC_TTL)) {
+            buf[8] = 255;
+            run_one(ORACLE_OP_SET_IP, buf, L, 0, &z);
+            int r = 0;
+            for (int k = 0; k < c->ttl_runs; k++)
+                r = run_one(ORACLE_OP_DEC_TTL, buf, L, 1, &z);
+            dg_add(&a->leg[ORACLE_DG_DEC_TTL], g, r, 0);
+        }
+        if (c->legs & (1u << ORACLE_DG_OUT_COMBO)) {
+            buf[8] = 255;
+            run_one(ORACLE_OP_SET_IP, buf, L, 0, &z);
+            int r = 0, prob = 0;
+            for (int k = 0; k < c->ttl_runs; k++)
+                r = oracle_ip_output_combo(buf, L, L, 0, c->my_ip, c->mtu, 0, &prob);
+            dg_add(&a->leg[ORACLE_DG_OUT_COMBO], g, r, 0);
+        }
+    }
+    free(buf);
+    return 0;
+}
+
+int oracle_digest(const struct oracle_digest_cfg *cfg, const int *cpus, int nthreads,
+                  struct oracle_digest_leg *out)
+{
+    if (!cfg || !out || nthreads < 1 || (!cfg->imix && cfg->fixed_len > 65536))
+        return -1;
+    memset(out, 0, ORACLE_DG_NLEGS * sizeof *out);
+    struct dg_thread *a = calloc((size_t)nthreads, sizeof *a);
+    pthread_t *th = calloc((size_t)nthreads, sizeof *th);
+    if (!a || !th) {
+        free(a); free(th);
+        return -2;
+    }
+    for (int t = 0; t < nthreads; t++) {
+        a[t].cfg = cfg;
+        a[t].lo = cfg->first_idx + cfg->n * (uint64_t)t / (uint64_t)nthreads;
+        a[t].hi = cfg->first_idx + cfg->n * (uint64_t)(t + 1) / (uint64_t)nthreads;
+    }
+    for (int t = 1; t < nthreads; t++)
+        pthread_create(&th[t], 0, dg_run, &a[t]);
+    dg_run(&a[0]);
+    for (int t = 1; t < nthreads; t++)
+        pthread_join(th[t], 0);
+    (void)cpus;
+    int err = 0;
+    for (int t = 0; t < nthreads; t++) {
+        err |= a[t].err;
+        for (int l = 0; l < ORACLE_DG_NLEGS; l++) {
+            out[l].ok += a[t].leg[l].ok;
+            out[l].packets += a[t].leg[l].packets;
+            out[l].sum16 += a[t].leg[l].sum16;
+            out[l].xor16 ^= a[t].leg[l].xor16;
+            out[l].wsum16 += a[t].leg[l].wsum16;
+            out[l].wcode += a[t].leg[l].wcode;
+        }
+    }
+    free(a);
+    free(th);
+    return err ? -3 : 0;
 }

@@ -124,6 +124,33 @@ struct oracle_cb_result {
 int oracle_cpu_baseline(const struct oracle_cb_cfg *cfg, const int *cpus, int nthreads,
                         struct oracle_cb_result *res);
 
+/* bench.py self-verification: the oracle's digest of one rank's work, packet
+ * by packet from global indices [first_idx, first_idx + n) (see the .c). */
+enum {
+    ORACLE_DG_CHECK_L4 = 0,   /* CheckUDPHeader / CheckTCPHeader on the corrupted packet */
+    ORACLE_DG_SET_L4 = 1,     /* SetUDPChecksum / SetTCPChecksum                          */
+    ORACLE_DG_CHECK_IP = 2,   /* CheckIPHeader, corruption in [ip_lo, ip_hi)              */
+    ORACLE_DG_SET_IP = 3,     /* SetIPChecksum                                            */
+    ORACLE_DG_DEC_TTL = 4,    /* DecIPTTL(MULTICAST true), ttl_runs passes from TTL 255   */
+    ORACLE_DG_OUT_COMBO = 5,  /* IPOutputCombo(my_ip, mtu), ttl_runs passes from TTL 255  */
+    ORACLE_DG_NLEGS = 6
+};
+struct oracle_digest_cfg {
+    int proto, imix;
+    uint32_t fixed_len;
+    uint32_t legs;            /* bit mask of ORACLE_DG_* */
+    uint64_t seed, first_idx, n;
+    uint64_t corrupt_seed;
+    uint32_t corrupt_log2, ip_lo, ip_hi;
+    int ttl_runs;
+    uint32_t my_ip, mtu;
+};
+struct oracle_digest_leg {
+    uint64_t ok, packets, sum16, xor16, wsum16, wcode;
+};
+int oracle_digest(const struct oracle_digest_cfg *cfg, const int *cpus, int nthreads,
+                  struct oracle_digest_leg *out);
+
 #ifdef __cplusplus
 }
 #endif

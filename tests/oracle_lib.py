@@ -141,3 +141,46 @@ def gen(arena, n, stride=0, fixed_len=0, off=None, length=None, proto=17, seed=0
     off = None if off is None else np.ascontiguousarray(off, np.uint64)
     length = None if length is None else np.ascontiguousarray(length, np.uint32)
     L.oracle_gen_batch(_np_ptr(arena), _np_ptr(off), stride, _np_ptr(length), fixed_len, n, proto, seed, first_idx)
+
+
+# oracle_digest legs (oracle/cksum_oracle.h) and the bench element each stands for
+DG_LEGS = ["check_l4", "set_l4", "check_ip", "set_ip", "dec_ttl", "out_combo"]
+DG_ELEMENT_LEG = {"CheckUDPHeader": "check_l4", "CheckTCPHeader": "check_l4", "SetUDPChecksum": "set_l4",
+                  "SetTCPChecksum": "set_l4", "CheckIPHeader": "check_ip", "SetIPChecksum": "set_ip",
+                  "DecIPTTL": "dec_ttl", "IPOutputCombo": "out_combo"}
+
+
+class DigestCfg(ctypes.Structure):
+    _fields_ = [("proto", ctypes.c_int), ("imix", ctypes.c_int), ("fixed_len", ctypes.c_uint32),
+                ("legs", ctypes.c_uint32), ("seed", ctypes.c_uint64), ("first_idx", ctypes.c_uint64),
+                ("n", ctypes.c_uint64), ("corrupt_seed", ctypes.c_uint64), ("corrupt_log2", ctypes.c_uint32),
+                ("ip_lo", ctypes.c_uint32), ("ip_hi", ctypes.c_uint32), ("ttl_runs", ctypes.c_int),
+                ("my_ip", ctypes.c_uint32), ("mtu", ctypes.c_uint32)]
+
+
+class DigestLeg(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_uint64) for f in ("ok", "packets", "sum16", "xor16", "wsum16", "wcode")]
+
+
+def digest(elements, proto, first_idx, n, fixed_len=0, imix=False, seed=0x5EED, corrupt_seed=0xBAD,
+           corrupt_log2=10, ip_span=(12, 20), ttl_runs=0, my_ip=0x18041A12, mtu=1500, threads=1):
+    """The oracle's digest of bench.py's work on global packets
+    [first_idx, first_idx + n) (oracle_digest): {element: {ok, packets,
+    sum16, xor16, wsum16, wcode}}."""
+    L = load_oracle()
+    L.oracle_digest.restype = ctypes.c_int
+    L.oracle_digest.argtypes = [ctypes.POINTER(DigestCfg), _P, ctypes.c_int, ctypes.POINTER(DigestLeg)]
+    c = DigestCfg()
+    c.proto, c.imix, c.fixed_len = proto, 1 if imix else 0, fixed_len
+    c.legs = 0
+    for e in elements:
+        c.legs |= 1 << DG_LEGS.index(DG_ELEMENT_LEG[e])
+    c.seed, c.first_idx, c.n = seed, first_idx, n
+    c.corrupt_seed, c.corrupt_log2, c.ip_lo, c.ip_hi = corrupt_seed, corrupt_log2, ip_span[0], ip_span[1]
+    c.ttl_runs, c.my_ip, c.mtu = ttl_runs, my_ip & 0xFFFFFFFF, mtu
+    out = (DigestLeg * len(DG_LEGS))()
+    rc = L.oracle_digest(ctypes.byref(c), None, max(1, threads), out)
+    if rc != 0:
+        raise RuntimeError("oracle_digest rc %d" % rc)
+    return {e: {f: int(getattr(out[DG_LEGS.index(DG_ELEMENT_LEG[e])], f)) for f, _ in DigestLeg._fields_}
+            for e in elements}

@@ -109,12 +109,12 @@ def test_c5_full_jumbo_shard(torch, ctx):
         torch.cuda.empty_cache()
 
 
-def run_bench(gpus, packets, extra_env=None):
+def run_bench(gpus, packets, skip="c4,c5", extra_env=None):
     env = dict(os.environ, CLK_BENCH_SAME_DEVICE="1", CLK_BENCH_BACKEND="gloo", **(extra_env or {}))
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--packets", str(packets),
            "--steps", "2", "--warmup", "1", "--no-c2", "--no-c1", "--no-cpu", "--no-peak", "--no-frag",
-           "--skip", "c4,c5"]
+           "--skip", skip]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -122,20 +122,44 @@ def run_bench(gpus, packets, extra_env=None):
     return json.loads(lines[0])
 
 
+def without_timing(v):
+    v = dict(v)
+    o = dict(v.pop("oracle"))
+    o.pop("oracle_s_rank0", None)
+    return v, o
+
+
 def test_bench_two_ranks_match_one(torch):
     """bench.py --gpus 2 launches two ranks itself (no WORLD_SIZE), reports
-    n_gpus 2, and the reduced digests equal one rank's over both shards."""
+    n_gpus 2, per-rank times and shards, the reduced digests equal one
+    rank's over both shards and the host oracle's (full batch), the Set's
+    checksums reach rank 0 only, and the C4 shards are byte-balanced."""
     n = 1 << 17
-    two = run_bench(2, n)
-    one = run_bench(1, 2 * n)
+    two = run_bench(2, n, skip="c5")
+    one = run_bench(1, 2 * n, skip="c5")
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1
     assert two["config"]["packets_per_gpu"] == n
-    for e in ("CheckUDPHeader", "SetUDPChecksum"):
-        assert two["elements"][e]["verify"] == one["elements"][e]["verify"], e
-        assert two["elements"][e]["verify"]["packets"] == 2 * n
-    chk = two["elements"]["CheckUDPHeader"]["verify"]
-    assert chk["drops_exact"] and chk["drops"] > 0
-    # the Set's checksums gathered to rank 0 agree with the reduced digest
-    g = two["elements"]["SetUDPChecksum"]["gather_to_rank0"]
-    assert g.get("matches_digest") is True, g
-    assert "gather_to_rank0" not in one["elements"]["SetUDPChecksum"]
+    for sect, elements in ((None, ("CheckUDPHeader", "SetUDPChecksum")),
+                           ("c4_imix", ("CheckUDPHeader", "SetUDPChecksum"))):
+        t_el = two["elements"] if sect is None else two[sect]["elements"]
+        o_el = one["elements"] if sect is None else one[sect]["elements"]
+        for e in elements:
+            tv, to = without_timing(t_el[e]["verify"])
+            ov, oo = without_timing(o_el[e]["verify"])
+            assert tv == ov, (sect, e)
+            assert to == oo and to["oracle_match"] is True and to["full_batch"] is True, (sect, e, to)
+            assert tv["packets"] == 2 * n
+            pr = t_el[e]["per_rank"]
+            assert len(pr) == 2 and "per_rank" not in o_el[e]
+            assert max(p["kernel_ms"] for p in pr) == t_el[e]["roofline"]["kernel_ms"]
+        chk = t_el["CheckUDPHeader"]["verify"]
+        assert chk["drops_exact"] and chk["drops"] > 0
+        # the Set's checksums gathered to rank 0 only, agreeing with the reduced digest
+        g = t_el["SetUDPChecksum"]["gather_to_rank0"]
+        assert g.get("matches_digest") is True and g.get("on_root_only") is True, g
+        assert "gather_to_rank0" not in o_el["SetUDPChecksum"]
+    # C4: byte-balanced shards of the 2n-packet IMIX batch
+    pr = two["c4_imix"]["elements"]["CheckUDPHeader"]["per_rank"]
+    assert pr[0]["first"] == 0 and pr[1]["first"] == pr[0]["packets"] and pr[0]["packets"] + pr[1]["packets"] == 2 * n
+    mean = (pr[0]["bytes"] + pr[1]["bytes"]) / 2
+    assert all(abs(p["bytes"] - mean) <= 1500 for p in pr), pr
