@@ -80,6 +80,34 @@ def build_examples(force=False):
     return out
 
 
+NATIVE_TESTS = ["hipcore_test"]
+
+
+def build_native_tests(force=False):
+    """Host-only C++ test programs (tests/native/*.cc) -> tests/native/bin/,
+    linked against the in-tree library and the test oracle (built here, on
+    the CPU; the GPU tests only run them)."""
+    lib = build_library()
+    oracle = build_oracle()
+    ndir = os.path.join(ROOT, "tests", "native")
+    os.makedirs(os.path.join(ndir, "bin"), exist_ok=True)
+    out = []
+    for name in NATIVE_TESTS:
+        src = os.path.join(ndir, name + ".cc")
+        exe = os.path.join(ndir, "bin", name)
+        deps = [src, lib, oracle, os.path.join(ROOT, "click_integration", "elements", "hip", "hipcore.hh")] + [
+            os.path.join(ROOT, "include", h) for h in ("click_amd_cksum.h", "click_amd_elements.h")]
+        if force or _stale(exe, deps):
+            subprocess.run(["g++", "-std=c++17", "-O2", "-g", "-Wall", "-Wextra", "-pthread",
+                            "-I" + os.path.join(ROOT, "include"), src,
+                            "-L" + PKG, "-lclick_amd_cksum", "-L" + os.path.join(ROOT, "oracle"), "-lcksum_oracle",
+                            "-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib",
+                            "-Wl,-rpath,$ORIGIN/../../../click_amd", "-Wl,-rpath,$ORIGIN/../../../oracle",
+                            "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
+        out.append(exe)
+    return out
+
+
 if __name__ == "__main__":
     force = "--force" in sys.argv
     print(build_library(force=force, verbose=True))
@@ -87,3 +115,5 @@ if __name__ == "__main__":
         print(build_oracle(force=force))
     if "--examples" in sys.argv:
         print(build_examples(force=force))
+    if "--native-tests" in sys.argv:
+        print(build_native_tests(force=force))

@@ -46,7 +46,12 @@ class Element:
 
     def last_error(self):
         return (self.lib.clk_element_last_error(self.h) or b"").decode()
-        self._keep = []          # host buffers that must outlive flush()
+
+    def abandon(self):
+        """Route every staged / in-flight packet as killed (clk_element_abandon)."""
+        k = int(self.lib.clk_element_abandon(self.h))
+        self._keep = []
+        return k
 
     def close(self):
         if getattr(self, "h", None):

@@ -177,8 +177,8 @@ BatchElement::BatchElement(clk_ctx *ctx, const std::string &name, int noutputs)
 
 void BatchElement::free_stage(Stage &g)
 {
-    for (void *q : {(void *)g.h_arena, (void *)g.h_off, (void *)g.h_len, (void *)g.h_codes, (void *)g.h_sums,
-                    (void *)g.h_anno, (void *)g.h_aux8})
+    for (void *q : {(void *)g.h_arena, (void *)g.h_back, (void *)g.h_off, (void *)g.h_len, (void *)g.h_codes,
+                    (void *)g.h_sums, (void *)g.h_anno, (void *)g.h_aux8})
         if (q)
             (void)hipHostFree(q);
     for (void *q : {(void *)g.d_arena, (void *)g.d_off, (void *)g.d_len, (void *)g.d_codes, (void *)g.d_sums,
@@ -339,6 +339,8 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
 // Test hook (clk_glue_inject_fault_internal): the n-th checked HIP call of
 // the flush path from now on fails as if the runtime had returned an error.
 static std::atomic<int> g_fault_at{0};
+// ... and with a negative value: the next completion wait fails (complete())
+static std::atomic<int> g_fault_complete{0};
 
 static hipError_t checked(hipError_t e)
 {
@@ -437,8 +439,15 @@ int BatchElement::launch(Stage &g)
             (e = checked(hipMemcpyAsync(g.h_sums, g.d_sums, n * 2, hipMemcpyDeviceToHost, s))) != hipSuccess)
             return launch_failed(g, e, "hipMemcpyAsync(checksums)");
         if (wants_arena_back()) {
+            // into h_back, not h_arena: if this batch fails after the copy,
+            // the retry starts from the bytes as staged (not rewritten twice)
+            if (!g.zc && host_grow(&g.h_back, &g.h_back_cap, g.h_used + 64, 0)) {
+                launch_failed(g, hipSuccess, "hipHostMalloc");
+                err_ = "out of pinned host memory";
+                return CLK_EINVAL;
+            }
             if (!g.zc &&
-                (e = checked(hipMemcpyAsync(g.h_arena, g.d_arena, g.h_used, hipMemcpyDeviceToHost, s))) != hipSuccess)
+                (e = checked(hipMemcpyAsync(g.h_back, g.d_arena, g.h_used, hipMemcpyDeviceToHost, s))) != hipSuccess)
                 return launch_failed(g, e, "hipMemcpyAsync(packets back)");
             if ((e = checked(hipMemcpyAsync(g.h_aux8, g.d_aux8, n, hipMemcpyDeviceToHost, s))) != hipSuccess)
                 return launch_failed(g, e, "hipMemcpyAsync(aux)");
@@ -455,15 +464,26 @@ int BatchElement::complete(Stage &g)
     if (!g.inflight)
         return 0;
     hipError_t e = checked(hipEventSynchronize((hipEvent_t)g.ev[2]));
+    if (g_fault_complete.exchange(0, std::memory_order_relaxed))
+        e = hipErrorInvalidValue;
     g.inflight = false;
+    int r = 0;
     if (e != hipSuccess) {
         err_ = std::string("hipEventSynchronize: ") + hipGetErrorString(e);
-        return CLK_EHIP;       // the batch stays staged; nothing is routed
+        r = CLK_EHIP;          // the batch stays staged; nothing is routed
+    } else if (g.n) {
+        r = verify(g.h_codes, g.n);          // a kernel's internal fault report
     }
-    if (g.n) {
-        int r = verify(g.h_codes, g.n);      // a kernel's internal fault report
-        if (r)
-            return r;
+    if (r) {
+        if (g.zc && !idempotent()) {
+            // the kernel may have rewritten the host packets in place: a
+            // retry would apply the element twice (a second TTL decrement, a
+            // fragment header fragmented again), so the batch is abandoned
+            const std::string why = err_;
+            abandon_stage(g);
+            err_ = why + " (ZEROCOPY batch of a rewriting element: its packets were killed, not retried)";
+        }
+        return r;
     }
     float ms = 0;
     if (g.n)
@@ -500,6 +520,32 @@ int BatchElement::complete(Stage &g)
     g.zc_host = nullptr;
     in_place_ = false;
     return 0;
+}
+
+// Route every packet of a stage as killed (CLK_PORT_KILL), in push order.
+int BatchElement::abandon_stage(Stage &g)
+{
+    if (g.inflight) {
+        (void)hipEventSynchronize((hipEvent_t)g.ev[2]);      // buffers quiet; errors ignored
+        g.inflight = false;
+    }
+    results_.reserve_more(g.pend.size());
+    for (const Pending &p : g.pend)
+        results_.push_back(Result{p.token, CLK_PORT_KILL, p.length, 0});
+    const int k = (int)g.pend.size();
+    lost_ += g.pend.size();
+    g.pend.clear();
+    g.h_used = 0;
+    g.zc_host = nullptr;
+    return k;
+}
+
+uint64_t BatchElement::abandon()
+{
+    // the older stage first: results stay in push order
+    uint64_t k = (uint64_t)abandon_stage(st_[cur_ ^ 1]);
+    k += (uint64_t)abandon_stage(st_[cur_]);
+    return k;
 }
 
 int BatchElement::flush_async()
@@ -539,7 +585,8 @@ void BatchElement::write_back(const Pending &p, uint32_t nbytes) const
 {
     if (in_place_)                       // zero-copy: the kernel wrote the packet itself
         return;
-    std::memcpy(p.data + p.span_off, rt_->h_arena + p.slot, std::min(nbytes, p.span_len));
+    std::memcpy(p.data + p.span_off, (wants_arena_back() ? rt_->h_back : rt_->h_arena) + p.slot,
+                std::min(nbytes, p.span_len));
 }
 
 uint32_t BatchElement::keep_packet(const uint8_t *bytes, uint32_t len)
@@ -572,6 +619,10 @@ std::string BatchElement::read_handler(const std::string &h) const
         return std::to_string(packets_);
     if (h == "gpu_ns")
         return std::to_string(gpu_ns_);
+    if (h == "lost")
+        return std::to_string(lost_);
+    if (h == "batch")
+        return std::to_string(batch_cap_);
     if (h == "device")
         return std::to_string(clk_ctx_device(ctx_));
     return std::string();
@@ -1673,7 +1724,13 @@ const char *clk_element_last_error(clk_element *w)
 
 void clk_glue_inject_fault_internal(int nth)
 {
+    if (nth < 0) {
+        clk::host::g_fault_complete.store(1, std::memory_order_relaxed);
+        return;
+    }
     clk::host::g_fault_at.store(nth, std::memory_order_relaxed);
+    if (nth == 0)
+        clk::host::g_fault_complete.store(0, std::memory_order_relaxed);
 }
 
 int clk_element_push(clk_element *w, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token)
@@ -1718,6 +1775,13 @@ int clk_element_flush_async(clk_element *w)
     if (!w)
         return CLK_EINVAL;
     return w->e->flush_async();
+}
+
+uint64_t clk_element_abandon(clk_element *w)
+{
+    if (!w)
+        return 0;
+    return w->e->abandon();
 }
 
 uint64_t clk_element_results(clk_element *w, uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint64_t cap)

@@ -106,6 +106,7 @@ class BatchElement {
     int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno = 0);
     int flush();          // run the staged batch, wait for every batch in flight, route
     int flush_async();    // route the batch in flight (if any), launch the staged one, return
+    uint64_t abandon();   // route every staged / in-flight packet as killed (a GPU that keeps failing)
     uint64_t pop_results(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap);
     int64_t take_packet(uint32_t key, uint8_t *buf, size_t cap);
     virtual std::string read_handler(const std::string &h) const;
@@ -137,6 +138,11 @@ class BatchElement {
     // copy the device batch back into the staging arena after run() (the
     // kernel rewrote bytes route() writes back into the packet)
     virtual bool wants_arena_back() const { return false; }
+    // false when running the element twice on the same packet bytes changes
+    // them again (DecIPTTL, IPGWOptions, IPOutputCombo, IPFragmenter): a
+    // ZEROCOPY batch of such an element whose kernel may have run is not
+    // retried after a failed completion but abandoned (its packets killed)
+    virtual bool idempotent() const { return true; }
     // upload anno & 0xFF of the staged packets; run() finds it in d_anno_
     virtual bool wants_anno() const { return false; }
     // called by flush() before route(): results() of the packet that precede
@@ -160,7 +166,7 @@ class BatchElement {
     int noutputs_;
     uint32_t batch_cap_ = 65536;
     std::string err_;
-    uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0;
+    uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0, lost_ = 0;
     bool zerocopy_ = false;          // ZEROCOPY: packets read/written in registered host memory
     bool in_place_ = false;          // routing a zero-copy batch: the kernel already wrote the packets
     // the launching stage's buffers (valid in run()) and the routing
@@ -179,6 +185,8 @@ class BatchElement {
         std::vector<Pending> pend;
         uint8_t *h_arena = nullptr;
         size_t h_arena_cap = 0, h_used = 0;
+        uint8_t *h_back = nullptr;          // the rewritten arena (wants_arena_back): h_arena stays as
+        size_t h_back_cap = 0;              // staged, so a failed batch is retried from its original bytes
         uint64_t *h_off = nullptr;
         uint32_t *h_len = nullptr;
         uint8_t *h_codes = nullptr, *h_anno = nullptr, *h_aux8 = nullptr;
@@ -202,6 +210,7 @@ class BatchElement {
     int launch(Stage &g);
     int launch_failed(Stage &g, hipError_t e, const char *what);
     int complete(Stage &g);
+    int abandon_stage(Stage &g);
     void free_stage(Stage &g);
     Stage st_[2];
     int cur_ = 0;
@@ -347,6 +356,7 @@ class DecIPTTL : public BatchElement {
     std::string read_handler(const std::string &h) const override;
 
   protected:
+    bool idempotent() const override { return false; }
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
@@ -368,6 +378,7 @@ class IPGWOptions : public BatchElement {
     std::string read_handler(const std::string &h) const override;
 
   protected:
+    bool idempotent() const override { return false; }
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
@@ -411,6 +422,7 @@ class IPOutputCombo : public BatchElement {
     std::string read_handler(const std::string &h) const override;
 
   protected:
+    bool idempotent() const override { return false; }
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void pre_route(Pending &p, ResultQueue &out) override;
@@ -437,6 +449,7 @@ class IPFragmenter : public BatchElement {
     std::string read_handler(const std::string &h) const override;
 
   protected:
+    bool idempotent() const override { return false; }
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;

@@ -1,0 +1,393 @@
+// -*- c-basic-offset: 4 -*-
+#ifndef CLICK_HIPCORE_HH
+#define CLICK_HIPCORE_HH
+/*
+ * hipcore.hh -- the Click-independent core of the GPU-backed elements'
+ * adapter (HIPBatchElement, hipbatch.hh): holding packets while their batch
+ * is on the GPU, tokens, routing results, the runcount, the latency flush,
+ * failed-flush retries and pull-mode batching.
+ *
+ * It is a template over the packet type P, the per-thread lock type L and
+ * the Host -- the adapter -- so the same code runs inside Click (P = Packet,
+ * L = Spinlock, Host = HIPBatchElement) and in tests/native/hipcore_test.cc
+ * (P = the test's packet, L = a std::mutex wrapper, Host = a test element
+ * that records its outputs), where it is driven on the GPU against the
+ * oracle.  Only include/click_amd_elements.h and the C++ library are used.
+ *
+ * Click's Element API hands over one packet at a time (element.cc:2891-2972);
+ * the GPU wants batches.  The reference classes on this path are agnostic
+ * (CheckIPHeader, CheckUDPHeader, CheckTCPHeader, CheckICMPHeader, DecIPTTL,
+ * SetUDPChecksum, IPGWOptions: PROCESSING_A_AH, checkipheader.hh:114;
+ * SetIPChecksum, SetTCPChecksum, FixIPSrc, IPInputCombo: AGNOSTIC, the
+ * default of element.cc:1127) or push (IPOutputCombo, IPFragmenter), so:
+ *   push context: push() stages the packet and holds it; a full batch is
+ *     launched double-buffered (the previous one is routed), a partial one
+ *     by the latency timer (timer()).  While a thread state holds packets it
+ *     holds one runcount reference (Router::adjust_runcount,
+ *     router.cc:832-846), so the router cannot stop before they are routed.
+ *   pull context: pull() on output 0 hands out one packet per call from a
+ *     ready queue; when it is empty, it pulls up to BATCH packets from input
+ *     0 (until the input returns null), runs them as one synchronous batch
+ *     and queues the output-0 packets; other results leave on their push
+ *     outputs as checked_output_push does (output 1 of a/ah).
+ * Results are taken from the glue under the thread state's lock but
+ * DELIVERED (annotations, output pushes) after it is released, in push
+ * order: a downstream element that re-enters this element on the same
+ * thread stages its packet and returns (the running delivery loop delivers
+ * the new results after the current ones), so there is no deadlock and no
+ * reordering.  cleanup() kills whatever is held; it pushes nothing
+ * downstream (router teardown may already have cleaned those elements up).
+ * A flush that fails leaves its batch staged (include/click_amd_elements.h);
+ * after `max_retries` consecutive failures the batch is abandoned
+ * (clk_element_abandon: every held packet killed, counted by the glue's
+ * "lost" handler) and the runcount released, so the router can stop.
+ *
+ * Host interface (all called on the thread that drives the core):
+ *   P *prepare(P *p, uint32_t *anno, P **extra)   before staging (uniqueify,
+ *        PaintTee clone ...); returns the packet to stage, 0 if consumed
+ *   uint8_t *data(P *p); uint32_t length(P *p); int32_t nh_offset(P *p)
+ *   bool primary(int32_t port, uint32_t aux)     false for a result that
+ *        comes with its packet's own (IPOutputCombo's clone, IPFragmenter's
+ *        fragments): the held packet stays
+ *   P *make_packet(clk_element *e, uint32_t key)  a new packet from the glue
+ *        (IPFragmenter's fragment), under the lock; 0 on failure
+ *   int finish(S &t, Routed &r, P **out)         the reference's side
+ *        effects for one result (no lock held); returns the output port of
+ *        the packet *out to emit, or -1 when nothing is emitted
+ *   void end_of_batch(S &t)                      after a batch's results
+ *   void output_push(int port, P *p)             checked_output_push
+ *   P *input_pull()                              input(0).pull(0)
+ *   void kill(P *p)
+ *   void adjust_runcount(int delta)
+ *   void schedule(S &t, unsigned ms); void unschedule(S &t); bool scheduled(S &t)
+ *   void chatter(const char *text)
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+#include <deque>
+#include <vector>
+#include "click_amd_elements.h"
+
+namespace hipcore {
+
+template <class P> struct Held {
+    P *p;           // the packet staged (writable if the element writes it)
+    P *extra;       // a second packet held with it (IPOutputCombo's PaintTee clone)
+    uint32_t anno;  // the CLK_ANNO_* bits it was staged with
+};
+
+// One result, handed to the host's finish() after the lock is released.
+template <class P> struct Routed {
+    P *p;           // the held packet (its primary result), 0 otherwise
+    P *extra;       // the held second packet (IPOutputCombo's clone result)
+    P *made;        // a new packet from the glue (IPFragmenter's fragment)
+    P *parent;      // for a fragment: the packet it was cut from (annotations)
+    uint32_t anno;
+    int32_t port;
+    uint32_t len, aux;
+    bool end;       // not a result: the end of a batch (host end_of_batch)
+};
+
+template <class P, class L> struct State {
+    clk_ctx *ctx;
+    clk_element *e;
+    int id;                       // the thread (Click: the RouterThread id)
+    std::deque<Held<P> > held;    // held[k] has token base + k
+    uint64_t base, next;
+    bool counted;                 // holds a runcount reference
+    unsigned fails;               // consecutive failed flushes
+    bool draining;                // a delivery loop is running on this state
+    std::vector<Routed<P> > outbox;
+    std::deque<P *> ready;        // pull context: output-0 packets ready to hand out
+    P *last_primary;              // route(): the packet of the last primary result
+    P *frag_parent;               // host use (IPFragmenter's first-fragment parent)
+    L lock;
+    State() : ctx(0), e(0), id(0), base(0), next(0), counted(false), fails(0), draining(false),
+              last_primary(0), frag_parent(0) { }
+};
+
+template <class P, class Host, class L> class Core {
+  public:
+    typedef State<P, L> S;
+    typedef Routed<P> R;
+
+    Core() : _batch(65536), _latency_ms(1), _max_retries(3) { }
+
+    void set_batch(uint32_t b)       { _batch = b ? b : 1; }
+    void set_latency(unsigned ms)    { _latency_ms = ms; }
+    void set_max_retries(unsigned k) { _max_retries = k ? k : 1; }
+    uint32_t batch() const           { return _batch; }
+
+    // ---- push context --------------------------------------------------------
+    void push(Host &h, S &t, P *p)
+    {
+        t.lock.acquire();
+        stage(h, t, p, true);
+        t.lock.release();
+        drain(h, t, false);
+    }
+
+    // the latency timer of state t fired: run its partial batch, route all
+    void timer(Host &h, S &t)
+    {
+        t.lock.acquire();
+        flush(h, t, true);
+        t.lock.release();
+        drain(h, t, false);
+    }
+
+    // ---- pull context (output 0) --------------------------------------------
+    P *pull(Host &h, S &t)
+    {
+        t.lock.acquire();
+        if (t.ready.empty()) {
+            t.lock.release();
+            // refill: up to one batch from the input, until it runs dry
+            uint32_t k = 0;
+            P *q;
+            while (k < _batch && (q = h.input_pull()) != 0) {
+                t.lock.acquire();
+                if (stage(h, t, q, false))
+                    k++;
+                t.lock.release();
+            }
+            t.lock.acquire();
+            if (k || !t.held.empty()) {
+                // synchronous: retried at once, abandoned after max_retries
+                while (!t.held.empty() && t.e) {
+                    flush(h, t, true);
+                    if (t.fails == 0 || !t.e)
+                        break;
+                }
+            }
+            t.lock.release();
+            drain(h, t, true);
+            t.lock.acquire();
+        }
+        P *p = 0;
+        if (!t.ready.empty()) {
+            p = t.ready.front();
+            t.ready.pop_front();
+        }
+        t.lock.release();
+        return p;
+    }
+
+    // ---- teardown: kill everything held; no downstream pushes ----------------
+    void cleanup(Host &h, S &t)
+    {
+        t.lock.acquire();
+        for (size_t i = 0; i < t.held.size(); i++) {
+            if (t.held[i].p)
+                h.kill(t.held[i].p);
+            if (t.held[i].extra)
+                h.kill(t.held[i].extra);
+        }
+        t.held.clear();
+        for (size_t i = 0; i < t.outbox.size(); i++) {
+            R &r = t.outbox[i];
+            if (r.p) h.kill(r.p);
+            if (r.extra) h.kill(r.extra);
+            if (r.made) h.kill(r.made);
+        }
+        t.outbox.clear();
+        while (!t.ready.empty()) {
+            h.kill(t.ready.front());
+            t.ready.pop_front();
+        }
+        if (t.frag_parent) {
+            h.kill(t.frag_parent);
+            t.frag_parent = 0;
+        }
+        if (t.counted) {
+            t.counted = false;
+            h.unschedule(t);
+            h.adjust_runcount(-1);
+        }
+        if (t.e) {
+            clk_element_destroy(t.e);
+            t.e = 0;
+        }
+        if (t.ctx) {
+            clk_ctx_destroy(t.ctx);
+            t.ctx = 0;
+        }
+        t.lock.release();
+    }
+
+  private:
+    // Stage one packet (locked).  Returns true if it is held.
+    bool stage(Host &h, S &t, P *p, bool push_ctx)
+    {
+        uint32_t anno = 0;
+        P *extra = 0;
+        if (!t.e) {                      // no GPU for this thread: as a failed uniqueify
+            h.kill(p);
+            return false;
+        }
+        if (!(p = h.prepare(p, &anno, &extra)))
+            return false;
+        Held<P> e = {p, extra, anno};
+        t.held.push_back(e);
+        if (push_ctx && !t.counted) {    // keep the router running until this batch is routed
+            h.adjust_runcount(1);
+            t.counted = true;
+            h.schedule(t, _latency_ms);
+        }
+        int r = clk_element_push_anno(t.e, h.data(p), h.length(p), h.nh_offset(p), anno, t.next);
+        if (r < 0) {                     // not staged (e.g. ZEROCOPY memory not registered)
+            h.chatter(clk_element_last_error(t.e));
+            t.held.pop_back();
+            h.kill(p);
+            if (extra)
+                h.kill(extra);
+            release_if_idle(h, t);
+            return false;
+        }
+        t.next++;
+        if (r == 1 && push_ctx)          // batch full: launch it, route the one before
+            flush(h, t, false);
+        return true;
+    }
+
+    // wait: route everything staged (timer, pull); otherwise double-buffered
+    // (launch the staged batch, route the previous one, return).  Locked.
+    void flush(Host &h, S &t, bool wait)
+    {
+        if (!t.e)
+            return;
+        int r = wait ? clk_element_flush(t.e) : clk_element_flush_async(t.e);
+        if (r != CLK_SUCCESS) {
+            // nothing of the failed batch was routed; it stays staged
+            t.fails++;
+            char buf[640];
+            if (t.fails >= _max_retries) {
+                uint64_t k = clk_element_abandon(t.e);
+                snprintf(buf, sizeof(buf), "GPU batch failed %u times, %llu packets killed: %s", t.fails,
+                         (unsigned long long) k, clk_element_last_error(t.e));
+                t.fails = 0;
+            } else
+                snprintf(buf, sizeof(buf), "GPU batch failed (retry %u of %u): %s", t.fails, _max_retries - 1,
+                         clk_element_last_error(t.e));
+            h.chatter(buf);
+        } else
+            t.fails = 0;
+        route(h, t);
+        release_if_idle(h, t);
+        if (t.counted && !h.scheduled(t))
+            h.schedule(t, _latency_ms);
+    }
+
+    void release_if_idle(Host &h, S &t)
+    {
+        if (t.held.empty() && t.counted) {
+            t.counted = false;
+            h.unschedule(t);
+            h.adjust_runcount(-1);       // stop may now proceed
+        }
+    }
+
+    // Move the glue's results into the outbox (locked).
+    void route(Host &h, S &t)
+    {
+        enum { CAP = 256 };
+        uint64_t tok[CAP];
+        int32_t port[CAP];
+        uint32_t len[CAP], aux[CAP];
+        uint64_t n;
+        bool any = false;
+        while ((n = clk_element_results_aux(t.e, tok, port, len, aux, CAP)) > 0) {
+            any = true;
+            for (uint64_t i = 0; i < n; i++) {
+                R r;
+                memset(&r, 0, sizeof(r));
+                r.port = port[i];
+                r.len = len[i];
+                r.aux = aux[i];
+                const bool have = tok[i] >= t.base && tok[i] - t.base < t.held.size();
+                Held<P> *e = have ? &t.held[(size_t) (tok[i] - t.base)] : 0;
+                if (e)
+                    r.anno = e->anno;
+                if (h.primary(port[i], aux[i])) {
+                    if (e) {
+                        r.p = e->p;
+                        e->p = 0;
+                        if (port[i] == CLK_PORT_KILL && e->extra) {   // e.g. a broadcast: no clone either
+                            r.extra = e->extra;
+                            e->extra = 0;
+                        }
+                    }
+                    t.last_primary = r.p;
+                } else if (aux[i] == CLK_AUX_CLONE) {
+                    if (e) {
+                        r.extra = e->extra;
+                        e->extra = 0;
+                    }
+                } else {                 // a new packet made by the element
+                    r.made = h.make_packet(t.e, aux[i]);
+                    r.parent = t.last_primary;
+                }
+                t.outbox.push_back(r);
+            }
+            while (!t.held.empty() && !t.held.front().p && !t.held.front().extra) {
+                t.held.pop_front();
+                t.base++;
+            }
+            if (n < CAP)
+                break;
+        }
+        if (any) {
+            R end;
+            memset(&end, 0, sizeof(end));
+            end.end = true;
+            t.outbox.push_back(end);
+        }
+    }
+
+    // Deliver the outbox in order, without the lock.  Re-entrant calls on
+    // the same state (a downstream element pushing back into this one) only
+    // append: the running loop delivers their results after these.
+    void drain(Host &h, S &t, bool pull_ctx)
+    {
+        std::vector<R> work;
+        t.lock.acquire();
+        if (t.draining) {
+            t.lock.release();
+            return;
+        }
+        t.draining = true;
+        while (!t.outbox.empty()) {
+            work.swap(t.outbox);
+            t.lock.release();
+            for (size_t i = 0; i < work.size(); i++) {
+                R &r = work[i];
+                if (r.end) {
+                    h.end_of_batch(t);
+                    continue;
+                }
+                P *out = 0;
+                int port = h.finish(t, r, &out);
+                if (port < 0 || !out)
+                    continue;
+                if (pull_ctx && port == 0) {
+                    t.lock.acquire();
+                    t.ready.push_back(out);
+                    t.lock.release();
+                } else
+                    h.output_push(port, out);
+            }
+            work.clear();
+            t.lock.acquire();
+        }
+        t.draining = false;
+        t.lock.release();
+    }
+
+    uint32_t _batch;
+    unsigned _latency_ms;
+    unsigned _max_retries;
+};
+
+} // namespace hipcore
+#endif

@@ -92,7 +92,8 @@ int clk_element_create(clk_ctx *ctx, const char *class_name, const char *config,
 int clk_element_destroy(clk_element *e);
 /* Why the element's last flush / push failed.  A flush that fails (a HIP
  * runtime error, or a kernel's internal fault report) routes nothing: the
- * batch stays staged and the next flush retries it.                       */
+ * batch stays staged, exactly as pushed, and the next flush retries it
+ * (except a ZEROCOPY batch of a rewriting element: clk_element_abandon). */
 const char *clk_element_last_error(clk_element *e);
 
 /* Stage one host packet.  data/length = Packet::data()/length();
@@ -129,6 +130,15 @@ int clk_element_flush(clk_element *e);
  * next batch while this one runs (push_burst flushes this way).  Results
  * of the launched batch arrive at the next flush / flush_async.           */
 int clk_element_flush_async(clk_element *e);
+
+/* Give up on the element's staged and in-flight packets (an adapter's retry
+ * limit after flushes keep failing): each is routed as CLK_PORT_KILL, in
+ * push order, and counted by the "lost" handler.  Returns how many.  A
+ * ZEROCOPY batch of an element that rewrites packets in place and is not
+ * idempotent (DecIPTTL, IPGWOptions, IPOutputCombo, IPFragmenter) is
+ * abandoned this way by the failing flush itself: its kernel may already
+ * have written the host packets, so it is never run twice.               */
+uint64_t clk_element_abandon(clk_element *e);
 
 /* Pop up to `cap` results: token, port (enum clk_port) and the packet's
  * new length (CheckIPHeader trims to ip_len, checkipheader.cc:216-217;

@@ -1,0 +1,38 @@
+"""The Click adapter's core (click_integration/elements/hip/hipcore.hh),
+Click-independent, driven on the GPU by tests/native/hipcore_test.cc with
+its own packet type, lock and host, every output checked against the CPU
+oracle: push context (double-buffered batches, latency timer, runcount),
+pull context (the reference classes are agnostic: PROCESSING_A_AH,
+checkipheader.hh:114), IPFragmenter extras, a failed flush and its retry
+(including the rewriting IPOutputCombo with the completion wait failing),
+the retry limit, a downstream element re-entering the element, four
+threads with home-thread timers, and cleanup of a held batch.
+The binary is built on the CPU by click_amd.build.build_native_tests()
+(__graft_entry__.build())."""
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "native", "bin", "hipcore_test")
+SCENARIOS = ["push_check_ip_header_double_buffered_and_timer", "pull_set_udp_checksum",
+             "ip_fragmenter_extras_and_annotations", "failed_flush_then_retry_SetUDPChecksum_fault4",
+             "failed_flush_then_retry_SetUDPChecksum_completion", "failed_flush_then_retry_IPOutputCombo_fault11",
+             "failed_flush_then_retry_IPOutputCombo_completion", "retry_limit_abandons_and_releases_runcount",
+             "reentrant_push_from_downstream", "four_threads_with_home_thread_timers",
+             "cleanup_kills_held_packets_pushes_nothing"]
+
+
+def test_adapter_core_on_gpu():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert os.path.exists(EXE), "build it first: python -m click_amd.build --native-tests"
+    r = subprocess.run([EXE], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-2000:]
+    passed = {l.split()[1] for l in r.stdout.splitlines() if l.startswith("PASS ")}
+    assert set(SCENARIOS) <= passed, set(SCENARIOS) - passed
+    assert "live packets at exit: 0" in r.stdout

@@ -106,3 +106,106 @@ def test_flush_failure_routes_nothing(ctx, nth):
     assert np.array_equal(arena, ref)
     assert e.read_handler("batches") == "1"
     e.close()
+
+
+def udp_600(n):
+    """n synthetic 600 B UDP/IPv4 packets (valid IP checksums) in 640 B
+    slots: longer than IPFragmenter(576)'s MTU."""
+    L, stride = 600, 640
+    arena = np.zeros(n * stride, np.uint8)
+    oracle_lib.gen(arena, n, stride=stride, fixed_len=L, proto=17, seed=7)
+    oracle_lib.batch("set_ip", arena, n, stride=stride, fixed_len=L)
+    return arena, L, stride
+
+
+# nth: the n-th checked HIP call of the flush fails (4: the packets' H2D,
+# before any kernel); -1: the completion wait, after the kernel ran and the
+# rewritten arena was copied back
+@pytest.mark.parametrize("cls,conf,nth", [("IPOutputCombo", "1, 18.26.4.24, 1500", k) for k in (4, 11, -1)] +
+                         [("IPFragmenter", "576", k) for k in (4, -1)] +
+                         [("DecIPTTL", "", k) for k in (4, -1)])
+def test_rewriting_element_retry_is_exact(ctx, cls, conf, nth):
+    """A rewriting element (IPOutputCombo, IPFragmenter, DecIPTTL) whose
+    flush fails at the n-th checked HIP call -- the completion wait
+    included, after the rewritten arena was copied back -- retries from the
+    bytes as staged: the packets are rewritten ONCE, exactly as the oracle
+    (the copy back went into the staging arena itself)."""
+    from click_amd import ClickAmdError
+    from click_amd.elements import Element
+    n = 200
+    arena, L, stride = udp_600(n)
+    ref = arena.copy()
+    if cls == "IPOutputCombo":
+        rc, _, _ = oracle_lib.ip_out_batch("ip_output_combo", ref, n, stride=stride, fixed_len=L, my_ip=0x18041A12,
+                                           mtu=1500)
+    elif cls == "DecIPTTL":
+        rc, _ = oracle_lib.batch("dec_ttl", ref, n, stride=stride, fixed_len=L)
+    else:
+        fr = oracle_lib.ip_fragment(ref, n, 576, True, stride=stride, fixed_len=L)
+        rc = fr["port"]
+    e = Element(ctx, cls, conf, noutputs=5 if cls == "IPOutputCombo" else 2)
+    ptrs = np.uint64(arena.ctypes.data) + np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    e.push_burst(ptrs, np.full(n, L, np.uint32), np.zeros(n, np.int32))
+    hook = ctx.lib.clk_glue_inject_fault_internal
+    hook.argtypes, hook.restype = [ctypes.c_int], None
+    hook(nth)
+    try:
+        with pytest.raises(ClickAmdError):
+            e.flush()
+    finally:
+        hook(0)
+    assert len(e.results()[0]) == 0
+    e.flush()
+    tok, port, ln, aux = e.results(aux=True)
+    prim = aux == 0 if cls == "IPFragmenter" else np.ones(len(tok), bool)
+    assert (tok[prim] == np.arange(n)).all()
+    if cls == "IPFragmenter":
+        assert (np.where(port[prim] == 0, np.where(ln[prim] < L, 2, 0), 1) == rc).all()
+        # first fragments written back in place, byte for byte
+        for i in range(n):
+            o = i * stride
+            assert np.array_equal(arena[o:o + int(fr["first_len"][i])], ref[o:o + int(fr["first_len"][i])]), i
+        extra = [e.take_packet(int(a)) for a in aux[~prim]]
+        assert extra == fr["frags"]
+    else:
+        assert (port == rc.astype(np.int32)).all()
+        assert np.array_equal(arena, ref)
+    e.close()
+
+
+def test_zerocopy_rewriting_batch_is_abandoned(ctx):
+    """ZEROCOPY DecIPTTL: the kernel decrements TTL in host memory itself,
+    so a batch whose completion wait fails is not retried (that would
+    decrement twice) but abandoned: every packet routed as killed, counted
+    by the "lost" handler, and no TTL decremented twice."""
+    from click_amd import ClickAmdError
+    from click_amd.elements import Element
+    n, L, stride = 300, 600, 640
+    raw = np.zeros(n * stride + 8192, np.uint8)
+    arena = raw[(-raw.ctypes.data) % 4096:][:n * stride]
+    a2, _, _ = udp_600(n)
+    arena[:] = a2
+    ttl0 = arena.reshape(n, stride)[:, 8].copy()
+    ctx.host_register(arena)
+    try:
+        e = Element(ctx, "DecIPTTL", "ZEROCOPY true", noutputs=2)
+        ptrs = np.uint64(arena.ctypes.data) + np.arange(n, dtype=np.uint64) * np.uint64(stride)
+        e.push_burst(ptrs, np.full(n, L, np.uint32), np.zeros(n, np.int32))
+        hook = ctx.lib.clk_glue_inject_fault_internal
+        hook.argtypes, hook.restype = [ctypes.c_int], None
+        hook(-1)                                   # the completion wait of the zero-copy flush
+        try:
+            with pytest.raises(ClickAmdError) as ei:
+                e.flush()
+        finally:
+            hook(0)
+        assert "not retried" in str(ei.value)
+        tok, port, _ = e.results()
+        assert (tok == np.arange(n)).all() and (port == -1).all()
+        assert e.read_handler("lost") == str(n)
+        e.flush()                                  # nothing left to retry
+        assert len(e.results()[0]) == 0
+        assert (arena.reshape(n, stride)[:, 8] >= ttl0 - 1).all()
+        e.close()
+    finally:
+        ctx.host_unregister(arena)
