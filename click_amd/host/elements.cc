@@ -245,8 +245,10 @@ int BatchElement::grow_host(Stage &g, size_t bytes, size_t n)
         return -1;
     if (g.h_n_cap < n) {
         size_t c1 = g.h_n_cap, c2 = g.h_n_cap, c3 = g.h_n_cap, c4 = g.h_n_cap, c5 = g.h_n_cap, c6 = g.h_n_cap;
-        if (host_grow(&g.h_off, &c1, n, 0) || host_grow(&g.h_len, &c2, n, 0) || host_grow(&g.h_codes, &c3, n, 0) ||
-            host_grow(&g.h_sums, &c4, n, 0) || host_grow(&g.h_anno, &c5, n, 0) || host_grow(&g.h_aux8, &c6, n, 0))
+        // h_off / h_len / h_anno hold the packets staged so far (filled at push)
+        if (host_grow(&g.h_off, &c1, n, g.ngpu) || host_grow(&g.h_len, &c2, n, g.ngpu) ||
+            host_grow(&g.h_codes, &c3, n, 0) || host_grow(&g.h_sums, &c4, n, 0) ||
+            host_grow(&g.h_anno, &c5, n, g.ngpu) || host_grow(&g.h_aux8, &c6, n, 0))
             return -1;
         g.h_n_cap = c1;
     }
@@ -279,12 +281,14 @@ int BatchElement::grow_dev(Stage &g, size_t bytes, size_t n)
     return 0;
 }
 
-int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
+template <class SpanF>
+inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token,
+                                  uint32_t anno)
 {
     Pending p{data, token, 0, length, nh_offset, 0, 0, 0, -1, (uint16_t)anno};
     uint32_t off = 0, len = 0;
     int32_t code = 0;
-    if (!span(p, &off, &len, &code)) {
+    if (!span_f(p, &off, &len, &code)) {
         p.host_code = (int16_t)code;
     } else if (zerocopy_) {
         // the kernel reads the span where it lies (clk_host_register)
@@ -315,10 +319,15 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
         p.slot = (uint64_t)(a - g.zc_host);
         p.span_off = off;
         p.span_len = len;
+        if (g.ngpu >= g.h_n_cap && grow_host(g, 0, g.ngpu + 1)) {
+            err_ = "out of pinned host memory";
+            return CLK_EINVAL;
+        }
     } else {
         Stage &g = st_[cur_];
         const size_t slot = (g.h_used + 63) & ~size_t(63);
-        if (grow_host(g, slot + len + 64, g.pend.size() + 1)) {
+        if ((slot + len + 64 > g.h_arena_cap || g.ngpu >= g.h_n_cap) &&
+            grow_host(g, slot + len + 64, g.ngpu + 1)) {
             err_ = "out of pinned host memory";
             return CLK_EINVAL;
         }
@@ -330,10 +339,47 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
         g.h_used = slot + len;
     }
     Stage &g = st_[cur_];
+    if (p.host_code < 0) {                                        // the GPU batch's SoA, filled here
+        p.index = (uint32_t)g.ngpu;
+        g.h_off[g.ngpu] = p.slot;
+        g.h_len[g.ngpu] = p.span_len;
+        g.h_anno[g.ngpu] = (uint8_t)p.anno;
+        g.maxlen = std::max(g.maxlen, p.span_len);
+        g.ngpu++;
+    }
     if (g.pend.capacity() < batch_cap_ && g.pend.empty())
         g.pend.reserve(std::min<size_t>(batch_cap_, 1u << 20));
     g.pend.push_back(p);
     return g.pend.size() >= batch_cap_ ? 1 : 0;
+}
+
+int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
+{
+    return push_one([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); }, data,
+                    length, nh_offset, token, anno);
+}
+
+template <class SpanF>
+int BatchElement::burst_loop(SpanF &&span_f, uint8_t *const *datas, const uint32_t *lengths,
+                             const int32_t *nh_offsets, uint64_t first_token, uint32_t n)
+{
+    for (uint32_t k = 0; k < n; k++) {
+        if (k + 8 < n)
+            __builtin_prefetch(datas[k + 8]);                     // the header span() reads
+        int r = push_one(span_f, datas[k], lengths[k], nh_offsets ? nh_offsets[k] : -1, first_token + k, 0);
+        if (r < 0)
+            return r;
+        if (r == 1 && (r = flush_async()) != 0)                  // stage the next batch while this one runs
+            return r;
+    }
+    return CLK_SUCCESS;
+}
+
+int BatchElement::push_burst(uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets,
+                             uint64_t first_token, uint32_t n)
+{
+    return burst_loop([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); },
+                      datas, lengths, nh_offsets, first_token, n);
 }
 
 // Test hook (clk_glue_inject_fault_internal): the n-th checked HIP call of
@@ -367,21 +413,12 @@ int BatchElement::launch_failed(Stage &g, hipError_t e, const char *what)
 int BatchElement::launch(Stage &g)
 {
     err_.clear();
-    size_t n = 0;
-    uint32_t maxlen = 0;
+    const size_t n = g.ngpu;                  // h_off / h_len / h_anno were filled at push
+    const uint32_t maxlen = g.maxlen;
     if (grow_host(g, g.h_used + 64, g.pend.size())) {
         err_ = "out of pinned host memory";
         return CLK_EINVAL;
     }
-    for (Pending &p : g.pend)
-        if (p.host_code < 0) {
-            g.h_off[n] = p.slot;
-            g.h_len[n] = p.span_len;
-            g.h_anno[n] = (uint8_t)p.anno;
-            p.index = (uint32_t)n;
-            maxlen = std::max(maxlen, p.span_len);
-            n++;
-        }
     g.n = n;
     g.zc = zerocopy_;
     hipStream_t s = (hipStream_t)clk_ctx_stream(ctx_);
@@ -491,6 +528,25 @@ int BatchElement::complete(Stage &g)
     rt_ = &g;
     h_aux8_ = g.h_aux8;
     in_place_ = g.zc;
+    route_stage(g);
+    batches_++;
+    packets_ += g.pend.size();
+    gpu_ns_ += (uint64_t)(ms * 1e6);
+    g.pend.clear();
+    g.h_used = 0;
+    g.ngpu = 0;
+    g.maxlen = 0;
+    g.zc_host = nullptr;
+    in_place_ = false;
+    return 0;
+}
+
+// Route a completed stage's packets in push order: the kernel's code (or the
+// host's decision) through the class's route(), plus the results that
+// precede / follow a packet's own (IPOutputCombo's clone, fragments).
+template <class RouteF>
+void BatchElement::route_loop(Stage &g, RouteF &&route_f)
+{
     size_t k = 0;
     const bool sums = wants_sums(), pre = has_pre_route_, post = has_post_route_;
     results_.reserve_more(g.pend.size());
@@ -507,19 +563,19 @@ int BatchElement::complete(Stage &g)
         Result r{p.token, 0, p.length, 0};
         if (pre)
             pre_route(p, results_);
-        route(p, code, sum, &r);
-        results_.push_back(r);
+        route_f(p, code, sum, &r);
+        if (pre || post)
+            results_.push_back(r);
+        else
+            results_.push_unchecked(r);
         if (post)
             post_route(p, code, results_);
     }
-    batches_++;
-    packets_ += g.pend.size();
-    gpu_ns_ += (uint64_t)(ms * 1e6);
-    g.pend.clear();
-    g.h_used = 0;
-    g.zc_host = nullptr;
-    in_place_ = false;
-    return 0;
+}
+
+void BatchElement::route_stage(Stage &g)
+{
+    route_loop(g, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
 }
 
 // Route every packet of a stage as killed (CLK_PORT_KILL), in push order.
@@ -536,6 +592,8 @@ int BatchElement::abandon_stage(Stage &g)
     lost_ += g.pend.size();
     g.pend.clear();
     g.h_used = 0;
+    g.ngpu = 0;
+    g.maxlen = 0;
     g.zc_host = nullptr;
     return k;
 }
@@ -1753,14 +1811,7 @@ int clk_element_push_burst(clk_element *w, uint8_t *const *datas, const uint32_t
 {
     if (!w || (n && (!datas || !lengths)))
         return CLK_EINVAL;
-    for (uint32_t k = 0; k < n; k++) {
-        int r = w->e->push(datas[k], lengths[k], nh_offsets ? nh_offsets[k] : -1, first_token + k);
-        if (r < 0)
-            return r;
-        if (r == 1 && (r = w->e->flush_async()) != 0)   // stage the next batch while this one runs
-            return r;
-    }
-    return CLK_SUCCESS;
+    return w->e->push_burst(datas, lengths, nh_offsets, first_token, n);
 }
 
 int clk_element_flush(clk_element *w)

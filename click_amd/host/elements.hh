@@ -7,6 +7,7 @@
 #pragma once
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -27,62 +28,88 @@ struct Result {
 };
 
 // Routed results in push order: appended by flush(), popped by the caller.
-// Struct of arrays with a read index: pops are bulk copies, storage is
-// reused once everything has been popped (no per-block allocations).
+// Struct of arrays over raw buffers with a read index: appends are plain
+// stores after one capacity check per batch (reserve_more), pops are bulk
+// copies, storage is reused once everything has been popped.
 class ResultQueue {
   public:
+    ResultQueue() = default;
+    ResultQueue(const ResultQueue &) = delete;
+    ResultQueue &operator=(const ResultQueue &) = delete;
+    ~ResultQueue()
+    {
+        std::free(tok_);
+        std::free(port_);
+        std::free(len_);
+        std::free(aux_);
+    }
     void reserve_more(size_t k)
     {
-        if (head_ > 4096 && head_ * 2 > tok_.size())      // a caller that never drains: drop the popped prefix
+        if (head_ > 4096 && head_ * 2 > n_)          // a caller that never drains: drop the popped prefix
             compact();
-        const size_t need = tok_.size() + k;
-        if (tok_.capacity() < need) {
-            tok_.reserve(need);
-            port_.reserve(need);
-            len_.reserve(need);
-            aux_.reserve(need);
-        }
+        if (n_ + k > cap_)
+            grow(n_ + k);
     }
     void push_back(const Result &r)
     {
-        tok_.push_back(r.token);
-        port_.push_back(r.port);
-        len_.push_back(r.length);
-        aux_.push_back(r.aux);
+        if (n_ == cap_)
+            grow(n_ + 1);
+        push_unchecked(r);
     }
-    bool empty() const { return head_ == tok_.size(); }
-    size_t size() const { return tok_.size() - head_; }
+    void push_unchecked(const Result &r)             // after reserve_more
+    {
+        tok_[n_] = r.token;
+        port_[n_] = r.port;
+        len_[n_] = r.length;
+        aux_[n_] = r.aux;
+        n_++;
+    }
+    bool empty() const { return head_ == n_; }
+    size_t size() const { return n_ - head_; }
     uint64_t pop(uint64_t *tokens, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap)
     {
         const size_t k = (size_t)std::min<uint64_t>(cap, size());
-        if (tokens) std::memcpy(tokens, tok_.data() + head_, k * sizeof(uint64_t));
-        if (ports) std::memcpy(ports, port_.data() + head_, k * sizeof(int32_t));
-        if (lengths) std::memcpy(lengths, len_.data() + head_, k * sizeof(uint32_t));
-        if (aux) std::memcpy(aux, aux_.data() + head_, k * sizeof(uint32_t));
+        if (tokens) std::memcpy(tokens, tok_ + head_, k * sizeof(uint64_t));
+        if (ports) std::memcpy(ports, port_ + head_, k * sizeof(int32_t));
+        if (lengths) std::memcpy(lengths, len_ + head_, k * sizeof(uint32_t));
+        if (aux) std::memcpy(aux, aux_ + head_, k * sizeof(uint32_t));
         head_ += k;
-        if (head_ == tok_.size()) {
-            tok_.clear();
-            port_.clear();
-            len_.clear();
-            aux_.clear();
-            head_ = 0;
-        }
+        if (head_ == n_)
+            head_ = n_ = 0;
         return k;
     }
 
   private:
+    void grow(size_t need)
+    {
+        const size_t c = std::max<size_t>(need, std::max<size_t>(cap_ * 2, 1024));
+        tok_ = (uint64_t *)realloc_or_die(tok_, c * sizeof(uint64_t));
+        port_ = (int32_t *)realloc_or_die(port_, c * sizeof(int32_t));
+        len_ = (uint32_t *)realloc_or_die(len_, c * sizeof(uint32_t));
+        aux_ = (uint32_t *)realloc_or_die(aux_, c * sizeof(uint32_t));
+        cap_ = c;
+    }
+    static void *realloc_or_die(void *p, size_t bytes)
+    {
+        void *q = std::realloc(p, bytes);
+        if (!q)
+            std::abort();                             // as std::vector's bad_alloc, without exceptions
+        return q;
+    }
     void compact()
     {
-        tok_.erase(tok_.begin(), tok_.begin() + (long)head_);
-        port_.erase(port_.begin(), port_.begin() + (long)head_);
-        len_.erase(len_.begin(), len_.begin() + (long)head_);
-        aux_.erase(aux_.begin(), aux_.begin() + (long)head_);
+        const size_t k = n_ - head_;
+        std::memmove(tok_, tok_ + head_, k * sizeof(uint64_t));
+        std::memmove(port_, port_ + head_, k * sizeof(int32_t));
+        std::memmove(len_, len_ + head_, k * sizeof(uint32_t));
+        std::memmove(aux_, aux_ + head_, k * sizeof(uint32_t));
+        n_ = k;
         head_ = 0;
     }
-    std::vector<uint64_t> tok_;
-    std::vector<int32_t> port_;
-    std::vector<uint32_t> len_, aux_;
-    size_t head_ = 0;
+    uint64_t *tok_ = nullptr;
+    int32_t *port_ = nullptr;
+    uint32_t *len_ = nullptr, *aux_ = nullptr;
+    size_t cap_ = 0, n_ = 0, head_ = 0;
 };
 
 // Click-style configuration: comma-separated arguments, "KEYWORD value".
@@ -97,6 +124,21 @@ bool parse_int(const std::string &s, long *v);
 bool parse_ip(const std::string &s, uint32_t *saddr);       // raw network-order s_addr
 bool parse_prefix(const std::string &s, uint32_t *saddr, uint32_t *mask);
 
+// The final classes' fast loops: push_burst() and route_stage() over the
+// class's own span() / route(), called qualified so they inline (no
+// virtual call per packet).
+#define CLK_GLUE_LOOPS(C)                                                                                       \
+    int push_burst(uint8_t *const *d_, const uint32_t *l_, const int32_t *nh_, uint64_t t0_, uint32_t n_) override \
+    {                                                                                                           \
+        return burst_loop([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {                       \
+            return this->C::span(p, o, l, c);                                                                   \
+        }, d_, l_, nh_, t0_, n_);                                                                               \
+    }                                                                                                           \
+    void route_stage(Stage &g_) override                                                                        \
+    {                                                                                                           \
+        route_loop(g_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
+    }
+
 class BatchElement {
   public:
     BatchElement(clk_ctx *ctx, const std::string &name, int noutputs);
@@ -104,6 +146,11 @@ class BatchElement {
     virtual const char *class_name() const = 0;
     virtual int configure(ConfArgs &args, std::string *err);
     int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno = 0);
+    // a burst of packets (tokens first_token + k), flushing double-buffered
+    // whenever the batch fills; the final classes run it with their span()
+    // inlined (CLK_GLUE_LOOPS)
+    virtual int push_burst(uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets,
+                           uint64_t first_token, uint32_t n);
     int flush();          // run the staged batch, wait for every batch in flight, route
     int flush_async();    // route the batch in flight (if any), launch the staged one, return
     uint64_t abandon();   // route every staged / in-flight packet as killed (a GPU that keeps failing)
@@ -155,27 +202,6 @@ class BatchElement {
     // after the batch completed, before any packet is routed: nonzero fails
     // the flush (a kernel's internal fault report in the codes)
     virtual int verify(const uint8_t *, size_t) { return 0; }
-    const uint8_t *staged(const Pending &p) const { return rt_->h_arena + p.slot; }
-    void write_back(const Pending &p, uint32_t nbytes) const;   // staged span -> packet
-    uint32_t keep_packet(const uint8_t *bytes, uint32_t len);   // new packet, returns its key
-    void chatter(const std::string &s) { msgs_.push_back(s); }
-    static uint32_t be16(const uint8_t *p) { return (uint32_t(p[0]) << 8) | p[1]; }
-
-    clk_ctx *ctx_;
-    std::string name_;
-    int noutputs_;
-    uint32_t batch_cap_ = 65536;
-    std::string err_;
-    uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0, lost_ = 0;
-    bool zerocopy_ = false;          // ZEROCOPY: packets read/written in registered host memory
-    bool in_place_ = false;          // routing a zero-copy batch: the kernel already wrote the packets
-    // the launching stage's buffers (valid in run()) and the routing
-    // stage's host results (valid in route())
-    uint8_t *d_anno_ = nullptr;      // per staged packet (wants_anno)
-    uint8_t *d_aux8_ = nullptr;      // per staged packet, element use (problem offsets)
-    uint8_t *h_aux8_ = nullptr;
-
-  private:
     // Double buffering: push() stages into st_[cur_]; flush_async() launches
     // it and flips cur_, so the host stages batch k+1 while batch k is on
     // the GPU.  At most one stage is in flight; its results are routed
@@ -203,8 +229,43 @@ class BatchElement {
         uint8_t *zc_dev = nullptr;
         void *ev[3] = {nullptr, nullptr, nullptr};   // kernel start, kernel end, batch done
         size_t n = 0;                       // packets on the GPU
+        size_t ngpu = 0;                    // staged packets for the GPU (h_off / h_len / h_anno filled at push)
+        uint32_t maxlen = 0;
         bool inflight = false, zc = false;
     };
+    // The per-packet loops, with the class's span() / route() given as
+    // callables: the generic push() and route pass virtual calls; the final
+    // classes pass qualified (inlined) ones through CLK_GLUE_LOOPS.
+    template <class SpanF>
+    int push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno);
+    template <class SpanF>
+    int burst_loop(SpanF &&span_f, uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets,
+                   uint64_t first_token, uint32_t n);
+    template <class RouteF>
+    void route_loop(Stage &g, RouteF &&route_f);
+    // route every packet of a completed stage, in push order (results_)
+    virtual void route_stage(Stage &g);
+
+    void write_back(const Pending &p, uint32_t nbytes) const;   // staged span -> packet
+    uint32_t keep_packet(const uint8_t *bytes, uint32_t len);   // new packet, returns its key
+    void chatter(const std::string &s) { msgs_.push_back(s); }
+    static uint32_t be16(const uint8_t *p) { return (uint32_t(p[0]) << 8) | p[1]; }
+
+    clk_ctx *ctx_;
+    std::string name_;
+    int noutputs_;
+    uint32_t batch_cap_ = 65536;
+    std::string err_;
+    uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0, lost_ = 0;
+    bool zerocopy_ = false;          // ZEROCOPY: packets read/written in registered host memory
+    bool in_place_ = false;          // routing a zero-copy batch: the kernel already wrote the packets
+    // the launching stage's buffers (valid in run()) and the routing
+    // stage's host results (valid in route())
+    uint8_t *d_anno_ = nullptr;      // per staged packet (wants_anno)
+    uint8_t *d_aux8_ = nullptr;      // per staged packet, element use (problem offsets)
+    uint8_t *h_aux8_ = nullptr;
+
+  private:
     int grow_host(Stage &g, size_t bytes, size_t n);
     int grow_dev(Stage &g, size_t bytes, size_t n);
     int launch(Stage &g);
@@ -252,6 +313,8 @@ class CheckIPHeader : public CheckElement {
     int configure(ConfArgs &args, std::string *err) override;
     std::string read_handler(const std::string &h) const override;   // + "offset" (OFFSET)
 
+    CLK_GLUE_LOOPS(CheckIPHeader)
+
   protected:
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
@@ -283,6 +346,8 @@ class IPInputCombo : public CheckIPHeader {
     int configure(ConfArgs &args, std::string *err) override;
     std::string read_handler(const std::string &h) const override;
 
+    CLK_GLUE_LOOPS(IPInputCombo)
+
   protected:
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
 
@@ -295,6 +360,8 @@ class SetIPChecksum : public BatchElement {
     using BatchElement::BatchElement;
     const char *class_name() const override { return "SetIPChecksum"; }
     std::string read_handler(const std::string &h) const override;
+
+    CLK_GLUE_LOOPS(SetIPChecksum)
 
   protected:
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
@@ -316,6 +383,8 @@ class CheckL4Header : public CheckElement {
     }
     int configure(ConfArgs &args, std::string *err) override;
 
+    CLK_GLUE_LOOPS(CheckL4Header)
+
   protected:
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
@@ -333,6 +402,8 @@ class SetL4Checksum : public BatchElement {
     SetL4Checksum(clk_ctx *ctx, const std::string &name, int noutputs, int proto);
     const char *class_name() const override { return proto_ == 17 ? "SetUDPChecksum" : "SetTCPChecksum"; }
     int configure(ConfArgs &args, std::string *err) override;
+
+    CLK_GLUE_LOOPS(SetL4Checksum)
 
   protected:
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
@@ -354,6 +425,8 @@ class DecIPTTL : public BatchElement {
     const char *class_name() const override { return "DecIPTTL"; }
     int configure(ConfArgs &args, std::string *err) override;
     std::string read_handler(const std::string &h) const override;
+
+    CLK_GLUE_LOOPS(DecIPTTL)
 
   protected:
     bool idempotent() const override { return false; }
@@ -377,6 +450,8 @@ class IPGWOptions : public BatchElement {
     int configure(ConfArgs &args, std::string *err) override;
     std::string read_handler(const std::string &h) const override;
 
+    CLK_GLUE_LOOPS(IPGWOptions)
+
   protected:
     bool idempotent() const override { return false; }
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
@@ -399,6 +474,8 @@ class FixIPSrc : public BatchElement {
     const char *class_name() const override { return "FixIPSrc"; }
     int configure(ConfArgs &args, std::string *err) override;
 
+    CLK_GLUE_LOOPS(FixIPSrc)
+
   protected:
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
@@ -420,6 +497,8 @@ class IPOutputCombo : public BatchElement {
     const char *class_name() const override { return "IPOutputCombo"; }
     int configure(ConfArgs &args, std::string *err) override;
     std::string read_handler(const std::string &h) const override;
+
+    CLK_GLUE_LOOPS(IPOutputCombo)
 
   protected:
     bool idempotent() const override { return false; }
@@ -447,6 +526,8 @@ class IPFragmenter : public BatchElement {
     const char *class_name() const override { return "IPFragmenter"; }
     int configure(ConfArgs &args, std::string *err) override;
     std::string read_handler(const std::string &h) const override;
+
+    CLK_GLUE_LOOPS(IPFragmenter)
 
   protected:
     bool idempotent() const override { return false; }

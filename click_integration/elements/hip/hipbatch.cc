@@ -1,8 +1,9 @@
 // -*- c-basic-offset: 4 -*-
 /*
- * hipbatch.{cc,hh} -- shared adapter of the GPU-backed checksum elements
- * (see hipbatch.hh).  Drop this directory into Click's elements/ as the
- * "hip" group; INTEGRATION.md has the build hooks.
+ * hipbatch.{cc,hh} -- Click's side of the GPU-backed checksum elements'
+ * shared adapter (see hipbatch.hh; the logic is hipcore.hh's).  Drop this
+ * directory into Click's elements/ as the "hip" group; INTEGRATION.md has
+ * the build hooks.
  */
 #include <click/config.h>
 #include "hipbatch.hh"
@@ -17,13 +18,14 @@
 CLICK_DECLS
 
 HIPBatchElement::HIPBatchElement()
-    : _device(-1), _latency_ms(1), _pt(0), _npt(0)
+    : _device(-1), _latency_ms(1), _retries(3), _pt(0), _timers(0), _npt(0)
 {
 }
 
 HIPBatchElement::~HIPBatchElement()
 {
     delete[] _pt;
+    delete[] _timers;
 }
 
 int
@@ -36,21 +38,24 @@ HIPBatchElement::configure(Vector<String> &conf, ErrorHandler *errh)
     if (Args(this, errh).bind(conf)
 	.read("LATENCY", _latency_ms)
 	.read("DEVICE", _device)
+	.read("RETRIES", _retries)
 	.consume() < 0)
 	return -1;
     _glue_conf = cp_unargvec(conf);
+    _core.set_latency(_latency_ms);
+    _core.set_max_retries(_retries);
     return 0;
 }
 
 int
-HIPBatchElement::ensure(PerThread &t, int thread, ErrorHandler *errh)
+HIPBatchElement::ensure(PerThread &t, ErrorHandler *errh)
 {
     if (t.e)
 	return 0;
     int ndev = clk_device_count();
     if (ndev <= 0)
 	return errh ? errh->error("no gfx950 GPU: %s", clk_last_error(0)) : -1;
-    int dev = _device >= 0 ? _device : thread % ndev;
+    int dev = _device >= 0 ? _device : t.id % ndev;
     if (dev >= ndev)
 	return errh ? errh->error("DEVICE %d: no such GPU (%d gfx950 devices)", dev, ndev) : -1;
     if (clk_ctx_create(dev, &t.ctx) != CLK_SUCCESS)
@@ -70,20 +75,40 @@ HIPBatchElement::initialize(ErrorHandler *errh)
 {
     _npt = click_max_cpu_ids();
     _pt = new PerThread[_npt];
+    _timers = new Timer[_npt];
     for (int k = 0; k < _npt; k++) {
-	_pt[k].timer.assign(this);
-	_pt[k].timer.initialize(this);
+	_pt[k].id = k;
+	_timers[k].assign(this);
+	_timers[k].initialize(this);
     }
     // the home thread's glue element now: configuration errors surface at
     // initialize time, as the reference element's configure() errors do
     int home = router()->home_thread_id(this);
     if (home < 0 || home >= _npt)
 	home = 0;
-    return ensure(_pt[home], home, errh);
+    if (ensure(_pt[home], errh) < 0)
+	return -1;
+    char buf[64];			// BATCH, parsed by the glue
+    clk_element_read_handler(_pt[home].e, "batch", buf, sizeof(buf));
+    _core.set_batch(strtoul(buf, 0, 10));
+    return 0;
 }
 
-int
-HIPBatchElement::nh_offset(const Packet *p) const
+HIPBatchElement::PerThread &
+HIPBatchElement::state()
+{
+    int thread = click_current_cpu_id();
+    PerThread &t = _pt[thread >= 0 && thread < _npt ? thread : 0];
+    if (!t.e) {
+	t.lock.acquire();
+	ensure(t, 0);			// no GPU for this thread: the core kills its packets
+	t.lock.release();
+    }
+    return t;
+}
+
+int32_t
+HIPBatchElement::nh_offset(Packet *p)
 {
     return p->has_network_header() ? p->network_header_offset() : -1;
 }
@@ -95,166 +120,85 @@ HIPBatchElement::prepare(Packet *p, uint32_t *anno, Packet **extra)
     return p;
 }
 
+Packet *
+HIPBatchElement::make_packet(clk_element *e, uint32_t key)
+{
+    int64_t n = clk_element_take_packet(e, key, 0, 0);
+    WritablePacket *q = n >= 0 ? Packet::make(n) : 0;
+    if (!q) {				// out of memory: release the glue's copy
+	unsigned char one;
+	if (n >= 0)
+	    clk_element_take_packet(e, key, &one, 1);
+	return 0;
+    }
+    clk_element_take_packet(e, key, q->data(), n);
+    return q;
+}
+
 void
 HIPBatchElement::push(int, Packet *p)
 {
-    int thread = click_current_cpu_id();
-    PerThread &t = _pt[thread < _npt ? thread : 0];
-    t.lock.acquire();
-    if (!t.e && ensure(t, thread, 0) < 0) {
-	t.lock.release();
-	p->kill();			// no GPU for this thread: as a failed uniqueify
-	return;
-    }
-    uint32_t anno = 0;
-    Packet *extra = 0;
-    if (!(p = prepare(p, &anno, &extra))) {
-	t.lock.release();
-	return;
-    }
-    Held h;
-    h.p = p;
-    h.extra = extra;
-    h.anno = anno;
-    t.held.push_back(h);
-    if (!t.counted) {		// keep the router running until this batch is routed
-	router()->adjust_runcount(1);
-	t.counted = true;
-	t.timer.schedule_after_msec(_latency_ms);
-    }
-    int r = clk_element_push_anno(t.e, const_cast<unsigned char *>(p->data()), p->length(),
-				  nh_offset(p), anno, t.next);
-    if (r < 0) {			// not staged (e.g. ZEROCOPY memory not registered)
-	click_chatter("%p{element}: %s", this, clk_element_last_error(t.e));
-	t.held.pop_back();
-	p->kill();
-	if (extra)
-	    extra->kill();
-	if (t.held.empty() && t.counted) {
-	    t.counted = false;
-	    t.timer.unschedule();
-	    router()->adjust_runcount(-1);
-	}
-    } else {
-	t.next++;
-	if (r == 1)			// batch full: launch it, route the one before
-	    flush(t, false);
-    }
-    t.lock.release();
+    _core.push(*this, state(), p);
+}
+
+Packet *
+HIPBatchElement::pull(int)
+{
+    return _core.pull(*this, state());
 }
 
 void
 HIPBatchElement::run_timer(Timer *timer)
 {
-    for (int k = 0; k < _npt; k++)
-	if (&_pt[k].timer == timer) {
-	    PerThread &t = _pt[k];
-	    t.lock.acquire();
-	    flush(t, true);
-	    t.lock.release();
-	    return;
-	}
+    int k = timer - _timers;
+    if (k >= 0 && k < _npt)
+	_core.timer(*this, _pt[k]);
 }
 
-// wait: route everything staged (timer, cleanup); otherwise double-buffered
-// (launch the staged batch, route the previous one, return)
-void
-HIPBatchElement::flush(PerThread &t, bool wait)
+int
+HIPBatchElement::pass(Routed &r, Packet **out)
 {
-    if (!t.e)
-	return;
-    int r = wait ? clk_element_flush(t.e) : clk_element_flush_async(t.e);
-    if (r != CLK_SUCCESS)
-	// nothing of the failed batch was routed; it stays staged and the
-	// next flush retries it (include/click_amd_elements.h)
-	click_chatter("%p{element}: GPU batch failed: %s", this, clk_element_last_error(t.e));
-    route_results(t);
-    if (t.held.empty()) {
-	if (t.counted) {
-	    t.counted = false;
-	    t.timer.unschedule();
-	    router()->adjust_runcount(-1);	// stop may now proceed
-	}
-    } else if (!t.timer.scheduled())
-	t.timer.schedule_after_msec(_latency_ms);
-}
-
-void
-HIPBatchElement::route_results(PerThread &t)
-{
-    enum { CAP = 256 };
-    uint64_t tok[CAP];
-    int32_t port[CAP];
-    uint32_t len[CAP], aux[CAP];
-    uint64_t n;
-    bool any = false;
-    while ((n = clk_element_results_aux(t.e, tok, port, len, aux, CAP)) > 0) {
-	any = true;
-	for (uint64_t i = 0; i < n; i++) {
-	    // a result that follows its packet's own (IPFragmenter's extra
-	    // fragments) may come after the entry was released
-	    Held gone = {0, 0, 0};
-	    Held &h = tok[i] >= t.base ? t.held[(int) (tok[i] - t.base)] : gone;
-	    deliver(t, h, port[i], len[i], aux[i]);
-	    if (primary(port[i], aux[i]))
-		h.p = 0;
-	}
-	release_front(t);
-	if (n < CAP)
-	    break;
+    if (!r.p)
+	return -1;
+    if (r.port == CLK_PORT_KILL) {	// drop() with no output 1 (checkipheader.cc:143-159)
+	r.p->kill();
+	return -1;
     }
-    if (any)
-	end_of_batch(t);
-    char buf[8192];
-    if (clk_element_take_messages(t.e, buf, sizeof(buf)) > 0)
-	for (char *s = buf, *e; *s; s = e) {
-	    if (!(e = strchr(s, '\n')))
-		e = s + strlen(s);
-	    else
-		*e++ = 0;
-	    click_chatter("%s", s);
-	}
+    *out = r.p;				// output 0, or 1 as checked_output_push
+    return r.port;
+}
+
+int
+HIPBatchElement::finish(PerThread &, Routed &r, Packet **out)
+{
+    return pass(r, out);
 }
 
 void
-HIPBatchElement::release_front(PerThread &t)
+HIPBatchElement::adjust_runcount(int delta)
 {
-    while (t.held.size() && !t.held.front().p && !t.held.front().extra) {
-	t.held.pop_front();
-	t.base++;
-    }
+    router()->adjust_runcount(delta);	// router.cc:832-846
 }
 
 void
-HIPBatchElement::kill_or_output1(Packet *p, int32_t port)
+HIPBatchElement::chatter(const char *text)
 {
-    if (port == CLK_PORT_OUT1)
-	checked_output_push(1, p);
-    else
-	p->kill();
+    click_chatter("%p{element}: %s", this, text);
+}
+
+void
+HIPBatchElement::message(const char *line)
+{
+    click_chatter("%s", line);		// already worded as the reference element's
 }
 
 void
 HIPBatchElement::cleanup(CleanupStage)
 {
-    for (int k = 0; k < _npt; k++) {
-	PerThread &t = _pt[k];
-	if (t.e) {
-	    flush(t, true);
-	    clk_element_destroy(t.e);
-	    clk_ctx_destroy(t.ctx);
-	    t.e = 0;
-	    t.ctx = 0;
-	}
-	while (t.held.size()) {		// a failed GPU: nothing can route them
-	    Held &h = t.held.front();
-	    if (h.p)
-		h.p->kill();
-	    if (h.extra)
-		h.extra->kill();
-	    t.held.pop_front();
-	}
-    }
+    // nothing is pushed downstream: held, routed-but-undelivered and ready
+    // packets are killed, the glue elements and contexts destroyed
+    for (int k = 0; k < _npt; k++)
+	_core.cleanup(*this, _pt[k]);
 }
 
 String
@@ -319,9 +263,9 @@ void
 HIPBatchElement::add_handlers()
 {
     // the reference element's handlers (e.g. checkipheader.cc:238-244)
-    // plus the glue's batches / packets / gpu_ns and the GPU in use
+    // plus the glue's batches / packets / gpu_ns / lost and the GPU in use
     static const char *const names[] = {"drops", "drop_details", "fragments", "batches", "packets",
-					"gpu_ns", "device", "color", "active"};
+					"gpu_ns", "lost", "device", "color", "active"};
     for (unsigned i = 0; i < sizeof(names) / sizeof(names[0]); i++)
 	add_read_handler(String(names[i]), read_handler, static_cast<const void *>(names[i]));
 }

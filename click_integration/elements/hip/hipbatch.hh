@@ -2,22 +2,28 @@
 #define CLICK_HIPBATCH_HH
 #include <click/element.hh>
 #include <click/timer.hh>
-#include <click/deque.hh>
 #include <click/sync.hh>
 #include "click_amd_elements.h"
+#include "hipcore.hh"
 CLICK_DECLS
 
 /*
  * HIPBatchElement -- what every GPU-backed checksum element of this group
- * shares (not an element itself).
+ * shares (not an element itself): Click's side of the core in hipcore.hh,
+ * which holds the packets while their batch is on the GPU, routes the
+ * results, keeps the runcount and the latency timer, retries a failed
+ * flush and batches in pull context.  The subclasses (one per reference
+ * class) do what the reference element's simple_action() does around its
+ * checksum: prepare() before staging (uniqueify, PaintTee clone) and
+ * finish() with the result (annotations, trims; the output to push to).
  *
- * Click's Element API hands over one packet at a time (element.cc:2891-2972);
- * the GPU wants batches.  The adapter stages each pushed packet into the
- * batched element glue (include/click_amd_elements.h), holds the Packet
- * until its batch comes back, and then does what the reference element's
- * simple_action() does after its checksum: the annotations, trims and
- * output pushes (the hooks deliver() and prepare() below, one subclass per
- * reference class).
+ * Processing: the reference's.  CheckIPHeader, CheckUDPHeader,
+ * CheckTCPHeader, CheckICMPHeader, DecIPTTL, SetUDPChecksum and IPGWOptions
+ * are PROCESSING_A_AH (checkipheader.hh:114); SetIPChecksum, SetTCPChecksum,
+ * FixIPSrc and IPInputCombo AGNOSTIC (element.cc:1127); IPOutputCombo and
+ * IPFragmenter PUSH.  In pull context pull() batches what input 0 has (up to
+ * BATCH packets) and hands the output-0 packets out one per call; the drop
+ * output stays push, as checked_output_push.
  *
  * Adapter keywords (removed before the rest of the configuration goes to the
  * glue, which parses the reference element's keywords itself):
@@ -25,87 +31,86 @@ CLICK_DECLS
  *                 (default 1)
  *   DEVICE   n    the GPU (default: RouterThread id % gfx950 devices; the
  *                 glue validates it: CLK_ENODEV for a GPU that is not there)
+ *   RETRIES  n    failed flushes of a batch before its packets are killed
+ *                 (default 3)
  * Glue keywords passed through: BATCH, ZEROCOPY, and the element's own.
  *
- * Threads (click -j N): one (context, glue element, held packets) per
- * RouterThread, chosen by click_current_cpu_id() (glue.hh:409-429), each
- * created the first time its thread pushes.  A Spinlock per thread state
- * serialises that thread's pushes with a flush from the home thread's timer
- * (timers run on the element's home thread, timer.cc:238-247, as in
- * ToDPDKDevice's per-thread queues, todpdkdevice.cc:85-86,176-179).
- *
- * Stop safety: while a thread state holds packets it holds one runcount
- * reference (Router::adjust_runcount, router.cc:832-846), so the driver
- * cannot stop the router (master.cc:283-303) before the batch is routed;
- * cleanup() flushes whatever is left.
+ * Threads (click -j N): one hipcore::State (context, glue element, held
+ * packets, lock) per RouterThread, chosen by click_current_cpu_id()
+ * (glue.hh:409-429), each created the first time its thread uses it.  Timers
+ * run on the element's home thread (timer.cc:238-247), as in ToDPDKDevice's
+ * per-thread queues (todpdkdevice.cc:85-86,176-179); the state's Spinlock
+ * serialises them with that thread's pushes.  No output is pushed while a
+ * lock is held.
  */
 class HIPBatchElement : public Element { public:
+
+    typedef hipcore::State<Packet, Spinlock> PerThread;
+    typedef hipcore::Routed<Packet> Routed;
 
     HIPBatchElement() CLICK_COLD;
     ~HIPBatchElement() CLICK_COLD;
 
-    const char *processing() const	{ return PUSH; }
+    const char *processing() const	{ return PROCESSING_A_AH; }
     int configure(Vector<String> &conf, ErrorHandler *errh) CLICK_COLD;
     int initialize(ErrorHandler *errh) CLICK_COLD;
     void cleanup(CleanupStage stage) CLICK_COLD;
     void add_handlers() CLICK_COLD;
 
     void push(int port, Packet *p);
+    Packet *pull(int port);
     void run_timer(Timer *t);
 
-  protected:
-
-    struct Held {
-	Packet *p;		// the packet pushed (made writable if the element writes it)
-	Packet *extra;		// a second packet held with it (IPOutputCombo's PaintTee clone)
-	uint32_t anno;		// the CLK_ANNO_* bits it was staged with
-    };
-
-    struct PerThread {
-	clk_ctx *ctx;
-	clk_element *e;
-	Deque<Held> held;	// held[k] is token base + k
-	uint64_t base;
-	uint64_t next;
-	Packet *frag_parent;	// IPFragmenter: the packet whose fragments follow
-	bool counted;		// holds a runcount reference
-	Timer timer;
-	Spinlock lock;
-	PerThread() : ctx(0), e(0), base(0), next(0), frag_parent(0), counted(false) { }
-    };
-
-    // the glue class (default: the reference class name this adapter takes)
-    virtual const char *glue_class() const	{ return class_name(); }
+    // ---- the core's host interface (hipcore.hh) ------------------------------
     // before staging: uniqueify if the element writes the packet (as the
     // reference element does), fill *anno (CLK_ANNO_*), optionally hold a
     // second packet in *extra; return the packet to stage (0: consumed)
     virtual Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
+    uint8_t *data(Packet *p)		{ return const_cast<unsigned char *>(p->data()); }
+    uint32_t length(Packet *p)		{ return p->length(); }
     // the byte offset of the header the glue looks at (network header)
-    virtual int nh_offset(const Packet *p) const;
-    // route one result (the reference's side effects, then the push)
-    virtual void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux) = 0;
+    virtual int32_t nh_offset(Packet *p);
     // false for a result that comes with another (IPOutputCombo's clone,
     // IPFragmenter's extra fragments): the held packet stays
     virtual bool primary(int32_t port, uint32_t aux) const	{ (void) port; (void) aux; return true; }
-    // after a batch's results: release per-batch state
+    virtual Packet *make_packet(clk_element *e, uint32_t key);
+    // one result: the reference's side effects; returns the output port of
+    // *out (core pushes it, or hands it out in pull context), -1 for none
+    virtual int finish(PerThread &t, Routed &r, Packet **out);
     virtual void end_of_batch(PerThread &t)	{ (void) t; }
+    void output_push(int port, Packet *p)	{ checked_output_push(port, p); }
+    Packet *input_pull()			{ return input(0).pull(); }
+    void kill(Packet *p)			{ p->kill(); }
+    void adjust_runcount(int delta);
+    void schedule(PerThread &t, unsigned ms)	{ _timers[t.id].schedule_after_msec(ms); }
+    void unschedule(PerThread &t)		{ _timers[t.id].unschedule(); }
+    bool scheduled(PerThread &t)		{ return _timers[t.id].scheduled(); }
+    void chatter(const char *text);
+    void message(const char *line);
+
+  protected:
+
+    // the glue class (default: the reference class name this adapter takes)
+    virtual const char *glue_class() const	{ return class_name(); }
     // glue handler text of the home thread's element (the element's
     // configuration, e.g. OFFSET, COLOR, MTU)
     String glue_handler(const char *name) const;
-    void kill_or_output1(Packet *p, int32_t port);
+    // the default finish(): output port as routed, killed on CLK_PORT_KILL
+    int pass(Routed &r, Packet **out);
 
     String _glue_conf;
     int _device;		// -1: per thread
     uint32_t _latency_ms;
+    uint32_t _retries;
     PerThread *_pt;
+    Timer *_timers;
     int _npt;
+    hipcore::Core<Packet, HIPBatchElement, Spinlock> _core;
 
   private:
 
-    int ensure(PerThread &t, int thread, ErrorHandler *errh);
-    void flush(PerThread &t, bool wait);
-    void route_results(PerThread &t);
-    void release_front(PerThread &t);
+    PerThread &state();
+    int ensure(PerThread &t, ErrorHandler *errh);
     static String read_handler(Element *e, void *thunk) CLICK_COLD;
 
 };

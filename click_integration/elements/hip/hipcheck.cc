@@ -21,21 +21,20 @@ HIPCheckIPHeader::initialize(ErrorHandler *errh)
     return 0;
 }
 
-void
-HIPCheckIPHeader::deliver(PerThread &, Held &h, int32_t port, uint32_t len, uint32_t)
+int
+HIPCheckIPHeader::finish(PerThread &, Routed &r, Packet **out)
 {
-    Packet *p = h.p;
-    if (port != CLK_PORT_OUT0) {		// drop(): output 1 if connected, else kill (143-159)
-	kill_or_output1(p, port);
-	return;
-    }
+    Packet *p = r.p;
+    if (!p || r.port != CLK_PORT_OUT0)		// drop(): output 1 if connected, else kill (143-159)
+	return pass(r, out);
     // checkipheader.cc:213-223: network header, trim to ip_len, dst annotation
     const click_ip *ip = reinterpret_cast<const click_ip *>(p->data() + _offset);
     p->set_ip_header(ip, ip->ip_hl << 2);
-    if (p->length() > len)			// len: the packet's length after the trim
-	p->take(p->length() - len);
+    if (p->length() > r.len)			// len: the packet's length after the trim
+	p->take(p->length() - r.len);
     p->set_dst_ip_anno(ip->ip_dst);
-    output(0).push(p);
+    *out = p;
+    return 0;
 }
 
 int
@@ -47,31 +46,25 @@ HIPIPInputCombo::initialize(ErrorHandler *errh)
     return 0;
 }
 
-void
-HIPIPInputCombo::deliver(PerThread &, Held &h, int32_t port, uint32_t len, uint32_t)
+int
+HIPIPInputCombo::finish(PerThread &, Routed &r, Packet **out)
 {
-    Packet *p = h.p;
-    if (port != CLK_PORT_OUT0) {		// bad: killed (ipinputcombo.cc:134-139)
+    Packet *p = r.p;
+    if (!p)
+	return -1;
+    if (r.port != CLK_PORT_OUT0) {		// bad: killed (ipinputcombo.cc:134-139)
 	p->kill();
-	return;
+	return -1;
     }
     SET_PAINT_ANNO(p, _color);			// Paint (71)
     p->pull(14);				// Strip(14) (74)
     const click_ip *ip = reinterpret_cast<const click_ip *>(p->data());
     p->set_ip_header(ip, ip->ip_hl << 2);	// 125
-    if (p->length() > len)			// 128-129
-	p->take(p->length() - len);
+    if (p->length() > r.len)			// 128-129
+	p->take(p->length() - r.len);
     p->set_dst_ip_anno(ip->ip_dst);		// 132
-    output(0).push(p);
-}
-
-void
-HIPCheckL4Header::deliver(PerThread &, Held &h, int32_t port, uint32_t, uint32_t)
-{
-    if (port == CLK_PORT_OUT0)
-	output(0).push(h.p);
-    else
-	kill_or_output1(h.p, port);
+    *out = p;
+    return 0;
 }
 
 CLICK_ENDDECLS

@@ -23,8 +23,8 @@ class HIPCheckIPHeader : public HIPBatchElement { public:
     const char *port_count() const	{ return PORTS_1_1X2; }
     const char *flags() const		{ return "A"; }
     int initialize(ErrorHandler *errh) CLICK_COLD;
+    int finish(PerThread &t, Routed &r, Packet **out);
   protected:
-    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
     int _offset;
 };
 
@@ -35,18 +35,17 @@ class HIPCheckIPHeader2 : public HIPCheckIPHeader { public:
 class HIPIPInputCombo : public HIPBatchElement { public:
     const char *class_name() const	{ return "IPInputCombo"; }
     const char *port_count() const	{ return PORTS_1_1; }
+    const char *processing() const	{ return AGNOSTIC; }
     const char *flags() const		{ return "A"; }
     int initialize(ErrorHandler *errh) CLICK_COLD;
+    int32_t nh_offset(Packet *)		{ return 14; }   // Strip(14): the header is at data() + 14
+    int finish(PerThread &t, Routed &r, Packet **out);
   protected:
-    int nh_offset(const Packet *) const	{ return 14; }   // Strip(14): the header is at data() + 14
-    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
     int _color;
 };
 
 class HIPCheckL4Header : public HIPBatchElement { public:
     const char *port_count() const	{ return PORTS_1_1X2; }
-  protected:
-    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
 };
 
 class HIPCheckUDPHeader : public HIPCheckL4Header { public:

@@ -60,7 +60,8 @@
  *   void kill(P *p)
  *   void adjust_runcount(int delta)
  *   void schedule(S &t, unsigned ms); void unschedule(S &t); bool scheduled(S &t)
- *   void chatter(const char *text)
+ *   void chatter(const char *text)               the adapter's own messages
+ *   void message(const char *line)               the element's chatter lines from the glue
  */
 #include <stddef.h>
 #include <stdint.h>
@@ -343,6 +344,16 @@ template <class P, class Host, class L> class Core {
             end.end = true;
             t.outbox.push_back(end);
         }
+        // the element's click_chatter lines (e.g. the first drop's reason)
+        char buf[8192];
+        if (clk_element_take_messages(t.e, buf, sizeof(buf)) > 0)
+            for (char *s = buf, *e; *s; s = e) {
+                if (!(e = strchr(s, '\n')))
+                    e = s + strlen(s);
+                else
+                    *e++ = 0;
+                h.message(s);
+            }
     }
 
     // Deliver the outbox in order, without the lock.  Re-entrant calls on

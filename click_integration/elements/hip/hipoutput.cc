@@ -23,17 +23,12 @@ HIPIPGWOptions::prepare(Packet *p, uint32_t *, Packet **)
     return p;
 }
 
-void
-HIPIPGWOptions::deliver(PerThread &, Held &h, int32_t port, uint32_t, uint32_t aux)
+int
+HIPIPGWOptions::finish(PerThread &, Routed &r, Packet **out)
 {
-    Packet *p = h.p;
-    if (port == CLK_PORT_OUT0)
-	output(0).push(p);
-    else if (port == CLK_PORT_OUT1) {		// send_error (162-165)
-	SET_ICMP_PARAMPROB_ANNO(p, aux);
-	checked_output_push(1, p);
-    } else
-	p->kill();
+    if (r.p && r.port == CLK_PORT_OUT1)		// send_error (162-165)
+	SET_ICMP_PARAMPROB_ANNO(r.p, r.aux);
+    return pass(r, out);
 }
 
 // ---- FixIPSrc ---------------------------------------------------------------
@@ -48,12 +43,12 @@ HIPFixIPSrc::prepare(Packet *p, uint32_t *anno, Packet **)
     return p;
 }
 
-void
-HIPFixIPSrc::deliver(PerThread &, Held &h, int32_t, uint32_t, uint32_t)
+int
+HIPFixIPSrc::finish(PerThread &, Routed &r, Packet **out)
 {
-    if (h.anno & CLK_ANNO_FIX_IP_SRC)
-	SET_FIX_IP_SRC_ANNO(h.p, 0);		// fix_it (fixipsrc.cc:59)
-    output(0).push(h.p);
+    if (r.p && (r.anno & CLK_ANNO_FIX_IP_SRC))
+	SET_FIX_IP_SRC_ANNO(r.p, 0);		// fix_it (fixipsrc.cc:59)
+    return pass(r, out);
 }
 
 // ---- IPOutputCombo ----------------------------------------------------------
@@ -81,34 +76,38 @@ HIPIPOutputCombo::prepare(Packet *p, uint32_t *anno, Packet **extra)
     if (PAINT_ANNO(p) == _color)
 	*extra = p->clone();
     WritablePacket *q = p->uniqueify();
-    if (!q && *extra) {			// the reference pushed the clone before the copy failed
-	output(1).push(*extra);
+    if (!q && *extra) {
+	// out of memory: the reference pushed the clone before the copy
+	// failed; prepare() runs under the thread state's lock, where nothing
+	// is pushed downstream (a re-entrant push would deadlock), so it dies
+	(*extra)->kill();
 	*extra = 0;
     }
     return q;
 }
 
-void
-HIPIPOutputCombo::deliver(PerThread &, Held &h, int32_t port, uint32_t, uint32_t aux)
+int
+HIPIPOutputCombo::finish(PerThread &, Routed &r, Packet **out)
 {
-    if (aux == CLK_AUX_CLONE) {			// the PaintTee clone, before the packet
-	output(1).push(h.extra);
-	h.extra = 0;
-	return;
+    if (r.extra && !r.p) {			// the PaintTee clone, before the packet
+	*out = r.extra;
+	return 1;
     }
-    Packet *p = h.p;
-    if (port == CLK_PORT_KILL) {
+    Packet *p = r.p;
+    if (!p)
+	return -1;
+    if (r.port == CLK_PORT_KILL) {		// DropBroadcasts (50-53)
 	p->kill();
-	return;
+	if (r.extra)
+	    r.extra->kill();
+	return -1;
     }
-    if (port == CLK_PORT_OUT2) {		// ipgw_send_error (202-204)
-	SET_ICMP_PARAMPROB_ANNO(p, aux);
-	output(2).push(p);
-	return;
-    }
-    if (h.anno & CLK_ANNO_FIX_IP_SRC)		// FixIPSrc step (169-170)
+    if (r.port == CLK_PORT_OUT2)		// ipgw_send_error (202-204)
+	SET_ICMP_PARAMPROB_ANNO(p, r.aux);
+    else if (r.anno & CLK_ANNO_FIX_IP_SRC)	// FixIPSrc step (169-170)
 	SET_FIX_IP_SRC_ANNO(p, 0);
-    output(port).push(p);			// 0, 3 (TTL expired), 4 (longer than the MTU)
+    *out = p;
+    return r.port;				// 0, 2, 3 (TTL expired), 4 (longer than the MTU)
 }
 
 // ---- IPFragmenter -----------------------------------------------------------
@@ -133,44 +132,51 @@ HIPIPFragmenter::prepare(Packet *p, uint32_t *, Packet **)
     return p;
 }
 
-void
-HIPIPFragmenter::deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux)
+Packet *
+HIPIPFragmenter::make_packet(clk_element *e, uint32_t key)
 {
-    if (aux != 0) {
-	// a fragment after the first (129-159): a new packet with the
-	// glue's bytes, annotations copied from the original
-	int64_t n = clk_element_take_packet(t.e, aux, 0, 0);
-	WritablePacket *q = n >= 0 ? Packet::make(_headroom, 0, n, 0) : 0;
-	if (!q) {			// out of memory: release the glue's copy, drop it
-	    unsigned char one;
-	    if (n >= 0)
-		clk_element_take_packet(t.e, aux, &one, 1);
-	    return;
-	}
-	clk_element_take_packet(t.e, aux, q->data(), n);
-	q->set_network_header(q->data(), (q->data()[0] & 0xF) << 2);
-	if (t.frag_parent)
-	    q->copy_annotations(t.frag_parent);
-	output(0).push(q);
-	return;
+    // a fragment after the first (129-159): a new packet with the glue's
+    // bytes and the element's HEADROOM; its annotations come in finish()
+    int64_t n = clk_element_take_packet(e, key, 0, 0);
+    WritablePacket *q = n >= 0 ? Packet::make(_headroom, 0, n, 0) : 0;
+    if (!q) {				// out of memory: release the glue's copy, drop it
+	unsigned char one;
+	if (n >= 0)
+	    clk_element_take_packet(e, key, &one, 1);
+	return 0;
     }
-    Packet *p = h.p;
-    if (port == CLK_PORT_OUT0 && len < (uint32_t) p->length()) {
+    clk_element_take_packet(e, key, q->data(), n);
+    q->set_network_header(q->data(), (q->data()[0] & 0xF) << 2);
+    return q;
+}
+
+int
+HIPIPFragmenter::finish(PerThread &t, Routed &r, Packet **out)
+{
+    if (r.made) {				// a fragment: annotations of the original (153)
+	if (r.parent)
+	    r.made->copy_annotations(r.parent);
+	*out = r.made;
+	return 0;
+    }
+    Packet *p = r.p;
+    if (!p)
+	return -1;
+    if (r.port == CLK_PORT_OUT0 && r.len < (uint32_t) p->length()) {
 	// the first fragment: the rewritten header is already in the packet
 	// (112-120); a clone cut to its length goes out first (121-124), the
 	// original stays for the annotations of the fragments that follow
 	Packet *first = p->clone();
-	if (first) {
-	    first->take(p->length() - len);
-	    output(0).push(first);
-	}
 	if (t.frag_parent)
 	    t.frag_parent->kill();
 	t.frag_parent = p;
-    } else if (port == CLK_PORT_OUT0)
-	output(0).push(p);
-    else				// DF with HONOR_DF or tiny MTU: checked_output_push(1) (96-102)
-	kill_or_output1(p, port);
+	if (!first)
+	    return -1;
+	first->take(p->length() - r.len);
+	*out = first;
+	return 0;
+    }
+    return pass(r, out);		// untouched, or DF with HONOR_DF / tiny MTU (96-102)
 }
 
 void

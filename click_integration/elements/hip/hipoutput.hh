@@ -17,39 +17,41 @@ CLICK_DECLS
 class HIPIPGWOptions : public HIPBatchElement { public:
     const char *class_name() const	{ return "IPGWOptions"; }
     const char *port_count() const	{ return PORTS_1_1X2; }
-  protected:
     Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
-    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+    int finish(PerThread &t, Routed &r, Packet **out);
 };
 
 class HIPFixIPSrc : public HIPBatchElement { public:
     const char *class_name() const	{ return "FixIPSrc"; }
     const char *port_count() const	{ return PORTS_1_1; }
-  protected:
+    const char *processing() const	{ return AGNOSTIC; }
     Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
-    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+    int finish(PerThread &t, Routed &r, Packet **out);
 };
 
 class HIPIPOutputCombo : public HIPBatchElement { public:
     const char *class_name() const	{ return "IPOutputCombo"; }
     const char *port_count() const	{ return "1/5"; }
+    const char *processing() const	{ return PUSH; }
     int initialize(ErrorHandler *errh) CLICK_COLD;
-  protected:
     Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
-    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+    int finish(PerThread &t, Routed &r, Packet **out);
     bool primary(int32_t port, uint32_t aux) const	{ (void) port; return aux != CLK_AUX_CLONE; }
+  protected:
     int _color;
 };
 
 class HIPIPFragmenter : public HIPBatchElement { public:
     const char *class_name() const	{ return "IPFragmenter"; }
     const char *port_count() const	{ return PORTS_1_1X2; }
+    const char *processing() const	{ return PUSH; }
     int initialize(ErrorHandler *errh) CLICK_COLD;
-  protected:
     Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
-    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
+    Packet *make_packet(clk_element *e, uint32_t key);
+    int finish(PerThread &t, Routed &r, Packet **out);
     bool primary(int32_t port, uint32_t aux) const	{ (void) port; return aux == 0; }
     void end_of_batch(PerThread &t);
+  protected:
     uint32_t _mtu;
     uint32_t _headroom;
 };

@@ -11,17 +11,10 @@ CLICK_DECLS
 Packet *
 HIPSetChecksum::prepare(Packet *p, uint32_t *, Packet **)
 {
-    // setipchecksum.cc:77, setudpchecksum.cc:40, settcpchecksum.cc:47
+    // setipchecksum.cc:77, setudpchecksum.cc:40, settcpchecksum.cc:47; the
+    // result routes by HIPBatchElement::pass(): output 0, SetUDPChecksum's
+    // output 1 (setudpchecksum.cc:60), killed on bad lengths
     return p->uniqueify();
-}
-
-void
-HIPSetChecksum::deliver(PerThread &, Held &h, int32_t port, uint32_t, uint32_t)
-{
-    if (port == CLK_PORT_OUT0)
-	output(0).push(h.p);
-    else				// SetUDPChecksum: output 1 (setudpchecksum.cc:60); bad lengths: killed
-	kill_or_output1(h.p, port);
 }
 
 Packet *
@@ -35,14 +28,6 @@ HIPDecIPTTL::prepare(Packet *p, uint32_t *, Packet **)
     return p;
 }
 
-void
-HIPDecIPTTL::deliver(PerThread &, Held &h, int32_t port, uint32_t, uint32_t)
-{
-    if (port == CLK_PORT_OUT0)
-	output(0).push(h.p);
-    else				// expired: checked_output_push(1, p) (54-57)
-	kill_or_output1(h.p, port);
-}
 
 CLICK_ENDDECLS
 ELEMENT_REQUIRES(HIPBatchElement)

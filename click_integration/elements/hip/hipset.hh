@@ -17,14 +17,13 @@ CLICK_DECLS
  */
 
 class HIPSetChecksum : public HIPBatchElement { public:
-  protected:
     Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
-    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
 };
 
 class HIPSetIPChecksum : public HIPSetChecksum { public:
     const char *class_name() const	{ return "SetIPChecksum"; }
     const char *port_count() const	{ return PORTS_1_1; }
+    const char *processing() const	{ return AGNOSTIC; }
 };
 
 class HIPSetUDPChecksum : public HIPSetChecksum { public:
@@ -35,14 +34,13 @@ class HIPSetUDPChecksum : public HIPSetChecksum { public:
 class HIPSetTCPChecksum : public HIPSetChecksum { public:
     const char *class_name() const	{ return "SetTCPChecksum"; }
     const char *port_count() const	{ return PORTS_1_1; }
+    const char *processing() const	{ return AGNOSTIC; }
 };
 
 class HIPDecIPTTL : public HIPBatchElement { public:
     const char *class_name() const	{ return "DecIPTTL"; }
     const char *port_count() const	{ return PORTS_1_1X2; }
-  protected:
     Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
-    void deliver(PerThread &t, Held &h, int32_t port, uint32_t len, uint32_t aux);
 };
 
 CLICK_ENDDECLS

@@ -80,7 +80,7 @@ class Host {
     std::atomic<int> runcount{0};
     std::vector<int> sched;                     // per state: scheduled flag
     std::deque<TPacket *> input;                // pull context source
-    std::vector<std::string> chat;
+    std::vector<std::string> chat, msgs;
     std::atomic<long> kills{0};
     uint32_t color = 0;
     // re-entrancy probe: called on every output-0 packet (may push back in)
@@ -242,6 +242,7 @@ class Host {
     void unschedule(St &t) { sched[(size_t)t.id] = 0; }
     bool scheduled(St &t) { return sched[(size_t)t.id] != 0; }
     void chatter(const char *s) { chat.push_back(s); }
+    void message(const char *s) { msgs.push_back(s); }
 
     void push(TPacket *p, int state = 0) { core.push(*this, st[(size_t)state], p); }
     TPacket *pull(int state = 0) { return core.pull(*this, st[(size_t)state]); }
@@ -318,6 +319,7 @@ void push_check_ip()
         last1 = p->id;
     }
     CHECK(h.handler("drops") == std::to_string(h.out[1].size()));
+    CHECK(h.msgs.size() == 1 && h.msgs[0].find("CheckIPHeader") != std::string::npos);   // the first drop only
     report("push_check_ip_header_double_buffered_and_timer", ok);
 }
 
@@ -420,6 +422,7 @@ void failed_flush_retry(const char *cls, const char *conf, int nth)
 {
     bool ok = true;
     Host h(cls, conf, std::string(cls) == "IPOutputCombo" ? 5 : 2);
+    h.color = 1;                                       // IPOutputCombo's COLOR: no packet is painted 1
     const int n = 300;
     std::vector<std::vector<uint8_t> > ref(n);
     std::vector<int> code(n);

@@ -159,3 +159,34 @@ def test_click_adapters_use_only_the_public_abi():
         # click-buildtool reads class names from single-line class_name() methods
         assert re.search(r'class HIP%s\b.*?\n\s*const char \*class_name\(\) const\s*\{ return "%s"; \}' % (n, n), hh,
                          re.S), n
+
+
+def test_click_adapters_keep_the_reference_processing():
+    """Each adapter declares the reference class's processing (agnostic
+    classes stay agnostic, so an unchanged graph that pulls through them
+    passes Click's push/pull check, router.cc:692): PROCESSING_A_AH for
+    CheckIPHeader (checkipheader.hh:114), CheckUDPHeader
+    (checkudpheader.hh:61), CheckTCPHeader (checktcpheader.hh:61),
+    CheckICMPHeader (checkicmpheader.hh:59), DecIPTTL (decipttl.hh:52),
+    SetUDPChecksum (setudpchecksum.hh:32), IPGWOptions (ipgwoptions.hh:43);
+    AGNOSTIC (element.cc:1127) for SetIPChecksum, SetTCPChecksum, FixIPSrc,
+    IPInputCombo; PUSH for IPOutputCombo (ipoutputcombo.hh:52) and
+    IPFragmenter (ipfragmenter.hh:65).  Every adapter with a pull side
+    implements pull() (HIPBatchElement::pull, over hipcore's pull())."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    hip = os.path.join(root, "click_integration", "elements", "hip")
+    hh = "".join(open(os.path.join(hip, f)).read() for f in sorted(os.listdir(hip)) if f.endswith(".hh"))
+    base = re.search(r"class HIPBatchElement\b.*?processing\(\) const\s*\{ return (\w+); \}", hh, re.S).group(1)
+    assert base == "PROCESSING_A_AH"
+    assert re.search(r"Packet \*pull\(int port\);", hh)
+    want = {"CheckIPHeader": "PROCESSING_A_AH", "CheckUDPHeader": "PROCESSING_A_AH",
+            "CheckTCPHeader": "PROCESSING_A_AH", "CheckICMPHeader": "PROCESSING_A_AH", "DecIPTTL": "PROCESSING_A_AH",
+            "SetUDPChecksum": "PROCESSING_A_AH", "IPGWOptions": "PROCESSING_A_AH", "SetIPChecksum": "AGNOSTIC",
+            "SetTCPChecksum": "AGNOSTIC", "FixIPSrc": "AGNOSTIC", "IPInputCombo": "AGNOSTIC", "IPOutputCombo": "PUSH",
+            "IPFragmenter": "PUSH"}
+    for n, proc in want.items():
+        body = re.search(r"class HIP%s\b[^{]*\{(.*?)\n\};" % n, hh, re.S).group(1)
+        m = re.search(r"processing\(\) const\s*\{ return (\w+); \}", body)
+        assert (m.group(1) if m else base) == proc, n
+    cc = open(os.path.join(hip, "hipbatch.cc")).read()
+    assert "_core.pull(*this, state())" in cc and "_core.push(*this, state(), p)" in cc

@@ -390,3 +390,69 @@ def test_tune_rejects_bad_values(torch):
         with pytest.raises(click_amd.ClickAmdError):
             c.tune(**{k: v})
     c.close()
+
+
+def dense_layout(rng, n, proto, kind):
+    """Packets of random sizes laid out for the packet-stream kernel's dense
+    (span) and generic runs: 'packed' (64 B-aligned, disjoint: dense),
+    'odd' (odd starts, >= 16 B gaps: disjoint chunk ranges, dense with byte
+    swaps), 'empty' (every 7th packet caplen 0), 'gaps' (a 4 KB hole every
+    50 packets: those runs exceed the span slack -> generic), 'shared' (no
+    gap: neighbours share a chunk -> generic), 'reversed' (every other run
+    in reverse address order -> generic)."""
+    pkts = []
+    for k in range(n):
+        L = int(rng.choice([40, 64, 300, 576, 1500, 1501]))
+        if kind == "empty" and k % 7 == 3:
+            pkts.append(b"")
+            continue
+        ow = int(rng.integers(1, 6)) if rng.random() < 0.15 else 0
+        pkts.append(fuzz.build(rng, proto, max(L, 28 + 4 * ow + 20), ow))
+    off = np.zeros(n, np.uint64)
+    pos = 0
+    for k, p in enumerate(pkts):
+        if kind in ("packed", "empty", "reversed"):
+            pos = (pos + 63) // 64 * 64
+        elif kind == "odd":
+            pos = (pos + 15) // 16 * 16 + 16 + 2 * int(rng.integers(0, 4)) + 1
+        elif kind == "gaps" and k % 50 == 0:
+            pos += 4096
+        off[k] = pos
+        pos += len(p)
+    size = int(max(off[k] + len(p) for k, p in enumerate(pkts))) + 64
+    arena = np.zeros(size, np.uint8)
+    for k, p in enumerate(pkts):
+        arena[int(off[k]):int(off[k]) + len(p)] = np.frombuffer(p, np.uint8)
+    caplen = np.array([len(p) for p in pkts], np.uint32)
+    if kind == "reversed":                         # every other 64-packet run in reverse address order
+        for r0 in range(0, n, 128):
+            off[r0:r0 + 64] = off[r0:r0 + 64][::-1].copy()
+            caplen[r0:r0 + 64] = caplen[r0:r0 + 64][::-1].copy()
+    oracle_lib.batch("set_ip", arena, n, off=off, length=caplen)
+    if proto == 1:
+        fuzz.set_icmp_checksums(arena, off, caplen)
+    else:
+        oracle_lib.batch("set_udp" if proto == 17 else "set_tcp", arena, n, off=off, length=caplen, arg=0)
+    bad = rng.random(n) < 0.1                      # some corrupted payload bytes
+    for k in np.nonzero(bad & (caplen > 60))[0]:
+        arena[int(off[k]) + 50] ^= 0x40
+    return arena, off, caplen, int(caplen.max())
+
+
+@pytest.mark.parametrize("kind", ["packed", "odd", "empty", "gaps", "shared", "reversed"])
+@pytest.mark.parametrize("mode", [-1, 1])
+def test_stream_dense_and_generic_runs(torch, kind, mode):
+    """The packet-stream kernel's two per-run paths -- the dense span
+    stream (CLK_SPAN) and the per-packet chunk list -- on layouts that pick
+    each (and mixes within one batch), Check and Set (fused and two-phase),
+    every protocol: oracle-exact."""
+    import click_amd
+    c = click_amd.Context(0).tune(stream_min=1, set_mode=mode)
+    rng = np.random.default_rng(hash(kind) % 1000 + mode)
+    for proto in (17, 6, 1):
+        arena, off, caplen, ml = dense_layout(rng, 700, proto, kind)
+        for op in OPS_L4[proto]:
+            compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=1)
+        if proto == 6:
+            compare(torch, c, "set_tcp", arena, len(off), off=off, length=caplen, max_len=ml, arg=0)
+    c.close()
