@@ -791,9 +791,10 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
     buffers.  Asserts all n forwarded on port 0 and identical bytes both
     ways (OUTA == OUTB)."""
     import numpy as np
-    from click_amd.elements import Element
+    from click_amd.elements import Element, ResultBuffers
     frame = c1_frame()
     out, arenas = {}, {}
+    rbufs = ResultBuffers(n + 1)              # the harness pops results into reused arrays
     runs = [(name, chain, False) for name, chain in C1_CHAINS.items()] + \
            [(name + "_zerocopy", chain, True) for name, chain in C1_CHAINS.items()]
     for name, chain, zc in runs:
@@ -817,7 +818,7 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
                 tb = time.perf_counter()
                 e.flush()
                 tc = time.perf_counter()
-                tok, port, _ = e.results(cap=len(ptrs) + 1)
+                tok, port, _ = e.results(bufs=rbufs)
                 keep = port == 0
                 fwd = int(keep.sum())
                 if fwd != len(ptrs):

@@ -27,12 +27,6 @@
 #ifndef CLK_STREAM_NT_CHECK
 #define CLK_STREAM_NT_CHECK 0   // packet-stream Check: nontemporal chunk loads (tuning knob)
 #endif
-#ifndef CLK_SPAN
-#define CLK_SPAN 1         // packet-stream kernel: dense runs stream their span (no per-chunk address lookup)
-#endif
-#ifndef CLK_SPAN_KV
-#define CLK_SPAN_KV 2      // ... chunks per lane per pass there (two passes in flight)
-#endif
 #ifndef CLK_SWPE_CHECK
 #define CLK_SWPE_CHECK 6   // ... the Check kernels, with 3 chunks per lane per pass (CLK_SKV_CHECK)
 #endif
@@ -997,40 +991,10 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         }
         const uint32_t total = __shfl(incl, 63, 64);
         const bool anyodd = __ballot(live && (a & 1)) != 0;  // wave-uniform
-        // Dense run (CLK_SPAN): the packets' chunk ranges are increasing and
-        // disjoint and their span [c0 of packet 0, end of the last) holds
-        // few gap chunks -- as a packed arena does.  The wave then streams
-        // the span itself: a chunk's address needs no lookup, so a pass's
-        // loads issue before any LDS read, and the next pass's loads are in
-        // flight while this one is summed.  Gap chunks are loaded and not
-        // summed (at most 1/8 + 64 chunks more).
-        bool dense = false;
-        uint64_t sbase = 0;
-        uint32_t span = 0;
-        if (CLK_SPAN) {
-            const uint64_t cend = c0 + 16ull * nch;
-            const uint32_t pe_lo = __shfl_up((uint32_t)cend, 1, 64), pe_hi = __shfl_up((uint32_t)(cend >> 32), 1, 64);
-            const uint64_t pend = (uint64_t)pe_lo | ((uint64_t)pe_hi << 32);
-            const bool bad = live && lane > 0 && c0 < pend;
-            const uint64_t nlive = __popcll(__ballot(live));          // live lanes are a prefix
-            sbase = (uint64_t)__shfl((uint32_t)c0, 0, 64) | ((uint64_t)__shfl((uint32_t)(c0 >> 32), 0, 64) << 32);
-            const uint32_t lastl = (uint32_t)nlive - 1;
-            const uint64_t send = (uint64_t)__shfl((uint32_t)cend, (int)lastl, 64) |
-                                  ((uint64_t)__shfl((uint32_t)(cend >> 32), (int)lastl, 64) << 32);
-            const uint64_t sp = send >= sbase ? (send - sbase) >> 4 : ~0ull;
-            dense = __ballot(bad) == 0 && sp <= (uint64_t)total + (total >> 3) + 64;
-            span = (uint32_t)sp;
-        }
-        if (dense) {
-            cst[wv][lane] = live ? (uint32_t)((c0 - sbase) >> 4) : span;
-            if (lane == 63)
-                cst[wv][64] = span;
-        } else {
-            cst[wv][lane] = incl - nch;
-            if (lane == 63)
-                cst[wv][64] = total;
-        }
-        pk[wv][lane] = u32x4{(uint32_t)c0, (uint32_t)(c0 >> 32), dense ? cst[wv][lane] : incl - nch,
+        cst[wv][lane] = incl - nch;
+        if (lane == 63)
+            cst[wv][64] = total;
+        pk[wv][lane] = u32x4{(uint32_t)c0, (uint32_t)(c0 >> 32), incl - nch,
                              nch | ((uint32_t)(a & 1) << 31)};
         acc[wv][lane] = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1107,88 +1071,11 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             if (cl < total)
                 atomicAdd(&acc[wv][cur], part);
         };
-        // dense: lane l takes chunks cb + l*SKV .. + SKV-1 of the span
-        constexpr int SKV = CLK_SPAN_KV;
-        auto span_load = [&](uint32_t cb, u32x4 (&v)[SKV]) {
-#pragma unroll
-            for (int k = 0; k < SKV; k++) {
-                const uint32_t c = cb + lane * SKV + k;
-                v[k] = c < span ? gload16(sbase + 16ull * c) : u32x4{0, 0, 0, 0};
-            }
-        };
-        auto span_eat = [&](uint32_t cb, const u32x4 (&v)[SKV]) {
-            const uint32_t cl = cb + lane * SKV;
-            if (cl >= span)
-                return;
-            uint32_t j = 0;                                    // last packet whose first chunk <= cl
-#pragma unroll
-            for (int step = 32; step >= 1; step >>= 1)
-                if (cst[wv][j + step] <= cl)
-                    j += step;
-            uint32_t sj = cst[wv][j], nxt = cst[wv][j + 1], pn = pk[wv][j][3];
-            uint32_t cur = j, part = 0;
-#pragma unroll
-            for (int k = 0; k < SKV; k++) {
-                const uint32_t c = cl + k;
-                if (c >= span)
-                    break;
-                if (c >= nxt) {
-                    do {
-                        j++;
-                        nxt = cst[wv][j + 1];
-                    } while (c >= nxt);
-                    sj = cst[wv][j];
-                    pn = pk[wv][j][3];
-                }
-                const uint32_t r = c - sj, pnch = pn & 0x7FFFFFFFu;
-                if (r >= pnch)                                 // a gap chunk
-                    continue;
-                if (j != cur) {
-                    atomicAdd(&acc[wv][cur], part);
-                    part = 0;
-                    cur = j;
-                }
-                const u32x4 V = v[k];
-                if (r < (uint32_t)HC)
-                    head[wv][j][r] = V;
-                if (r == pnch - 1)
-                    tail[wv][j] = V;
-                if (anyodd) {
-                    const uint32_t sel = (pn >> 31) ? 0x02030001u : 0x03020100u;
-#pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        part = dot_words(__builtin_amdgcn_perm(V[q], V[q], sel), part);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        part = dot_words(V[q], part);
-                }
-            }
-            if (part)
-                atomicAdd(&acc[wv][cur], part);
-        };
-        if (dense) {
-            // two register sets: the next pass's loads fly while this one is summed
-            constexpr uint32_t PASS = 64 * SKV;
-            u32x4 va[SKV], vb[SKV];
-            span_load(0, va);
-            for (uint32_t cb = 0; cb < span; cb += 2 * PASS) {   // wave-uniform
-                if (cb + PASS < span)
-                    span_load(cb + PASS, vb);
-                span_eat(cb, va);
-                if (cb + PASS < span) {
-                    if (cb + 2 * PASS < span)
-                        span_load(cb + 2 * PASS, va);
-                    span_eat(cb + PASS, vb);
-                }
-            }
-        } else {
-            for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
-                u32x4 v[KV];
-                uint32_t jk[KV], inf[KV];
-                issue(cb, v, jk, inf);
-                consume(cb, v, jk, inf);
-            }
+        for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
+            u32x4 v[KV];
+            uint32_t jk[KV], inf[KV];
+            issue(cb, v, jk, inf);
+            consume(cb, v, jk, inf);
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

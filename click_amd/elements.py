@@ -26,6 +26,20 @@ def anno_paint(color):
     return (color & 0xFF) << 8
 
 
+class ResultBuffers:
+    """Preallocated result arrays for Element.results(bufs=...): a caller
+    that pops batch after batch reuses them instead of allocating (and
+    page-faulting) four arrays per call."""
+
+    def __init__(self, cap):
+        self.tok = np.empty(cap, np.uint64)
+        self.port = np.empty(cap, np.int32)
+        self.len = np.empty(cap, np.uint32)
+        self.aux = np.empty(cap, np.uint32)
+        self.tok.fill(0), self.port.fill(0), self.len.fill(0), self.aux.fill(0)     # touch the pages once
+        self.ptrs = [a.ctypes.data_as(ctypes.c_void_p) for a in (self.tok, self.port, self.len, self.aux)]
+
+
 class Element:
     def __init__(self, ctx, class_name, config="", name=None, noutputs=1):
         """ctx: a click_amd.Context, or None: the element makes its own
@@ -110,9 +124,16 @@ class Element:
         if rc != 0:
             raise ClickAmdError("flush_async failed: %d (%s)" % (rc, self.last_error()))
 
-    def results(self, cap=1 << 20, aux=False):
+    def results(self, cap=1 << 20, aux=False, bufs=None):
         """(tokens, ports, lengths[, aux]) of every flushed packet, in order
-        (popped `cap` at a time: pass about the number expected)."""
+        (popped `cap` at a time: pass about the number expected).  bufs: a
+        ResultBuffers to pop into (reused across calls; the arrays returned
+        are then views of it, valid until its next use)."""
+        if bufs is not None:
+            n = self.lib.clk_element_results_aux(self.h, bufs.ptrs[0], bufs.ptrs[1], bufs.ptrs[2], bufs.ptrs[3],
+                                                 len(bufs.tok))
+            r = (bufs.tok[:n], bufs.port[:n], bufs.len[:n], bufs.aux[:n])
+            return r if aux else r[:3]
         out = []
         while True:
             t = np.empty(cap, np.uint64)

@@ -326,17 +326,18 @@ inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length
     } else {
         Stage &g = st_[cur_];
         const size_t slot = (g.h_used + 63) & ~size_t(63);
-        if ((slot + len + 64 > g.h_arena_cap || g.ngpu >= g.h_n_cap) &&
-            grow_host(g, slot + len + 64, g.ngpu + 1)) {
+        const uint32_t copy = std::min(len, stage_cap_);        // the bytes the kernel reads
+        if ((slot + copy + 64 > g.h_arena_cap || g.ngpu >= g.h_n_cap) &&
+            grow_host(g, slot + copy + 64, g.ngpu + 1)) {
             err_ = "out of pinned host memory";
             return CLK_EINVAL;
         }
-        if (len)
-            std::memcpy(g.h_arena + slot, data + off, len);
+        if (copy)
+            std::memcpy(g.h_arena + slot, data + off, copy);
         p.slot = slot;
         p.span_off = off;
         p.span_len = len;
-        g.h_used = slot + len;
+        g.h_used = slot + copy;
     }
     Stage &g = st_[cur_];
     if (p.host_code < 0) {                                        // the GPU batch's SoA, filled here
@@ -847,6 +848,10 @@ int CheckIPHeader::configure(ConfArgs &args, std::string *err)
     if (BatchElement::configure(args, err) || upload_addresses(err))
         return -1;
     reason_drops_.resize(details_ ? 6 : 0, 0);
+    // the kernel reads the header only (<= 60 bytes from OFFSET: options are
+    // summed only when ip_hl*4 <= ip_len <= the length) and checks ip_len
+    // against the packet's length: stage the header, report the length
+    stage_cap_ = offset_ + 60;
     return 0;
 }
 
@@ -937,6 +942,7 @@ int IPInputCombo::configure(ConfArgs &args, std::string *err)
     }
     if (BatchElement::configure(args, err) || upload_addresses(err))
         return -1;
+    stage_cap_ = offset_ + 60;                               // as CheckIPHeader
     return 0;
 }
 
@@ -1160,6 +1166,7 @@ int DecIPTTL::configure(ConfArgs &args, std::string *err)
         *err = "too many arguments";
         return -1;
     }
+    stage_cap_ = 20;          // the kernel reads ip_ttl..ip_sum and ip_dst's first byte (len >= 20)
     return BatchElement::configure(args, err);
 }
 

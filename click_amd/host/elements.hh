@@ -255,6 +255,11 @@ class BatchElement {
     std::string name_;
     int noutputs_;
     uint32_t batch_cap_ = 65536;
+    // staged (gather) batches copy at most this many bytes of a packet's span
+    // while its full length is what the kernel is told: for kernels that read
+    // only the header but check lengths against the packet (CheckIPHeader:
+    // OFFSET + 60, DecIPTTL: 20)
+    uint32_t stage_cap_ = 0xFFFFFFFFu;
     std::string err_;
     uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0, lost_ = 0;
     bool zerocopy_ = false;          // ZEROCOPY: packets read/written in registered host memory

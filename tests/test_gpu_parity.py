@@ -130,15 +130,22 @@ def test_fuzz_parity(torch, ctx, proto, max_total, align):
 
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 130, 257])
 @pytest.mark.parametrize("proto,max_total", [(17, 1600), (6, 1600), (17, 20000), (6, 20000)])
-def test_run_tails(torch, ctx, n, proto, max_total):
+@pytest.mark.parametrize("set_mode", [-1, 0])
+def test_run_tails(torch, n, proto, max_total, set_mode):
     """The fixed-geometry kernels store their outputs per run of 64 packets
     (CLK_L4_RUNS): batch sizes around a run boundary, 16 and 64 lanes per
-    packet, Check and Set (fused and two-phase), FIXOFF on and off."""
+    packet, Check and Set (two-phase by default; set_mode 0: fused, the
+    run's patched 64 B blocks stored whole after its barrier,
+    CLK_SET_RUNBLK), FIXOFF on and off, 64 B-aligned and any alignment."""
+    import click_amd
+    c = click_amd.Context(0).tune(set_mode=set_mode)
     rng = np.random.default_rng(n * 31 + proto + max_total)
-    arena, off, caplen, ml = fuzz.make_batch(rng, n, proto, max_total=max_total, align="any")
-    for op in OPS_L4[proto]:
-        compare(torch, ctx, op, arena, n, off=off, length=caplen, max_len=ml, arg=1)
-    compare(torch, ctx, OPS_L4[proto][1], arena, n, off=off, length=caplen, max_len=ml, arg=0)
+    for align in ("any", 64):
+        arena, off, caplen, ml = fuzz.make_batch(rng, n, proto, max_total=max_total, align=align)
+        for op in OPS_L4[proto]:
+            compare(torch, c, op, arena, n, off=off, length=caplen, max_len=ml, arg=1)
+        compare(torch, c, OPS_L4[proto][1], arena, n, off=off, length=caplen, max_len=ml, arg=0)
+    c.close()
 
 
 def test_run_outputs_at_odd_address(torch, ctx):

@@ -53,13 +53,6 @@ VARIANTS = {
     "hdrc0": (["-DCLK_HDR_FROM_CHUNKS=0"], {}),
     "ffu0": (["-DCLK_FRAG_FUSED=0"], {}),
     "ft512": (["-DCLK_FRAG_TILE=512"], {}),
-    "span0": (["-DCLK_SPAN=0"], {}),
-    "spkv1": (["-DCLK_SPAN_KV=1"], {}),
-    "spkv3": (["-DCLK_SPAN_KV=3"], {}),
-    "spkv4": (["-DCLK_SPAN_KV=4"], {}),
-    "spw8": (["-DCLK_SWPE_CHECK=8"], {}),
-    "spkv1w8": (["-DCLK_SPAN_KV=1", "-DCLK_SWPE_CHECK=8"], {}),
-    "spw5": (["-DCLK_SWPE_CHECK=5"], {}),
     "fusednt": (["-DCLK_NT_LOADS=1"], {"set_mode": 0}),
     "fusedsw5": (["-DCLK_L4_WPE_SET=5"], {"set_mode": 0}),
 }
