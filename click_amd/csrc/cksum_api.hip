@@ -131,7 +131,7 @@ constexpr int k_for(int G) { return G == 16 ? CLK_K16 : K; }
 #define CLK_SKV 2          // chunks per lane per pass of the packet-stream kernel (Set)
 #endif
 #ifndef CLK_SKV_CHECK
-#define CLK_SKV_CHECK 3    // ... Check, at CLK_SWPE_CHECK waves per SIMD (C4 Check 4.01 vs 4.08 ms with 2 at 8)
+#define CLK_SKV_CHECK 4    // ... Check, at CLK_SWPE_CHECK waves per SIMD (C4 Check 3.74 vs 3.89 ms with 3 at 6)
 #endif
 
 // Lanes per packet: the fewest (of 1, 4, 16, 64) whose K-deep pass covers
@@ -161,9 +161,11 @@ unsigned grid_for(const clk_ctx *ctx, uint64_t threads)
 // Scratch for n packets: the two-phase Set's work words (u32 x n).
 size_t work_bytes(uint64_t n) { return (n * 4 + 255) & ~size_t(255); }
 
+// The packet-stream kernel keeps a run's chunk counts in 32 bits and a
+// packet's in 27: it takes packets of known length up to 16 MiB.
 bool use_stream(const clk_ctx *ctx, const clk_batch *b)
 {
-    return b->len && !ctx->force_group && b->n >= ctx->stream_min;
+    return b->len && !ctx->force_group && b->n >= ctx->stream_min && b->max_len && b->max_len <= (1u << 24);
 }
 
 template <int G>

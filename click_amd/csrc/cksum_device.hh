@@ -71,6 +71,17 @@ __device__ __forceinline__ uint32_t lowmask(int k)
     return k >= 4 ? 0xFFFFFFFFu : ((1u << (8 * k)) - 1u);
 }
 
+// Chunk V with its bytes at positions eo..15 zeroed (eo 0: whole chunk).
+__device__ __forceinline__ u32x4 keep_below(u32x4 V, uint32_t eo)
+{
+    if (eo) {
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            V[q] &= lowmask((int)eo - 4 * q);
+    }
+    return V;
+}
+
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // v_dot2_u32_u16: acc + lo16(d) + hi16(d), wrapping mod 2^32 (no clamp) --
@@ -138,6 +149,16 @@ __device__ __forceinline__ uint32_t word_sum(const RangeAcc &acc, bool odd)
 __device__ __forceinline__ uint32_t ld_u8(const uint8_t *p)
 {
     return *(const __attribute__((address_space(1))) uint8_t *)p;
+}
+
+// Retire this wave's outstanding vector-memory loads here, inside the branch
+// that issued a rare load: the join after the branch then needs no wait.  A
+// kernel that keeps loads in flight across such code (the packet stream's
+// next-run pass) would otherwise wait for all of them at the join, since
+// vmcnt retires in order.  (gfx9 encoding: vmcnt 0, expcnt and lgkmcnt free.)
+__device__ __forceinline__ void vm_retire()
+{
+    __builtin_amdgcn_s_waitcnt(0x0F70);
 }
 
 __device__ __forceinline__ uint32_t ld_u32_unaligned(const uint8_t *p)

@@ -28,7 +28,13 @@
 #define CLK_STREAM_NT_CHECK 0   // packet-stream Check: nontemporal chunk loads (tuning knob)
 #endif
 #ifndef CLK_SWPE_CHECK
-#define CLK_SWPE_CHECK 6   // ... the Check kernels, with 3 chunks per lane per pass (CLK_SKV_CHECK)
+#define CLK_SWPE_CHECK 5   // ... the Check kernels, with 4 chunks per lane per pass (CLK_SKV_CHECK; LDS allows 5)
+#endif
+#ifndef CLK_DENSE
+#define CLK_DENSE 1        // packet-stream Check: dense runs load coalesced + nontemporal, through LDS
+#endif
+#ifndef CLK_DENSE_SET
+#define CLK_DENSE_SET 0    // ... the Set kernels too
 #endif
 #ifndef CLK_L4_RUNS
 #define CLK_L4_RUNS 1      // l4_kernel: a workgroup owns runs of packets and stores their outputs whole
@@ -377,7 +383,9 @@ __device__ __forceinline__ void l4_parse_words(uint8_t *nh, uint32_t caplen, int
             const uint32_t o = 20 + r;
             return (h[o >> 2] >> (8 * (o & 3))) & 0xFF;
         }
-        return ld_u8(nh + hl + r);
+        const uint32_t v = ld_u8(nh + hl + r);
+        vm_retire();
+        return v;
     };
     st.code = OK;
     st.rlen = 0;
@@ -963,23 +971,42 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
     constexpr int HC = SET && !DEFER && CLK_SET_REGBLK && HC0 < 4 ? 4 : HC0;
     constexpr bool COAL = SET && !DEFER && CLK_SET_REGBLK && CLK_STASH_COALESCE;
     __shared__ u32x4 head[4][64][HC];
-    __shared__ u32x4 tail[4][64];
-    __shared__ u32x4 pk[4][64];       // {c0 lo, c0 hi, chunk start, nch | odd << 31}
-    __shared__ uint32_t cst[4][68];   // chunk starts; cst[64] = total
+    // dense runs: the pass's chunks, coalesced order in, lane-consecutive out;
+    // the generic path keeps its packet records in the first 64 entries
+    constexpr bool DENSE = CLK_DENSE && (!SET || CLK_DENSE_SET);
+    __shared__ u32x4 stg[4][DENSE ? 64 * KV : 64];
+    __shared__ uint32_t cst[4][68];   // chunk starts; cst[64] = total (dense: span)
     __shared__ uint32_t acc[4][64];
+    __shared__ uint32_t pnf[4][DENSE ? 64 : 1];   // dense: nch | odd << 31
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u32x4 *const pk = stg[wv];       // {c0 lo, c0 hi, chunk start, nch | odd << 31}
     const uint64_t nruns = (b.n + 63) / 64;
     const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
-    for (uint64_t run = (uint64_t)blockIdx.x * (blockDim.x / 64) + wv; run < nruns; run += wstride) {
-        const uint64_t i = run * 64 + lane;
-        const bool live = i < b.n;
-        uint8_t *nh = b.base;
-        uint32_t caplen = 0;
-        if (live) {
-            nh = b.base + pkt_off(b, i);
-            caplen = pkt_len(b, i);
-        }
-        const uint64_t a = (uint64_t)nh;
+    uint64_t run = (uint64_t)blockIdx.x * (blockDim.x / 64) + wv;
+    if (run >= nruns)
+        return;                      // wave-uniform; no workgroup barrier below
+    // Phase A of one run: this lane's packet and the wave's chunk list.
+    struct RunA {
+        uint64_t a;                  // the packet's first byte (b.base for no packet)
+        uint32_t caplen, nch;
+        uint32_t start;              // first chunk in the wave's list (dense: in the span)
+        uint32_t total;              // wave-uniform: chunks in the list (dense: the span)
+        uint64_t sbase;              // dense: the span's first chunk address
+        bool anyodd, dense;
+    };
+    // the raw descriptors, loaded unconditionally (index clamped) and not
+    // yet used, so that a prefetch leaves them in flight
+    auto load_desc = [&](uint64_t r, uint64_t &off, uint32_t &len) {
+        const uint64_t i = r * 64 + lane;
+        const uint64_t ii = i < b.n ? i : 0;
+        off = pkt_off(b, ii);
+        len = pkt_len(b, ii);
+    };
+    auto phase_a = [&](uint64_t off, uint32_t len, uint64_t r) {
+        RunA R;
+        const bool live = r * 64 + lane < b.n;
+        const uint64_t a = live ? (uint64_t)b.base + off : (uint64_t)b.base;
+        const uint32_t caplen = live ? len : 0u;
         const uint64_t c0 = a & ~15ull;
         const uint32_t nch = caplen ? (uint32_t)((((a + caplen + 15) & ~15ull) - c0) >> 4) : 0u;
         uint32_t incl = nch;                                   // wave-inclusive scan
@@ -990,107 +1017,263 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                 incl += t;
         }
         const uint32_t total = __shfl(incl, 63, 64);
-        const bool anyodd = __ballot(live && (a & 1)) != 0;  // wave-uniform
-        cst[wv][lane] = incl - nch;
-        if (lane == 63)
-            cst[wv][64] = total;
-        pk[wv][lane] = u32x4{(uint32_t)c0, (uint32_t)(c0 >> 32), incl - nch,
-                             nch | ((uint32_t)(a & 1) << 31)};
-        acc[wv][lane] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // issue: find the packets of this lane's KV chunks at cb and load them
-        // per chunk the consumer needs its packet (jk) and inf = its index r in
-        // the packet | last chunk << 30 | odd packet << 31 (2 VGPRs per chunk
-        // rather than the packet's 4-word record: KV = 4 fits 8 waves)
-        auto issue = [&](uint32_t cb, u32x4 (&v)[KV], uint32_t (&jk)[KV], uint32_t (&inf)[KV]) {
-            const uint32_t cl = cb + lane * KV;
-            uint32_t j = 0;                                    // last packet whose chunk start <= cl
-#pragma unroll
-            for (int step = 32; step >= 1; step >>= 1)
-                if (cst[wv][j + step] <= cl)
-                    j += step;
-            uint32_t nxt = cst[wv][j + 1];
-#pragma unroll
-            for (int k = 0; k < KV; k++) {
-                const uint32_t c = cl + k;
-                if (c < total && c >= nxt) {
-                    do {
-                        j++;
-                        nxt = cst[wv][j + 1];
-                    } while (c >= nxt);
-                }
-                jk[k] = j;
+        R.a = a;
+        R.caplen = caplen;
+        R.nch = nch;
+        R.anyodd = __ballot(live && (a & 1)) != 0;
+        R.dense = false;
+        R.sbase = 0;
+        R.start = incl - nch;
+        R.total = total;
+        // Dense run: the packets' chunk ranges are increasing and disjoint
+        // and their span [c0 of packet 0, end of the last) holds few gap
+        // chunks -- as a packed arena does.  A chunk's address is then
+        // sbase + 16 c with no lookup, so the wave loads the span coalesced
+        // (lane l: chunks k*64 + l of the pass, one 1 KiB line-run per
+        // instruction) and nontemporal -- 6.9-7.1 TB/s where the
+        // lane-consecutive shape reads 6.2-6.3 (default policy) or 4.6
+        // (nontemporal: a line's pieces come from three instructions;
+        // tools/probes/shape_probe.hip) -- and hands the chunks to their
+        // lane-consecutive owners through LDS.  Gap chunks are loaded, not
+        // summed (at most total/8 + 64 of them).
+        if (DENSE) {
+            const uint64_t cend = c0 + 16ull * nch;
+            const uint32_t pe_lo = __shfl_up((uint32_t)cend, 1, 64), pe_hi = __shfl_up((uint32_t)(cend >> 32), 1, 64);
+            const uint64_t pend = (uint64_t)pe_lo | ((uint64_t)pe_hi << 32);
+            const bool bad = live && lane > 0 && c0 < pend;
+            const uint64_t nlive = __popcll(__ballot(live));          // live lanes are a prefix
+            const uint64_t sb = (uint64_t)__shfl((uint32_t)c0, 0, 64) | ((uint64_t)__shfl((uint32_t)(c0 >> 32), 0, 64) << 32);
+            const uint32_t lastl = nlive ? (uint32_t)nlive - 1 : 0u;
+            const uint64_t send = (uint64_t)__shfl((uint32_t)cend, (int)lastl, 64) |
+                                  ((uint64_t)__shfl((uint32_t)(cend >> 32), (int)lastl, 64) << 32);
+            const uint64_t sp = send >= sb ? (send - sb) >> 4 : ~0ull;
+            if (__ballot(bad) == 0 && total > 0 && sp <= (uint64_t)total + (total >> 3) + 64) {
+                R.dense = true;
+                R.sbase = sb;
+                R.total = (uint32_t)sp;
+                R.start = live ? (uint32_t)((c0 - sb) >> 4) : (uint32_t)sp;
             }
-#pragma unroll
-            for (int k = 0; k < KV; k++) {
-                const uint32_t c = cl + k;
-                const u32x4 P = pk[wv][jk[k]];
-                const uint32_t r = c - P[2];
-                inf[k] = r | (r == (P[3] & 0x7FFFFFFFu) - 1 ? 1u << 30 : 0u) | (P[3] & 0x80000000u);
-                const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
-                if (UseNT<CLK_STREAM_NT_CHECK && !SET>::value)
-                    v[k] = c < total ? __builtin_nontemporal_load((const u32x4 *)(cf + 16ull * (c - P[2])))
-                                     : u32x4{0, 0, 0, 0};
-                else
-                    v[k] = c < total ? gload16(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
-            }
-        };
-        // consume: whole-chunk sums into the packets' accumulators, stash
-        auto consume = [&](uint32_t cb, const u32x4 (&v)[KV], const uint32_t (&jk)[KV], const uint32_t (&inf)[KV]) {
-            const uint32_t cl = cb + lane * KV;
-            uint32_t cur = jk[0], part = 0;
-#pragma unroll
-            for (int k = 0; k < KV; k++) {
-                const uint32_t c = cl + k;
-                if (c >= total)
-                    break;
-                if (jk[k] != cur) {
-                    atomicAdd(&acc[wv][cur], part);
-                    part = 0;
-                    cur = jk[k];
-                }
-                const u32x4 V = v[k];
-                const uint32_t r = inf[k] & 0x3FFFFFFFu;       // chunk index within the packet
-                if (r < (uint32_t)HC)
-                    head[wv][jk[k]][r] = V;
-                if (inf[k] & (1u << 30))
-                    tail[wv][jk[k]] = V;
-                if (anyodd) {
-                    const uint32_t sel = (inf[k] >> 31) ? 0x02030001u : 0x03020100u;
-#pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        part = dot_words(__builtin_amdgcn_perm(V[q], V[q], sel), part);
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        part = dot_words(V[q], part);
-                }
-            }
-            if (cl < total)
-                atomicAdd(&acc[wv][cur], part);
-        };
-        for (uint32_t cb = 0; cb < total; cb += 64 * KV) {     // wave-uniform
-            u32x4 v[KV];
-            uint32_t jk[KV], inf[KV];
-            issue(cb, v, jk, inf);
-            consume(cb, v, jk, inf);
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        return R;
+    };
+    uint64_t na;
+    uint32_t ncap;
+    load_desc(run, na, ncap);
+    // issue: find the packets of this lane's KV chunks at cb and load them
+    // per chunk the consumer needs its packet (jk) and inf = its index r in
+    // the packet | last chunk << 30 | odd packet << 31 (2 VGPRs per chunk
+    // rather than the packet's 4-word record: KV = 4 fits 8 waves)
+    auto issue = [&](const RunA &R, uint32_t cb, u32x4 (&v)[KV], uint32_t (&jk)[KV], uint32_t (&inf)[KV]) {
+        const uint32_t cl = cb + lane * KV, total = R.total;
+        uint32_t j = 0;                                    // last packet whose chunk start <= cl
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+            if (cst[wv][j + step] <= cl)
+                j += step;
+        uint32_t nxt = cst[wv][j + 1];
+#pragma unroll
+        for (int k = 0; k < KV; k++) {
+            const uint32_t c = cl + k;
+            if (c < total && c >= nxt) {
+                do {
+                    j++;
+                    nxt = cst[wv][j + 1];
+                } while (c >= nxt);
+            }
+            jk[k] = j;
+        }
+#pragma unroll
+        for (int k = 0; k < KV; k++) {
+            const uint32_t c = cl + k;
+            const u32x4 P = pk[jk[k]];
+            const uint32_t r = c - P[2];
+            // r | (last chunk: 1 << 30 | end offset << 26) | odd start << 31
+            inf[k] = r | (r == (P[3] & 0x07FFFFFFu) - 1 ? (1u << 30) | (((P[3] >> 27) & 15) << 26) : 0u) |
+                     (P[3] & 0x80000000u);
+            const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
+            if (UseNT<CLK_STREAM_NT_CHECK && !SET>::value)
+                v[k] = c < total ? __builtin_nontemporal_load((const u32x4 *)(cf + 16ull * (c - P[2])))
+                                 : u32x4{0, 0, 0, 0};
+            else
+                v[k] = c < total ? gload16(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
+        }
+    };
+    // consume: whole-chunk sums into the packets' accumulators, stash
+    auto consume = [&](const RunA &R, uint32_t cb, const u32x4 (&v)[KV], const uint32_t (&jk)[KV],
+                       const uint32_t (&inf)[KV]) {
+        const uint32_t cl = cb + lane * KV, total = R.total;
+        uint32_t cj = jk[0], part = 0;
+#pragma unroll
+        for (int k = 0; k < KV; k++) {
+            const uint32_t c = cl + k;
+            if (c >= total)
+                break;
+            if (jk[k] != cj) {
+                atomicAdd(&acc[wv][cj], part);
+                part = 0;
+                cj = jk[k];
+            }
+            u32x4 V = v[k];
+            const uint32_t r = inf[k] & 0x03FFFFFFu;       // chunk index within the packet
+            if (inf[k] & (1u << 30))                      // the last chunk: bytes past the packet out
+                V = keep_below(V, (inf[k] >> 26) & 15);
+            if (r < (uint32_t)HC)
+                head[wv][jk[k]][r] = V;
+            if (R.anyodd) {
+                const uint32_t sel = (inf[k] >> 31) ? 0x02030001u : 0x03020100u;
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    part = dot_words(__builtin_amdgcn_perm(V[q], V[q], sel), part);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    part = dot_words(V[q], part);
+            }
+        }
+        if (cl < total)
+            atomicAdd(&acc[wv][cj], part);
+    };
+    // dense: lane l eats chunks cb + l*KV .. + KV-1 of the span from LDS
+    auto dense_eat = [&](const RunA &R, uint32_t cb) {
+        const uint32_t cl = cb + lane * KV, span = R.total;
+        if (cl >= span)
+            return;
+        uint32_t j = 0;                                    // last packet whose first chunk <= cl
+#pragma unroll
+        for (int step = 32; step >= 1; step >>= 1)
+            if (cst[wv][j + step] <= cl)
+                j += step;
+        uint32_t sj = cst[wv][j], nxt = cst[wv][j + 1], pn = pnf[wv][j];
+        uint32_t cj = j, part = 0;
+#pragma unroll
+        for (int k = 0; k < KV; k++) {
+            const uint32_t c = cl + k;
+            if (c >= span)
+                break;
+            if (c >= nxt) {
+                do {
+                    j++;
+                    nxt = cst[wv][j + 1];
+                } while (c >= nxt);
+                sj = cst[wv][j];
+                pn = pnf[wv][j];
+            }
+            const uint32_t r = c - sj, pnch = pn & 0x07FFFFFFu;
+            if (r >= pnch)                                 // a gap chunk
+                continue;
+            if (j != cj) {
+                atomicAdd(&acc[wv][cj], part);
+                part = 0;
+                cj = j;
+            }
+            u32x4 V = stg[wv][lane * KV + k];
+            if (r == pnch - 1)                             // the last chunk: bytes past the packet out
+                V = keep_below(V, (pn >> 27) & 15);
+            if (r < (uint32_t)HC)
+                head[wv][j][r] = V;
+            if (R.anyodd) {
+                const uint32_t sel = (pn >> 31) ? 0x02030001u : 0x03020100u;
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    part = dot_words(__builtin_amdgcn_perm(V[q], V[q], sel), part);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    part = dot_words(V[q], part);
+            }
+        }
+        if (part)
+            atomicAdd(&acc[wv][cj], part);
+    };
+    // dense loads: coalesced, nontemporal, addresses clamped into the span
+    // rather than the loads predicated (a predicated load forces its wait
+    // before the next use of the register)
+    constexpr uint32_t PASS = 64 * KV;
+    u32x4 dv[DENSE ? KV : 1];
+    auto dense_load = [&](const RunA &R, uint32_t cb) {
+#pragma unroll
+        for (int k = 0; k < KV; k++) {
+            const uint32_t c = min(cb + (uint32_t)k * 64 + lane, R.total - 1);
+            dv[k] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4 *)(R.sbase + 16ull * c));
+        }
+    };
+    for (;;) {
+        // (the descriptors are used from here on, not earlier: the compiler
+        // would hoist their use, and its wait, above the previous run)
+        asm volatile("" : "+v"(na), "+v"(ncap));
+        const RunA cur = phase_a(na, ncap, run);
+        {   // publish the run's phase A
+            const uint64_t c0 = cur.a & ~15ull;
+            // nch | end offset in the last chunk << 27 | odd start << 31
+            const uint32_t pnv = cur.nch | ((uint32_t)((cur.a + cur.caplen) & 15) << 27) | ((uint32_t)(cur.a & 1) << 31);
+            cst[wv][lane] = cur.start;
+            if (lane == 63)
+                cst[wv][64] = cur.total;
+            if (DENSE && cur.dense)
+                pnf[wv][lane] = pnv;
+            else
+                pk[lane] = u32x4{(uint32_t)c0, (uint32_t)(c0 >> 32), cur.start, pnv};
+            acc[wv][lane] = 0;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        // the next run's descriptors load while this run streams; a dense
+        // run's last pass also computes the next run's phase A and issues its
+        // first pass, so the wave's loads do not drain between runs
+        const uint64_t nrun = run + wstride;
+        if (DENSE && cur.dense) {
+            dense_load(cur, 0);
+            load_desc(nrun, na, ncap);
+            for (uint32_t cb = 0; cb < cur.total; cb += PASS) {     // wave-uniform
+#pragma unroll
+                for (int k = 0; k < KV; k++)
+                    stg[wv][k * 64 + lane] = dv[k];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                if (cb + PASS < cur.total)
+                    dense_load(cur, cb + PASS);
+                dense_eat(cur, cb);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        } else {
+            load_desc(nrun, na, ncap);
+            for (uint32_t cb = 0; cb < cur.total; cb += 64 * KV) {     // wave-uniform
+                u32x4 v[KV];
+                uint32_t jk[KV], inf[KV];
+                issue(cur, cb, v, jk, inf);
+                consume(cur, cb, v, jk, inf);
+            }
+            vm_retire();             // chunks past the list were loaded and not used
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        // Phase C
+        const uint64_t i = run * 64 + lane;
+        const uint64_t a = cur.a, c0 = a & ~15ull;
+        const uint32_t caplen = cur.caplen, nch = cur.nch;
+        uint8_t *nh = (uint8_t *)a;
         uint64_t blk_q0 = 0;         // COAL: the patched block's address | its first stash chunk
-        if (live) {
+        if (i < b.n) {
             const uint32_t *hw = (const uint32_t *)&head[wv][lane][0];
             const uint32_t q0 = (uint32_t)((a & ~3ull) - c0) >> 2;   // first header dword in the stash
             const uint64_t end = a + caplen;
             uint32_t d[HDR_DW];
 #pragma unroll
-            for (int k = 0; k < HDR_DW; k++)
-                d[k] = (a & ~3ull) + 4 * k >= end ? 0u
-                       : q0 + k < 4u * HC      ? hw[q0 + k]
-                                               : gload4((a & ~3ull) + 4 * k);
+            for (int k = 0; k < HDR_DW; k++) {
+                if ((a & ~3ull) + 4 * k >= end) {
+                    d[k] = 0u;
+                } else if (q0 + k < 4u * HC) {
+                    d[k] = hw[q0 + k];
+                } else {                 // past the stash (unaligned or option-bearing header)
+                    d[k] = gload4((a & ~3ull) + 4 * k);
+                    vm_retire();
+                }
+            }
             L4State st;
             l4_parse_words<PROTO, SET>(nh, caplen, fixoff, d, st);
             uint32_t sum = 0;
@@ -1105,8 +1288,18 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                     const uint32_t nh_ = nch < (uint32_t)HC ? nch : (uint32_t)HC;
                     for (uint32_t k = 0; k < nh_; k++)
                         out = chunk_outside(head[wv][lane][k], c0 + 16ull * k, s, rlen, sel, out);
-                    if (nch > (uint32_t)HC)
-                        out = chunk_outside(tail[wv][lane], c0 + 16ull * (nch - 1), s, rlen, sel, out);
+                    const uint64_t cl = c0 + 16ull * (nch - 1);
+                    if (nch > (uint32_t)HC && (e < a + caplen || s > cl)) {
+                        // the last chunk was summed up to the packet's end:
+                        // its bytes outside [s, e) -- in [e, end) (link-layer
+                        // padding, bytes past the transport length), or before
+                        // s (a short packet with options) -- are re-read and
+                        // taken out
+                        u32x4 T = gload16(cl);
+                        vm_retire();
+                        T = keep_below(T, (uint32_t)((a + caplen) & 15));
+                        out = chunk_outside(T, cl, s, rlen, sel, out);
+                    }
                     sum = acc[wv][lane] - out;
                 } else {
                     sum = lane_range_sum(s, rlen);
@@ -1130,14 +1323,14 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             // the patched blocks leave by 4 store instructions, each writing
             // 16 whole blocks: lanes 4p'..4p'+3 store quarters 0..3 of packet
             // 16 s + p' (a full 64 B write per 4 lanes)
-            pk[wv][lane] = u32x4{(uint32_t)blk_q0, (uint32_t)(blk_q0 >> 32), 0, 0};
+            pk[lane] = u32x4{(uint32_t)blk_q0, (uint32_t)(blk_q0 >> 32), 0, 0};
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
             for (uint32_t s4 = 0; s4 < 4; s4++) {
                 const uint32_t p = 16 * s4 + (lane >> 2), q = lane & 3;
-                const u32x4 P = pk[wv][p];
+                const u32x4 P = pk[p];
                 const uint64_t bq = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
                 if (bq) {
                     const uint64_t ca = (bq & ~63ull) + 16ull * q;
@@ -1149,7 +1342,12 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                 }
             }
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        run = nrun;
+        if (run >= nruns)
+            break;
     }
 }
 

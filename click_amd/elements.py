@@ -67,6 +67,14 @@ class Element:
         self._keep = []
         return k
 
+    def share_messages(self, other):
+        """Count this element's once-only chatter with other's
+        (clk_element_share_messages): one reference element's glue elements
+        on several threads speak once."""
+        if self.lib.clk_element_share_messages(self.h, other.h) != 0:
+            raise ValueError("clk_element_share_messages failed")
+        return self
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.clk_element_destroy(self.h)

@@ -11,6 +11,8 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <memory>
+#include <atomic>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -158,6 +160,7 @@ class BatchElement {
     int64_t take_packet(uint32_t key, uint8_t *buf, size_t cap);
     virtual std::string read_handler(const std::string &h) const;
     std::string take_messages();
+    void share_messages(const BatchElement &with) { gate_ = with.gate_; }
     const std::string &name() const { return name_; }
     std::string declaration() const { return name_ + " :: " + class_name(); }
     const std::string &last_error() const { return err_; }
@@ -262,6 +265,12 @@ class BatchElement {
     uint32_t stage_cap_ = 0xFFFFFFFFu;
     std::string err_;
     uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0, lost_ = 0;
+    // counts the events that gate once-only chatter (the first drop's
+    // reason, SetUDPChecksum's fragment warning, IPFragmenter's first five
+    // DF lines); shared by the elements that stand for one reference
+    // element (clk_element_share_messages)
+    std::shared_ptr<std::atomic<uint64_t>> gate_ = std::make_shared<std::atomic<uint64_t>>(0);
+    uint64_t gate_bump() { return gate_->fetch_add(1, std::memory_order_relaxed); }
     bool zerocopy_ = false;          // ZEROCOPY: packets read/written in registered host memory
     bool in_place_ = false;          // routing a zero-copy batch: the kernel already wrote the packets
     // the launching stage's buffers (valid in run()) and the routing
@@ -419,7 +428,6 @@ class SetL4Checksum : public BatchElement {
   private:
     int proto_;
     bool fixoff_ = false;
-    bool warned_ = false;   // router()->force_attachment("SetUDPChecksum_message")
 };
 
 // DecIPTTL (elements/ip/decipttl.cc): ACTIVE, MULTICAST; handlers drops,

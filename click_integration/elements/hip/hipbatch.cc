@@ -18,7 +18,7 @@
 CLICK_DECLS
 
 HIPBatchElement::HIPBatchElement()
-    : _device(-1), _latency_ms(1), _retries(3), _pt(0), _timers(0), _npt(0)
+    : _device(-1), _latency_ms(1), _retries(3), _pt(0), _timers(0), _npt(0), _gate(0)
 {
 }
 
@@ -67,6 +67,10 @@ HIPBatchElement::ensure(PerThread &t, ErrorHandler *errh)
 	t.ctx = 0;
 	return r;
     }
+    // this thread's element speaks its once-only chatter (first drop...)
+    // together with the home thread's, as the one reference element does
+    if (_gate && _gate != t.e)
+	clk_element_share_messages(t.e, _gate);
     return 0;
 }
 
@@ -88,6 +92,16 @@ HIPBatchElement::initialize(ErrorHandler *errh)
 	home = 0;
     if (ensure(_pt[home], errh) < 0)
 	return -1;
+    _gate = _pt[home].e;
+    if (const char *att = message_attachment()) {
+	// a router-wide once-only message (setudpchecksum.cc:53-57): the
+	// first such element's glue element counts for every one of them
+	void *&x = router()->force_attachment(att);
+	if (!x)
+	    x = _gate;
+	else
+	    clk_element_share_messages(_gate, static_cast<clk_element *>(x));
+    }
     char buf[64];			// BATCH, parsed by the glue
     clk_element_read_handler(_pt[home].e, "batch", buf, sizeof(buf));
     _core.set_batch(strtoul(buf, 0, 10));

@@ -97,6 +97,9 @@ class HIPBatchElement : public Element { public:
     String glue_handler(const char *name) const;
     // the default finish(): output port as routed, killed on CLK_PORT_KILL
     int pass(Routed &r, Packet **out);
+    // the router attachment naming a once-per-router message, if the
+    // reference element has one (SetUDPChecksum); 0: once per element
+    virtual const char *message_attachment() const	{ return 0; }
 
     String _glue_conf;
     int _device;		// -1: per thread
@@ -105,6 +108,7 @@ class HIPBatchElement : public Element { public:
     PerThread *_pt;
     Timer *_timers;
     int _npt;
+    clk_element *_gate;		// whose once-only chatter the thread elements share
     hipcore::Core<Packet, HIPBatchElement, Spinlock> _core;
 
   private:

@@ -28,6 +28,7 @@ class HIPSetIPChecksum : public HIPSetChecksum { public:
 
 class HIPSetUDPChecksum : public HIPSetChecksum { public:
     const char *class_name() const	{ return "SetUDPChecksum"; }
+    const char *message_attachment() const	{ return "HIPSetUDPChecksum_message"; }
     const char *port_count() const	{ return PORTS_1_1X2; }
 };
 

@@ -133,10 +133,10 @@ typedef struct clk_batch {
     const uint32_t *len;
     uint32_t fixed_len;
     uint32_t max_len;   /* optional upper bound on len_i (0 = unknown).  With
-                           len != NULL, large batches run by the packet-stream
-                           kernel (whole-chunk sums, lengths free per packet);
-                           smaller ones in one lanes-per-packet geometry
-                           picked from max_len                               */
+                           len != NULL and max_len <= 16 MiB, large batches
+                           run by the packet-stream kernel (whole-chunk sums,
+                           lengths free per packet); others in one
+                           lanes-per-packet geometry picked from max_len     */
     uint64_t n;
 } clk_batch;
 

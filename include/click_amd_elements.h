@@ -140,6 +140,15 @@ int clk_element_flush_async(clk_element *e);
  * have written the host packets, so it is never run twice.               */
 uint64_t clk_element_abandon(clk_element *e);
 
+/* Count e's once-only chatter together with `with`'s: the first drop's
+ * reason of the Check elements and IPInputCombo (checkipheader.cc:145-147,
+ * ipinputcombo.cc:135-137), SetUDPChecksum's fragment warning
+ * (setudpchecksum.cc:52-58, once per router there) and IPFragmenter's first
+ * five DF lines (ipfragmenter.cc:96-102).  The Click adapter keeps one glue
+ * element per RouterThread; sharing makes them speak once, as the one
+ * reference element does.  CLK_EINVAL for a null element. */
+int clk_element_share_messages(clk_element *e, const clk_element *with);
+
 /* Pop up to `cap` results: token, port (enum clk_port) and the packet's
  * new length (CheckIPHeader trims to ip_len, checkipheader.cc:216-217;
  * otherwise unchanged).  Returns the number popped.                        */

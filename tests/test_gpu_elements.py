@@ -275,3 +275,42 @@ def test_new_element_configure_errors(ctx):
             Element(ctx, cls, conf)
     Element(ctx, "IPInputCombo", "COLOR 1, 18.26.4.255 18.26.7.255")
     Element(ctx, "DecIPTTL", "MULTICAST false, ACTIVE true")
+
+
+@pytest.mark.parametrize("cls,config,noutputs,reasons,prefix", [
+    ("CheckIPHeader", "OFFSET 14", 2, IP_REASONS, "e0: IP header check failed: "),
+    ("SetUDPChecksum", "", 1, None, "e0 :: SetUDPChecksum: fragment or short packet")])
+def test_shared_messages_speak_once(ctx, cls, config, noutputs, reasons, prefix):
+    """Two glue elements standing for one reference element (the Click
+    adapter's per-thread elements) share their once-only chatter
+    (clk_element_share_messages): the first drop's reason, or
+    SetUDPChecksum's fragment warning (once per router,
+    setudpchecksum.cc:52-58), is said once over both -- by whichever element
+    meets it first -- and each keeps its own drop counter."""
+    from click_amd.elements import Element
+    rng = np.random.default_rng(7)
+    arena, foff, flen = frames(rng, 1200, 17)
+    half = len(foff) // 2
+    a = Element(ctx, cls, config, name="e0", noutputs=noutputs)
+    b = Element(ctx, cls, config, name="e0", noutputs=noutputs).share_messages(a)
+    base = arena.ctypes.data
+    nh = -1 if cls == "CheckIPHeader" else 14
+    ref = arena.copy()
+    for e, rng_ in ((a, range(half)), (b, range(half, len(foff)))):
+        for i in rng_:
+            e.push_ptr(base + int(foff[i]), int(flen[i]), nh, token=i)
+        e.flush()
+        e.results()
+    msgs = a.messages() + b.messages()
+    if cls == "CheckIPHeader":
+        L = oracle_lib.load_oracle()
+        rb = ref.ctypes.data
+        codes = np.array([L.oracle_check_ip_header(rb + int(foff[i]), int(flen[i]), 14, 1, None, 0, None, 0)
+                          for i in range(len(foff))])
+        assert (codes[:half] != 0).any() and (codes[half:] != 0).any()
+        assert msgs == expected_drop_messages(prefix, codes, reasons, False)
+        assert int(a.read_handler("drops")) + int(b.read_handler("drops")) == int((codes != 0).sum())
+    else:
+        codes, _ = oracle_lib.batch("set_udp", ref, len(foff), off=foff + 14, length=flen - 14, arg=0)
+        assert (codes[:half] != 0).any() and (codes[half:] != 0).any()
+        assert msgs == [prefix]

@@ -406,7 +406,8 @@ def dense_layout(rng, n, proto, kind):
     swaps), 'empty' (every 7th packet caplen 0), 'gaps' (a 4 KB hole every
     50 packets: those runs exceed the span slack -> generic), 'shared' (no
     gap: neighbours share a chunk -> generic), 'reversed' (every other run
-    in reverse address order -> generic)."""
+    in reverse address order -> generic), 'padded' / 'padded_odd' (as
+    packed / odd, 60 % of the packets with 1-39 bytes past ip_len)."""
     pkts = []
     for k in range(n):
         L = int(rng.choice([40, 64, 300, 576, 1500, 1501]))
@@ -414,13 +415,18 @@ def dense_layout(rng, n, proto, kind):
             pkts.append(b"")
             continue
         ow = int(rng.integers(1, 6)) if rng.random() < 0.15 else 0
-        pkts.append(fuzz.build(rng, proto, max(L, 28 + 4 * ow + 20), ow))
+        p = fuzz.build(rng, proto, max(L, 28 + 4 * ow + 20), ow)
+        if kind.startswith("padded") and rng.random() < 0.6:
+            # bytes past ip_len / the transport length (link-layer padding):
+            # the kernel re-reads the last chunk to take them out
+            p = p + bytes(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8))
+        pkts.append(p)
     off = np.zeros(n, np.uint64)
     pos = 0
     for k, p in enumerate(pkts):
-        if kind in ("packed", "empty", "reversed"):
+        if kind in ("packed", "empty", "reversed", "padded"):
             pos = (pos + 63) // 64 * 64
-        elif kind == "odd":
+        elif kind in ("odd", "padded_odd"):
             pos = (pos + 15) // 16 * 16 + 16 + 2 * int(rng.integers(0, 4)) + 1
         elif kind == "gaps" and k % 50 == 0:
             pos += 4096
@@ -446,12 +452,13 @@ def dense_layout(rng, n, proto, kind):
     return arena, off, caplen, int(caplen.max())
 
 
-@pytest.mark.parametrize("kind", ["packed", "odd", "empty", "gaps", "shared", "reversed"])
+@pytest.mark.parametrize("kind", ["packed", "odd", "empty", "gaps", "shared", "reversed", "padded", "padded_odd"])
 @pytest.mark.parametrize("mode", [-1, 1])
 def test_stream_dense_and_generic_runs(torch, kind, mode):
-    """The packet-stream kernel's two per-run paths -- the dense span
-    stream (CLK_SPAN) and the per-packet chunk list -- on layouts that pick
-    each (and mixes within one batch), Check and Set (fused and two-phase),
+    """The packet-stream kernel's two per-run paths -- the dense span loaded
+    coalesced through LDS (CLK_DENSE) and the per-packet chunk list -- on
+    layouts that pick each (and mixes within one batch), with and without
+    bytes past the transport length, Check and Set (fused and two-phase),
     every protocol: oracle-exact."""
     import click_amd
     c = click_amd.Context(0).tune(stream_min=1, set_mode=mode)

@@ -54,6 +54,12 @@ VARIANTS = {
     "ffu0": (["-DCLK_FRAG_FUSED=0"], {}),
     "ft512": (["-DCLK_FRAG_TILE=512"], {}),
     "fusednt": (["-DCLK_NT_LOADS=1"], {"set_mode": 0}),
+    "dense0": (["-DCLK_DENSE=0", "-DCLK_SKV_CHECK=3", "-DCLK_SWPE_CHECK=6"], {}),
+    "dk3w6": (["-DCLK_SKV_CHECK=3", "-DCLK_SWPE_CHECK=6"], {}),
+    "dk5": (["-DCLK_SKV_CHECK=5", "-DCLK_SWPE_CHECK=5"], {}),
+    "dk2w8": (["-DCLK_SKV_CHECK=2", "-DCLK_SWPE_CHECK=8"], {}),
+    "dk6w4": (["-DCLK_SKV_CHECK=6", "-DCLK_SWPE_CHECK=4"], {}),
+    "dset": (["-DCLK_DENSE_SET=1"], {}),
     "fusedsw5": (["-DCLK_L4_WPE_SET=5"], {"set_mode": 0}),
 }
 
