@@ -110,8 +110,11 @@ class OracleVerify:
     """The oracle's digest (tests/oracle_lib.digest over oracle/cksum_oracle.c
     oracle_digest) of exactly this rank's work -- global packets
     [first, first + m), m = n or the prefix that fits VERIFY_BUDGET_S on
-    `threads` host threads -- run in a background thread (ctypes releases
-    the GIL) while the GPU measures; joined before any host timing."""
+    `threads` host threads -- run after the workload's timed regions (start()
+    then join()), never beside them: with the oracle's threads using the
+    box's whole CPU quota, the cgroup throttled the launching thread and the
+    GPU idled inside a timed region (C4 Check: 4.22 ms per step around
+    3.79 ms kernels, profiles/r03/bench_overlap_note.txt)."""
 
     def __init__(self, wname, elements, first, n, ttl_runs, threads):
         import threading
@@ -134,6 +137,8 @@ class OracleVerify:
             except Exception as e:            # reported in the record
                 self.error = repr(e)
         self.t = threading.Thread(target=run, daemon=True)
+
+    def start(self):
         self.t.start()
 
     def join(self):
@@ -299,6 +304,7 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, pa
     del arena, status, b, l4sums
     torch.cuda.empty_cache()
     if ver:
+        ver.start()
         res = ver.join()
         for e, r in out.items():
             o = oracle_check(torch, dist, coll_dev, ver, res, e, r["sub"])

@@ -33,6 +33,9 @@
 #ifndef CLK_DENSE
 #define CLK_DENSE 1        // packet-stream Check: dense runs load coalesced + nontemporal, through LDS
 #endif
+#ifndef CLK_DENSE_DEPTH
+#define CLK_DENSE_DEPTH 1  // ... passes in flight behind the one being summed (tuning knob)
+#endif
 #ifndef CLK_DENSE_SET
 #define CLK_DENSE_SET 0    // ... the Set kernels too
 #endif
@@ -330,8 +333,8 @@ __global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_s
 // ---------------------------------------------------------------------------
 // UDP / TCP check and set (checkudpheader.cc:84-107, setudpchecksum.cc:37-69,
 // checktcpheader.cc:85-107, settcpchecksum.cc:44-75), split in three steps
-// shared by the fixed-geometry kernel (l4_kernel) and the variable-length
-// kernel (l4_varlen_kernel):
+// shared by the fixed-geometry kernel (l4_kernel) and the packet-stream
+// kernel (l4_stream_kernel, which parses from its LDS stash: l4_parse_words):
 //   l4_parse  -- header checks; the summed range [nh+hl, nh+hl+rlen)
 //   (range sum by the caller)
 //   l4_finish -- Set field correction, fold, pseudo-header, verdict / store
@@ -1189,13 +1192,32 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
     // rather than the loads predicated (a predicated load forces its wait
     // before the next use of the register)
     constexpr uint32_t PASS = 64 * KV;
-    u32x4 dv[DENSE ? KV : 1];
-    auto dense_load = [&](const RunA &R, uint32_t cb) {
+    u32x4 dv[DENSE ? KV : 1], dw[DENSE && CLK_DENSE_DEPTH > 1 ? KV : 1];
+    auto dense_load_to = [&](const RunA &R, uint32_t cb, auto &d) {
 #pragma unroll
         for (int k = 0; k < KV; k++) {
             const uint32_t c = min(cb + (uint32_t)k * 64 + lane, R.total - 1);
-            dv[k] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4 *)(R.sbase + 16ull * c));
+            d[k] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4 *)(R.sbase + 16ull * c));
         }
+    };
+    auto dense_load = [&](const RunA &R, uint32_t cb) { dense_load_to(R, cb, dv); };
+    // one pass parked in LDS and eaten while the next ones load
+    auto dense_step = [&](const RunA &R, uint32_t cb, auto &d, uint32_t ahead) {
+#pragma unroll
+        for (int k = 0; k < KV; k++)
+            stg[wv][k * 64 + lane] = d[k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // two deep: issued unconditionally (past the span the clamped
+        // addresses all name its last chunk: one request per instruction), so
+        // the compiler's counted wait for this set does not drain the other
+        if (CLK_DENSE_DEPTH > 1 || cb + ahead < R.total)
+            dense_load_to(R, cb + ahead, d);
+        dense_eat(R, cb);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     };
     for (;;) {
         // (the descriptors are used from here on, not earlier: the compiler
@@ -1218,27 +1240,39 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        // the next run's descriptors load while this run streams; a dense
-        // run's last pass also computes the next run's phase A and issues its
-        // first pass, so the wave's loads do not drain between runs
+        // the next run's descriptors load while this run streams (a wave
+        // takes several runs only under a grid cap; issuing the next run's
+        // first dense pass ahead of phase C was tried, tools/gpu_r03f.sh and
+        // r03g, and is not kept)
         const uint64_t nrun = run + wstride;
-        if (DENSE && cur.dense) {
+        if (DENSE && cur.dense && CLK_DENSE_DEPTH > 1) {
+            // two passes in flight behind the one being eaten (two register
+            // sets, alternated so no register is copied while its load is
+            // pending): the kernel is LDS-bound at 5 waves per SIMD and has
+            // VGPRs to spare
+            // the next run's descriptors first: the oldest loads, so the
+            // counted wait for a pass is the same on entry and in the loop
+            load_desc(nrun, na, ncap);
+            dense_load(cur, 0);
+            dense_load_to(cur, PASS, dw);
+            // pairs of passes, no exit between them: every path into the
+            // loop head has the same loads in flight, so the counted wait
+            // for one set leaves the other's loads outstanding
+            // (the pass count in an SGPR: the loop branches on a scalar, so
+            // the compiler sees no exec-masked path into the loop head)
+            const uint32_t np = __builtin_amdgcn_readfirstlane((cur.total + PASS - 1) / PASS);
+            uint32_t cb = 0;
+            for (uint32_t p = 1; p < np; p += 2, cb += 2 * PASS) {
+                dense_step(cur, cb, dv, 2 * PASS);
+                dense_step(cur, cb + PASS, dw, 2 * PASS);
+            }
+            if (np & 1)
+                dense_step(cur, cb, dv, 2 * PASS);
+        } else if (DENSE && cur.dense) {
             dense_load(cur, 0);
             load_desc(nrun, na, ncap);
-            for (uint32_t cb = 0; cb < cur.total; cb += PASS) {     // wave-uniform
-#pragma unroll
-                for (int k = 0; k < KV; k++)
-                    stg[wv][k * 64 + lane] = dv[k];
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                if (cb + PASS < cur.total)
-                    dense_load(cur, cb + PASS);
-                dense_eat(cur, cb);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
+            for (uint32_t cb = 0; cb < cur.total; cb += PASS)           // wave-uniform
+                dense_step(cur, cb, dv, PASS);
         } else {
             load_desc(nrun, na, ncap);
             for (uint32_t cb = 0; cb < cur.total; cb += 64 * KV) {     // wave-uniform

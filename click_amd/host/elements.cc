@@ -281,6 +281,27 @@ int BatchElement::grow_dev(Stage &g, size_t bytes, size_t n)
     return 0;
 }
 
+// Copy n staged bytes.  Headers (n <= 64) move as whole 16 B pieces when
+// the packet has them (avail: bytes readable from src): fixed-size moves
+// instead of a variable-length memcpy call.  The bytes copied past n stay
+// inside the 64 B of slack every staging slot is grown with and are
+// overwritten by the next packet's slot.
+static inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail)
+{
+    const uint32_t q = (n + 15) >> 4;
+    if (q <= 4 && 16 * q <= avail) {
+        std::memcpy(dst, src, 16);
+        if (q > 1)
+            std::memcpy(dst + 16, src + 16, 16);
+        if (q > 2)
+            std::memcpy(dst + 32, src + 32, 16);
+        if (q > 3)
+            std::memcpy(dst + 48, src + 48, 16);
+    } else if (n) {
+        std::memcpy(dst, src, n);
+    }
+}
+
 template <class SpanF>
 inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token,
                                   uint32_t anno)
@@ -329,14 +350,16 @@ inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length
         // slots cut the bytes the host writes and the DMA moves (114 B
         // frames, 74 B staged: 80 B per packet instead of 128)
         const size_t slot = (g.h_used + 15) & ~size_t(15);
-        const uint32_t copy = std::min(len, stage_cap_);        // the bytes the kernel reads
+        uint32_t cap = stage_cap_;                               // the bytes the kernel reads
+        if (len > stage_hl_off_)
+            cap = std::min(cap, stage_hl_off_ + std::max(20u, (uint32_t)(data[off + stage_hl_off_] & 15) * 4));
+        const uint32_t copy = std::min(len, cap);
         if ((slot + copy + 64 > g.h_arena_cap || g.ngpu >= g.h_n_cap) &&
             grow_host(g, slot + copy + 64, g.ngpu + 1)) {
             err_ = "out of pinned host memory";
             return CLK_EINVAL;
         }
-        if (copy)
-            std::memcpy(g.h_arena + slot, data + off, copy);
+        stage_copy(g.h_arena + slot, data + off, copy, len);
         p.slot = slot;
         p.span_off = off;
         p.span_len = len;
@@ -855,6 +878,7 @@ int CheckIPHeader::configure(ConfArgs &args, std::string *err)
     // summed only when ip_hl*4 <= ip_len <= the length) and checks ip_len
     // against the packet's length: stage the header, report the length
     stage_cap_ = offset_ + 60;
+    stage_hl_off_ = offset_;
     return 0;
 }
 
@@ -946,6 +970,7 @@ int IPInputCombo::configure(ConfArgs &args, std::string *err)
     if (BatchElement::configure(args, err) || upload_addresses(err))
         return -1;
     stage_cap_ = offset_ + 60;                               // as CheckIPHeader
+    stage_hl_off_ = offset_;
     return 0;
 }
 

@@ -263,6 +263,10 @@ class BatchElement {
     // only the header but check lengths against the packet (CheckIPHeader:
     // OFFSET + 60, DecIPTTL: 20)
     uint32_t stage_cap_ = 0xFFFFFFFFu;
+    // ... and at most stage_hl_off_ + the IP header's length (ip_hl * 4, at
+    // least 20) for elements that read no byte past the header there
+    // (CheckIPHeader, IPInputCombo; disabled: ~0u)
+    uint32_t stage_hl_off_ = 0xFFFFFFFFu;
     std::string err_;
     uint64_t batches_ = 0, packets_ = 0, gpu_ns_ = 0, lost_ = 0;
     // counts the events that gate once-only chatter (the first drop's

@@ -11,5 +11,5 @@ for f in $(git ls-files click_amd/csrc click_amd/host include); do
 done
 mkdir -p build/variants
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -I"$T/include" \
-    -o build/variants/lib_prev.so "$T/click_amd/csrc/cksum_api.hip" "$T/click_amd/host/elements.cc"
+    -o build/variants/lib_prev.so "$T/click_amd/csrc/cksum_api.hip" "$T/click_amd/host/elements.cc" "$T/click_amd/host/ingest.cc"
 rm -rf "$T"

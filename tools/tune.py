@@ -27,6 +27,7 @@ VDIR = os.path.join(ROOT, "build", "variants")
 # name -> (compile flags, Context.tune knobs)
 VARIANTS = {
     "base": ([], {}),
+    "prev": (["<tools/build_prev.sh>"], {}),     # the last commit's sources
     "k6": (["-DCLK_K=6"], {}),
     "k16_8": (["-DCLK_K16=8"], {}),
     "nt": (["-DCLK_NT_LOADS=1"], {}),
@@ -35,6 +36,10 @@ VARIANTS = {
     "g32": ([], {"group": 32}),
     "fused": ([], {"set_mode": 0}),
     "two": ([], {"set_mode": 1}),
+    "mb1280": ([], {"max_blocks": 1280}),
+    "mb2560": ([], {"max_blocks": 2560}),
+    "mb4k": ([], {"max_blocks": 4096}),
+    "mb8k": ([], {"max_blocks": 8192}),
     "mb16k": ([], {"max_blocks": 16384}),
     "mb32k": ([], {"max_blocks": 32768}),
     "mb64k": ([], {"max_blocks": 65536}),
@@ -60,6 +65,11 @@ VARIANTS = {
     "dk2w8": (["-DCLK_SKV_CHECK=2", "-DCLK_SWPE_CHECK=8"], {}),
     "dk6w4": (["-DCLK_SKV_CHECK=6", "-DCLK_SWPE_CHECK=4"], {}),
     "dset": (["-DCLK_DENSE_SET=1"], {}),
+    "dd2": (["-DCLK_DENSE_DEPTH=2"], {}),
+    "dd2k3w6": (["-DCLK_DENSE_DEPTH=2", "-DCLK_SKV_CHECK=3", "-DCLK_SWPE_CHECK=6"], {}),
+    "dd2k2w8": (["-DCLK_DENSE_DEPTH=2", "-DCLK_SKV_CHECK=2", "-DCLK_SWPE_CHECK=8"], {}),
+    "dsetk3": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=3"], {}),
+    "dsetk4": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=4", "-DCLK_SWPE=4"], {}),
     "fusedsw5": (["-DCLK_L4_WPE_SET=5"], {"set_mode": 0}),
 }
 
@@ -77,7 +87,7 @@ def build(names):
     os.makedirs(VDIR, exist_ok=True)
     for n in names:
         flags, _ = VARIANTS[n]
-        if not flags:
+        if not flags or flags[0].startswith("<"):
             continue
         out = lib_for(n)
         cmd = [b._hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
