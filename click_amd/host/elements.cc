@@ -288,7 +288,9 @@ int BatchElement::grow_dev(Stage &g, size_t bytes, size_t n)
 // overwritten by the next packet's slot.
 static inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail)
 {
-    const uint32_t q = (n + 15) >> 4;
+    if (n == 0)
+        return;
+    const uint64_t q = ((uint64_t)n + 15) >> 4;
     if (q <= 4 && 16 * q <= avail) {
         std::memcpy(dst, src, 16);
         if (q > 1)
@@ -297,7 +299,7 @@ static inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint
             std::memcpy(dst + 32, src + 32, 16);
         if (q > 3)
             std::memcpy(dst + 48, src + 48, 16);
-    } else if (n) {
+    } else {
         std::memcpy(dst, src, n);
     }
 }
