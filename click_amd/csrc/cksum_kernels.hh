@@ -42,6 +42,9 @@
 #ifndef CLK_L4_RUNS
 #define CLK_L4_RUNS 1      // l4_kernel: a workgroup owns runs of packets and stores their outputs whole
 #endif
+#ifndef CLK_HDRC_CHECK
+#define CLK_HDRC_CHECK 0   // Check kernels in runs: header words from the pass-0 chunk registers (tuning knob)
+#endif
 #ifndef CLK_L4_RUNS_SET_G
 #define CLK_L4_RUNS_SET_G 16   // Set kernels use runs from this G up (C5 -6 %; C3 -5 % with nontemporal scatter stores: DESIGN.md §6)
 #endif
@@ -815,7 +818,7 @@ __device__ __forceinline__ L4Out l4_group(const BatchArgs &b, int fixoff, uint64
     constexpr bool NT = UseNT<!SET || DEFER>::value;
     load_pass<G, K, NT>(c0, nch, 0, gl, v);  // issued before the header loads
     L4State st;
-    if (SET && DEFER && HDRC && G >= 4)    // two-phase compute pass, grid-stride loop
+    if ((!SET || DEFER) && HDRC && G >= 4) // two-phase compute pass, grid-stride loop; Check: CLK_HDRC_CHECK
         l4_parse_from_chunks<PROTO, SET, G, K>(nh, caplen, fixoff, (uint64_t)c0, lane, v, st);
     else
         l4_parse<PROTO, SET>(nh, caplen, fixoff, st);
@@ -866,7 +869,7 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             for (uint32_t p = 0; p < RB / PPB; p++) {
                 const uint32_t q = p * PPB + threadIdx.x / G;
                 if (i0 + q < b.n) {
-                    const L4Out o = l4_group<PROTO, SET, G, K, DEFER, false>(b, fixoff, i0 + q, lane, gl);
+                    const L4Out o = l4_group<PROTO, SET, G, K, DEFER, !SET && CLK_HDRC_CHECK>(b, fixoff, i0 + q, lane, gl);
                     if (gl == 0) {
                         if (SET && DEFER) {
                             r_work[q] = o.work;
@@ -895,7 +898,7 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
     }
     const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
     for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; i < b.n; i += groups) {
-        const L4Out o = l4_group<PROTO, SET, G, K, DEFER, CLK_HDR_FROM_CHUNKS != 0>(b, fixoff, i, lane, gl);
+        const L4Out o = l4_group<PROTO, SET, G, K, DEFER, (SET && DEFER && CLK_HDR_FROM_CHUNKS != 0) || (!SET && CLK_HDRC_CHECK)>(b, fixoff, i, lane, gl);
         if (gl == 0) {
             if (SET && DEFER) {
                 work[i] = o.work;

@@ -1,0 +1,11 @@
+#!/bin/bash
+# r03n: check of the tree: every -m gpu test, smoke, default bench, then
+# C4 / C5 / C2 profiles (trace + FETCH/WRITE) for profiles/
+O=gpurun_out/r03n; mkdir -p $O
+. tools/gpu_step.sh
+step tests timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1
+step smoke timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+step bench timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+step prof_c4 timeout -k 10 900 tools/profile.sh r03 c4
+step prof_c5 timeout -k 10 900 tools/profile.sh r03 c5
+step prof_c2 timeout -k 10 900 tools/profile.sh r03 c2

@@ -66,6 +66,7 @@ VARIANTS = {
     "dk6w4": (["-DCLK_SKV_CHECK=6", "-DCLK_SWPE_CHECK=4"], {}),
     "dset": (["-DCLK_DENSE_SET=1"], {}),
     "dd2": (["-DCLK_DENSE_DEPTH=2"], {}),
+    "hdrc": (["-DCLK_HDRC_CHECK=1"], {}),
     "dd2k3w6": (["-DCLK_DENSE_DEPTH=2", "-DCLK_SKV_CHECK=3", "-DCLK_SWPE_CHECK=6"], {}),
     "dd2k2w8": (["-DCLK_DENSE_DEPTH=2", "-DCLK_SKV_CHECK=2", "-DCLK_SWPE_CHECK=8"], {}),
     "dsetk3": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=3"], {}),
