@@ -33,17 +33,11 @@
 #ifndef CLK_DENSE
 #define CLK_DENSE 1        // packet-stream Check: dense runs load coalesced + nontemporal, through LDS
 #endif
-#ifndef CLK_DENSE_DEPTH
-#define CLK_DENSE_DEPTH 1  // ... passes in flight behind the one being summed (tuning knob)
-#endif
 #ifndef CLK_DENSE_SET
 #define CLK_DENSE_SET 0    // ... the Set kernels too
 #endif
 #ifndef CLK_L4_RUNS
 #define CLK_L4_RUNS 1      // l4_kernel: a workgroup owns runs of packets and stores their outputs whole
-#endif
-#ifndef CLK_HDRC_CHECK
-#define CLK_HDRC_CHECK 0   // Check kernels in runs: header words from the pass-0 chunk registers (tuning knob)
 #endif
 #ifndef CLK_L4_RUNS_SET_G
 #define CLK_L4_RUNS_SET_G 16   // Set kernels use runs from this G up (C5 -6 %; C3 -5 % with nontemporal scatter stores: DESIGN.md §6)
@@ -818,7 +812,7 @@ __device__ __forceinline__ L4Out l4_group(const BatchArgs &b, int fixoff, uint64
     constexpr bool NT = UseNT<!SET || DEFER>::value;
     load_pass<G, K, NT>(c0, nch, 0, gl, v);  // issued before the header loads
     L4State st;
-    if ((!SET || DEFER) && HDRC && G >= 4) // two-phase compute pass, grid-stride loop; Check: CLK_HDRC_CHECK
+    if (SET && DEFER && HDRC && G >= 4)    // two-phase compute pass, grid-stride loop
         l4_parse_from_chunks<PROTO, SET, G, K>(nh, caplen, fixoff, (uint64_t)c0, lane, v, st);
     else
         l4_parse<PROTO, SET>(nh, caplen, fixoff, st);
@@ -869,7 +863,7 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             for (uint32_t p = 0; p < RB / PPB; p++) {
                 const uint32_t q = p * PPB + threadIdx.x / G;
                 if (i0 + q < b.n) {
-                    const L4Out o = l4_group<PROTO, SET, G, K, DEFER, !SET && CLK_HDRC_CHECK>(b, fixoff, i0 + q, lane, gl);
+                    const L4Out o = l4_group<PROTO, SET, G, K, DEFER, false>(b, fixoff, i0 + q, lane, gl);
                     if (gl == 0) {
                         if (SET && DEFER) {
                             r_work[q] = o.work;
@@ -898,7 +892,7 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
     }
     const uint64_t groups = (uint64_t)gridDim.x * blockDim.x / G;
     for (uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G; i < b.n; i += groups) {
-        const L4Out o = l4_group<PROTO, SET, G, K, DEFER, (SET && DEFER && CLK_HDR_FROM_CHUNKS != 0) || (!SET && CLK_HDRC_CHECK)>(b, fixoff, i, lane, gl);
+        const L4Out o = l4_group<PROTO, SET, G, K, DEFER, CLK_HDR_FROM_CHUNKS != 0>(b, fixoff, i, lane, gl);
         if (gl == 0) {
             if (SET && DEFER) {
                 work[i] = o.work;
@@ -1195,7 +1189,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
     // rather than the loads predicated (a predicated load forces its wait
     // before the next use of the register)
     constexpr uint32_t PASS = 64 * KV;
-    u32x4 dv[DENSE ? KV : 1], dw[DENSE && CLK_DENSE_DEPTH > 1 ? KV : 1];
+    u32x4 dv[DENSE ? KV : 1];
     auto dense_load_to = [&](const RunA &R, uint32_t cb, auto &d) {
 #pragma unroll
         for (int k = 0; k < KV; k++) {
@@ -1212,10 +1206,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // two deep: issued unconditionally (past the span the clamped
-        // addresses all name its last chunk: one request per instruction), so
-        // the compiler's counted wait for this set does not drain the other
-        if (CLK_DENSE_DEPTH > 1 || cb + ahead < R.total)
+        if (cb + ahead < R.total)
             dense_load_to(R, cb + ahead, d);
         dense_eat(R, cb);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1248,30 +1239,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         // first dense pass ahead of phase C was tried, tools/gpu_r03f.sh and
         // r03g, and is not kept)
         const uint64_t nrun = run + wstride;
-        if (DENSE && cur.dense && CLK_DENSE_DEPTH > 1) {
-            // two passes in flight behind the one being eaten (two register
-            // sets, alternated so no register is copied while its load is
-            // pending): the kernel is LDS-bound at 5 waves per SIMD and has
-            // VGPRs to spare
-            // the next run's descriptors first: the oldest loads, so the
-            // counted wait for a pass is the same on entry and in the loop
-            load_desc(nrun, na, ncap);
-            dense_load(cur, 0);
-            dense_load_to(cur, PASS, dw);
-            // pairs of passes, no exit between them: every path into the
-            // loop head has the same loads in flight, so the counted wait
-            // for one set leaves the other's loads outstanding
-            // (the pass count in an SGPR: the loop branches on a scalar, so
-            // the compiler sees no exec-masked path into the loop head)
-            const uint32_t np = __builtin_amdgcn_readfirstlane((cur.total + PASS - 1) / PASS);
-            uint32_t cb = 0;
-            for (uint32_t p = 1; p < np; p += 2, cb += 2 * PASS) {
-                dense_step(cur, cb, dv, 2 * PASS);
-                dense_step(cur, cb + PASS, dw, 2 * PASS);
-            }
-            if (np & 1)
-                dense_step(cur, cb, dv, 2 * PASS);
-        } else if (DENSE && cur.dense) {
+        if (DENSE && cur.dense) {
             dense_load(cur, 0);
             load_desc(nrun, na, ncap);
             for (uint32_t cb = 0; cb < cur.total; cb += PASS)           // wave-uniform

@@ -65,10 +65,6 @@ VARIANTS = {
     "dk2w8": (["-DCLK_SKV_CHECK=2", "-DCLK_SWPE_CHECK=8"], {}),
     "dk6w4": (["-DCLK_SKV_CHECK=6", "-DCLK_SWPE_CHECK=4"], {}),
     "dset": (["-DCLK_DENSE_SET=1"], {}),
-    "dd2": (["-DCLK_DENSE_DEPTH=2"], {}),
-    "hdrc": (["-DCLK_HDRC_CHECK=1"], {}),
-    "dd2k3w6": (["-DCLK_DENSE_DEPTH=2", "-DCLK_SKV_CHECK=3", "-DCLK_SWPE_CHECK=6"], {}),
-    "dd2k2w8": (["-DCLK_DENSE_DEPTH=2", "-DCLK_SKV_CHECK=2", "-DCLK_SWPE_CHECK=8"], {}),
     "dsetk3": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=3"], {}),
     "dsetk4": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=4", "-DCLK_SWPE=4"], {}),
     "fusedsw5": (["-DCLK_L4_WPE_SET=5"], {"set_mode": 0}),
