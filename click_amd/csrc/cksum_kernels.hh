@@ -123,14 +123,28 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
     // request per packet carries its header (CLK_IPH_PAIR)
     constexpr bool PAIR = MODE != IP_SET && CLK_IPH_PAIR;
     constexpr uint32_t PL = PAIR ? 2 : 1;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < PL * b.n; j += nthreads) {
+    typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+    typedef __attribute__((address_space(1))) u32x3 __attribute__((aligned(4))) g3;
+    // the packet of work item j: its header address and length after OFFSET
+    auto locate = [&](uint64_t j, uint8_t *&ip, uint32_t &plen) {
         const uint64_t i = PAIR ? j >> 1 : j;
-        uint8_t *ip = b.base + pkt_off(b, i);
-        uint32_t plen = pkt_len(b, i);
+        ip = b.base + pkt_off(b, i);
+        plen = pkt_len(b, i);
         if (MODE != IP_SET) {           // data() + OFFSET, length() - OFFSET (checkipheader.cc:163-164)
             ip += offset;
             plen -= offset;
         }
+    };
+    // PAIR: lane 0 of the pair loads dwords 0-2 of the dword below ip, lane 1
+    // dwords 3-5 (ip not 4-aligned) or 2-4
+    auto pair_load = [&](uint64_t j, const uint8_t *ip) -> u32x3 {
+        const uint64_t a = (uint64_t)ip;
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint8_t *q = (const uint8_t *)(a & ~3ull);
+        return __builtin_nontemporal_load((const g3 *)(q + (((uint32_t)j & 1) ? (sh ? 12 : 8) : 0)));
+    };
+    auto one = [&](uint64_t j, uint8_t *ip, uint32_t plen, u32x3 m) {
+        const uint64_t i = PAIR ? j >> 1 : j;
         uint32_t code = OK, stored = 0;
         if ((int)plen < 20) {           // checkipheader.cc:168-170 / setipchecksum.cc:82
             code = MODE == IP_SET ? SET_KILL : IP_MINISCULE;
@@ -142,11 +156,7 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
             u32x4 d0;
             uint32_t d4, d5;
             if (PAIR) {
-                // lane 0: dwords 0-2 of q; lane 1: dwords 3-5 (sh != 0) or 2-4
-                typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-                typedef __attribute__((address_space(1))) u32x3 __attribute__((aligned(4))) g3;
                 const uint32_t odd = (uint32_t)j & 1;
-                const u32x3 m = __builtin_nontemporal_load((const g3 *)(q + (odd ? (sh ? 12 : 8) : 0)));
                 const uint32_t o0 = __shfl_xor(m.x, 1, 64), o1 = __shfl_xor(m.y, 1, 64), o2 = __shfl_xor(m.z, 1, 64);
                 const u32x3 lo = odd ? u32x3{o0, o1, o2} : m, hi = odd ? m : u32x3{o0, o1, o2};
                 d0 = u32x4{lo.x, lo.y, lo.z, sh ? hi.x : hi.y};
@@ -222,6 +232,12 @@ __global__ void __launch_bounds__(256) ip_header_kernel(BatchArgs b, uint32_t of
             out_code[i] = (uint8_t)code;
         if (MODE == IP_SET && out_sum)
             out_sum[i] = (uint16_t)stored;
+    };
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < PL * b.n; j += nthreads) {
+        uint8_t *ip;
+        uint32_t plen;
+        locate(j, ip, plen);
+        one(j, ip, plen, PAIR && (int)plen >= 20 ? pair_load(j, ip) : u32x3{0, 0, 0});
     }
 }
 
