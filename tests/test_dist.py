@@ -80,7 +80,7 @@ def run_world(world, n_imix=5000):
     return out
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])        # 8: the driver's largest node, as gloo ranks
 def test_sharded_digest_matches_single_process(world):
     n_imix = 5000
     out = run_world(world, n_imix)
