@@ -135,8 +135,8 @@ def test_run_tails(torch, n, proto, max_total, set_mode):
     """The fixed-geometry kernels store their outputs per run of 64 packets
     (CLK_L4_RUNS): batch sizes around a run boundary, 16 and 64 lanes per
     packet, Check and Set (two-phase by default; set_mode 0: fused, the
-    run's patched 64 B blocks stored whole after its barrier,
-    CLK_SET_RUNBLK), FIXOFF on and off, 64 B-aligned and any alignment."""
+    field's 64 B block stored whole from the pass-0 registers where it lies
+    in the packet), FIXOFF on and off, 64 B-aligned and any alignment."""
     import click_amd
     c = click_amd.Context(0).tune(set_mode=set_mode)
     rng = np.random.default_rng(n * 31 + proto + max_total)
@@ -469,4 +469,57 @@ def test_stream_dense_and_generic_runs(torch, kind, mode):
             compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=1)
         if proto == 6:
             compare(torch, c, "set_tcp", arena, len(off), off=off, length=caplen, max_len=ml, arg=0)
+    c.close()
+
+
+def test_empty_batches(torch, ctx):
+    """n = 0 through every entry point (fixed stride, descriptors, packet
+    stream): success, empty outputs, nothing written."""
+    import click_amd
+    arena = np.full(256, 0xA5, np.uint8)
+    for kw in (dict(stride=64, fixed_len=46), dict(off=np.zeros(0, np.uint64), length=np.zeros(0, np.uint32),
+                                                    max_len=1500)):
+        for stream_min in (1, 100000000):
+            c = click_amd.Context(0).tune(stream_min=stream_min)
+            for op in ("in_cksum", "check_ip", "set_ip", "check_udp", "set_udp", "check_tcp", "set_tcp",
+                       "check_icmp", "dec_ttl"):
+                b = dev_batch(torch, arena, 0, **kw)
+                codes, sums = run_gpu(c, op, b)
+                c.sync()
+                for t in (codes, sums):
+                    assert t is None or t.numel() == 0, op
+                assert np.array_equal(b.base.cpu().numpy(), arena), op
+            c.close()
+
+
+@pytest.mark.parametrize("stream_min,group", [(1, 0), (100000000, 0)])
+def test_maximum_ip_length(torch, stream_min, group):
+    """Packets at the largest IP total length (65535 B: a 65515 B UDP
+    datagram / TCP segment) mixed with small ones, through the packet
+    stream and the fixed 64-lane geometry: Check and Set (FIXOFF on and off)
+    bit-exact against the oracle, every arena byte compared."""
+    import click_amd
+    c = click_amd.Context(0).tune(stream_min=stream_min, group=group)
+    rng = np.random.default_rng(65535 + stream_min % 7)
+    for proto in (17, 6):
+        sizes = [65535, 65535, 64, 1500, 65535, 40000, 576] * 10
+        pkts = [fuzz.build(rng, proto, t) for t in sizes]
+        n = len(pkts)
+        caplen = np.array([len(p) for p in pkts], np.uint32)
+        off = np.zeros(n, np.uint64)
+        pos = 0
+        for i, p in enumerate(pkts):
+            pos += int(rng.integers(0, 4)) * 16 + (i & 1)       # 16 B-aligned and odd starts
+            off[i] = pos
+            pos += len(p)
+        arena = np.zeros(pos + 64, np.uint8)
+        for i, p in enumerate(pkts):
+            arena[int(off[i]):int(off[i]) + len(p)] = np.frombuffer(p, np.uint8)
+        oracle_lib.batch("set_ip", arena, n, off=off, length=caplen)
+        oracle_lib.batch(OPS_L4[proto][1], arena, n, off=off, length=caplen, arg=0)
+        for i in range(0, n, 3):                                  # a third corrupted: Check must drop them
+            arena[int(off[i]) + int(caplen[i]) - 1] ^= 0x10
+        for op in OPS_L4[proto]:
+            compare(torch, c, op, arena, n, off=off, length=caplen, max_len=int(caplen.max()), arg=1)
+        compare(torch, c, OPS_L4[proto][1], arena, n, off=off, length=caplen, max_len=int(caplen.max()), arg=0)
     c.close()
