@@ -1252,7 +1252,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         }
         // the next run's descriptors load while this run streams (a wave
         // takes several runs only under a grid cap; issuing the next run's
-        // first dense pass ahead of phase C was tried, tools/gpu_r03f.sh and
+        // first dense pass ahead of phase C was tried, tools/gpu_runs/r03/gpu_r03f.sh and
         // r03g, and is not kept)
         const uint64_t nrun = run + wstride;
         if (DENSE && cur.dense) {
