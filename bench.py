@@ -942,7 +942,11 @@ def main():
     torch.cuda.set_device(dev)
     dist = None
     coll_dev = "cuda"
-    if world > 1:
+    # CLK_BENCH_DIST_WORLD1=1 (tests): one rank through the communicator
+    # anyway (WORLD_SIZE=1 and the MASTER_* variables set), so the RCCL code
+    # path -- init, barriers, all-reduce / all-gather of device tensors,
+    # grouped send/recv -- runs on a one-GPU box
+    if world > 1 or os.environ.get("CLK_BENCH_DIST_WORLD1") == "1":
         import torch.distributed as dist
         backend = os.environ.get("CLK_BENCH_BACKEND", "nccl")
         if backend == "nccl":

@@ -163,3 +163,40 @@ def test_bench_two_ranks_match_one(torch):
     assert pr[0]["first"] == 0 and pr[1]["first"] == pr[0]["packets"] and pr[0]["packets"] + pr[1]["packets"] == 2 * n
     mean = (pr[0]["bytes"] + pr[1]["bytes"]) / 2
     assert all(abs(p["bytes"] - mean) <= 1500 for p in pr), pr
+
+
+def test_bench_rccl_one_rank(torch):
+    """The RCCL (nccl backend) code path of bench.py on one GPU: the
+    communicator with one rank (device-bound init, barriers, all-reduce and
+    all-gather of device tensors, C4's byte-balanced cuts, the grouped
+    send/recv of the gather to rank 0) gives the same digests as the run
+    without a communicator, and the oracle matches."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    n = 1 << 17
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", LOCAL_WORLD_SIZE="1",
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), CLK_BENCH_DIST_WORLD1="1")
+    env.pop("CLK_BENCH_BACKEND", None)
+    env.pop("CLK_BENCH_SAME_DEVICE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--packets", str(n),
+           "--steps", "2", "--warmup", "1", "--no-c2", "--no-c1", "--no-cpu", "--no-peak", "--no-frag",
+           "--skip", "c5"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rccl = json.loads(lines[0])
+    plain = run_bench(1, n, skip="c5")
+    assert rccl["n_gpus"] == 1 and rccl["clk_env"].get("CLK_BENCH_DIST_WORLD1") == "1"
+    for sect in (None, "c4_imix"):
+        r_el = rccl["elements"] if sect is None else rccl[sect]["elements"]
+        p_el = plain["elements"] if sect is None else plain[sect]["elements"]
+        for e in ("CheckUDPHeader", "SetUDPChecksum"):
+            rv, ro = without_timing(r_el[e]["verify"])
+            pv, po = without_timing(p_el[e]["verify"])
+            assert rv == pv and ro == po and ro["oracle_match"] is True, (sect, e)
+        g = r_el["SetUDPChecksum"]["gather_to_rank0"]
+        assert g.get("matches_digest") is True and g.get("on_root_only") is True, g
