@@ -3,8 +3,10 @@ bench's multi-rank path.
 
 * C4: the full 64M-packet IMIX batch of bench.py (64/576/1500 B, 7:4:1,
   packed at 64 B-aligned offsets) through the packet-stream kernels: Set
-  then Check pass everywhere, a random sample matches the oracle byte for
-  byte, and one flipped bit in 1/1024 packets is caught exactly on those
+  then Check pass everywhere, the Set's checksums and the corrupted
+  Check's verdicts of the WHOLE batch match the host oracle's digest, a
+  random sample matches the oracle byte for byte, and one flipped bit in
+  1/1024 packets is caught exactly on those
   packets (except where SetUDPChecksum stored uh_sum = 0, which
   CheckUDPHeader does not verify: checkudpheader.cc:100).
 * C5: one GPU's 16M x 9000 B TCP shard (128M over 8 GPUs), same checks.
@@ -49,12 +51,19 @@ def oracle_packet(L, proto, idx):
     return ref
 
 
-def check_full_batch(torch, ctx, b, n, proto, off_np, len_np, sample=384):
+def check_full_batch(torch, ctx, b, n, proto, off_np, len_np, sample=384, fixed_len=0, imix=False):
     import bench
+    from click_amd import shard
+    check_el, set_el = ("CheckUDPHeader", "SetUDPChecksum") if proto == 17 else ("CheckTCPHeader", "SetTCPChecksum")
+    # the host oracle's digest of the whole batch (as bench.py's verify), Set and corrupted Check
+    od = oracle_lib.digest([check_el, set_el], proto, 0, n, fixed_len=fixed_len, imix=imix,
+                           threads=bench.verify_threads(1))
     st, _ = ctx.set_ip_checksum(b, want_sums=False)
     assert int(ctx.count_codes(st)[0]) == n
     st, sums = ctx.set_udp_checksum(b) if proto == 17 else ctx.set_tcp_checksum(b)
     assert int(ctx.count_codes(st)[0]) == n
+    gd = shard.digest(torch, st, sums, 0)
+    assert {f: gd[f] for f in shard.DIGEST_FIELDS} == od[set_el], (gd, od[set_el])
     v = ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)
     assert int(ctx.count_codes(v)[0]) == n
     assert int(ctx.count_codes(ctx.check_ip_header(b))[0]) == n
@@ -68,7 +77,10 @@ def check_full_batch(torch, ctx, b, n, proto, off_np, len_np, sample=384):
     # corruption caught exactly (the bench's timed Check batches)
     picks = bench.corrupt_picks(0, n)
     ctx.gen_corrupt(b, seed=bench.CORRUPT_SEED, rate_log2=bench.CORRUPT_LOG2, first_idx=0)
-    v = (ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)).cpu().numpy()
+    vt = ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)
+    gd = shard.digest(torch, vt, None, 0)
+    assert {f: gd[f] for f in shard.DIGEST_FIELDS} == od[check_el], (gd, od[check_el])
+    v = vt.cpu().numpy()
     detect = picks & (sums.cpu().numpy() != 0) if proto == 17 else picks
     assert detect.sum() > 0
     assert np.array_equal(v == 3, detect)
@@ -87,7 +99,7 @@ def test_c4_full_imix_batch(torch, ctx):
     b = click_amd.Batch(arena, n, off=off, length=ln, max_len=1500)
     ctx.gen_packets(b, proto=17)
     try:
-        check_full_batch(torch, ctx, b, n, 17, off.cpu().numpy(), ln.cpu().numpy())
+        check_full_batch(torch, ctx, b, n, 17, off.cpu().numpy(), ln.cpu().numpy(), imix=True)
     finally:
         del arena, b
         torch.cuda.empty_cache()
@@ -103,7 +115,7 @@ def test_c5_full_jumbo_shard(torch, ctx):
     ctx.gen_packets(b, proto=6)
     try:
         check_full_batch(torch, ctx, b, n, 6, np.arange(n, dtype=np.uint64) * np.uint64(stride),
-                         np.full(n, L, np.uint32), sample=128)
+                         np.full(n, L, np.uint32), sample=128, fixed_len=L)
     finally:
         del arena, b
         torch.cuda.empty_cache()
