@@ -257,19 +257,32 @@ def splitmix64_np(x):
 @pytest.mark.parametrize("proto,L,stride,n", [(17, 1500, 1536, 16 << 20), (17, 46, 64, 16 << 20),
                                               (6, 9000, 9024, 1 << 20)])
 def test_full_size_properties(torch, ctx, proto, L, stride, n):
-    """Set then Check passes everywhere; one flipped bit in 1/1024 packets is
-    caught exactly on those packets; a random sample of packets matches the
-    oracle byte for byte."""
+    """Set then Check passes everywhere; the whole batch's SetIPChecksum and
+    Set L4 checksums, and the corrupted L4 Check's verdicts, match the host
+    oracle's digest (as bench.py's verify); one flipped bit in 1/1024
+    packets is caught exactly on those packets; a random sample of packets
+    matches the oracle byte for byte."""
+    import bench
     import click_amd
+    from click_amd import shard
+    check_el, set_el = ("CheckUDPHeader", "SetUDPChecksum") if proto == 17 else ("CheckTCPHeader", "SetTCPChecksum")
+    els = ["SetIPChecksum"] + ([check_el, set_el] if L >= 28 else [])
+    od = oracle_lib.digest(els, proto, 0, n, fixed_len=L, threads=bench.verify_threads(1))
+
+    def same(codes, sums, e):
+        gd = shard.digest(torch, codes, sums, 0)
+        assert {f: gd[f] for f in shard.DIGEST_FIELDS} == od[e], (e, gd, od[e])
     with np.errstate(over="ignore"):
         arena = torch.empty(n * stride, dtype=torch.uint8, device="cuda:0")
         b = click_amd.Batch(arena, n, stride=stride, fixed_len=L)
         ctx.gen_packets(b, proto=proto)
         st, sums = ctx.set_ip_checksum(b)
         assert int(ctx.count_codes(st)[0]) == n
+        same(st, sums, "SetIPChecksum")
         if L >= 28:
             st, sums = (ctx.set_udp_checksum(b) if proto == 17 else ctx.set_tcp_checksum(b))
             assert int(ctx.count_codes(st)[0]) == n
+            same(st, sums, set_el)
             v = ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)
             assert int(ctx.count_codes(v)[0]) == n
         v = ctx.check_ip_header(b)
@@ -290,7 +303,9 @@ def test_full_size_properties(torch, ctx, proto, L, stride, n):
         # corruption is caught exactly where it was injected
         if L >= 28:
             ctx.gen_corrupt(b, seed=0xBAD, rate_log2=10)
-            v = (ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)).cpu().numpy()
+            vt = ctx.check_udp_header(b) if proto == 17 else ctx.check_tcp_header(b)
+            same(vt, None, check_el)
+            v = vt.cpu().numpy()
             i64 = np.arange(n, dtype=np.uint64)
             h = splitmix64_np(np.uint64(0xBAD) ^ (i64 * np.uint64(0xD1B54A32D192ED03)))
             sel = (h & np.uint64(1023)) == 0
