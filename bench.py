@@ -179,6 +179,20 @@ def run_element(ctx, name, b, status):
         raise ValueError(name)
 
 
+def load_torch_kernels(torch):
+    """Run once, on tiny tensors, the torch operations measure() issues
+    between a workload's GPU preparation and its warm-ups (a strided byte
+    fill, a clone): the first use of a torch kernel in a process loads its
+    code object, tens of milliseconds in which the GPU idles and drops its
+    clocks right before a warm-up."""
+    x = torch.zeros(64 * 64, dtype=torch.uint8, device="cuda")
+    x.view(64, 64)[:, 8] = 255
+    y = x.clone()
+    z = torch.zeros(64, dtype=torch.uint16, device="cuda")
+    int((y[:64].bool() & (z.view(torch.int16) != 0)).sum())
+    torch.cuda.synchronize()
+
+
 def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, packets=None, coll_dev="cuda",
             verify=True):
     """Generate the shard in HBM, make every checksum valid (untimed), then
@@ -213,6 +227,12 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, pa
         alg = {e: ALG[e](w["L"]) * n for e in w["elements"]}
     shards = shard.all_gather_ints(torch, dist, coll_dev, [first, n, ck_bytes])   # [first, packets, bytes] per rank
     ver = OracleVerify(wname, w["elements"], first, n, warmup + steps, verify_threads(world)) if verify else None
+    # host-side preparation first: the GPU work from generation through the
+    # last timed element then runs back to back, so the GPU does not idle
+    # (and drop its clocks) between the preparation and a warm-up
+    picks = corrupt_picks(first, n)
+    n_picks = int(picks.sum())
+    picks_t = torch.from_numpy(picks).to("cuda")
     status = torch.empty(n, dtype=torch.uint8, device="cuda")
     ctx.reserve(n)
     ctx.gen_packets(b, proto=w["proto"], seed=seed, first_idx=first)
@@ -220,15 +240,14 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, pa
     l4sums = torch.empty(n, dtype=torch.uint16, device="cuda")
     (ctx.set_tcp_checksum if w["proto"] == 6 else ctx.set_udp_checksum)(b, status=status, sums=l4sums)
     stream = torch.cuda.current_stream()
-    out = {}
-    picks = corrupt_picks(first, n)
+    timed = []
     for e in w["elements"]:
         if e in ("DecIPTTL", "IPOutputCombo"):
             # untimed: TTL 255 so that every timed pass decrements (<= 254 passes)
             arena.view(n, w["stride"])[:, 8] = 255
             ctx.set_ip_checksum(b, status=status, want_sums=False)
         corrupt = None
-        expect_drops = 0
+        expect = 0
         if e.startswith("Check"):
             # IP: a bit of ip_src/ip_dst (only the checksum can see it);
             # L4: a payload bit (CheckUDPHeader skips uh_sum == 0,
@@ -236,10 +255,7 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, pa
             corrupt = dict(seed=CORRUPT_SEED, rate_log2=CORRUPT_LOG2, first_idx=first,
                            lo=12 if e == "CheckIPHeader" else None, hi=20 if e == "CheckIPHeader" else 0)
             ctx.gen_corrupt(b, **corrupt)
-            if e == "CheckUDPHeader":
-                expect_drops = int((picks & (l4sums.cpu().numpy() != 0)).sum())
-            else:
-                expect_drops = int(picks.sum())
+            expect = "picks with uh_sum != 0" if e == "CheckUDPHeader" else n_picks    # counted after the timing
         for _ in range(warmup):
             run_element(ctx, e, b, status)
         torch.cuda.synchronize()
@@ -256,21 +272,28 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, pa
         wall = time.perf_counter() - t0
         if dist:
             dist.barrier()
-        kms = [a.elapsed_time(z) for a, z in ev]
-        kernel_ms = sum(kms) / len(kms)
-        # untimed: the result digest (Set: with the checksums it wrote)
+        # untimed, on the GPU only (the host work waits until every element
+        # of the workload is timed): the Set's checksums as it wrote them,
+        # this element's outputs kept, the corruption undone
         sums = None
         if e.startswith("Set"):
             sums = torch.empty(n, dtype=torch.uint16, device="cuda")
             {"SetUDPChecksum": ctx.set_udp_checksum, "SetTCPChecksum": ctx.set_tcp_checksum,
              "SetIPChecksum": ctx.set_ip_checksum}[e](b, status=status, sums=sums)
-        torch.cuda.synchronize()
-        dig = shard.digest(torch, status, sums, first)
-        # the same digest over the oracle-verified prefix of the shard
-        m = ver.m if ver else 0
-        sub = shard.digest(torch, status[:m], None if sums is None else sums[:m], first) if ver else None
+        codes = status.clone()
         if corrupt:
             ctx.gen_corrupt(b, **corrupt)             # flip the same bits back (untimed)
+        timed.append((e, wall, ev, codes, sums, expect))
+    torch.cuda.synchronize()
+    out = {}
+    for e, wall, ev, codes, sums, expect in timed:
+        kms = [a.elapsed_time(z) for a, z in ev]
+        kernel_ms = sum(kms) / len(kms)
+        expect_drops = int((picks_t & (l4sums.view(torch.int16) != 0)).sum()) if isinstance(expect, str) else expect
+        dig = shard.digest(torch, codes, sums, first)
+        # the same digest over the oracle-verified prefix of the shard
+        m = ver.m if ver else 0
+        sub = shard.digest(torch, codes[:m], None if sums is None else sums[:m], first) if ver else None
         wall, kernel_ms, dig, (expect_drops,), per_rank = shard.reduce_results(
             torch, dist, coll_dev, wall, kernel_ms, dig, [expect_drops])
         if sub is not None:
@@ -300,7 +323,7 @@ def measure(torch, ctx, dist, rank, world, wname, steps, warmup, seed=0x5EED, pa
                       digest=dict(dig, drops=dig["packets"] - dig["ok"], expected_drops=expect_drops,
                                   drops_exact=dig["packets"] - dig["ok"] == expect_drops),
                       gather=gather)
-        del sums
+    del timed, picks_t
     del arena, status, b, l4sums
     torch.cuda.empty_cache()
     if ver:
@@ -955,6 +978,7 @@ def main():
             dist.init_process_group(backend)
             coll_dev = "cpu"
     ctx = click_amd.Context(dev)
+    load_torch_kernels(torch)
     if args.e2e:
         w = WORKLOADS[args.workload]
         res = [e2e(torch, ctx, args.workload, el) for el in w["elements"]]
