@@ -68,6 +68,10 @@ VARIANTS = {
     "dsetk3": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=3"], {}),
     "dsetk4": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=4", "-DCLK_SWPE=4"], {}),
     "fusedsw5": (["-DCLK_L4_WPE_SET=5"], {"set_mode": 0}),
+    "fusedrb0": (["-DCLK_SET_REGBLK=0"], {"set_mode": 0}),
+    "fusedrb0nt": (["-DCLK_SET_REGBLK=0", "-DCLK_NT_LOADS=1"], {"set_mode": 0}),
+    "fusedrb0nts": (["-DCLK_SET_REGBLK=0", "-DCLK_NT_LOADS=1", "-DCLK_NT_STORES=1"], {"set_mode": 0}),
+    "occ4": (["-DCLK_SET_OCC_PAD=36864"], {}),
 }
 
 
