@@ -128,7 +128,7 @@ constexpr int K = CLK_K;   // 16-byte chunk loads in flight per lane per pass
 // sizes G by K; a G = 16 packet past 16 * CLK_K16 chunks takes two passes.
 constexpr int k_for(int G) { return G == 16 ? CLK_K16 : K; }
 #ifndef CLK_SKV
-#define CLK_SKV 2          // chunks per lane per pass of the packet-stream kernel (Set)
+#define CLK_SKV 4          // chunks per lane per pass of the packet-stream kernel (Set; dense path: 3 / 5 chunks 5.18 / 5.11 vs 5.08 ms)
 #endif
 #ifndef CLK_SKV_CHECK
 #define CLK_SKV_CHECK 4    // ... Check, at CLK_SWPE_CHECK waves per SIMD (C4 Check 3.74 vs 3.89 ms with 3 at 6)

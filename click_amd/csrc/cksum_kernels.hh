@@ -22,7 +22,7 @@
 #define CLK_NT_STORES 0    // tuning knob: nontemporal checksum-field stores
 #endif
 #ifndef CLK_SWPE
-#define CLK_SWPE 8         // packet-stream kernel: request this many waves per SIMD (TCP: at most 7, its 3 stashed head chunks)
+#define CLK_SWPE 4         // packet-stream Set kernels: request this many waves per SIMD (the dense path's LDS allows 4 at CLK_SKV 4)
 #endif
 #ifndef CLK_STREAM_NT_CHECK
 #define CLK_STREAM_NT_CHECK 0   // packet-stream Check: nontemporal chunk loads (tuning knob)
@@ -34,16 +34,39 @@
 #define CLK_DENSE 1        // packet-stream Check: dense runs load coalesced + nontemporal, through LDS
 #endif
 #ifndef CLK_DENSE_SET
-#define CLK_DENSE_SET 0    // ... the Set kernels too
+#define CLK_DENSE_SET 1    // ... the Set kernels too (with XCD-contiguous runs and 4 chunks per lane: C4 Set 5.08 vs 5.33 ms)
 #endif
 #ifndef CLK_L4_RUNS
 #define CLK_L4_RUNS 1      // l4_kernel: a workgroup owns runs of packets and stores their outputs whole
+#endif
+#ifndef CLK_XCD_BLOCKS
+#define CLK_XCD_BLOCKS 0   // tuning: every run loop walks XCD-contiguous runs (reads: C3 / C4 / C5 Check 2-8 % slower)
+#endif
+#ifndef CLK_XCD_SET
+#define CLK_XCD_SET 1      // the fused packet-stream Set does (C4 Set 5.38 vs 6.01 ms: DESIGN.md §6)
 #endif
 #ifndef CLK_L4_RUNS_SET_G
 #define CLK_L4_RUNS_SET_G 16   // Set kernels use runs from this G up (C5 -6 %; C3 -5 % with nontemporal scatter stores: DESIGN.md §6)
 #endif
 
 namespace clk {
+
+// The workgroup's place in the run order.  XCD-contiguous (XCD): workgroup b
+// (dispatched to XCD b % 8) takes position (b % 8) * q + min(b % 8, r) + b / 8
+// (q = grid / 8, r = grid % 8), a bijection under which each XCD walks one
+// contiguous share of the runs.  The two-byte field stores of neighbouring
+// packets in different runs (IMIX packets share 64 B blocks) then meet in one
+// L2 and leave it merged, instead of reaching the memory controller as
+// partial-block writes from two XCDs.  Read-only kernels keep the dealt
+// order: with eight separate read fronts they run 2-8 % slower.
+template <bool XCD>
+__device__ __forceinline__ uint32_t run_block()
+{
+    if (!XCD)
+        return blockIdx.x;
+    const uint32_t g = gridDim.x, x = blockIdx.x & 7, q = g >> 3, r = g & 7;
+    return x * q + (x < r ? x : r) + (blockIdx.x >> 3);
+}
 
 // NT: nontemporal loads (once-read stream; measured faster for the
 // fixed-geometry Check kernels, slower for the Set and packet-stream ones,
@@ -317,7 +340,7 @@ __global__ void __launch_bounds__(256) range_kernel(BatchArgs b, uint16_t *out_s
         constexpr uint32_t PPB = 256 / G, RB = PPB < 64 ? 64 : PPB;
         __shared__ uint16_t r_sum[RB];
         const uint64_t nruns = (b.n + RB - 1) / RB;
-        for (uint64_t run = blockIdx.x; run < nruns; run += gridDim.x) {       // uniform per workgroup
+        for (uint64_t run = run_block<CLK_XCD_BLOCKS != 0>(); run < nruns; run += gridDim.x) {       // uniform per workgroup
             const uint64_t i0 = run * RB;
 #pragma unroll 1
             for (uint32_t p = 0; p < RB / PPB; p++) {
@@ -873,7 +896,7 @@ l4_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         __shared__ uint32_t r_work[SET && DEFER ? RB : 1];
         __shared__ uint16_t r_sum[SET && !DEFER ? RB : 1];
         const uint64_t nruns = (b.n + RB - 1) / RB;
-        for (uint64_t run = blockIdx.x; run < nruns; run += gridDim.x) {       // uniform per workgroup
+        for (uint64_t run = run_block<CLK_XCD_BLOCKS != 0>(); run < nruns; run += gridDim.x) {       // uniform per workgroup
             const uint64_t i0 = run * RB;
 #pragma unroll 1
             for (uint32_t p = 0; p < RB / PPB; p++) {
@@ -998,7 +1021,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
     u32x4 *const pk = stg[wv];       // {c0 lo, c0 hi, chunk start, nch | odd << 31}
     const uint64_t nruns = (b.n + 63) / 64;
     const uint64_t wstride = (uint64_t)gridDim.x * (blockDim.x / 64);
-    uint64_t run = (uint64_t)blockIdx.x * (blockDim.x / 64) + wv;
+    uint64_t run = (uint64_t)run_block<CLK_XCD_BLOCKS || (SET && !DEFER && CLK_XCD_SET)>() * (blockDim.x / 64) + wv;
     if (run >= nruns)
         return;                      // wave-uniform; no workgroup barrier below
     // Phase A of one run: this lane's packet and the wave's chunk list.
