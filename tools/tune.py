@@ -74,6 +74,7 @@ VARIANTS = {
     "occ4": (["-DCLK_SET_OCC_PAD=36864"], {}),
     "xcd": (["-DCLK_XCD_BLOCKS=1"], {}),
     "xcdset0": (["-DCLK_XCD_SET=0"], {}),
+    "fusedxcd": (["-DCLK_XCD_BLOCKS=1"], {"set_mode": 0}),
     "oldset": (["-DCLK_DENSE_SET=0", "-DCLK_SKV=2", "-DCLK_SWPE=8"], {}),
     "dsetk5": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=5", "-DCLK_SWPE=4"], {}),
     "dsetk6w3": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=6", "-DCLK_SWPE=3"], {}),
