@@ -241,6 +241,9 @@ __device__ __forceinline__ u32x4 load16_guarded(uint64_t p, uint64_t hi)
 #ifndef CLK_FRAG_HDR_NT
 #define CLK_FRAG_HDR_NT 0   // ... nontemporal (tuning knob)
 #endif
+#ifndef CLK_FRAG_XCD
+#define CLK_FRAG_XCD 0      // unfused write kernel: XCD-contiguous tiles (tuning knob)
+#endif
 #ifndef CLK_FRAG_NT_STORE
 #define CLK_FRAG_NT_STORE 0
 #endif
@@ -376,7 +379,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
     __shared__ uint32_t lhdr[FUSED && CLK_FRAG_PRO ? FRAG_TILE : 1][5];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t gl = lane & (FRAG_G - 1), grp = threadIdx.x / FRAG_G, g0 = lane & ~(FRAG_G - 1);
-    uint32_t tix = blockIdx.x;
+    // unfused: the tiles' prefixes are known, so any order will do
+    uint32_t tix = run_block<!FUSED && CLK_FRAG_XCD>();
     if (FUSED) {
         if (threadIdx.x == 0) {
             lb_tile = atomicAdd(lb.ticket, 1u);

@@ -75,6 +75,7 @@ VARIANTS = {
     "xcd": (["-DCLK_XCD_BLOCKS=1"], {}),
     "xcdset0": (["-DCLK_XCD_SET=0"], {}),
     "fusedxcd": (["-DCLK_XCD_BLOCKS=1"], {"set_mode": 0}),
+    "ffu0xcd": (["-DCLK_FRAG_FUSED=0", "-DCLK_FRAG_XCD=1"], {}),
     "oldset": (["-DCLK_DENSE_SET=0", "-DCLK_SKV=2", "-DCLK_SWPE=8"], {}),
     "dsetk5": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=5", "-DCLK_SWPE=4"], {}),
     "dsetk6w3": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=6", "-DCLK_SWPE=3"], {}),
