@@ -905,6 +905,62 @@ def config1_cpu(n=C1_PACKETS):
                     "survey VM (BASELINE.md §3)"}
 
 
+def comm_info(torch, dist, dev):
+    """Which communicator the run had: backend, world size as the process
+    group reports it, and every rank's (rank, device index, device name,
+    PCI bus id), gathered over the group -- an N-rank run shows N ranks."""
+    name = torch.cuda.get_device_name(dev)
+    try:
+        bus = torch.cuda.get_device_properties(dev).pci_bus_id
+    except Exception:                       # older torch: no pci_bus_id
+        bus = None
+    mine = [int(os.environ.get("RANK", "0")), dev, name, bus]
+    if dist is None:
+        return {"backend": None, "world_size": 1, "devices": [mine]}
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, mine)
+    return {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "devices": allr}
+
+
+def compact_legs(legs):
+    """cpu_baseline legs for the line: [GiB/s, Mpps] for one thread and
+    [GiB/s, Mpps, threads] for all cores per workload; config 1 in Mpps."""
+    out = {}
+    for wl, leg in legs.items():
+        if wl == "c1":
+            out[wl] = {k: leg[k]["mpps"] for k in ("elements", "combos") if k in leg}
+            continue
+        one, al = leg.get("single_thread", {}), leg.get("all_cores", {})
+        out[wl] = {"element": leg.get("element"), "1t": [one.get("value"), one.get("mpps")],
+                   "all": [al.get("value"), al.get("mpps"), al.get("threads")]}
+    return out
+
+
+def bench_summary(line):
+    """{workload/element: [kernel_ms, roofline frac, oracle_match, drops_exact]}
+    over every timed element of the line (fragmenter: [kernel_ms, frac,
+    all fragmented, null])."""
+    out = {}
+    wl0 = line["config"]["workload"].split(":")[0]
+    sects = [(wl0, line.get("elements", {}))] + [(line[k]["workload"].split(":")[0], line[k]["elements"])
+                                                 for k in ("c2_64b", "c4_imix", "c5_jumbo") if k in line]
+    for wl, els in sects:
+        for e, r in els.items():
+            v = r.get("verify", {})
+            out["%s %s" % (wl, e)] = [r["roofline"]["kernel_ms"], r["roofline"]["frac"],
+                                      v.get("oracle", {}).get("oracle_match"), v.get("drops_exact")]
+    f = line.get("fragmenter")
+    if f:
+        vf = f.get("verify", {})
+        out["C3 IPFragmenter"] = [f["kernel_ms"], f["roofline"]["frac"],
+                                  vf.get("fragmented") == vf.get("packets") and vf.get("packets", 0) > 0, None]
+    c1 = line.get("c1_fake_iprouter")
+    if c1:
+        out["C1 mpps"] = {k: c1[k]["mpps"] for k in c1 if isinstance(c1[k], dict) and "mpps" in c1[k]}
+        out["C1 ok"] = c1.get("ok")
+    return out
+
+
 def spawn_ranks(args):
     """--gpus N > 1 without a torchrun environment: launch N ranks (one per
     GPU) under torch.distributed.run as a child process before anything
@@ -1008,6 +1064,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_c1:
         c1 = config1(ctx)
 
+    comm = comm_info(torch, dist, dev)         # a collective: every rank joins
     if rank == 0:
         w = WORKLOADS[args.workload]
         head = main_res[w["elements"][0]]
@@ -1027,6 +1084,7 @@ def main():
             # switches present in this run are recorded here
             "clk_env": {k: v for k, v in sorted(os.environ.items()) if k.startswith("CLK_")},
             "elements": {e: summarize(r, args.steps, args.workload) for e, r in main_res.items()},
+            "comm": comm,
         }
         if c2:
             line["c2_64b"] = {"workload": WORKLOADS["c2"]["desc"],
@@ -1046,6 +1104,7 @@ def main():
                 cb = cpu_baseline()
                 if c1:
                     cb["legs"]["c1"] = config1_cpu()
+                log("bench: cpu_baseline detail " + json.dumps(cb))     # the full legs, on stderr
                 head_leg = cb["legs"].get(args.workload, {}).get("all_cores", {})
                 line["cpu_baseline"] = {
                     "value": head_leg.get("value"), "unit": "GiB/s", "cores": cb["threads"], "kind": "port",
@@ -1053,9 +1112,13 @@ def main():
                     "sample": "%s over %s packets (%s B, DRAM-resident, NUMA-local shards), median of 5"
                               % (cb["legs"][args.workload]["element"], head_leg.get("packets"),
                                  head_leg.get("sample_bytes")),
-                    "cpu": cb["host"]["model"], **cb}
+                    "cpu": cb["host"]["model"], "quota": cb["host"]["quota"], "method": cb["method"],
+                    "legs": compact_legs(cb["legs"])}
             except Exception as e:        # reported, not fatal
                 line["cpu_baseline"] = {"error": repr(e)}
+        # last key: one entry per timed element, so that the tail of the line
+        # alone (the driver keeps the last few KB of stdout) carries them all
+        line["summary"] = bench_summary(line)
         print(json.dumps(line), flush=True)
     ctx.close()
     if dist:

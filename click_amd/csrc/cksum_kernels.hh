@@ -49,7 +49,45 @@
 #define CLK_L4_RUNS_SET_G 16   // Set kernels use runs from this G up (C5 -6 %; C3 -5 % with nontemporal scatter stores: DESIGN.md §6)
 #endif
 
+// Tools-only load-address check (tools/addr_check, built with
+// -DCLK_ADDR_CHECK=1; never in the product library).  Each load site of the
+// packet-stream kernel passes its address through chk_addr: an address whose
+// bytes leave the window registered by clk_dbg_window() is counted per site,
+// the first such address kept, and the load redirected to the window's start,
+// so a bad address is reported instead of faulting the GPU.
+#ifndef CLK_ADDR_CHECK
+#define CLK_ADDR_CHECK 0
+#endif
+#ifndef CLK_PHASEA_SGPR
+#define CLK_PHASEA_SGPR 0  // tools-only: 1 = round 3's readfirstlane phase A (int result widened: sign-extends), 2 = widened as unsigned
+#endif
+
 namespace clk {
+
+#if CLK_ADDR_CHECK
+enum { CHK_GENERIC = 0, CHK_DENSE = 1, CHK_HDR = 2, CHK_LAST = 3, CHK_RANGE = 4, CHK_UNDERFLOW = 5, CHK_SITES = 8 };
+__device__ uint64_t dbg_lo, dbg_hi;
+__device__ unsigned long long dbg_count[CHK_SITES], dbg_first[CHK_SITES];
+__device__ __forceinline__ void chk_note(int site, uint64_t a)
+{
+    atomicAdd(&dbg_count[site], 1ull);
+    atomicCAS(&dbg_first[site], 0ull, (unsigned long long)a);
+}
+__device__ __forceinline__ uint64_t chk_addr(uint64_t a, uint32_t bytes, int site)
+{
+    const uint64_t lo = dbg_lo, hi = dbg_hi;
+    if (hi && (a < lo || a + bytes > hi)) {
+        chk_note(site, a);
+        return lo;
+    }
+    return a;
+}
+#define CLK_CHK(a, n, site) ::clk::chk_addr((a), (n), ::clk::site)
+#define CLK_CHK_IF(cond, site, a) do { if (cond) ::clk::chk_note(::clk::site, (a)); } while (0)
+#else
+#define CLK_CHK(a, n, site) (a)
+#define CLK_CHK_IF(cond, site, a) do { } while (0)
+#endif
 
 // The workgroup's place in the run order.  XCD-contiguous (XCD): workgroup b
 // (dispatched to XCD b % 8) takes position (b % 8) * q + min(b % 8, r) + b / 8
@@ -955,7 +993,7 @@ __device__ __noinline__ uint32_t lane_range_sum(uint64_t s, int len)
     const uint64_t c = s & ~15ull;
     const uint32_t nch = (uint32_t)((((s + (uint64_t)len + 15) & ~15ull) - c) >> 4);
     for (uint32_t k = 0; k < nch; k++)
-        chunk_accumulate(gload16(c + 16ull * k), (int)(c + 16ull * k - s), len, odd, acc);
+        chunk_accumulate(gload16(CLK_CHK(c + 16ull * k, 16, CHK_RANGE)), (int)(c + 16ull * k - s), len, odd, acc);
     return word_sum(acc, odd);
 }
 
@@ -1093,6 +1131,20 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                 R.start = live ? (uint32_t)((c0 - sb) >> 4) : (uint32_t)sp;
             }
         }
+#if CLK_PHASEA_SGPR == 1   // tools-only: round 3's faulting variant (the builtin returns int: sign-extended)
+        R.total = __builtin_amdgcn_readfirstlane(R.total);
+        R.sbase = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)R.sbase) |
+                  ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(R.sbase >> 32)) << 32);
+#elif CLK_PHASEA_SGPR == 2 // tools-only: the same, each half widened as unsigned
+        R.total = (uint32_t)__builtin_amdgcn_readfirstlane(R.total);
+        R.sbase = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)R.sbase) |
+                  ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(R.sbase >> 32)) << 32);
+#elif CLK_PHASEA_SGPR == 3 // tools-only: the chunk total alone
+        R.total = __builtin_amdgcn_readfirstlane(R.total);
+#elif CLK_PHASEA_SGPR == 4 // tools-only: the span base alone, as variant 1
+        R.sbase = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)R.sbase) |
+                  ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(R.sbase >> 32)) << 32);
+#endif
         return R;
     };
     uint64_t na;
@@ -1130,11 +1182,13 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             inf[k] = r | (r == (P[3] & 0x07FFFFFFu) - 1 ? (1u << 30) | (((P[3] >> 27) & 15) << 26) : 0u) |
                      (P[3] & 0x80000000u);
             const uint64_t cf = (uint64_t)P[0] | ((uint64_t)P[1] << 32);
+            CLK_CHK_IF(c < total && c < P[2], CHK_UNDERFLOW, cf);
             if (UseNT<CLK_STREAM_NT_CHECK && !SET>::value)
-                v[k] = c < total ? __builtin_nontemporal_load((const u32x4 *)(cf + 16ull * (c - P[2])))
+                v[k] = c < total ? __builtin_nontemporal_load(
+                                       (const u32x4 *)CLK_CHK(cf + 16ull * (c - P[2]), 16, CHK_GENERIC))
                                  : u32x4{0, 0, 0, 0};
             else
-                v[k] = c < total ? gload16(cf + 16ull * (c - P[2])) : u32x4{0, 0, 0, 0};
+                v[k] = c < total ? gload16(CLK_CHK(cf + 16ull * (c - P[2]), 16, CHK_GENERIC)) : u32x4{0, 0, 0, 0};
         }
     };
     // consume: whole-chunk sums into the packets' accumulators, stash
@@ -1233,7 +1287,8 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
 #pragma unroll
         for (int k = 0; k < KV; k++) {
             const uint32_t c = min(cb + (uint32_t)k * 64 + lane, R.total - 1);
-            d[k] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4 *)(R.sbase + 16ull * c));
+            d[k] = __builtin_nontemporal_load(
+                (const __attribute__((address_space(1))) u32x4 *)CLK_CHK(R.sbase + 16ull * c, 16, CHK_DENSE));
         }
     };
     auto dense_load = [&](const RunA &R, uint32_t cb) { dense_load_to(R, cb, dv); };
@@ -1314,7 +1369,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                 } else if (q0 + k < 4u * HC) {
                     d[k] = hw[q0 + k];
                 } else {                 // past the stash (unaligned or option-bearing header)
-                    d[k] = gload4((a & ~3ull) + 4 * k);
+                    d[k] = gload4(CLK_CHK((a & ~3ull) + 4 * k, 4, CHK_HDR));
                     vm_retire();
                 }
             }
@@ -1339,7 +1394,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                         // padding, bytes past the transport length), or before
                         // s (a short packet with options) -- are re-read and
                         // taken out
-                        u32x4 T = gload16(cl);
+                        u32x4 T = gload16(CLK_CHK(cl, 16, CHK_LAST));
                         vm_retire();
                         T = keep_below(T, (uint32_t)((a + caplen) & 15));
                         out = chunk_outside(T, cl, s, rlen, sel, out);

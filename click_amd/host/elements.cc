@@ -493,35 +493,49 @@ int BatchElement::launch(Stage &g)
         int r = run(&b, g.d_codes, g.d_sums);
         if (r) {
             const std::string why = err_.empty() ? clk_last_error(ctx_) : err_;
-            launch_failed(g, hipSuccess, "run");
-            err_ = why;
-            return r;
+            return failed_after_run(g, hipSuccess, "run", why, r);
         }
         if ((e = checked(hipEventRecord((hipEvent_t)g.ev[1], s))) != hipSuccess)
-            return launch_failed(g, e, "hipEventRecord");
+            return failed_after_run(g, e, "hipEventRecord");
         if ((e = checked(hipMemcpyAsync(g.h_codes, g.d_codes, n, hipMemcpyDeviceToHost, s))) != hipSuccess)
-            return launch_failed(g, e, "hipMemcpyAsync(verdicts)");
+            return failed_after_run(g, e, "hipMemcpyAsync(verdicts)");
         if (wants_sums() &&
             (e = checked(hipMemcpyAsync(g.h_sums, g.d_sums, n * 2, hipMemcpyDeviceToHost, s))) != hipSuccess)
-            return launch_failed(g, e, "hipMemcpyAsync(checksums)");
+            return failed_after_run(g, e, "hipMemcpyAsync(checksums)");
         if (wants_arena_back()) {
             // into h_back, not h_arena: if this batch fails after the copy,
             // the retry starts from the bytes as staged (not rewritten twice)
-            if (!g.zc && host_grow(&g.h_back, &g.h_back_cap, g.h_used + 64, 0)) {
-                launch_failed(g, hipSuccess, "hipHostMalloc");
-                err_ = "out of pinned host memory";
-                return CLK_EINVAL;
-            }
+            if (!g.zc && host_grow(&g.h_back, &g.h_back_cap, g.h_used + 64, 0))
+                return failed_after_run(g, hipSuccess, "hipHostMalloc", "out of pinned host memory", CLK_EINVAL);
             if (!g.zc &&
                 (e = checked(hipMemcpyAsync(g.h_back, g.d_arena, g.h_used, hipMemcpyDeviceToHost, s))) != hipSuccess)
-                return launch_failed(g, e, "hipMemcpyAsync(packets back)");
+                return failed_after_run(g, e, "hipMemcpyAsync(packets back)");
             if ((e = checked(hipMemcpyAsync(g.h_aux8, g.d_aux8, n, hipMemcpyDeviceToHost, s))) != hipSuccess)
-                return launch_failed(g, e, "hipMemcpyAsync(aux)");
+                return failed_after_run(g, e, "hipMemcpyAsync(aux)");
         }
     }
     if ((e = checked(hipEventRecord((hipEvent_t)g.ev[2], s))) != hipSuccess)
-        return launch_failed(g, e, "hipEventRecord");
+        return failed_after_run(g, e, "hipEventRecord");
     return 0;
+}
+
+// A launch step failed once the element's kernels may have been queued.  As
+// launch_failed(); in addition, a ZEROCOPY batch of a rewriting element is
+// abandoned (its packets killed, counted as lost): the kernel has rewritten
+// the host packets in place by the time the stream is drained, so a retry
+// would apply the element twice (complete() does the same for a failed
+// completion wait).
+int BatchElement::failed_after_run(Stage &g, hipError_t e, const char *what, const std::string &why, int rc)
+{
+    launch_failed(g, e, what);
+    if (!why.empty())
+        err_ = why;
+    if (g.zc && !idempotent()) {
+        const std::string msg = err_;
+        abandon_stage(g);
+        err_ = msg + " (ZEROCOPY batch of a rewriting element: its packets were killed, not retried)";
+    }
+    return rc;
 }
 
 // Wait for a launched stage and route its packets, in push order.

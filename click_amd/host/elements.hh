@@ -288,6 +288,8 @@ class BatchElement {
     int grow_dev(Stage &g, size_t bytes, size_t n);
     int launch(Stage &g);
     int launch_failed(Stage &g, hipError_t e, const char *what);
+    int failed_after_run(Stage &g, hipError_t e, const char *what, const std::string &why = std::string(),
+                         int rc = CLK_EHIP);
     int complete(Stage &g);
     int abandon_stage(Stage &g);
     void free_stage(Stage &g);

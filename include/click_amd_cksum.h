@@ -125,7 +125,15 @@ int clk_abi_version(void);
  * For the IP/UDP/TCP elements the header is the packet's network (L3)
  * header; the transport header is taken at L3 + ip_hl*4, as CheckIPHeader /
  * MarkIPHeader set it.  Offsets may have any alignment (Click requires 2).
- * Set elements write their checksum field in place into `base`. */
+ * Set elements write their checksum field in place into `base`.
+ * Readable memory: the kernels read whole 16-byte-aligned chunks, so the
+ * chunk-aligned bytes around [off_i, off_i + len_i) must be readable (never
+ * past its 4 KiB page).  The packet-stream kernel (below) also loads, without
+ * using them, the bytes BETWEEN packets i and i+1 of one 64-packet run when
+ * their offsets increase and the run's packets fill at least 8/9 of the
+ * span less 1 KiB (a packed arena); such gaps must be readable too.  Every
+ * packet in one device arena (the glue's staging, a registered ZEROCOPY
+ * region, a generated batch) satisfies this. */
 typedef struct clk_batch {
     uint8_t *base;
     const uint64_t *off;

@@ -816,6 +816,60 @@ struct bench_arg {
     volatile uint64_t sink;
 };
 
+/* Run fn over args[0..n-1] (elements of `size` bytes): args[1..] on threads
+ * of their own, args[0] on the caller's.  The threads wait at a gate until
+ * every one of them was created, so a failed pthread_create leaves no thread
+ * running (or stuck at a barrier of the job) and nothing joined that was not
+ * started: the job is not run and -1 is returned. */
+struct gate {
+    pthread_mutex_t m;
+    pthread_cond_t c;
+    int state;                       /* 0 wait, 1 go, -1 abort */
+};
+struct gated {
+    struct gate *g;
+    void *(*fn)(void *);
+    void *arg;
+};
+static void *gated_entry(void *p)
+{
+    struct gated *x = p;
+    pthread_mutex_lock(&x->g->m);
+    while (x->g->state == 0)
+        pthread_cond_wait(&x->g->c, &x->g->m);
+    const int go = x->g->state > 0;
+    pthread_mutex_unlock(&x->g->m);
+    return go ? x->fn(x->arg) : 0;
+}
+static int run_threads(int n, void *(*fn)(void *), void *args, size_t size)
+{
+    struct gate g = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, 0};
+    pthread_t *th = calloc((size_t)n, sizeof *th);
+    struct gated *x = calloc((size_t)n, sizeof *x);
+    if (!th || !x) {
+        free(th);
+        free(x);
+        return -1;
+    }
+    int started = 1;
+    for (int t = 1; t < n; t++, started++) {
+        x[t] = (struct gated){&g, fn, (char *)args + (size_t)t * size};
+        if (pthread_create(&th[t], 0, gated_entry, &x[t]) != 0)
+            break;
+    }
+    pthread_mutex_lock(&g.m);
+    g.state = started == n ? 1 : -1;
+    pthread_cond_broadcast(&g.c);
+    pthread_mutex_unlock(&g.m);
+    if (started == n)
+        fn(args);
+    for (int t = 1; t < started; t++)
+        pthread_join(th[t], 0);
+    free(th);
+    free(x);
+    return started == n ? 0 : -1;
+}
+
 static void *bench_thread(void *vp)
 {
     struct bench_arg *a = (struct bench_arg *)vp;
@@ -842,7 +896,6 @@ double oracle_bench(int op, uint8_t *base, uint64_t stride, uint32_t fixed_len,
     if (nthreads < 1)
         nthreads = 1;
     struct bench_arg *args = calloc((size_t)nthreads, sizeof *args);
-    pthread_t *th = calloc((size_t)nthreads, sizeof *th);
     for (int t = 0; t < nthreads; t++) {
         args[t].op = op; args[t].reps = reps; args[t].arg = 1;
         args[t].base = base; args[t].stride = stride; args[t].fixed_len = fixed_len;
@@ -850,14 +903,9 @@ double oracle_bench(int op, uint8_t *base, uint64_t stride, uint32_t fixed_len,
         args[t].hi = n * (uint64_t)(t + 1) / (uint64_t)nthreads;
     }
     double t0 = now_s();
-    for (int t = 1; t < nthreads; t++)
-        pthread_create(&th[t], 0, bench_thread, &args[t]);
-    bench_thread(&args[0]);
-    for (int t = 1; t < nthreads; t++)
-        pthread_join(th[t], 0);
-    double dt = now_s() - t0;
+    const int rc = run_threads(nthreads, bench_thread, args, sizeof *args);
+    double dt = rc ? -1.0 : now_s() - t0;
     free(args);
-    free(th);
     return dt;
 }
 
@@ -996,7 +1044,6 @@ int oracle_cpu_baseline(const struct oracle_cb_cfg *cfg, const int *cpus, int nt
     pthread_barrier_t bar;
     pthread_barrier_init(&bar, 0, (unsigned)nthreads);
     struct cb_thread *a = calloc((size_t)nthreads, sizeof *a);
-    pthread_t *th = calloc((size_t)nthreads, sizeof *th);
     double rep_s[64];
     for (int t = 0; t < nthreads; t++) {
         a[t].cfg = cfg;
@@ -1005,13 +1052,8 @@ int oracle_cpu_baseline(const struct oracle_cb_cfg *cfg, const int *cpus, int nt
         a[t].bar = &bar;
         a[t].rep_s = rep_s;
     }
-    for (int t = 1; t < nthreads; t++)
-        pthread_create(&th[t], 0, cb_run, &a[t]);
-    cb_run(&a[0]);
-    for (int t = 1; t < nthreads; t++)
-        pthread_join(th[t], 0);
+    int err = run_threads(nthreads, cb_run, a, sizeof *a) ? 1 : 0;
     pthread_barrier_destroy(&bar);
-    int err = 0;
     for (int t = 0; t < nthreads; t++) {
         err |= a[t].err;
         res->packets += a[t].packets;
@@ -1026,7 +1068,6 @@ int oracle_cpu_baseline(const struct oracle_cb_cfg *cfg, const int *cpus, int nt
     res->min_s = rep_s[0];
     res->max_s = rep_s[cfg->reps - 1];
     free(a);
-    free(th);
     return err ? -2 : 0;
 }
 
@@ -1146,9 +1187,8 @@ int oracle_digest(const struct oracle_digest_cfg *cfg, const int *cpus, int nthr
         return -1;
     memset(out, 0, ORACLE_DG_NLEGS * sizeof *out);
     struct dg_thread *a = calloc((size_t)nthreads, sizeof *a);
-    pthread_t *th = calloc((size_t)nthreads, sizeof *th);
-    if (!a || !th) {
-        free(a); free(th);
+    if (!a) {
+        free(a);
         return -2;
     }
     for (int t = 0; t < nthreads; t++) {
@@ -1156,13 +1196,8 @@ int oracle_digest(const struct oracle_digest_cfg *cfg, const int *cpus, int nthr
         a[t].lo = cfg->first_idx + cfg->n * (uint64_t)t / (uint64_t)nthreads;
         a[t].hi = cfg->first_idx + cfg->n * (uint64_t)(t + 1) / (uint64_t)nthreads;
     }
-    for (int t = 1; t < nthreads; t++)
-        pthread_create(&th[t], 0, dg_run, &a[t]);
-    dg_run(&a[0]);
-    for (int t = 1; t < nthreads; t++)
-        pthread_join(th[t], 0);
+    int err = run_threads(nthreads, dg_run, a, sizeof *a) ? 1 : 0;
     (void)cpus;
-    int err = 0;
     for (int t = 0; t < nthreads; t++) {
         err |= a[t].err;
         for (int l = 0; l < ORACLE_DG_NLEGS; l++) {
@@ -1175,6 +1210,5 @@ int oracle_digest(const struct oracle_digest_cfg *cfg, const int *cpus, int nthr
         }
     }
     free(a);
-    free(th);
     return err ? -3 : 0;
 }

@@ -68,3 +68,33 @@ def test_cpu_baseline_object_code(oracle):
     ok, rep, body = m.check()
     assert ok, rep
     assert any(i.startswith("movzwl") for i in body)
+
+
+def test_line_summary_is_last_and_complete(monkeypatch):
+    """The bench line ends with `summary`: one entry per timed element of
+    every workload section plus the fragmenter and config 1, so the tail of
+    the line alone carries them (the driver keeps only the last few KB);
+    cpu_baseline legs are compact; comm names the communicator."""
+    import json
+    import bench
+    monkeypatch.setenv("CLK_CPU_SAMPLE_BYTES", str(8 << 20))
+    monkeypatch.setenv("CLK_CPU_THREADS", "2")
+    el = lambda ms, fr, m: {"roofline": {"kernel_ms": ms, "frac": fr},
+                            "verify": {"drops_exact": True, "oracle": {"oracle_match": m}}}
+    line = {"config": {"workload": "C3: x"},
+            "elements": {"CheckUDPHeader": el(3.68, 0.855, True), "SetUDPChecksum": el(4.4, 0.71, True)},
+            "c2_64b": {"workload": "C2: y", "elements": {"CheckIPHeader": el(0.17, 0.25, True)}},
+            "c4_imix": {"workload": "C4: z", "elements": {"CheckUDPHeader": el(3.8, 0.82, True),
+                                                         "SetUDPChecksum": el(5.3, 0.58, False)}},
+            "fragmenter": {"kernel_ms": 8.9, "roofline": {"frac": 0.45},
+                           "verify": {"fragmented": 5, "packets": 5, "appended_fragments": 10}},
+            "c1_fake_iprouter": {"ok": True, "elements": {"mpps": 20.1}, "combos": {"mpps": 40.2}}}
+    s = bench.bench_summary(line)
+    assert s["C3 CheckUDPHeader"] == [3.68, 0.855, True, True]
+    assert s["C4 SetUDPChecksum"][2] is False and s["C2 CheckIPHeader"][1] == 0.25
+    assert s["C3 IPFragmenter"][2] is True and s["C1 mpps"] == {"elements": 20.1, "combos": 40.2}
+    legs = bench.compact_legs(dict(bench.cpu_baseline(legs=("c2", "c3"))["legs"], c1=bench.config1_cpu(2000)))
+    assert set(legs) == {"c2", "c3", "c1"} and len(legs["c3"]["all"]) == 3 and legs["c1"]["combos"] > 0
+    assert len(json.dumps(legs)) + len(json.dumps(s)) < 2000
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'line["summary"] = bench_summary(line)\n        print(json.dumps(line)' in src

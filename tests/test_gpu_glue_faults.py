@@ -209,3 +209,50 @@ def test_zerocopy_rewriting_batch_is_abandoned(ctx):
         e.close()
     finally:
         ctx.host_unregister(arena)
+
+
+@pytest.mark.parametrize("nth", list(range(1, 13)))
+def test_zerocopy_rewriting_batch_any_failed_step(ctx, nth):
+    """ZEROCOPY DecIPTTL with the nth checked HIP call of its flush failing
+    (event creation, descriptor copies, the records around the kernel, the
+    verdict / checksum / aux copies back): whatever step fails, no TTL is
+    decremented twice.  A failure before the kernel leaves the batch staged
+    and the retry forwards every packet decremented once; a failure after it
+    abandons the batch (every packet killed, counted as lost) -- the
+    kernel already rewrote the host packets, so a retry would decrement
+    again."""
+    from click_amd import ClickAmdError
+    from click_amd.elements import Element
+    n, L, stride = 300, 600, 640
+    raw = np.zeros(n * stride + 8192, np.uint8)
+    arena = raw[(-raw.ctypes.data) % 4096:][:n * stride]
+    a2, _, _ = udp_600(n)
+    arena[:] = a2
+    ttl0 = arena.reshape(n, stride)[:, 8].copy()
+    ctx.host_register(arena)
+    try:
+        e = Element(ctx, "DecIPTTL", "ZEROCOPY true", noutputs=2)
+        ptrs = np.uint64(arena.ctypes.data) + np.arange(n, dtype=np.uint64) * np.uint64(stride)
+        e.push_burst(ptrs, np.full(n, L, np.uint32), np.zeros(n, np.int32))
+        hook = ctx.lib.clk_glue_inject_fault_internal
+        hook.argtypes, hook.restype = [ctypes.c_int], None
+        hook(nth)
+        failed = None
+        try:
+            e.flush()
+        except ClickAmdError as ex:
+            failed = str(ex)
+        finally:
+            hook(0)
+        e.flush()                                  # the retry, if the batch is still staged
+        tok, port, _ = e.results()
+        assert (np.sort(tok) == np.arange(n)).all()
+        ttl = arena.reshape(n, stride)[:, 8]
+        assert (ttl >= ttl0 - 1).all(), "a TTL was decremented twice"
+        if failed and "not retried" in failed:
+            assert (port == -1).all() and e.read_handler("lost") == str(n)
+        else:                                      # no failure reached, or one before the kernel: retried
+            assert (port == 0).all() and (ttl == ttl0 - 1).all() and e.read_handler("lost") == "0"
+        e.close()
+    finally:
+        ctx.host_unregister(arena)

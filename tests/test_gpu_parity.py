@@ -36,9 +36,11 @@ def ctx(torch):
     c.close()
 
 
-def dev_batch(torch, arena, n, off=None, length=None, stride=0, fixed_len=0, max_len=0):
+def dev_batch(torch, arena, n, off=None, length=None, stride=0, fixed_len=0, max_len=0, place=None):
+    """A device batch over a copy of `arena`; `place(arena)` may put that copy
+    at a chosen device address (a view into a larger buffer)."""
     import click_amd
-    base = torch.from_numpy(arena).to("cuda:0")
+    base = torch.from_numpy(arena).to("cuda:0") if place is None else place(arena)
     o = torch.from_numpy(off.astype(np.uint64).view(np.int64)).to("cuda:0") if off is not None else None
     ln = torch.from_numpy(length.astype(np.uint32).view(np.int32)).to("cuda:0") if length is not None else None
     return click_amd.Batch(base, n, stride=stride, fixed_len=fixed_len, off=o, length=ln, max_len=max_len)
@@ -66,9 +68,9 @@ def run_gpu(ctx, op, b, arg=1):
     raise ValueError(op)
 
 
-def compare(torch, ctx, op, arena, n, off=None, length=None, stride=0, fixed_len=0, max_len=0, arg=1):
+def compare(torch, ctx, op, arena, n, off=None, length=None, stride=0, fixed_len=0, max_len=0, arg=1, place=None):
     """Run op on GPU and oracle over identical inputs; assert bit-exactness."""
-    b = dev_batch(torch, arena, n, off, length, stride, fixed_len, max_len)
+    b = dev_batch(torch, arena, n, off, length, stride, fixed_len, max_len, place)
     codes, sums = run_gpu(ctx, op, b, arg)
     ctx.sync()
     ref = arena.copy()
@@ -403,6 +405,56 @@ def test_variable_length_paths_bit_exact(torch, stream_min, group):
         compare(torch, c, op, arena, n, off=off, length=L, max_len=1500)
         oracle_lib.batch(op, arena, n, off=off, length=L)
     c.close()
+
+
+class HighPlacer:
+    """Places an arena copy at a device address whose low 32 bits are just
+    below `low` (2^31 or 2^32), inside one buffer a little over 4 GiB, so the
+    batch's chunk spans cross bit 31 of the address's low word or a 4 GiB
+    boundary.  Round 3's readfirstlane variant of the packet-stream kernel
+    widened the span base's low word as a signed int and faulted on exactly
+    these addresses (DESIGN.md "Stream-kernel fault")."""
+
+    def __init__(self, torch, room=1 << 24):
+        self.torch = torch
+        self.room = room
+        self.buf = torch.empty((1 << 32) + 2 * room, dtype=torch.uint8, device="cuda:0")
+        self.p = self.buf.data_ptr()
+
+    def at(self, low, back):
+        def place(arena):
+            assert arena.size <= self.room
+            o = ((low - back - self.p) % (1 << 32)) & ~15   # (p + o) mod 2^32 = low - back, 16 B-aligned
+            v = self.buf[o:o + arena.size]
+            v.copy_(self.torch.from_numpy(arena))
+            return v
+        return place
+
+
+@pytest.mark.parametrize("low", [1 << 31, 1 << 32])
+def test_stream_high_address_bits(torch, low):
+    """Packet-stream batches (seed 41, as test_variable_length_paths_bit_exact,
+    and the dense / generic layouts) placed so that their runs straddle bit
+    31 of the address's low word (low = 2^31) or a 4 GiB boundary (low =
+    2^32): every chunk address is formed in 64 bits, oracle-exact."""
+    import click_amd
+    hp = HighPlacer(torch)
+    c = click_amd.Context(0).tune(stream_min=1)
+    rng = np.random.default_rng(41)
+    for proto, mt in ((17, 1600), (6, 9000), (1, 1600)):
+        arena, off, caplen, ml = fuzz.make_batch(rng, 2000, proto, max_total=mt)
+        for back in (4096, arena.size // 2):
+            for op in ("in_cksum",) + OPS_L4[proto]:
+                compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=1,
+                        place=hp.at(low, back))
+    for kind in ("packed", "odd", "shared"):
+        arena, off, caplen, ml = dense_layout(rng, 700, 17, kind)
+        for back in (4096, arena.size // 2):
+            for op in OPS_L4[17]:
+                compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=1,
+                        place=hp.at(low, back))
+    c.close()
+    del hp
 
 
 def test_tune_rejects_bad_values(torch):
