@@ -165,7 +165,7 @@ size_t work_bytes(uint64_t n) { return (n * 4 + 255) & ~size_t(255); }
 // packet's in 27: it takes packets of known length up to 16 MiB.
 bool use_stream(const clk_ctx *ctx, const clk_batch *b)
 {
-    return b->len && !ctx->force_group && b->n >= ctx->stream_min && b->max_len && b->max_len <= (1u << 24);
+    return b->len && !ctx->force_group && b->n >= ctx->stream_min && b->max_len && b->max_len <= clk::STREAM_MAX_LEN;
 }
 
 template <int G>

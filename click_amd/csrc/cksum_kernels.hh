@@ -76,7 +76,7 @@ __device__ __forceinline__ void chk_note(int site, uint64_t a)
 __device__ __forceinline__ uint64_t chk_addr(uint64_t a, uint32_t bytes, int site)
 {
     const uint64_t lo = dbg_lo, hi = dbg_hi;
-    if (hi && (a < lo || a + bytes > hi)) {
+    if (hi && (a < lo || a > hi - bytes)) {     // (a + bytes would wrap for a sign-extended base)
         chk_note(site, a);
         return lo;
     }
@@ -133,6 +133,9 @@ __device__ __forceinline__ uint32_t pkt_len(const BatchArgs &b, uint64_t i)
 }
 
 enum Proto { ICMP = 1, UDP = 17, TCP = 6 };
+
+// The packet-stream kernel's packet-length bound (cksum_api.hip use_stream).
+constexpr uint32_t STREAM_MAX_LEN = 1u << 24;
 
 // codes (include/click_amd_cksum.h)
 constexpr uint32_t OK = 0;
@@ -1070,6 +1073,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         uint32_t total;              // wave-uniform: chunks in the list (dense: the span)
         uint64_t sbase;              // dense: the span's first chunk address
         bool anyodd, dense;
+        bool huge;                   // a packet longer than 16 MiB: per-lane sums from memory
     };
     // the raw descriptors, loaded unconditionally (index clamped) and not
     // yet used, so that a prefetch leaves them in flight
@@ -1102,6 +1106,17 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
         R.sbase = 0;
         R.start = incl - nch;
         R.total = total;
+        // The chunk list packs a packet's chunk index into 26 bits and the
+        // run's count into 32: both hold for packets up to 16 MiB (the host
+        // sends only batches with max_len <= 16 MiB here, use_stream()).  A
+        // run with a longer packet -- a descriptor past its batch's max_len
+        // -- streams nothing: phase C sums each packet from memory, so no
+        // index can wrap whatever the lengths are.
+        R.huge = __ballot(caplen > STREAM_MAX_LEN) != 0;
+        if (R.huge) {
+            R.start = 0;
+            R.total = 0;
+        }
         // Dense run: the packets' chunk ranges are increasing and disjoint
         // and their span [c0 of packet 0, end of the last) holds few gap
         // chunks -- as a packed arena does.  A chunk's address is then
@@ -1124,7 +1139,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             const uint64_t send = (uint64_t)__shfl((uint32_t)cend, (int)lastl, 64) |
                                   ((uint64_t)__shfl((uint32_t)(cend >> 32), (int)lastl, 64) << 32);
             const uint64_t sp = send >= sb ? (send - sb) >> 4 : ~0ull;
-            if (__ballot(bad) == 0 && total > 0 && sp <= (uint64_t)total + (total >> 3) + 64) {
+            if (!R.huge && __ballot(bad) == 0 && total > 0 && sp <= (uint64_t)total + (total >> 3) + 64) {
                 R.dense = true;
                 R.sbase = sb;
                 R.total = (uint32_t)sp;
@@ -1366,7 +1381,7 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             for (int k = 0; k < HDR_DW; k++) {
                 if ((a & ~3ull) + 4 * k >= end) {
                     d[k] = 0u;
-                } else if (q0 + k < 4u * HC) {
+                } else if (!cur.huge && q0 + k < 4u * HC) {
                     d[k] = hw[q0 + k];
                 } else {                 // past the stash (unaligned or option-bearing header)
                     d[k] = gload4(CLK_CHK((a & ~3ull) + 4 * k, 4, CHK_HDR));
@@ -1380,8 +1395,8 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             if (rlen > 0) {
                 const uint64_t s = a + st.hl, e = s + (uint64_t)rlen;
                 const uint32_t sel = (a & 1) ? 0x02030001u : 0x03020100u;
-                const bool stashed = nch <= (uint32_t)HC + 1 ||
-                                     (s <= c0 + 16 * HC && e >= c0 + 16ull * (nch - 1));
+                const bool stashed = !cur.huge && (nch <= (uint32_t)HC + 1 ||
+                                                   (s <= c0 + 16 * HC && e >= c0 + 16ull * (nch - 1)));
                 if (stashed) {
                     uint32_t out = 0;
                     const uint32_t nh_ = nch < (uint32_t)HC ? nch : (uint32_t)HC;
@@ -1406,13 +1421,13 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
             }
             if (COAL)
                 l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work, [&](uint32_t r) {
-                    blk_q0 = set_block_patch_stash<PROTO, HC>(nh, st, r, c0, head[wv][lane]);
+                    blk_q0 = cur.huge ? 0 : set_block_patch_stash<PROTO, HC>(nh, st, r, c0, head[wv][lane]);
                     if (!blk_q0)
                         set_field_store<PROTO>(nh, st, r, true);
                 });
             else if (SET && !DEFER && CLK_SET_REGBLK)
                 l4_finish_with<PROTO, SET, DEFER>(nh, i, sum, st, true, out_code, out_sum, work, [&](uint32_t r) {
-                    if (!set_block_store_stash<PROTO, HC>(nh, st, r, c0, head[wv][lane]))
+                    if (cur.huge || !set_block_store_stash<PROTO, HC>(nh, st, r, c0, head[wv][lane]))
                         set_field_store<PROTO>(nh, st, r, true);
                 });
             else

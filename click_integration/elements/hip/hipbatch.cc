@@ -15,17 +15,22 @@
 #include <click/straccum.hh>
 #include <stdlib.h>
 #include <string.h>
+#include <new>
 CLICK_DECLS
 
 HIPBatchElement::HIPBatchElement()
-    : _device(-1), _latency_ms(1), _retries(3), _pt(0), _timers(0), _npt(0), _gate(0)
+    : _device(-1), _latency_ms(1), _retries(3), _pt(0), _tasks(0), _npt(0), _gate(0)
 {
 }
 
 HIPBatchElement::~HIPBatchElement()
 {
     delete[] _pt;
-    delete[] _timers;
+    if (_tasks) {
+	for (int k = 0; k < _npt; k++)
+	    _tasks[k].~Task();
+	operator delete[](static_cast<void *>(_tasks));
+    }
 }
 
 int
@@ -79,11 +84,14 @@ HIPBatchElement::initialize(ErrorHandler *errh)
 {
     _npt = click_max_cpu_ids();
     _pt = new PerThread[_npt];
-    _timers = new Timer[_npt];
+    // one Task per state, moved to its RouterThread (task.hh:275), not
+    // scheduled until the state holds packets (hipcore: wake / poll)
+    _tasks = static_cast<Task *>(operator new[](sizeof(Task) * _npt));
     for (int k = 0; k < _npt; k++) {
 	_pt[k].id = k;
-	_timers[k].assign(this);
-	_timers[k].initialize(this);
+	new (&_tasks[k]) Task(this);
+	_tasks[k].initialize(this, false);
+	_tasks[k].move_thread(k);
     }
     // the home thread's glue element now: configuration errors surface at
     // initialize time, as the reference element's configure() errors do
@@ -121,34 +129,6 @@ HIPBatchElement::state()
     return t;
 }
 
-int32_t
-HIPBatchElement::nh_offset(Packet *p)
-{
-    return p->has_network_header() ? p->network_header_offset() : -1;
-}
-
-Packet *
-HIPBatchElement::prepare(Packet *p, uint32_t *anno, Packet **extra)
-{
-    (void) anno, (void) extra;
-    return p;
-}
-
-Packet *
-HIPBatchElement::make_packet(clk_element *e, uint32_t key)
-{
-    int64_t n = clk_element_take_packet(e, key, 0, 0);
-    WritablePacket *q = n >= 0 ? Packet::make(n) : 0;
-    if (!q) {				// out of memory: release the glue's copy
-	unsigned char one;
-	if (n >= 0)
-	    clk_element_take_packet(e, key, &one, 1);
-	return 0;
-    }
-    clk_element_take_packet(e, key, q->data(), n);
-    return q;
-}
-
 void
 HIPBatchElement::push(int, Packet *p)
 {
@@ -161,31 +141,16 @@ HIPBatchElement::pull(int)
     return _core.pull(*this, state());
 }
 
-void
-HIPBatchElement::run_timer(Timer *timer)
+bool
+HIPBatchElement::run_task(Task *task)
 {
-    int k = timer - _timers;
-    if (k >= 0 && k < _npt)
-	_core.timer(*this, _pt[k]);
-}
-
-int
-HIPBatchElement::pass(Routed &r, Packet **out)
-{
-    if (!r.p)
-	return -1;
-    if (r.port == CLK_PORT_KILL) {	// drop() with no output 1 (checkipheader.cc:143-159)
-	r.p->kill();
-	return -1;
-    }
-    *out = r.p;				// output 0, or 1 as checked_output_push
-    return r.port;
-}
-
-int
-HIPBatchElement::finish(PerThread &, Routed &r, Packet **out)
-{
-    return pass(r, out);
+    // state k's latency deadline, on state k's RouterThread
+    int k = task - _tasks;
+    if (k < 0 || k >= _npt)
+	return false;
+    if (_core.poll(*this, _pt[k]))
+	task->fast_reschedule();	// still holding packets: look again
+    return true;
 }
 
 void

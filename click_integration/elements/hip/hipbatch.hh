@@ -1,11 +1,49 @@
 #ifndef CLICK_HIPBATCH_HH
 #define CLICK_HIPBATCH_HH
 #include <click/element.hh>
-#include <click/timer.hh>
+#include <click/task.hh>
+#include <click/timestamp.hh>
 #include <click/sync.hh>
+#include <click/packet_anno.hh>
+#include <clicknet/ip.h>
 #include "click_amd_elements.h"
 #include "hipcore.hh"
+#include "hipclasses.hh"
 CLICK_DECLS
+
+/*
+ * ClickPacketOps -- the packet operations trait of hipclasses.hh over
+ * Click's Packet: each is one Packet call.
+ */
+struct ClickPacketOps {
+    static Packet *uniqueify(Packet *p)		{ return p->uniqueify(); }
+    static Packet *clone(Packet *p)		{ return p->clone(); }
+    static void kill(Packet *p)			{ p->kill(); }
+    static uint8_t *data(Packet *p)		{ return const_cast<unsigned char *>(p->data()); }
+    static uint32_t length(Packet *p)		{ return p->length(); }
+    static bool has_network_header(Packet *p)	{ return p->has_network_header(); }
+    static const uint8_t *network_header(Packet *p)	{ return p->network_header(); }
+    static int32_t network_header_offset(Packet *p)	{ return p->network_header_offset(); }
+    static int network_length(Packet *p)	{ return p->network_length(); }
+    static void set_ip_header(Packet *p, const uint8_t *ip, uint32_t hlen) {
+	p->set_ip_header(reinterpret_cast<const click_ip *>(ip), hlen);
+    }
+    static void take(Packet *p, uint32_t n)	{ p->take(n); }
+    static void pull(Packet *p, uint32_t n)	{ p->pull(n); }
+    static void set_dst_ip_anno(Packet *p, uint32_t a)	{ p->set_dst_ip_anno(IPAddress(a)); }
+    static uint32_t paint(Packet *p)		{ return PAINT_ANNO(p); }
+    static void set_paint(Packet *p, uint32_t c)	{ SET_PAINT_ANNO(p, c); }
+    static bool fix_ip_src(Packet *p)		{ return FIX_IP_SRC_ANNO(p); }
+    static void clear_fix_ip_src(Packet *p)	{ SET_FIX_IP_SRC_ANNO(p, 0); }
+    static void set_icmp_paramprob(Packet *p, uint32_t v)	{ SET_ICMP_PARAMPROB_ANNO(p, v); }
+    static bool broadcast_or_multicast(Packet *p) {
+	return p->packet_type_anno() == Packet::BROADCAST || p->packet_type_anno() == Packet::MULTICAST;
+    }
+    static void copy_annotations(Packet *to, Packet *from)	{ to->copy_annotations(from); }
+    static Packet *make(uint32_t headroom, uint32_t len) {
+	return headroom ? Packet::make(headroom, 0, len, 0) : Packet::make(len);
+    }
+};
 
 /*
  * HIPBatchElement -- what every GPU-backed checksum element of this group
@@ -37,11 +75,16 @@ CLICK_DECLS
  *
  * Threads (click -j N): one hipcore::State (context, glue element, held
  * packets, lock) per RouterThread, chosen by click_current_cpu_id()
- * (glue.hh:409-429), each created the first time its thread uses it.  Timers
- * run on the element's home thread (timer.cc:238-247), as in ToDPDKDevice's
- * per-thread queues (todpdkdevice.cc:85-86,176-179); the state's Spinlock
- * serialises them with that thread's pushes.  No output is pushed while a
- * lock is held.
+ * (glue.hh:409-429), each created the first time its thread uses it.  Each
+ * state has a Task moved to its RouterThread (Task::move_thread,
+ * task.hh:275): while the state holds packets the Task polls its latency
+ * deadline (hipcore::Core::poll), so a partial batch is flushed, and its
+ * packets pushed downstream, on the thread that pushed them.  No output is
+ * pushed while a lock is held.
+ *
+ * The element classes' own logic (what the reference element does around
+ * its checksum) is hipclasses.hh's, instantiated with ClickPacketOps;
+ * HIPClassElement<C> forwards the core's hooks to it.
  */
 class HIPBatchElement : public Element { public:
 
@@ -59,34 +102,27 @@ class HIPBatchElement : public Element { public:
 
     void push(int port, Packet *p);
     Packet *pull(int port);
-    void run_timer(Timer *t);
 
     // ---- the core's host interface (hipcore.hh) ------------------------------
-    // before staging: uniqueify if the element writes the packet (as the
-    // reference element does), fill *anno (CLK_ANNO_*), optionally hold a
-    // second packet in *extra; return the packet to stage (0: consumed)
-    virtual Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
-    uint8_t *data(Packet *p)		{ return const_cast<unsigned char *>(p->data()); }
+    // the class hooks (hipclasses.hh): the plain check elements' here,
+    // HIPClassElement<C> forwards them to its class
+    virtual Packet *prepare(Packet *p, uint32_t *anno, Packet **extra)	{ return _plain.prepare(p, anno, extra); }
+    virtual int32_t nh_offset(Packet *p)	{ return _plain.nh_offset(p); }
+    virtual bool primary(int32_t port, uint32_t aux) const	{ return _plain.primary(port, aux); }
+    virtual Packet *make_packet(clk_element *e, uint32_t key)	{ return _plain.make_packet(e, key); }
+    virtual int finish(PerThread &t, Routed &r, Packet **out)	{ return _plain.finish(t, r, out); }
+    virtual void end_of_batch(PerThread &t)	{ _plain.end_of_batch(t); }
+    uint8_t *data(Packet *p)		{ return ClickPacketOps::data(p); }
     uint32_t length(Packet *p)		{ return p->length(); }
-    // the byte offset of the header the glue looks at (network header)
-    virtual int32_t nh_offset(Packet *p);
-    // false for a result that comes with another (IPOutputCombo's clone,
-    // IPFragmenter's extra fragments): the held packet stays
-    virtual bool primary(int32_t port, uint32_t aux) const	{ (void) port; (void) aux; return true; }
-    virtual Packet *make_packet(clk_element *e, uint32_t key);
-    // one result: the reference's side effects; returns the output port of
-    // *out (core pushes it, or hands it out in pull context), -1 for none
-    virtual int finish(PerThread &t, Routed &r, Packet **out);
-    virtual void end_of_batch(PerThread &t)	{ (void) t; }
     void output_push(int port, Packet *p)	{ checked_output_push(port, p); }
     Packet *input_pull()			{ return input(0).pull(); }
     void kill(Packet *p)			{ p->kill(); }
     void adjust_runcount(int delta);
-    void schedule(PerThread &t, unsigned ms)	{ _timers[t.id].schedule_after_msec(ms); }
-    void unschedule(PerThread &t)		{ _timers[t.id].unschedule(); }
-    bool scheduled(PerThread &t)		{ return _timers[t.id].scheduled(); }
+    uint64_t now_ns()			{ return Timestamp::now_steady().nsecval(); }
+    void wake(PerThread &t)		{ _tasks[t.id].reschedule(); }
     void chatter(const char *text);
     void message(const char *line);
+    bool run_task(Task *task);
 
   protected:
 
@@ -95,8 +131,6 @@ class HIPBatchElement : public Element { public:
     // glue handler text of the home thread's element (the element's
     // configuration, e.g. OFFSET, COLOR, MTU)
     String glue_handler(const char *name) const;
-    // the default finish(): output port as routed, killed on CLK_PORT_KILL
-    int pass(Routed &r, Packet **out);
     // the router attachment naming a once-per-router message, if the
     // reference element has one (SetUDPChecksum); 0: once per element
     virtual const char *message_attachment() const	{ return 0; }
@@ -106,10 +140,11 @@ class HIPBatchElement : public Element { public:
     uint32_t _latency_ms;
     uint32_t _retries;
     PerThread *_pt;
-    Timer *_timers;
+    Task *_tasks;			// one per state, on its RouterThread
     int _npt;
     clk_element *_gate;		// whose once-only chatter the thread elements share
     hipcore::Core<Packet, HIPBatchElement, Spinlock> _core;
+    hipcore::Plain<Packet, ClickPacketOps> _plain;
 
   private:
 
@@ -117,6 +152,22 @@ class HIPBatchElement : public Element { public:
     int ensure(PerThread &t, ErrorHandler *errh);
     static String read_handler(Element *e, void *thunk) CLICK_COLD;
 
+};
+
+/*
+ * HIPClassElement<C> -- a GPU-backed element whose reference behaviour is
+ * class C of hipclasses.hh (instantiated with ClickPacketOps).
+ */
+template <class C>
+class HIPClassElement : public HIPBatchElement { public:
+    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra)	{ return _cls.prepare(p, anno, extra); }
+    int32_t nh_offset(Packet *p)	{ return _cls.nh_offset(p); }
+    bool primary(int32_t port, uint32_t aux) const	{ return _cls.primary(port, aux); }
+    Packet *make_packet(clk_element *e, uint32_t key)	{ return _cls.make_packet(e, key); }
+    int finish(PerThread &t, Routed &r, Packet **out)	{ return _cls.finish(t, r, out); }
+    void end_of_batch(PerThread &t)	{ _cls.end_of_batch(t); }
+  protected:
+    C _cls;
 };
 
 CLICK_ENDDECLS

@@ -18,30 +18,23 @@ CLICK_DECLS
  *   CheckICMPHeader checkicmpheader.cc:83-141
  */
 
-class HIPCheckIPHeader : public HIPBatchElement { public:
+class HIPCheckIPHeader : public HIPClassElement<hipcore::CheckIPHeaderClass<Packet, ClickPacketOps> > { public:
     const char *class_name() const	{ return "CheckIPHeader"; }
     const char *port_count() const	{ return PORTS_1_1X2; }
     const char *flags() const		{ return "A"; }
     int initialize(ErrorHandler *errh) CLICK_COLD;
-    int finish(PerThread &t, Routed &r, Packet **out);
-  protected:
-    int _offset;
 };
 
 class HIPCheckIPHeader2 : public HIPCheckIPHeader { public:
     const char *class_name() const	{ return "CheckIPHeader2"; }
 };
 
-class HIPIPInputCombo : public HIPBatchElement { public:
+class HIPIPInputCombo : public HIPClassElement<hipcore::IPInputComboClass<Packet, ClickPacketOps> > { public:
     const char *class_name() const	{ return "IPInputCombo"; }
     const char *port_count() const	{ return PORTS_1_1; }
     const char *processing() const	{ return AGNOSTIC; }
     const char *flags() const		{ return "A"; }
     int initialize(ErrorHandler *errh) CLICK_COLD;
-    int32_t nh_offset(Packet *)		{ return 14; }   // Strip(14): the header is at data() + 14
-    int finish(PerThread &t, Routed &r, Packet **out);
-  protected:
-    int _color;
 };
 
 class HIPCheckL4Header : public HIPBatchElement { public:

@@ -43,26 +43,35 @@
  * "lost" handler) and the runcount released, so the router can stop.
  *
  * Host interface (all called on the thread that drives the core):
- *   P *prepare(P *p, uint32_t *anno, P **extra)   before staging (uniqueify,
- *        PaintTee clone ...); returns the packet to stage, 0 if consumed
- *   uint8_t *data(P *p); uint32_t length(P *p); int32_t nh_offset(P *p)
- *   bool primary(int32_t port, uint32_t aux)     false for a result that
- *        comes with its packet's own (IPOutputCombo's clone, IPFragmenter's
- *        fragments): the held packet stays
- *   P *make_packet(clk_element *e, uint32_t key)  a new packet from the glue
- *        (IPFragmenter's fragment), under the lock; 0 on failure
- *   int finish(S &t, Routed &r, P **out)         the reference's side
- *        effects for one result (no lock held); returns the output port of
- *        the packet *out to emit, or -1 when nothing is emitted
- *   void end_of_batch(S &t)                      after a batch's results
+ *   the class hooks of hipclasses.hh -- prepare(), nh_offset(), primary(),
+ *        make_packet(), finish(), end_of_batch() -- which the host forwards
+ *        to the element class's shipped logic (the Click adapter and the
+ *        native test instantiate the same classes)
+ *   uint8_t *data(P *p); uint32_t length(P *p)
  *   void output_push(int port, P *p)             checked_output_push
  *   P *input_pull()                              input(0).pull(0)
  *   void kill(P *p)
  *   void adjust_runcount(int delta)
- *   void schedule(S &t, unsigned ms); void unschedule(S &t); bool scheduled(S &t)
+ *   uint64_t now_ns()                            a steady clock
+ *   void wake(S &t)                              make sure poll(t) runs on t's
+ *        thread soon (Click: the state's Task, moved to that RouterThread)
  *   void chatter(const char *text)               the adapter's own messages
  *   void message(const char *line)               the element's chatter lines from the glue
- */
+ *
+ * Latency flush on the state's own thread: a state that holds packets has a
+ * deadline (LATENCY after its batch started); poll(t), run by the thread's
+ * Task, flushes and delivers once it has passed.  So every packet of thread
+ * k is staged, flushed and pushed downstream on thread k (the reference's
+ * per-thread model; a Timer would run on the element's home thread,
+ * timer.cc:245-246).
+ *
+ * Pull context, double-buffered: when the ready queue is empty, pull() takes
+ * up to BATCH packets from input 0 (until it returns null), launches them
+ * (clk_element_flush_async) and so routes the batch launched by the previous
+ * refill: those packets are handed out while the new batch is on the GPU.
+ * Only when nothing is ready after that (the first refill, or a batch that
+ * kept no packet) does pull() wait for the batch in flight.
+  */
 #include <stddef.h>
 #include <stdint.h>
 #include <string.h>
@@ -99,13 +108,16 @@ template <class P, class L> struct State {
     bool counted;                 // holds a runcount reference
     unsigned fails;               // consecutive failed flushes
     bool draining;                // a delivery loop is running on this state
+    bool armed;                   // the latency deadline is set
+    uint64_t deadline;            // now_ns() at which poll() flushes
+    uint64_t push_errors;         // packets push() could not stage (chatter is rate-limited)
     std::vector<Routed<P> > outbox;
     std::deque<P *> ready;        // pull context: output-0 packets ready to hand out
     P *last_primary;              // route(): the packet of the last primary result
     P *frag_parent;               // host use (IPFragmenter's first-fragment parent)
     L lock;
-    State() : ctx(0), e(0), id(0), base(0), next(0), counted(false), fails(0), draining(false),
-              last_primary(0), frag_parent(0) { }
+    State() : ctx(0), e(0), id(0), base(0), next(0), counted(false), fails(0), draining(false), armed(false),
+              deadline(0), push_errors(0), last_primary(0), frag_parent(0) { }
 };
 
 template <class P, class Host, class L> class Core {
@@ -129,7 +141,8 @@ template <class P, class Host, class L> class Core {
         drain(h, t, false);
     }
 
-    // the latency timer of state t fired: run its partial batch, route all
+    // run state t's partial batch now and route everything (the deadline
+    // passed, or the router asks)
     void timer(Host &h, S &t)
     {
         t.lock.acquire();
@@ -138,33 +151,57 @@ template <class P, class Host, class L> class Core {
         drain(h, t, false);
     }
 
+    // the state's Task: flush once its deadline has passed.  Returns true
+    // while the state still holds a deadline (the Task runs again).
+    bool poll(Host &h, S &t)
+    {
+        t.lock.acquire();
+        if (!t.armed) {
+            t.lock.release();
+            return false;
+        }
+        if (h.now_ns() < t.deadline) {
+            t.lock.release();
+            return true;
+        }
+        flush(h, t, true);
+        t.lock.release();
+        drain(h, t, false);
+        t.lock.acquire();
+        const bool again = t.armed;
+        t.lock.release();
+        return again;
+    }
+
+    bool armed(S &t)
+    {
+        t.lock.acquire();
+        const bool a = t.armed;
+        t.lock.release();
+        return a;
+    }
+
     // ---- pull context (output 0) --------------------------------------------
     P *pull(Host &h, S &t)
     {
         t.lock.acquire();
         if (t.ready.empty()) {
             t.lock.release();
-            // refill: up to one batch from the input, until it runs dry
-            uint32_t k = 0;
-            P *q;
-            while (k < _batch && (q = h.input_pull()) != 0) {
-                t.lock.acquire();
-                if (stage(h, t, q, false))
-                    k++;
+            refill_and_launch(h, t);     // launches a batch, routes the one in flight
+            t.lock.acquire();
+            // nothing ready (the first refill, or a batch that kept no packet
+            // for output 0): wait for what is in flight -- retried at once,
+            // abandoned after max_retries -- and launch the next batch before
+            // handing these out
+            while (t.ready.empty() && !t.held.empty() && t.e) {
+                flush(h, t, true);
+                const bool failed = t.fails != 0;
                 t.lock.release();
+                drain(h, t, true);
+                if (!failed)
+                    refill_and_launch(h, t);
+                t.lock.acquire();
             }
-            t.lock.acquire();
-            if (k || !t.held.empty()) {
-                // synchronous: retried at once, abandoned after max_retries
-                while (!t.held.empty() && t.e) {
-                    flush(h, t, true);
-                    if (t.fails == 0 || !t.e)
-                        break;
-                }
-            }
-            t.lock.release();
-            drain(h, t, true);
-            t.lock.acquire();
         }
         P *p = 0;
         if (!t.ready.empty()) {
@@ -201,9 +238,9 @@ template <class P, class Host, class L> class Core {
             h.kill(t.frag_parent);
             t.frag_parent = 0;
         }
+        t.armed = false;
         if (t.counted) {
             t.counted = false;
-            h.unschedule(t);
             h.adjust_runcount(-1);
         }
         if (t.e) {
@@ -218,6 +255,26 @@ template <class P, class Host, class L> class Core {
     }
 
   private:
+    // Pull context (unlocked): up to one batch from input 0, until it runs
+    // dry, staged and launched; the batch in flight before is routed and
+    // delivered (its output-0 packets to the ready queue).
+    void refill_and_launch(Host &h, S &t)
+    {
+        uint32_t k = 0;
+        P *q;
+        while (k < _batch && (q = h.input_pull()) != 0) {
+            t.lock.acquire();
+            if (stage(h, t, q, false))
+                k++;
+            t.lock.release();
+        }
+        t.lock.acquire();
+        if (!t.held.empty())
+            flush(h, t, false);
+        t.lock.release();
+        drain(h, t, true);
+    }
+
     // Stage one packet (locked).  Returns true if it is held.
     bool stage(Host &h, S &t, P *p, bool push_ctx)
     {
@@ -227,22 +284,41 @@ template <class P, class Host, class L> class Core {
             h.kill(p);
             return false;
         }
-        if (!(p = h.prepare(p, &anno, &extra)))
+        if (!(p = h.prepare(p, &anno, &extra))) {
+            if (extra) {                 // consumed, with a result of its own (IPOutputCombo's
+                R r;                     // clone when the copy failed): delivered as it stands
+                memset(&r, 0, sizeof(r));
+                r.extra = extra;
+                r.port = CLK_PORT_OUT1;
+                t.outbox.push_back(r);
+            }
             return false;
+        }
         Held<P> e = {p, extra, anno};
         t.held.push_back(e);
         if (push_ctx && !t.counted) {    // keep the router running until this batch is routed
             h.adjust_runcount(1);
             t.counted = true;
-            h.schedule(t, _latency_ms);
+            arm(h, t);
         }
         int r = clk_element_push_anno(t.e, h.data(p), h.length(p), h.nh_offset(p), anno, t.next);
-        if (r < 0) {                     // not staged (e.g. ZEROCOPY memory not registered)
-            h.chatter(clk_element_last_error(t.e));
+        if (r < 0) {                     // not staged
             t.held.pop_back();
             h.kill(p);
             if (extra)
                 h.kill(extra);
+            if (r == CLK_EHIP) {
+                // a flush inside the push failed (a ZEROCOPY batch ends where
+                // the next packet's memory region starts): the staged batch
+                // counts a failed flush, as a timer flush would
+                failed_flush(h, t);
+                route(h, t);
+            } else if (t.push_errors++ == 0 || (t.push_errors & 0xFFFF) == 0) {
+                char buf[640];           // per-packet errors, once per 65536
+                snprintf(buf, sizeof(buf), "%llu packet(s) not staged: %s", (unsigned long long) t.push_errors,
+                         clk_element_last_error(t.e));
+                h.chatter(buf);
+            }
             release_if_idle(h, t);
             return false;
         }
@@ -252,6 +328,32 @@ template <class P, class Host, class L> class Core {
         return true;
     }
 
+    void arm(Host &h, S &t)
+    {
+        t.deadline = h.now_ns() + (uint64_t) _latency_ms * 1000000u;
+        if (!t.armed) {
+            t.armed = true;
+            h.wake(t);
+        }
+    }
+
+    // one failed flush of the staged batch (locked): counted, the batch
+    // abandoned after max_retries in a row
+    void failed_flush(Host &h, S &t)
+    {
+        t.fails++;
+        char buf[640];
+        if (t.fails >= _max_retries) {
+            uint64_t k = clk_element_abandon(t.e);
+            snprintf(buf, sizeof(buf), "GPU batch failed %u times, %llu packets killed: %s", t.fails,
+                     (unsigned long long) k, clk_element_last_error(t.e));
+            t.fails = 0;
+        } else
+            snprintf(buf, sizeof(buf), "GPU batch failed (retry %u of %u): %s", t.fails, _max_retries - 1,
+                     clk_element_last_error(t.e));
+        h.chatter(buf);
+    }
+
     // wait: route everything staged (timer, pull); otherwise double-buffered
     // (launch the staged batch, route the previous one, return).  Locked.
     void flush(Host &h, S &t, bool wait)
@@ -259,33 +361,24 @@ template <class P, class Host, class L> class Core {
         if (!t.e)
             return;
         int r = wait ? clk_element_flush(t.e) : clk_element_flush_async(t.e);
-        if (r != CLK_SUCCESS) {
-            // nothing of the failed batch was routed; it stays staged
-            t.fails++;
-            char buf[640];
-            if (t.fails >= _max_retries) {
-                uint64_t k = clk_element_abandon(t.e);
-                snprintf(buf, sizeof(buf), "GPU batch failed %u times, %llu packets killed: %s", t.fails,
-                         (unsigned long long) k, clk_element_last_error(t.e));
-                t.fails = 0;
-            } else
-                snprintf(buf, sizeof(buf), "GPU batch failed (retry %u of %u): %s", t.fails, _max_retries - 1,
-                         clk_element_last_error(t.e));
-            h.chatter(buf);
-        } else
+        if (r != CLK_SUCCESS)            // nothing of the failed batch was routed; it stays staged
+            failed_flush(h, t);
+        else
             t.fails = 0;
         route(h, t);
         release_if_idle(h, t);
-        if (t.counted && !h.scheduled(t))
-            h.schedule(t, _latency_ms);
+        if (t.counted)                   // a new deadline for what is still held
+            arm(h, t);
     }
 
     void release_if_idle(Host &h, S &t)
     {
-        if (t.held.empty() && t.counted) {
-            t.counted = false;
-            h.unschedule(t);
-            h.adjust_runcount(-1);       // stop may now proceed
+        if (t.held.empty()) {
+            t.armed = false;
+            if (t.counted) {
+                t.counted = false;
+                h.adjust_runcount(-1);   // stop may now proceed
+            }
         }
     }
 

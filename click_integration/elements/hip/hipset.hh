@@ -16,9 +16,7 @@ CLICK_DECLS
  * writable packet when its batch is routed.
  */
 
-class HIPSetChecksum : public HIPBatchElement { public:
-    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
-};
+typedef HIPClassElement<hipcore::SetChecksumClass<Packet, ClickPacketOps> > HIPSetChecksum;
 
 class HIPSetIPChecksum : public HIPSetChecksum { public:
     const char *class_name() const	{ return "SetIPChecksum"; }
@@ -38,10 +36,9 @@ class HIPSetTCPChecksum : public HIPSetChecksum { public:
     const char *processing() const	{ return AGNOSTIC; }
 };
 
-class HIPDecIPTTL : public HIPBatchElement { public:
+class HIPDecIPTTL : public HIPClassElement<hipcore::DecIPTTLClass<Packet, ClickPacketOps> > { public:
     const char *class_name() const	{ return "DecIPTTL"; }
     const char *port_count() const	{ return PORTS_1_1X2; }
-    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
 };
 
 CLICK_ENDDECLS

@@ -1,21 +1,32 @@
 // Test harness (not product code): drives the Click adapter's core
-// (click_integration/elements/hip/hipcore.hh) with a packet type, lock and
+// (click_integration/elements/hip/hipcore.hh) AND the element classes' shipped
+// logic (hipclasses.hh) with a packet type, packet-operations trait, lock and
 // host of its own -- no Click headers -- on the GPU through the element glue
 // (include/click_amd_elements.h), and checks every output against the CPU
 // oracle (oracle/cksum_oracle.h).  tests/test_gpu_adapter_core.py runs it.
 //
-// Scenarios: push context with double-buffered batches and the latency
-// timer; pull context (one batch per refill, output 1 pushed); IPFragmenter
-// extras with annotations copied from their parent; a failed flush, then
-// the retry; the retry limit (abandon, runcount released); a downstream
-// element that pushes back into the element while it delivers; four
-// threads with a state each while a "home" thread fires their timers;
-// cleanup of a held partial batch.  Prints one line per scenario and exits
-// nonzero if any fails.
+// The test packet models what the classes depend on in Click's Packet:
+// buffers shared by clones until uniqueify() copies them, data()/length()
+// moved by pull()/take(), a network header offset, and an annotation area
+// (paint, dst, ICMP parameter problem, FIX_IP_SRC, packet type, and an id
+// the test traces packets by) that copy_annotations() copies.
+//
+// Scenarios: every element class over fuzzed packets (outputs, bytes, trims,
+// Strip, annotations, clones, uniqueify against a clone the test holds);
+// push context with double-buffered batches and the latency deadline; pull
+// context, double-buffered, and through two GPU-backed elements in a row;
+// IPFragmenter extras; IPOutputCombo when the copy fails; a failed flush
+// and its retry; the retry limit; a downstream element that pushes back into
+// the element while it delivers; four threads each polling its own state
+// (packets delivered on their own thread only); cleanup of a held batch.
+// Prints one line per scenario and exits nonzero if any fails.
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -24,39 +35,91 @@
 #include "click_amd_elements.h"
 #include "../../oracle/cksum_oracle.h"
 #include "../../click_integration/elements/hip/hipcore.hh"
+#include "../../click_integration/elements/hip/hipclasses.hh"
 
 extern "C" void clk_glue_inject_fault_internal(int nth);
 
 namespace {
 
-struct TPacket {
-    std::vector<uint8_t> mem;
-    size_t off = 0, len = 0;
-    int nh = -1;
+const uint32_t MY_IP = 0x18041A12;   // as the glue reads "18.26.4.24" (network order in memory)
+const char *MY_IP_TXT = "18.26.4.24";
+
+struct TAnno {
     long id = 0;
     uint32_t paint = 0, dst = 0, prob = 0;
     bool fix_src = false, bcast = false;
-    uint8_t *data() { return mem.data() + off; }
+};
+
+struct TPacket {
+    std::shared_ptr<std::vector<uint8_t> > buf;
+    size_t off = 0, len = 0;
+    long nh = -1;                    // absolute offset of the network header in buf
+    TAnno a;
 };
 
 std::atomic<long> g_live{0};
+std::atomic<long> g_kills{0};        // packets killed (by the core or a class)
+std::atomic<int> g_uniq_fail{0};     // the n-th uniqueify() that must copy fails
 
-TPacket *make(const uint8_t *bytes, size_t len, long id)
+TPacket *make(const uint8_t *bytes, size_t len, long id, size_t headroom = 0)
 {
     TPacket *p = new TPacket;
-    p->mem.assign(bytes, bytes + len);
+    p->buf = std::make_shared<std::vector<uint8_t> >(headroom + len);
+    if (len && bytes)
+        std::memcpy(p->buf->data() + headroom, bytes, len);
+    p->off = headroom;
     p->len = len;
-    p->id = id;
+    p->a.id = id;
     g_live++;
     return p;
 }
 
-TPacket *clone(const TPacket *q)
-{
-    TPacket *p = new TPacket(*q);
-    g_live++;
-    return p;
-}
+// The packet operations trait (hipclasses.hh) over TPacket, as
+// ClickPacketOps is over Click's Packet.
+struct TOps {
+    static TPacket *uniqueify(TPacket *p)
+    {
+        if (p->buf.use_count() > 1) {
+            int v = g_uniq_fail.load();
+            if (v > 0 && g_uniq_fail.fetch_sub(1) == 1) {
+                kill(p);                 // Packet::uniqueify kills on failure
+                return nullptr;
+            }
+            p->buf = std::make_shared<std::vector<uint8_t> >(*p->buf);
+        }
+        return p;
+    }
+    static TPacket *clone(TPacket *p)
+    {
+        TPacket *q = new TPacket(*p);
+        g_live++;
+        return q;
+    }
+    static void kill(TPacket *p)
+    {
+        g_kills++;
+        g_live--;
+        delete p;
+    }
+    static uint8_t *data(TPacket *p) { return p->buf->data() + p->off; }
+    static uint32_t length(TPacket *p) { return (uint32_t)p->len; }
+    static bool has_network_header(TPacket *p) { return p->nh >= 0; }
+    static const uint8_t *network_header(TPacket *p) { return p->buf->data() + p->nh; }
+    static int32_t network_header_offset(TPacket *p) { return (int32_t)(p->nh - (long)p->off); }
+    static int network_length(TPacket *p) { return (int)((long)(p->off + p->len) - p->nh); }
+    static void set_ip_header(TPacket *p, const uint8_t *ip, uint32_t) { p->nh = ip - p->buf->data(); }
+    static void take(TPacket *p, uint32_t n) { p->len -= n; }
+    static void pull(TPacket *p, uint32_t n) { p->off += n, p->len -= n; }
+    static void set_dst_ip_anno(TPacket *p, uint32_t a) { p->a.dst = a; }
+    static uint32_t paint(TPacket *p) { return p->a.paint; }
+    static void set_paint(TPacket *p, uint32_t c) { p->a.paint = c; }
+    static bool fix_ip_src(TPacket *p) { return p->a.fix_src; }
+    static void clear_fix_ip_src(TPacket *p) { p->a.fix_src = false; }
+    static void set_icmp_paramprob(TPacket *p, uint32_t v) { p->a.prob = v; }
+    static bool broadcast_or_multicast(TPacket *p) { return p->a.bcast; }
+    static void copy_annotations(TPacket *to, TPacket *from) { to->a = from->a; }
+    static TPacket *make(uint32_t headroom, uint32_t len) { return ::make(nullptr, len, -1, headroom); }
+};
 
 struct TLock {
     std::mutex m;
@@ -64,36 +127,37 @@ struct TLock {
     void release() { m.unlock(); }
 };
 
-class Host;
-typedef hipcore::Core<TPacket, Host, TLock> Core;
 typedef hipcore::State<TPacket, TLock> St;
+template <class C> class Host;
 
-// The test's "element": what HIPBatchElement and its subclasses do in Click,
-// with the outputs recorded.
+// The test's "element": HIPBatchElement's host interface, with the outputs
+// recorded (and the thread that pushed each), around class C's shipped logic.
+template <class C>
 class Host {
   public:
-    std::string cls;
+    typedef hipcore::Core<TPacket, Host<C>, TLock> Core;
+    C cls;
     Core core;
     std::vector<St> st;
     std::mutex out_mu;
-    std::vector<std::vector<TPacket *> > out;   // per output port, in push order
+    std::vector<std::vector<TPacket *> > out;          // per output port, in push order
+    std::vector<std::vector<std::thread::id> > out_thread;
     std::atomic<int> runcount{0};
-    std::vector<int> sched;                     // per state: scheduled flag
-    std::deque<TPacket *> input;                // pull context source
-    std::vector<std::string> chat, msgs;
-    std::atomic<long> kills{0};
-    uint32_t color = 0;
-    // re-entrancy probe: called on every output-0 packet (may push back in)
-    void (*on_out0)(Host &, TPacket *) = nullptr;
+    std::deque<TPacket *> input;                        // pull context source
+    std::function<TPacket *()> upstream;                // or another element's pull()
+    std::vector<std::string> chat, msgs;        // (under out_mu: states on several threads)
+    std::atomic<int> wakes{0};
+    void (*on_out0)(Host &, TPacket *) = nullptr;       // re-entrancy probe
 
-    Host(const std::string &c, const std::string &conf, int noutputs, int nstates = 1)
-        : cls(c), st(nstates), out(5), sched(nstates, 0)
+    Host(const char *glue_class, const std::string &conf, int noutputs, int nstates = 1)
+        : st(nstates), out(5), out_thread(5)
     {
         for (int k = 0; k < nstates; k++) {
             st[k].id = k;
             if (clk_ctx_create(0, &st[k].ctx) != CLK_SUCCESS ||
-                clk_element_create(st[k].ctx, c.c_str(), conf.c_str(), c.c_str(), noutputs, &st[k].e) != CLK_SUCCESS) {
-                std::fprintf(stderr, "create %s(%s): %s\n", c.c_str(), conf.c_str(), clk_last_error(st[k].ctx));
+                clk_element_create(st[k].ctx, glue_class, conf.c_str(), glue_class, noutputs, &st[k].e) !=
+                    CLK_SUCCESS) {
+                std::fprintf(stderr, "create %s(%s): %s\n", glue_class, conf.c_str(), clk_last_error(st[k].ctx));
                 std::exit(3);
             }
         }
@@ -107,146 +171,62 @@ class Host {
             core.cleanup(*this, t);
         for (auto &v : out)
             for (TPacket *p : v)
-                kill(p);
+                TOps::kill(p);
     }
 
-    // ---- the core's host interface --------------------------------------------
-    TPacket *prepare(TPacket *p, uint32_t *anno, TPacket **extra)
-    {
-        if (cls == "IPOutputCombo") {
-            if (p->bcast) {
-                *anno = CLK_ANNO_BCAST;
-                return p;
-            }
-            *anno = CLK_ANNO_PAINT(p->paint) | (p->fix_src ? CLK_ANNO_FIX_IP_SRC : 0);
-            if (p->paint == color)
-                *extra = clone(p);
-        }
-        return p;
-    }
-    uint8_t *data(TPacket *p) { return p->data(); }
-    uint32_t length(TPacket *p) { return (uint32_t)p->len; }
-    int32_t nh_offset(TPacket *p) { return p->nh; }
-    bool primary(int32_t port, uint32_t aux)
-    {
-        if (cls == "IPOutputCombo")
-            return aux != CLK_AUX_CLONE;
-        if (cls == "IPFragmenter")
-            return aux == 0;
-        (void)port;
-        return true;
-    }
-    TPacket *make_packet(clk_element *e, uint32_t key)
-    {
-        int64_t n = clk_element_take_packet(e, key, nullptr, 0);
-        if (n < 0)
-            return nullptr;
-        std::vector<uint8_t> b((size_t)n);
-        clk_element_take_packet(e, key, b.data(), b.size());
-        TPacket *p = make(b.data(), b.size(), -1);
-        p->nh = 0;
-        return p;
-    }
-    int finish(St &t, hipcore::Routed<TPacket> &r, TPacket **outp)
-    {
-        if (cls == "IPOutputCombo") {
-            if (r.extra && !r.p) {               // the PaintTee clone
-                *outp = r.extra;
-                return 1;
-            }
-            if (r.port == CLK_PORT_KILL) {
-                if (r.p) kill(r.p);
-                if (r.extra) kill(r.extra);
-                return -1;
-            }
-            if (r.port == CLK_PORT_OUT2)
-                r.p->prob = r.aux;
-            if (r.anno & CLK_ANNO_FIX_IP_SRC)
-                r.p->fix_src = false;
-            *outp = r.p;
-            return r.port;
-        }
-        if (cls == "IPFragmenter") {
-            if (r.made) {                        // a fragment after the first
-                if (r.parent)
-                    r.made->paint = r.parent->paint, r.made->id = r.parent->id;
-                *outp = r.made;
-                return 0;
-            }
-            TPacket *p = r.p;
-            if (!p)
-                return -1;
-            if (r.port == CLK_PORT_OUT0 && r.len < p->len) {   // the first fragment: a clone cut to len
-                TPacket *first = clone(p);
-                first->len = r.len;
-                if (t.frag_parent)
-                    kill(t.frag_parent);
-                t.frag_parent = p;
-                *outp = first;
-                return 0;
-            }
-            if (r.port == CLK_PORT_KILL) {
-                kill(p);
-                return -1;
-            }
-            *outp = p;
-            return r.port;
-        }
-        TPacket *p = r.p;
-        if (!p)
-            return -1;
-        if (r.port == CLK_PORT_KILL) {
-            kill(p);
-            return -1;
-        }
-        if (cls == "CheckIPHeader" && r.port == CLK_PORT_OUT0) {   // checkipheader.cc:213-223
-            if (p->len > r.len)
-                p->len = r.len;
-            std::memcpy(&p->dst, p->data() + 16, 4);
-        }
-        *outp = p;
-        return r.port;
-    }
-    void end_of_batch(St &t)
-    {
-        if (t.frag_parent) {
-            kill(t.frag_parent);
-            t.frag_parent = nullptr;
-        }
-    }
+    // ---- the core's host interface (as HIPBatchElement / HIPClassElement) -----
+    TPacket *prepare(TPacket *p, uint32_t *anno, TPacket **extra) { return cls.prepare(p, anno, extra); }
+    int32_t nh_offset(TPacket *p) { return cls.nh_offset(p); }
+    bool primary(int32_t port, uint32_t aux) { return cls.primary(port, aux); }
+    TPacket *make_packet(clk_element *e, uint32_t key) { return cls.make_packet(e, key); }
+    int finish(St &t, hipcore::Routed<TPacket> &r, TPacket **o) { return cls.finish(t, r, o); }
+    void end_of_batch(St &t) { cls.end_of_batch(t); }
+    uint8_t *data(TPacket *p) { return TOps::data(p); }
+    uint32_t length(TPacket *p) { return TOps::length(p); }
     void output_push(int port, TPacket *p)
     {
         {
             std::lock_guard<std::mutex> g(out_mu);
             out[(size_t)port].push_back(p);
+            out_thread[(size_t)port].push_back(std::this_thread::get_id());
         }
         if (port == 0 && on_out0)
             on_out0(*this, p);
     }
     TPacket *input_pull()
     {
+        if (upstream)
+            return upstream();
         if (input.empty())
             return nullptr;
         TPacket *p = input.front();
         input.pop_front();
         return p;
     }
-    void kill(TPacket *p)
-    {
-        kills++;
-        g_live--;
-        delete p;
-    }
+    void kill(TPacket *p) { TOps::kill(p); }
     void adjust_runcount(int d) { runcount += d; }
-    void schedule(St &t, unsigned) { sched[(size_t)t.id] = 1; }
-    void unschedule(St &t) { sched[(size_t)t.id] = 0; }
-    bool scheduled(St &t) { return sched[(size_t)t.id] != 0; }
-    void chatter(const char *s) { chat.push_back(s); }
-    void message(const char *s) { msgs.push_back(s); }
+    uint64_t now_ns()
+    {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    void wake(St &) { wakes++; }
+    void chatter(const char *s)
+    {
+        std::lock_guard<std::mutex> g(out_mu);
+        chat.push_back(s);
+    }
+    void message(const char *s)
+    {
+        std::lock_guard<std::mutex> g(out_mu);
+        msgs.push_back(s);
+    }
 
     void push(TPacket *p, int state = 0) { core.push(*this, st[(size_t)state], p); }
     TPacket *pull(int state = 0) { return core.pull(*this, st[(size_t)state]); }
     void timer(int state = 0) { core.timer(*this, st[(size_t)state]); }
+    bool poll(int state = 0) { return core.poll(*this, st[(size_t)state]); }
+    bool armed(int state = 0) { return core.armed(st[(size_t)state]); }
     std::string handler(const char *h, int state = 0)
     {
         char buf[256];
@@ -254,6 +234,16 @@ class Host {
         return buf;
     }
 };
+
+typedef hipcore::Plain<TPacket, TOps> PlainC;
+typedef hipcore::CheckIPHeaderClass<TPacket, TOps> CheckIPC;
+typedef hipcore::IPInputComboClass<TPacket, TOps> InputComboC;
+typedef hipcore::SetChecksumClass<TPacket, TOps> SetC;
+typedef hipcore::DecIPTTLClass<TPacket, TOps> DecTTLC;
+typedef hipcore::IPGWOptionsClass<TPacket, TOps> GWOptC;
+typedef hipcore::FixIPSrcClass<TPacket, TOps> FixSrcC;
+typedef hipcore::IPOutputComboClass<TPacket, TOps> OutComboC;
+typedef hipcore::IPFragmenterClass<TPacket, TOps> FragC;
 
 int g_fail = 0;
 #define CHECK(c)                                                                    \
@@ -267,74 +257,480 @@ int g_fail = 0;
 void report(const char *name, bool ok)
 {
     std::printf("%s %s\n", ok ? "PASS" : "FAIL", name);
+    std::fflush(stdout);
     if (!ok)
         g_fail++;
 }
 
-// An IPv4/UDP packet of L bytes (synthetic, checksums set by the oracle).
-std::vector<uint8_t> udp_bytes(uint32_t L, long id, int proto = 17)
+uint64_t g_rng = 0x9E3779B97F4A7C15ull;
+uint32_t rnd(uint32_t n)
+{
+    g_rng = oracle_splitmix64(g_rng);
+    return (uint32_t)(g_rng % n);
+}
+
+// An IPv4 packet of L bytes (synthetic, checksums set by the oracle).
+std::vector<uint8_t> ip_bytes(uint32_t L, long id, int proto = 17)
 {
     std::vector<uint8_t> b(L);
     oracle_gen_packet(b.data(), L, proto, 0x5EED, (uint64_t)id);
     oracle_set_ip_checksum(b.data(), L);
     if (proto == 17 && L >= 28)
         oracle_set_udp_checksum(b.data(), L);
+    if (proto == 6 && L >= 40)
+        oracle_set_tcp_checksum(b.data(), L, 0);
     return b;
 }
 
-// 1. push context: CheckIPHeader, double-buffered full batches, the timer
+// `words` 32-bit words of Record Route / NOP / EOL options inserted after the
+// 20-byte header (ip_hl, ip_len and the IP checksum fixed): the option walk
+// of IPGWOptions / IPOutputCombo, with pointers before, at and past the end.
+std::vector<uint8_t> with_options(const std::vector<uint8_t> &b, int words)
+{
+    std::vector<uint8_t> o(4 * words, 1);            // NOPs
+    const int ln = 4 * words - 1;
+    if (ln >= 7) {
+        o[0] = 7;                                    // RR
+        o[1] = (uint8_t)ln;
+        const uint8_t ptrs[] = {4, 8, (uint8_t)(ln + 1), 3, (uint8_t)(ln - 2)};
+        o[2] = ptrs[rnd(5)];
+        for (int k = 3; k < ln; k++)
+            o[k] = (uint8_t)rnd(256);
+        o[ln] = 0;                                   // EOL
+    }
+    std::vector<uint8_t> r(b.begin(), b.begin() + 20);
+    r.insert(r.end(), o.begin(), o.end());
+    r.insert(r.end(), b.begin() + 20, b.end());
+    r[0] = (uint8_t)(0x40 | (5 + words));
+    const uint16_t ipl = (uint16_t)r.size();
+    r[2] = (uint8_t)(ipl >> 8), r[3] = (uint8_t)ipl;
+    r[10] = r[11] = 0;
+    oracle_set_ip_checksum(r.data(), (uint32_t)r.size());
+    return r;
+}
+
+// ---------------------------------------------------------------------------
+// 1. Every element class: the shipped class logic over fuzzed packets.
+//    What the test expects per packet is the reference's behaviour: the
+//    oracle's verdict / rewritten bytes, the port the reference pushes to,
+//    and what its simple_action does to the Packet (trim, Strip, annotations,
+//    clone order).  The test holds a clone of every pushed packet: an element
+//    that writes must have uniqueified first, so the clone keeps its bytes.
+// ---------------------------------------------------------------------------
+struct Expect {
+    long id;
+    std::vector<uint8_t> bytes;      // data() .. data() + length()
+    int nh;                          // network_header_offset(), -2: not checked
+    TAnno a;
+};
+
+struct Case {
+    std::vector<uint8_t> frame;      // what is pushed
+    int nh;                          // its network header offset (-1 none)
+    TAnno a;
+};
+
+template <class C>
+bool run_class(const char *name, Host<C> &h, std::vector<Case> &cases,
+               std::vector<std::vector<Expect> > &want, long *killed = nullptr)
+{
+    bool ok = true;
+    const long k0 = g_kills;
+    std::vector<TPacket *> held;                     // the test's clones
+    for (size_t i = 0; i < cases.size(); i++) {
+        TPacket *p = make(cases[i].frame.data(), cases[i].frame.size(), (long)i);
+        p->nh = cases[i].nh >= 0 ? cases[i].nh : -1;
+        long id = p->a.id;
+        p->a = cases[i].a;
+        p->a.id = id;
+        held.push_back(TOps::clone(p));
+        h.push(p);
+    }
+    h.timer();
+    CHECK(h.runcount == 0 && !h.armed());
+    if (killed)
+        *killed = g_kills - k0;
+    for (int port = 0; port < 5; port++) {
+        const auto &got = h.out[(size_t)port];
+        const auto &exp = want[(size_t)port];
+        CHECK(got.size() == exp.size());
+        if (got.size() != exp.size())
+            std::printf("  %s port %d: %zu results, want %zu\n", name, port, got.size(), exp.size());
+        for (size_t k = 0; k < got.size() && k < exp.size(); k++) {
+            TPacket *q = got[k];
+            const Expect &e = exp[k];
+            const bool same = q->a.id == e.id && q->len == e.bytes.size() &&
+                              std::memcmp(TOps::data(q), e.bytes.data(), q->len) == 0 &&
+                              (e.nh == -2 || TOps::network_header_offset(q) == e.nh) &&
+                              q->a.paint == e.a.paint && q->a.dst == e.a.dst && q->a.prob == e.a.prob &&
+                              q->a.fix_src == e.a.fix_src;
+            if (!same && ok)
+                std::printf("  %s port %d #%zu: id %ld/%ld len %zu/%zu nh %d/%d paint %u/%u dst %08x/%08x "
+                            "prob %u/%u fix %d/%d bytes %s\n",
+                            name, port, k, q->a.id, e.id, q->len, e.bytes.size(),
+                            TOps::network_header_offset(q), e.nh, q->a.paint, e.a.paint, q->a.dst, e.a.dst,
+                            q->a.prob, e.a.prob, q->a.fix_src, e.a.fix_src,
+                            q->len == e.bytes.size() && !std::memcmp(TOps::data(q), e.bytes.data(), q->len)
+                                ? "same" : "differ");
+            CHECK(same);
+        }
+    }
+    for (size_t i = 0; i < cases.size(); i++)        // nothing written through a shared buffer
+            CHECK(held[i]->len == cases[i].frame.size() &&
+                  std::memcmp(TOps::data(held[i]), cases[i].frame.data(), held[i]->len) == 0);
+    for (TPacket *q : held)
+        TOps::kill(q);
+    return ok;
+}
+
+Expect expect_of(long id, const std::vector<uint8_t> &bytes, int nh, TAnno a)
+{
+    a.id = id;
+    return Expect{id, bytes, nh, a};
+}
+
+uint32_t ld32(const uint8_t *p)
+{
+    uint32_t v;
+    std::memcpy(&v, p, 4);
+    return v;
+}
+
+// IP packets with every verdict the checks distinguish
+std::vector<Case> fuzz_cases(int n, int proto, int eth, bool for_check)
+{
+    std::vector<Case> cs;
+    for (int i = 0; i < n; i++) {
+        uint32_t L = proto == 1 ? 28 + rnd(600) : 40 + rnd(1400);
+        std::vector<uint8_t> b = ip_bytes(L, i, proto);
+        if (for_check) {
+            switch (rnd(12)) {
+            case 0: b[13] ^= 0x10; break;                          // IP checksum (and pseudo-header)
+            case 1: b[L - 1] ^= 0x04; break;                       // payload: L4 checksum
+            case 2: b[0] = 0x65; break;                            // version
+            case 3: b.resize(L + 1 + rnd(20), 0xAB); break;        // link padding: trimmed to ip_len
+            case 4: b.resize(10); break;                           // tiny
+            case 5: b[2] ^= 0x40; oracle_set_ip_checksum(b.data(), (uint32_t)b.size()); break;   // ip_len
+            default: break;
+            }
+        }
+        Case c;
+        c.frame.assign((size_t)eth, 0xEE);
+        c.frame.insert(c.frame.end(), b.begin(), b.end());
+        c.nh = eth ? -1 : 0;
+        cs.push_back(c);
+    }
+    return cs;
+}
+
+void every_class()
+{
+    // CheckIPHeader(OFFSET 14): output 0 trimmed to ip_len, network header at
+    // 14, dst annotation; output 1 untouched (checkipheader.cc:143-159,213-223)
+    {
+        bool ok = true;
+        Host<CheckIPC> h("CheckIPHeader", "OFFSET 14, BATCH 300", 2);
+        h.cls.offset = 14;
+        std::vector<Case> cs = fuzz_cases(1000, 17, 14, true);
+        std::vector<std::vector<Expect> > w(5);
+        for (size_t i = 0; i < cs.size(); i++) {
+            const auto &f = cs[i].frame;
+            int code = oracle_check_ip_header(f.data(), (uint32_t)f.size(), 14, 1, nullptr, 0, nullptr, 0);
+            if (code == 0) {
+                const uint32_t ipl = (uint32_t)f[16] << 8 | f[17];
+                std::vector<uint8_t> t(f.begin(), f.begin() + 14 + ipl);
+                TAnno a;
+                a.dst = ld32(f.data() + 14 + 16);
+                w[0].push_back(expect_of((long)i, t, 14, a));
+            } else
+                w[1].push_back(expect_of((long)i, f, -2, TAnno()));
+        }
+        ok = run_class("CheckIPHeader", h, cs, w) && ok;
+        report("class_CheckIPHeader", ok);
+    }
+    // CheckIPHeader2: no checksum test (checkipheader2.cc)
+    {
+        bool ok = true;
+        Host<CheckIPC> h("CheckIPHeader2", "BATCH 256", 2);
+        std::vector<Case> cs = fuzz_cases(700, 6, 0, true);
+        std::vector<std::vector<Expect> > w(5);
+        for (size_t i = 0; i < cs.size(); i++) {
+            const auto &f = cs[i].frame;
+            int code = oracle_check_ip_header(f.data(), (uint32_t)f.size(), 0, 0, nullptr, 0, nullptr, 0);
+            if (code == 0) {
+                const uint32_t ipl = (uint32_t)f[2] << 8 | f[3];
+                TAnno a;
+                a.dst = ld32(f.data() + 16);
+                w[0].push_back(expect_of((long)i, std::vector<uint8_t>(f.begin(), f.begin() + ipl), 0, a));
+            } else
+                w[1].push_back(expect_of((long)i, f, -2, TAnno()));
+        }
+        ok = run_class("CheckIPHeader2", h, cs, w) && ok;
+        report("class_CheckIPHeader2", ok);
+    }
+    // IPInputCombo(COLOR 2): Paint, Strip(14), the checks; bad packets killed
+    // (ipinputcombo.cc:66-140)
+    {
+        bool ok = true;
+        Host<InputComboC> h("IPInputCombo", "2, BATCH 400", 1);
+        h.cls.color = 2;
+        std::vector<Case> cs = fuzz_cases(1000, 17, 14, true);
+        std::vector<std::vector<Expect> > w(5);
+        size_t bad = 0;
+        for (size_t i = 0; i < cs.size(); i++) {
+            const auto &f = cs[i].frame;
+            cs[i].a.paint = 7;
+            int code = oracle_check_ip_header(f.data(), (uint32_t)f.size(), 14, 1, nullptr, 0, nullptr, 0);
+            if (code == 0) {
+                const uint32_t ipl = (uint32_t)f[16] << 8 | f[17];
+                TAnno a;
+                a.paint = 2;
+                a.dst = ld32(f.data() + 14 + 16);
+                w[0].push_back(expect_of((long)i, std::vector<uint8_t>(f.begin() + 14, f.begin() + 14 + ipl), 0, a));
+            } else
+                bad++;
+        }
+        long killed = 0;
+        ok = run_class("IPInputCombo", h, cs, w, &killed) && ok;
+        CHECK(killed == (long)bad && bad > 0);
+        report("class_IPInputCombo", ok);
+    }
+    // CheckUDPHeader / CheckTCPHeader / CheckICMPHeader: untouched, 0 or 1
+    {
+        const struct { const char *cls; int proto; } ls[] = {{"CheckUDPHeader", 17}, {"CheckTCPHeader", 6},
+                                                             {"CheckICMPHeader", 1}};
+        for (const auto &l : ls) {
+            bool ok = true;
+            Host<PlainC> h(l.cls, "BATCH 333", 2);
+            std::vector<Case> cs = fuzz_cases(900, l.proto, 0, true);
+            std::vector<std::vector<Expect> > w(5);
+            for (size_t i = 0; i < cs.size(); i++) {
+                const auto &f = cs[i].frame;
+                const uint32_t c = (uint32_t)f.size();
+                int code = l.proto == 17 ? oracle_check_udp_header(f.data(), c)
+                           : l.proto == 6 ? oracle_check_tcp_header(f.data(), c) : oracle_check_icmp_header(f.data(), c);
+                w[code ? 1 : 0].push_back(expect_of((long)i, f, 0, TAnno()));
+            }
+            ok = run_class(l.cls, h, cs, w) && ok;
+            report((std::string("class_") + l.cls).c_str(), ok);
+        }
+    }
+    // SetIPChecksum / SetUDPChecksum / SetTCPChecksum: uniqueify, the field
+    // written; SetUDPChecksum's fragments to output 1; bad lengths killed
+    {
+        const struct { const char *cls; int proto; } ls[] = {{"SetIPChecksum", 17}, {"SetUDPChecksum", 17},
+                                                             {"SetTCPChecksum", 6}};
+        for (const auto &l : ls) {
+            bool ok = true;
+            Host<SetC> h(l.cls, "BATCH 500", std::string(l.cls) == "SetUDPChecksum" ? 2 : 1);
+            std::vector<Case> cs = fuzz_cases(900, l.proto, 0, false);
+            std::vector<std::vector<Expect> > w(5);
+            for (size_t i = 0; i < cs.size(); i++) {
+                auto &f = cs[i].frame;
+                if (rnd(10) == 0)
+                    f[6] |= 0x20;                                  // IP_MF: SetUDPChecksum's output 1
+                if (rnd(15) == 0)
+                    f.resize(f.size() > 30 ? 30 : f.size());       // short
+                std::vector<uint8_t> r = f;
+                const uint32_t c = (uint32_t)r.size();
+                int code = std::string(l.cls) == "SetIPChecksum" ? oracle_set_ip_checksum(r.data(), c)
+                           : l.proto == 17 ? oracle_set_udp_checksum(r.data(), c) : oracle_set_tcp_checksum(r.data(), c, 0);
+                if (code == CLK_SET_OK)
+                    w[0].push_back(expect_of((long)i, r, 0, TAnno()));
+                else if (code == CLK_SET_OUTPUT1)
+                    w[1].push_back(expect_of((long)i, r, 0, TAnno()));
+            }
+            ok = run_class(l.cls, h, cs, w) && ok;
+            report((std::string("class_") + l.cls).c_str(), ok);
+        }
+    }
+    // DecIPTTL: writable only when decremented; expired to output 1
+    {
+        bool ok = true;
+        Host<DecTTLC> h("DecIPTTL", "BATCH 300", 2);
+        std::vector<Case> cs = fuzz_cases(800, 17, 0, false);
+        std::vector<std::vector<Expect> > w(5);
+        for (size_t i = 0; i < cs.size(); i++) {
+            auto &f = cs[i].frame;
+            f[8] = (uint8_t)(rnd(4) == 0 ? rnd(3) : 2 + rnd(250));
+            oracle_set_ip_checksum(f.data(), (uint32_t)f.size());
+            std::vector<uint8_t> r = f;
+            int code = oracle_dec_ip_ttl(r.data(), (uint32_t)r.size(), 1);
+            w[code == CLK_TTL_EXPIRED ? 1 : 0].push_back(expect_of((long)i, r, 0, TAnno()));
+        }
+        ok = run_class("DecIPTTL", h, cs, w) && ok;
+        report("class_DecIPTTL", ok);
+    }
+    // IPGWOptions(MYADDR): Record Route rewrites, parameter problems to 1
+    // with ICMP_PARAMPROB_ANNO (ipgwoptions.cc:53-172)
+    {
+        bool ok = true;
+        Host<GWOptC> h("IPGWOptions", std::string(MY_IP_TXT) + ", BATCH 250", 2);
+        std::vector<Case> cs = fuzz_cases(700, 17, 0, false);
+        std::vector<std::vector<Expect> > w(5);
+        size_t nprob = 0;
+        for (size_t i = 0; i < cs.size(); i++) {
+            auto &f = cs[i].frame;
+            if (rnd(2))
+                f = with_options(f, 1 + (int)rnd(9));
+            std::vector<uint8_t> r = f;
+            int prob = 0;
+            int code = oracle_ip_gw_options_element(r.data(), (uint32_t)r.size(), MY_IP, &MY_IP, 1, 0, &prob);
+            TAnno a;
+            if (code == CLK_GWOPT_ERROR) {
+                a.prob = (uint32_t)prob;
+                nprob++;
+                w[1].push_back(expect_of((long)i, r, 0, a));
+            } else
+                w[0].push_back(expect_of((long)i, r, 0, a));
+        }
+        ok = run_class("IPGWOptions", h, cs, w) && ok;
+        CHECK(nprob > 0);
+        report("class_IPGWOptions", ok);
+    }
+    // FixIPSrc(IPADDR): annotated packets rewritten, annotation cleared
+    {
+        bool ok = true;
+        Host<FixSrcC> h("FixIPSrc", std::string("IPADDR ") + MY_IP_TXT + ", BATCH 200", 1);
+        std::vector<Case> cs = fuzz_cases(600, 17, 0, false);
+        std::vector<std::vector<Expect> > w(5);
+        for (size_t i = 0; i < cs.size(); i++) {
+            cs[i].a.fix_src = rnd(3) == 0;
+            std::vector<uint8_t> r = cs[i].frame;
+            oracle_fix_ip_src(r.data(), (uint32_t)r.size(), cs[i].a.fix_src, MY_IP);
+            w[0].push_back(expect_of((long)i, r, 0, TAnno()));
+        }
+        ok = run_class("FixIPSrc", h, cs, w) && ok;
+        report("class_FixIPSrc", ok);
+    }
+    // IPOutputCombo(COLOR 1, IPADDR, MTU 700): broadcast killed (no clone),
+    // the painted clone to 1 before its packet with the bytes as pushed,
+    // parameter problem 2, TTL 3, MTU 4 (ipoutputcombo.cc:44-205)
+    {
+        bool ok = true;
+        Host<OutComboC> h("IPOutputCombo", std::string("1, ") + MY_IP_TXT + ", 700, BATCH 300", 5);
+        h.cls.color = 1;
+        std::vector<Case> cs = fuzz_cases(900, 17, 0, false);
+        std::vector<std::vector<Expect> > w(5);
+        size_t nb = 0;
+        for (size_t i = 0; i < cs.size(); i++) {
+            auto &f = cs[i].frame;
+            if (rnd(3) == 0)
+                f = with_options(f, 1 + (int)rnd(9));
+            if (rnd(6) == 0) {
+                f[8] = (uint8_t)rnd(2);                   // TTL 0/1: expired
+                oracle_set_ip_checksum(f.data(), (uint32_t)f.size());
+            }
+            cs[i].a.paint = rnd(3);
+            cs[i].a.fix_src = rnd(4) == 0;
+            cs[i].a.bcast = rnd(20) == 0;
+            if (cs[i].a.bcast) {
+                nb++;
+                continue;
+            }
+            if (cs[i].a.paint == 1)
+                w[1].push_back(expect_of((long)i, f, 0, cs[i].a));
+            std::vector<uint8_t> r = f;
+            int prob = 0;
+            int port = oracle_ip_output_combo(r.data(), (uint32_t)r.size(), (uint32_t)r.size(),
+                                              cs[i].a.fix_src ? 1 : 0, MY_IP, 700, 0, &prob);
+            TAnno a = cs[i].a;
+            if (port == 2)
+                a.prob = (uint32_t)prob;
+            else if (a.fix_src)
+                a.fix_src = false;
+            w[(size_t)port].push_back(expect_of((long)i, r, 0, a));
+        }
+        long killed = 0;
+        // the clones on output 1 come out in packet order, with the bytes
+        // as pushed (w[1])
+        ok = run_class("IPOutputCombo", h, cs, w, &killed) && ok;
+        CHECK(killed == (long)nb && nb > 0);
+        report("class_IPOutputCombo", ok);
+    }
+}
+
+// 2. IPOutputCombo when uniqueify fails: the reference has already pushed the
+//    PaintTee clone (ipoutputcombo.cc:56-60); the clone leaves on output 1,
+//    the packet is gone, nothing is staged
+void output_combo_copy_fails()
+{
+    bool ok = true;
+    Host<OutComboC> h("IPOutputCombo", std::string("1, ") + MY_IP_TXT + ", 1500", 5);
+    h.cls.color = 1;
+    std::vector<uint8_t> b = ip_bytes(200, 1);
+    TPacket *p = make(b.data(), b.size(), 1);
+    p->nh = 0;
+    p->a.paint = 1;
+    TPacket *keep = TOps::clone(p);                  // shared: uniqueify must copy
+    g_uniq_fail = 1;                                 // ... and that copy fails
+    h.push(p);
+    g_uniq_fail = 0;
+    CHECK(h.out[1].size() == 1 && h.out[0].empty() && h.runcount == 0);
+    if (h.out[1].size() == 1)
+        CHECK(h.out[1][0]->a.id == 1 && std::memcmp(TOps::data(h.out[1][0]), b.data(), b.size()) == 0);
+    CHECK(h.handler("packets") == "0");
+    TOps::kill(keep);
+    report("output_combo_clone_survives_failed_copy", ok);
+}
+
+// 3. push context: CheckIPHeader, double-buffered full batches, the deadline
 void push_check_ip()
 {
     bool ok = true;
-    Host h("CheckIPHeader", "BATCH 1000", 2);
+    Host<CheckIPC> h("CheckIPHeader", "BATCH 1000", 2);
+    h.core.set_latency(200);                           // LATENCY 200 ms: the pushes below take less
     const int n = 2500;
     std::vector<int> expect_code(n);
     std::vector<uint32_t> expect_len(n);
     for (int i = 0; i < n; i++) {
-        std::vector<uint8_t> b = udp_bytes(100, i);
-        if (i % 7 == 3) b[13] ^= 0x10;                 // bad checksum
-        if (i % 13 == 5) b[0] = 0x65;                  // version 6
-        if (i % 11 == 2) b.resize(108, 0xAB);          // trailing bytes: trimmed to ip_len
-        if (i % 29 == 7) b.resize(10);                 // tiny
+        std::vector<uint8_t> b = ip_bytes(100, i);
+        if (i % 7 == 3) b[13] ^= 0x10;
+        if (i % 13 == 5) b[0] = 0x65;
+        if (i % 11 == 2) b.resize(108, 0xAB);
+        if (i % 29 == 7) b.resize(10);
         expect_code[i] = oracle_check_ip_header(b.data(), (uint32_t)b.size(), 0, 1, nullptr, 0, nullptr, 0);
         expect_len[i] = expect_code[i] == 0 ? 100 : (uint32_t)b.size();
         h.push(make(b.data(), b.size(), i));
         if (i == 1999) {
-            // batch 1 launched at push 1000 and routed when batch 2 launched
             CHECK(h.out[0].size() + h.out[1].size() == 1000);
             CHECK(h.runcount == 1);
         }
     }
-    CHECK(h.runcount == 1 && h.scheduled(h.st[0]));
-    h.timer();                                         // the partial batch
-    CHECK(h.runcount == 0 && !h.scheduled(h.st[0]));
+    CHECK(h.runcount == 1 && h.armed() && h.wakes >= 1);
+    CHECK(h.poll());                                   // before the deadline: nothing flushed
+    CHECK(h.out[0].size() + h.out[1].size() == 2000);
+    std::this_thread::sleep_for(std::chrono::milliseconds(210));
+    CHECK(!h.poll());                                  // past it: flushed, nothing left
+    CHECK(h.runcount == 0 && !h.armed());
     CHECK(h.out[0].size() + h.out[1].size() == (size_t)n);
     long last0 = -1, last1 = -1;
     for (TPacket *p : h.out[0]) {
-        CHECK(p->id > last0 && expect_code[p->id] == 0 && p->len == expect_len[p->id]);
-        last0 = p->id;
+        CHECK(p->a.id > last0 && expect_code[p->a.id] == 0 && p->len == expect_len[p->a.id]);
+        last0 = p->a.id;
     }
     for (TPacket *p : h.out[1]) {
-        CHECK(p->id > last1 && expect_code[p->id] != 0);
-        last1 = p->id;
+        CHECK(p->a.id > last1 && expect_code[p->a.id] != 0);
+        last1 = p->a.id;
     }
     CHECK(h.handler("drops") == std::to_string(h.out[1].size()));
-    CHECK(h.msgs.size() == 1 && h.msgs[0].find("CheckIPHeader") != std::string::npos);   // the first drop only
-    report("push_check_ip_header_double_buffered_and_timer", ok);
+    CHECK(h.msgs.size() == 1 && h.msgs[0].find("CheckIPHeader") != std::string::npos);
+    report("push_check_ip_header_double_buffered_and_deadline", ok);
 }
 
-// 2. pull context: SetUDPChecksum (a/ah): output 0 pulled, output 1 pushed
+// 4. pull context, double-buffered: SetUDPChecksum (a/ah): output 0 pulled,
+//    output 1 pushed; each refill launches a batch and hands out the one before
 void pull_set_udp()
 {
     bool ok = true;
-    Host h("SetUDPChecksum", "BATCH 700", 2);
+    Host<SetC> h("SetUDPChecksum", "BATCH 700", 2);
     const int n = 3000;
     std::vector<std::vector<uint8_t> > ref(n);
     std::vector<int> code(n);
     for (int i = 0; i < n; i++) {
-        std::vector<uint8_t> b = udp_bytes(200 + (i % 5) * 300, i);
-        b[26] = b[27] = 0;                             // uh_sum zero: the Set fills it
-        if (i % 17 == 4) b[6] |= 0x20;                 // IP_MF: a fragment -> output 1
+        std::vector<uint8_t> b = ip_bytes(200 + (i % 5) * 300, i);
+        b[26] = b[27] = 0;
+        if (i % 17 == 4) b[6] |= 0x20;
         ref[i] = b;
         code[i] = oracle_set_udp_checksum(ref[i].data(), (uint32_t)b.size());
         TPacket *p = make(b.data(), b.size(), i);
@@ -343,45 +739,95 @@ void pull_set_udp()
     }
     std::vector<TPacket *> got;
     TPacket *p;
-    int refills = 0;
+    size_t max_inflight = 0;
     while ((p = h.pull()) != nullptr) {
         got.push_back(p);
-        if (h.input.empty() && refills == 0)
-            refills = 1;
         CHECK(h.runcount == 0);
+        // the packets taken from the input and not yet handed out or pushed
+        const size_t taken = (size_t)n - h.input.size();
+        const size_t done = got.size() + h.out[1].size();
+        max_inflight = std::max(max_inflight, taken - done);
     }
-    CHECK(h.pull() == nullptr);                        // the input is dry
+    CHECK(h.pull() == nullptr);
+    // double-buffered: a refill launches batch k+1 while batch k is handed out
+    CHECK(max_inflight > 700);
     size_t n0 = 0;
     long last = -1;
     for (TPacket *q : got) {
-        CHECK(q->id > last && code[q->id] == 0);
-        CHECK(q->len == ref[q->id].size() && std::memcmp(q->data(), ref[q->id].data(), q->len) == 0);
-        last = q->id;
+        CHECK(q->a.id > last && code[q->a.id] == 0);
+        CHECK(q->len == ref[q->a.id].size() && std::memcmp(TOps::data(q), ref[q->a.id].data(), q->len) == 0);
+        last = q->a.id;
         n0++;
     }
     for (TPacket *q : h.out[1])
-        CHECK(code[q->id] == 1);
+        CHECK(code[q->a.id] == 1);
     CHECK(n0 + h.out[1].size() == (size_t)n && h.out[0].empty());
     CHECK(h.handler("batches") == std::to_string((n + 699) / 700));
     for (TPacket *q : got)
-        h.kill(q);
-    report("pull_set_udp_checksum", ok);
+        TOps::kill(q);
+    report("pull_set_udp_checksum_double_buffered", ok);
 }
 
-// 3. IPFragmenter (push): fragments after their first, annotations copied
+// 5. pull through two GPU-backed elements in a row: CheckIPHeader's pull()
+//    is SetUDPChecksum's input (a Queue -> CheckIPHeader -> SetUDPChecksum ->
+//    ToDevice graph in pull mode)
+void pull_two_elements()
+{
+    bool ok = true;
+    Host<CheckIPC> a("CheckIPHeader", "BATCH 512", 2);
+    Host<SetC> b("SetUDPChecksum", "BATCH 300", 2);
+    b.upstream = [&a]() { return a.pull(); };
+    const int n = 2000;
+    std::vector<std::vector<uint8_t> > ref(n);
+    std::vector<int> ipc(n), sc(n);
+    for (int i = 0; i < n; i++) {
+        std::vector<uint8_t> x = ip_bytes(60 + (i * 37) % 1400, i);
+        if (i % 9 == 2) x[13] ^= 1;                   // bad IP checksum: CheckIPHeader's output 1
+        x[26] = x[27] = 0;
+        if (i % 23 == 5) { x[6] |= 0x20; oracle_set_ip_checksum(x.data(), (uint32_t)x.size()); }
+        ref[i] = x;
+        ipc[i] = oracle_check_ip_header(x.data(), (uint32_t)x.size(), 0, 1, nullptr, 0, nullptr, 0);
+        sc[i] = ipc[i] ? -1 : oracle_set_udp_checksum(ref[i].data(), (uint32_t)x.size());
+        TPacket *p = make(x.data(), x.size(), i);
+        a.input.push_back(p);
+    }
+    std::vector<TPacket *> got;
+    TPacket *p;
+    while ((p = b.pull()) != nullptr)
+        got.push_back(p);
+    size_t want0 = 0, want_a1 = 0, want_b1 = 0;
+    for (int i = 0; i < n; i++) {
+        want_a1 += ipc[i] != 0;
+        want0 += sc[i] == 0;
+        want_b1 += sc[i] == 1;
+    }
+    CHECK(got.size() == want0 && a.out[1].size() == want_a1 && b.out[1].size() == want_b1);
+    long last = -1;
+    for (TPacket *q : got) {
+        CHECK(q->a.id > last && sc[q->a.id] == 0);
+        CHECK(q->len == ref[q->a.id].size() && std::memcmp(TOps::data(q), ref[q->a.id].data(), q->len) == 0);
+        CHECK(q->a.dst == ld32(ref[q->a.id].data() + 16));    // CheckIPHeader's annotation came along
+        last = q->a.id;
+    }
+    for (TPacket *q : got)
+        TOps::kill(q);
+    report("pull_through_two_gpu_elements", ok);
+}
+
+// 6. IPFragmenter (push): fragments after their first, annotations copied
 void fragmenter()
 {
     bool ok = true;
-    Host h("IPFragmenter", "MTU 576, BATCH 64", 2);
+    Host<FragC> h("IPFragmenter", "MTU 576, BATCH 64", 2);
+    h.cls.mtu = 576;
     const int n = 150;
     std::vector<std::vector<uint8_t> > expect0;
     std::vector<long> expect0_id, expect1_id;
     for (int i = 0; i < n; i++) {
         const uint32_t L = i % 5 == 0 ? 400 : 1500;
-        std::vector<uint8_t> b = udp_bytes(L, 1000 + i);
-        if (i % 9 == 1) b[6] |= 0x40;                  // DF with HONOR_DF: output 1
+        std::vector<uint8_t> b = ip_bytes(L, 1000 + i);
+        if (i % 9 == 1) b[6] |= 0x40;
         if (i % 9 == 1) oracle_set_ip_checksum(b.data(), L);
-        // oracle: first fragment then the rest, in order
         std::vector<uint8_t> c = b, arena(4 * 1600);
         uint64_t pos = 0, nfrag = 0, foff[8];
         uint32_t flen[8], first = 0;
@@ -399,40 +845,47 @@ void fragmenter()
         }
         TPacket *p = make(b.data(), b.size(), i);
         p->nh = 0;
-        p->paint = (uint32_t)(i % 200);
+        p->a.paint = (uint32_t)(i % 200);
+        TPacket *keep = TOps::clone(p);              // the pushed packet is shared: uniqueify copies
         h.push(p);
+        TOps::kill(keep);
     }
     h.timer();
     CHECK(h.runcount == 0);
     CHECK(h.out[0].size() == expect0.size());
     for (size_t k = 0; k < h.out[0].size() && k < expect0.size(); k++) {
         TPacket *q = h.out[0][k];
-        CHECK(q->len == expect0[k].size() && std::memcmp(q->data(), expect0[k].data(), q->len) == 0);
-        CHECK(q->id == expect0_id[k] && q->paint == (uint32_t)(expect0_id[k] % 200));
+        CHECK(q->len == expect0[k].size() && std::memcmp(TOps::data(q), expect0[k].data(), q->len) == 0);
+        CHECK(q->a.id == expect0_id[k] && q->a.paint == (uint32_t)(expect0_id[k] % 200));
+        CHECK(TOps::network_header_offset(q) == 0);
     }
     CHECK(h.out[1].size() == expect1_id.size());
     for (size_t k = 0; k < h.out[1].size() && k < expect1_id.size(); k++)
-        CHECK(h.out[1][k]->id == expect1_id[k]);
+        CHECK(h.out[1][k]->a.id == expect1_id[k]);
     report("ip_fragmenter_extras_and_annotations", ok);
 }
 
-// 4. a failed flush, then the retry (SetUDPChecksum and the rewriting
+// 7. a failed flush, then the retry (SetUDPChecksum and the rewriting
 //    IPOutputCombo, staged -- retried from the bytes as staged)
+void set_color(OutComboC &c, uint32_t color) { c.color = color; }
+void set_color(SetC &, uint32_t) { }
+
+template <class C>
 void failed_flush_retry(const char *cls, const char *conf, int nth)
 {
     bool ok = true;
-    Host h(cls, conf, std::string(cls) == "IPOutputCombo" ? 5 : 2);
-    h.color = 1;                                       // IPOutputCombo's COLOR: no packet is painted 1
+    const bool combo = std::string(cls) == "IPOutputCombo";
+    Host<C> h(cls, conf, combo ? 5 : 2);
+    set_color(h.cls, 1);                               // COLOR 1: no packet is painted 1
     const int n = 300;
     std::vector<std::vector<uint8_t> > ref(n);
     std::vector<int> code(n);
     for (int i = 0; i < n; i++) {
-        std::vector<uint8_t> b = udp_bytes(600, 5000 + i);
+        std::vector<uint8_t> b = ip_bytes(600, 5000 + i);
         ref[i] = b;
         int prob = 0;
-        code[i] = std::string(cls) == "IPOutputCombo"
-                      ? oracle_ip_output_combo(ref[i].data(), 600, 600, 0, 0x18041A12, 1500, 0, &prob)
-                      : oracle_set_udp_checksum(ref[i].data(), 600);
+        code[i] = combo ? oracle_ip_output_combo(ref[i].data(), 600, 600, 0, MY_IP, 1500, 0, &prob)
+                        : oracle_set_udp_checksum(ref[i].data(), 600);
         TPacket *p = make(b.data(), b.size(), i);
         p->nh = 0;
         h.push(p);
@@ -440,12 +893,12 @@ void failed_flush_retry(const char *cls, const char *conf, int nth)
     clk_glue_inject_fault_internal(nth);
     h.timer();                                         // fails: nothing routed, still held
     clk_glue_inject_fault_internal(0);
-    CHECK(h.out[0].empty() && h.runcount == 1 && h.scheduled(h.st[0]));
+    CHECK(h.out[0].empty() && h.runcount == 1 && h.armed());
     CHECK(!h.chat.empty() && h.chat.back().find("retry") != std::string::npos);
     h.timer();                                         // the retry
     CHECK(h.runcount == 0 && h.out[0].size() == (size_t)n);
     for (TPacket *q : h.out[0])
-        CHECK(code[q->id] == 0 && std::memcmp(q->data(), ref[q->id].data(), 600) == 0);
+        CHECK(code[q->a.id] == 0 && std::memcmp(TOps::data(q), ref[q->a.id].data(), 600) == 0);
     char name[128];
     if (nth < 0)
         std::snprintf(name, sizeof name, "failed_flush_then_retry_%s_completion", cls);
@@ -454,32 +907,31 @@ void failed_flush_retry(const char *cls, const char *conf, int nth)
     report(name, ok);
 }
 
-// 5. the retry limit: abandon, every held packet killed, runcount released
+// 8. the retry limit: abandon, every held packet killed, runcount released
 void retry_limit()
 {
     bool ok = true;
-    Host h("SetUDPChecksum", "", 2);
+    Host<SetC> h("SetUDPChecksum", "", 2);
     h.core.set_max_retries(3);
     const int n = 200;
     for (int i = 0; i < n; i++) {
-        std::vector<uint8_t> b = udp_bytes(300, i);
+        std::vector<uint8_t> b = ip_bytes(300, i);
         TPacket *p = make(b.data(), b.size(), i);
         p->nh = 0;
         h.push(p);
     }
-    const long k0 = h.kills;
+    const long k0 = g_kills;
     for (int k = 0; k < 3; k++) {
         CHECK(h.runcount == 1);
         clk_glue_inject_fault_internal(1);
         h.timer();
     }
     clk_glue_inject_fault_internal(0);
-    CHECK(h.runcount == 0 && !h.scheduled(h.st[0]));
-    CHECK(h.kills - k0 == n && h.out[0].empty() && h.out[1].empty());
+    CHECK(h.runcount == 0 && !h.armed());
+    CHECK(g_kills - k0 == n && h.out[0].empty() && h.out[1].empty());
     CHECK(h.handler("lost") == std::to_string(n));
     CHECK(!h.chat.empty() && h.chat.back().find("packets killed") != std::string::npos);
-    // the element works again afterwards
-    std::vector<uint8_t> b = udp_bytes(300, 7);
+    std::vector<uint8_t> b = ip_bytes(300, 7);
     TPacket *p = make(b.data(), b.size(), 7);
     p->nh = 0;
     h.push(p);
@@ -488,33 +940,34 @@ void retry_limit()
     report("retry_limit_abandons_and_releases_runcount", ok);
 }
 
-// 6. a downstream element pushing back into this one while it delivers
+// 9. a downstream element pushing back into this one while it delivers
 void reentrant_push()
 {
     bool ok = true;
-    Host h("CheckIPHeader", "BATCH 64", 2);
-    h.on_out0 = [](Host &hh, TPacket *p) {
-        if (p->id < 40) {                              // a copy of it, pushed back in on the same thread
-            TPacket *q = clone(p);
-            q->id = p->id + 100000;
+    Host<CheckIPC> h("CheckIPHeader", "BATCH 64", 2);
+    h.on_out0 = [](Host<CheckIPC> &hh, TPacket *p) {
+        if (p->a.id < 40) {
+            TPacket *q = TOps::clone(p);
+            q->buf = std::make_shared<std::vector<uint8_t> >(*p->buf);
+            q->a.id = p->a.id + 100000;
             hh.push(q);
         }
     };
     const int n = 300;
     for (int i = 0; i < n; i++) {
-        std::vector<uint8_t> b = udp_bytes(80, i);
+        std::vector<uint8_t> b = ip_bytes(80, i);
         h.push(make(b.data(), b.size(), i));
     }
     h.timer();
-    h.timer();                                         // the copies staged by the last delivery
+    h.timer();
     CHECK(h.runcount == 0);
     CHECK(h.out[0].size() == (size_t)n + 40);
     std::vector<long> pos(n + 100000 + 40, -1);
     for (size_t k = 0; k < h.out[0].size(); k++)
-        pos[(size_t)h.out[0][k]->id] = (long)k;
+        pos[(size_t)h.out[0][k]->a.id] = (long)k;
     long last = -1;
     for (int i = 0; i < n; i++) {
-        CHECK(pos[(size_t)i] > last);                 // originals in order
+        CHECK(pos[(size_t)i] > last);
         last = pos[(size_t)i];
     }
     for (int i = 0; i < 40; i++)
@@ -522,60 +975,66 @@ void reentrant_push()
     report("reentrant_push_from_downstream", ok);
 }
 
-// 7. four pushing threads (a state each) while the home thread fires timers
+// 10. four pushing threads, each with its own state whose deadline it polls
+//     itself (the Click adapter's per-RouterThread Task): every packet is
+//     delivered on the thread that pushed it, in push order
 void threads()
 {
     bool ok = true;
     const int T = 4, n = 20000;
-    Host h("CheckIPHeader", "BATCH 4096", 2, T);
-    std::atomic<int> done{0};
+    Host<CheckIPC> h("CheckIPHeader", "BATCH 4096", 2, T);
     std::vector<std::thread> th;
+    std::vector<std::thread::id> tid(T);
     for (int t = 0; t < T; t++)
-        th.emplace_back([&h, &done, t]() {
+        th.emplace_back([&h, &tid, t]() {
+            tid[(size_t)t] = std::this_thread::get_id();
             for (int i = 0; i < n; i++) {
-                std::vector<uint8_t> b = udp_bytes(64, (long)t * n + i);
+                std::vector<uint8_t> b = ip_bytes(64, (long)t * n + i);
                 if (i % 97 == 0) b[12] ^= 1;
                 h.push(make(b.data(), b.size(), (long)t * n + i), t);
+                if (i % 512 == 0)
+                    h.poll(t);                         // the thread's Task between pushes
             }
-            done++;
+            while (h.poll(t))                          // the Task until the deadline flushes the rest
+                std::this_thread::sleep_for(std::chrono::microseconds(200));
         });
-    while (done < T)
-        for (int t = 0; t < T; t++)
-            h.timer(t);                                // the home thread's latency timers
     for (std::thread &x : th)
         x.join();
-    for (int t = 0; t < T; t++)
-        h.timer(t);
     CHECK(h.runcount == 0);
     std::vector<long> last(T, -1);
-    size_t bad = 0;
-    for (TPacket *p : h.out[0]) {
-        const int t = (int)(p->id / n);
-        CHECK(p->id > last[(size_t)t] && (p->id % n) % 97 != 0);
-        last[(size_t)t] = p->id;
-    }
-    for (TPacket *p : h.out[1])
-        bad += (p->id % n) % 97 == 0;
+    size_t bad = 0, wrong_thread = 0;
+    for (int port = 0; port < 2; port++)
+        for (size_t k = 0; k < h.out[(size_t)port].size(); k++) {
+            TPacket *p = h.out[(size_t)port][k];
+            const int t = (int)(p->a.id / n);
+            wrong_thread += h.out_thread[(size_t)port][k] != tid[(size_t)t];
+            if (port == 0) {
+                CHECK(p->a.id > last[(size_t)t] && (p->a.id % n) % 97 != 0);
+                last[(size_t)t] = p->a.id;
+            } else
+                bad += (p->a.id % n) % 97 == 0;
+        }
+    CHECK(wrong_thread == 0);
     CHECK(h.out[0].size() + h.out[1].size() == (size_t)T * n && bad == h.out[1].size());
-    report("four_threads_with_home_thread_timers", ok);
+    report("four_threads_each_delivered_on_its_own_thread", ok);
 }
 
-// 8. cleanup of a held partial batch: everything killed, nothing pushed
+// 11. cleanup of a held partial batch: everything killed, nothing pushed
 void cleanup_partial()
 {
     bool ok = true;
-    const long live0 = g_live;
+    const long live0 = g_live, k0 = g_kills;
     {
-        Host h("SetUDPChecksum", "", 2);
+        Host<SetC> h("SetUDPChecksum", "", 2);
         for (int i = 0; i < 500; i++) {
-            std::vector<uint8_t> b = udp_bytes(300, i);
+            std::vector<uint8_t> b = ip_bytes(300, i);
             TPacket *p = make(b.data(), b.size(), i);
             p->nh = 0;
             h.push(p);
         }
         CHECK(h.runcount == 1);
         h.core.cleanup(h, h.st[0]);
-        CHECK(h.runcount == 0 && h.out[0].empty() && h.out[1].empty() && h.kills == 500);
+        CHECK(h.runcount == 0 && h.out[0].empty() && h.out[1].empty() && g_kills - k0 == 500 && !h.armed());
     }
     CHECK(g_live == live0);
     report("cleanup_kills_held_packets_pushes_nothing", ok);
@@ -589,16 +1048,19 @@ int main()
         std::printf("SKIP no gfx950 GPU\n");
         return 0;
     }
+    every_class();
+    output_combo_copy_fails();
     push_check_ip();
     pull_set_udp();
+    pull_two_elements();
     fragmenter();
     // the n-th checked HIP call of the first flush fails: the packets H2D
     // (4), a verdict D2H (SetUDPChecksum 9, IPOutputCombo 10), the packets
     // back D2H (IPOutputCombo 11); -1: the completion wait
     for (int nth : {4, 9, -1})
-        failed_flush_retry("SetUDPChecksum", "", nth);
+        failed_flush_retry<SetC>("SetUDPChecksum", "", nth);
     for (int nth : {4, 10, 11, -1})
-        failed_flush_retry("IPOutputCombo", "1, 18.26.4.24, 1500", nth);
+        failed_flush_retry<OutComboC>("IPOutputCombo", "1, 18.26.4.24, 1500", nth);
     retry_limit();
     reentrant_push();
     threads();

@@ -145,7 +145,7 @@ def test_click_adapters_use_only_the_public_abi():
     hip = os.path.join(root, "click_integration", "elements", "hip")
     used = set()
     for f in os.listdir(hip):
-        text = re.sub(r"//.*|/\*.*?\*/", "", open(os.path.join(hip, f)).read(), flags=re.S)
+        text = re.sub(r"//[^\n]*", "", re.sub(r"/\*.*?\*/", "", open(os.path.join(hip, f)).read(), flags=re.S))
         used |= set(re.findall(r"\b(clk_\w+)\s*\(", text)) | set(re.findall(r"\b(CLK_\w+)\b", text))
     assert used and used <= declared, sorted(used - declared)
     dropin = open(os.path.join(hip, "hipdropin.cc")).read()

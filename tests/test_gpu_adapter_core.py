@@ -1,12 +1,16 @@
-"""The Click adapter's core (click_integration/elements/hip/hipcore.hh),
-Click-independent, driven on the GPU by tests/native/hipcore_test.cc with
-its own packet type, lock and host, every output checked against the CPU
-oracle: push context (double-buffered batches, latency timer, runcount),
-pull context (the reference classes are agnostic: PROCESSING_A_AH,
-checkipheader.hh:114), IPFragmenter extras, a failed flush and its retry
-(including the rewriting IPOutputCombo with the completion wait failing),
-the retry limit, a downstream element re-entering the element, four
-threads with home-thread timers, and cleanup of a held batch.
+"""The Click adapter's core (click_integration/elements/hip/hipcore.hh) and
+every element class's shipped logic (hipclasses.hh: what the reference
+element does around its checksum -- trims, Strip, annotations, uniqueify,
+the PaintTee clone, the first-fragment clone), Click-independent, driven on
+the GPU by tests/native/hipcore_test.cc with its own packet type (shared
+buffers, annotation area), lock and host; every output checked against the
+CPU oracle: each of the 14 classes over fuzzed packets, push context
+(double-buffered batches, latency deadline, runcount), pull context
+double-buffered and through two GPU-backed elements in a row (the reference
+classes are agnostic: PROCESSING_A_AH, checkipheader.hh:114), IPFragmenter
+extras, IPOutputCombo's clone when the copy fails, a failed flush and its
+retry, the retry limit, a downstream element re-entering the element, four
+threads each delivered on its own thread, and cleanup of a held batch.
 The binary is built on the CPU by click_amd.build.build_native_tests()
 (__graft_entry__.build())."""
 import os
@@ -17,12 +21,15 @@ import pytest
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "native", "bin", "hipcore_test")
-SCENARIOS = ["push_check_ip_header_double_buffered_and_timer", "pull_set_udp_checksum",
-             "ip_fragmenter_extras_and_annotations", "failed_flush_then_retry_SetUDPChecksum_fault4",
-             "failed_flush_then_retry_SetUDPChecksum_completion", "failed_flush_then_retry_IPOutputCombo_fault11",
-             "failed_flush_then_retry_IPOutputCombo_completion", "retry_limit_abandons_and_releases_runcount",
-             "reentrant_push_from_downstream", "four_threads_with_home_thread_timers",
-             "cleanup_kills_held_packets_pushes_nothing"]
+CLASSES = ["CheckIPHeader", "CheckIPHeader2", "IPInputCombo", "CheckUDPHeader", "CheckTCPHeader", "CheckICMPHeader",
+           "SetIPChecksum", "SetUDPChecksum", "SetTCPChecksum", "DecIPTTL", "IPGWOptions", "FixIPSrc", "IPOutputCombo"]
+SCENARIOS = ["class_" + c for c in CLASSES] + [
+    "output_combo_clone_survives_failed_copy", "push_check_ip_header_double_buffered_and_deadline",
+    "pull_set_udp_checksum_double_buffered", "pull_through_two_gpu_elements", "ip_fragmenter_extras_and_annotations",
+    "failed_flush_then_retry_SetUDPChecksum_fault4", "failed_flush_then_retry_SetUDPChecksum_completion",
+    "failed_flush_then_retry_IPOutputCombo_fault11", "failed_flush_then_retry_IPOutputCombo_completion",
+    "retry_limit_abandons_and_releases_runcount", "reentrant_push_from_downstream",
+    "four_threads_each_delivered_on_its_own_thread", "cleanup_kills_held_packets_pushes_nothing"]
 
 
 def test_adapter_core_on_gpu():

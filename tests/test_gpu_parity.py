@@ -457,6 +457,30 @@ def test_stream_high_address_bits(torch, low):
     del hp
 
 
+def test_stream_descriptor_past_max_len(torch):
+    """A len[] entry longer than the batch's max_len (a caller's contract
+    slip) and longer than the packet stream's 16 MiB chunk-index bound: the
+    run holding it sums each packet from memory (no chunk index wraps), and
+    every result still equals the oracle's over the true lengths."""
+    import click_amd
+    c = click_amd.Context(0).tune(stream_min=1)
+    rng = np.random.default_rng(17)
+    for proto in (17, 6):
+        arena, off, caplen, ml = fuzz.make_batch(rng, 300, proto, max_total=1600)
+        big = (1 << 24) + 4096 + 3
+        tail = int(off.max()) + int(caplen.max()) + 64
+        big_pkt = np.frombuffer(fuzz.build(rng, proto, 1400), np.uint8)
+        arena = np.concatenate([arena[:tail], np.zeros(tail + big + 64 - arena[:tail].size, np.uint8)])
+        arena[tail:tail + big_pkt.size] = big_pkt
+        off = off.copy()
+        caplen = caplen.copy()
+        off[150], caplen[150] = tail, big       # 1400 B of IP packet, then zeros to 16 MiB + 4 KiB
+        oracle_lib.batch("set_ip", arena, len(off), off=off, length=caplen)
+        for op in ("in_cksum",) + OPS_L4[proto]:
+            compare(torch, c, op, arena, len(off), off=off, length=caplen, max_len=ml, arg=1)
+    c.close()
+
+
 def test_tune_rejects_bad_values(torch):
     import click_amd
     c = click_amd.Context(0)
