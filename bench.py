@@ -26,6 +26,7 @@ cpu_baseline: the oracle restatement of lib/in_cksum.c + the element (-O2 -g)
 on the host cores, on a bounded sample of the same workload.
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -863,6 +864,44 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
                      "mpps": round(n / dt / 1e6, 2),
                      "per_element_ms": {c[0]: {"push": round(a * 1e3, 2), "flush": round(b * 1e3, 2),
                                                "results": round(r * 1e3, 2)} for c, (a, b, r) in zip(chain, parts)}}
+    # the same chains on one device-resident batch (clk_chain_*: one gather,
+    # one H2D, each member's kernel over what the members before it passed,
+    # one D2H, one routing pass per packet)
+    from click_amd.elements import Chain
+    cbufs = [np.empty(n + 1, t) for t in (np.uint64, np.int32, np.int32, np.uint32, np.uint32)]
+    cptrs = [b.ctypes.data_as(ctypes.c_void_p) for b in cbufs]
+    for name, chain in C1_CHAINS.items():
+        els = [Element(ctx, cls, ", ".join(x for x in (conf, "BATCH %d" % batch) if x), noutputs=nout)
+               for cls, conf, nout in chain]
+        ch = Chain(els)
+        for timed in (False, True):
+            raw = np.empty(n * len(frame) + 8192, np.uint8)
+            arena = raw[(-raw.ctypes.data) % 4096:][:n * len(frame)]
+            arena[:] = np.tile(np.frombuffer(frame, np.uint8), n)
+            ptrs = np.uint64(arena.ctypes.data) + np.arange(n, dtype=np.uint64) * np.uint64(len(frame))
+            lens = np.full(n, len(frame), np.uint32)
+            t0 = time.perf_counter()
+            ch.push_burst(ptrs, lens, None, first_token=0)
+            tb = time.perf_counter()
+            ch.flush()
+            tc = time.perf_counter()
+            k = int(ch.lib.clk_chain_results(ch.h, *cptrs, n + 1))
+            dt = time.perf_counter() - t0
+            fwd = int(((cbufs[1][:k] == len(chain) - 1) & (cbufs[2][:k] == 0)).sum())
+        st = (ctypes.c_double * 8)()
+        ch.lib.clk_chain_stats(ch.h, ctypes.cast(st, ctypes.c_void_p), 8)
+        ch.close()
+        for e in els:
+            e.close()
+        arenas[name + "_chain"] = arena
+        out[name + "_chain"] = {"chain": [c[0] for c in chain], "forwarded": fwd, "wall_s": round(dt, 4),
+                                "mpps": round(n / dt / 1e6, 2),
+                                "ms": {"push": round((tb - t0) * 1e3, 2), "flush": round((tc - tb) * 1e3, 2),
+                                       "results": round((t0 + dt - tc) * 1e3, 2)},
+                                # host ns per packet by phase, both runs (warm-up + timed)
+                                "ns_per_packet": {k: round(v * 1e9 / (2 * n), 1) for k, v in zip(
+                                    ("stage", "descriptors", "gpu_round_trips", "next_views", "h2d", "d2h_back",
+                                     "route", "copy_back"), list(st))}}
     same = all(np.array_equal(arenas["elements"], arenas[k]) for k in arenas)
     return {"workload": "C1: conf/fake-iprouter.click forwarding path, %d x %d B frames, element glue on the GPU "
                         "(staged: push() gathers into pinned staging; _zerocopy: registered host arena)"

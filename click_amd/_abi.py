@@ -172,6 +172,14 @@ SIGNATURES = {
     "clk_element_share_messages": (ctypes.c_int, [_P, _P]),
     "clk_element_read_handler": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
     "clk_element_take_messages": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),
+    "clk_chain_create": (ctypes.c_int, [_P, ctypes.c_int, _P]),
+    "clk_chain_destroy": (ctypes.c_int, [_P]),
+    "clk_chain_last_error": (ctypes.c_char_p, [_P]),
+    "clk_chain_push_anno": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64]),
+    "clk_chain_push_burst": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_uint64, ctypes.c_uint32]),
+    "clk_chain_flush": (ctypes.c_int, [_P]),
+    "clk_chain_results": (ctypes.c_uint64, [_P, _P, _P, _P, _P, _P, ctypes.c_uint64]),
+    "clk_chain_stats": (ctypes.c_int, [_P, _P, ctypes.c_int]),
 }
 
 _lib = None

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "click_amd")
 LIB = os.path.join(PKG, "libclick_amd_cksum.so")
 SOURCES = [os.path.join(PKG, "csrc", "cksum_api.hip"), os.path.join(PKG, "host", "elements.cc"),
-           os.path.join(PKG, "host", "ingest.cc")]
+           os.path.join(PKG, "host", "chain.cc"), os.path.join(PKG, "host", "ingest.cc")]
 DEPS = SOURCES + [os.path.join(PKG, "csrc", f) for f in ("cksum_kernels.hh", "cksum_device.hh", "frag_kernels.hh",
                                                                     "internal.hh")] + [
     os.path.join(PKG, "host", "elements.hh")] + [

@@ -178,3 +178,78 @@ class Element:
         buf = ctypes.create_string_buffer(1 << 20)
         self.lib.clk_element_take_messages(self.h, buf, len(buf))
         return [m for m in buf.value.decode().split("\n") if m]
+
+
+class Chain:
+    """Consecutive elements on one device-resident batch (clk_chain_*):
+    members[k+1] takes members[k]'s output 0.  Each packet is staged once,
+    each member's kernel runs over what the members before it passed, and
+    each packet is routed once; results name the member they leave.
+
+        ch = Chain([Element(ctx, "CheckIPHeader", "OFFSET 14", noutputs=2),
+                    Element(ctx, "DecIPTTL", "", noutputs=2)])
+        ch.push_burst(ptrs, lengths, nh_offsets)
+        ch.flush()
+        tok, member, port, length, aux = ch.results()
+    """
+
+    def __init__(self, members):
+        self.members = list(members)
+        self.lib = self.members[0].lib
+        arr = (ctypes.c_void_p * len(self.members))(*[m.h.value for m in self.members])
+        h = ctypes.c_void_p()
+        rc = self.lib.clk_chain_create(ctypes.cast(arr, ctypes.c_void_p), len(self.members), ctypes.byref(h))
+        if rc != 0:
+            err = ClickAmdError((self.lib.clk_last_error(None) or b"").decode())
+            err.rc = rc
+            raise err
+        self.h = h
+
+    def last_error(self):
+        return (self.lib.clk_chain_last_error(self.h) or b"").decode()
+
+    def push_anno(self, ptr, length, nh_offset=-1, anno=0, token=0):
+        rc = self.lib.clk_chain_push_anno(self.h, ctypes.c_void_p(ptr), length, nh_offset, anno, token)
+        if rc < 0:
+            raise ClickAmdError("push failed: %d (%s)" % (rc, self.last_error()))
+        return rc == 1
+
+    def push_burst(self, ptrs, lengths, nh_offsets=None, first_token=0):
+        ptrs = np.ascontiguousarray(ptrs, np.uint64)
+        lengths = np.ascontiguousarray(lengths, np.uint32)
+        nh = None if nh_offsets is None else np.ascontiguousarray(nh_offsets, np.int32)
+        rc = self.lib.clk_chain_push_burst(self.h, ptrs.ctypes.data_as(ctypes.c_void_p),
+                                           lengths.ctypes.data_as(ctypes.c_void_p),
+                                           None if nh is None else nh.ctypes.data_as(ctypes.c_void_p),
+                                           first_token, len(ptrs))
+        if rc != 0:
+            raise ClickAmdError("push_burst failed: %d (%s)" % (rc, self.last_error()))
+
+    def flush(self):
+        rc = self.lib.clk_chain_flush(self.h)
+        if rc != 0:
+            err = ClickAmdError("flush failed: %d (%s)" % (rc, self.last_error()))
+            err.rc = rc
+            raise err
+
+    def results(self, cap=1 << 20):
+        """(tokens, members, ports, lengths, aux) of every routed result, in order."""
+        out = []
+        while True:
+            a = [np.empty(cap, t) for t in (np.uint64, np.int32, np.int32, np.uint32, np.uint32)]
+            n = self.lib.clk_chain_results(self.h, *[x.ctypes.data_as(ctypes.c_void_p) for x in a], cap)
+            out.append([x[:n] for x in a])
+            if n < cap:
+                break
+        return tuple(np.concatenate([o[k] for o in out]) for k in range(5))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.clk_chain_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

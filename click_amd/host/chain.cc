@@ -1,0 +1,543 @@
+// chain.cc -- consecutive GPU-backed elements on one device-resident batch.
+//
+// In the reference, an element's output 0 pushes straight into the next
+// element (element.cc:2891-2972), and click-xform fuses common chains into
+// combo elements so the per-element cost is paid once (ipinputcombo.cc:66-140,
+// ipoutputcombo.cc:44-205).  Here a chain of glue elements in one thread --
+// member k+1 connected to member k's output 0 -- shares one staged batch:
+//   push     each packet's bytes are gathered once (the most any member reads);
+//   flush    one H2D of the batch; member k's kernel runs over the packets
+//            members 0..k-1 passed on output 0 (its descriptors built on the
+//            host from the members' verdicts, BatchElement::passes()); one D2H
+//            of the rewritten bytes; then each packet is routed once, through
+//            each member's own route() in order (counters, handlers, chatter
+//            exactly as if the member had run it alone), and leaves the chain
+//            at the member and output where the reference would push it.
+// A flush that fails at any step routes nothing: the batch stays staged and
+// the next flush runs it again from the bytes as staged.
+#include "elements.hh"
+#include "../../include/click_amd_elements.h"
+#include "../csrc/internal.hh"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cstring>
+#include <new>
+
+namespace clk {
+namespace host {
+
+static inline double now_s()
+{
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void stage_copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail);
+
+template <typename T>
+static int pinned_grow(T **p, size_t *cap, size_t need, size_t keep)
+{
+    if (*cap >= need)
+        return 0;
+    const size_t c = std::max(need, *cap * 2);
+    void *q = nullptr;
+    if (hipHostMalloc(&q, c * sizeof(T), hipHostMallocDefault) != hipSuccess)
+        return -1;
+    if (*p && keep)
+        std::memcpy(q, *p, keep * sizeof(T));
+    if (*p)
+        (void)hipHostFree(*p);
+    *p = (T *)q;
+    *cap = c;
+    return 0;
+}
+
+Chain::~Chain()
+{
+    if (init_)
+        (void)clk_ctx_sync(m_[0]->ctx_);
+    for (void *q : {(void *)h_arena_, (void *)h_back_})
+        if (q)
+            (void)hipHostFree(q);
+    if (d_arena_)
+        (void)hipFree(d_arena_);
+    for (Member &M : mm_) {
+        for (void *q : {(void *)M.h_off, (void *)M.h_len, (void *)M.h_codes, (void *)M.h_anno, (void *)M.h_aux8,
+                        (void *)M.h_sums})
+            if (q)
+                (void)hipHostFree(q);
+        for (void *q : {(void *)M.d_off, (void *)M.d_len, (void *)M.d_codes, (void *)M.d_anno, (void *)M.d_aux8,
+                        (void *)M.d_sums})
+            if (q)
+                (void)hipFree(q);
+        for (void *e : M.ev)
+            if (e)
+                (void)hipEventDestroy((hipEvent_t)e);
+    }
+}
+
+int Chain::check(std::string *err) const
+{
+    if (m_.empty()) {
+        *err = "a chain needs at least one element";
+        return CLK_EINVAL;
+    }
+    for (size_t k = 0; k < m_.size(); k++) {
+        const BatchElement *e = m_[k];
+        if (e->ctx_ != m_[0]->ctx_) {
+            *err = e->name() + ": chain members must share one context (stream)";
+            return CLK_EINVAL;
+        }
+        if (e->zerocopy_) {
+            *err = e->name() + ": ZEROCOPY elements do not join a chain";
+            return CLK_EINVAL;
+        }
+        if (e->has_post_route_ && k + 1 != m_.size()) {
+            *err = e->name() + ": " + e->class_name() + " must be the last element of a chain";
+            return CLK_EINVAL;
+        }
+    }
+    return CLK_SUCCESS;
+}
+
+// The bytes from data() any member's kernel can read of a packet pushed with
+// network header nh: the largest chain_extent() over the members, following
+// the view (Strip, network header) from member to member.  ~0u: all.
+uint32_t Chain::extent(int32_t nh, uint32_t length)
+{
+    if (nh == ext_nh_ && length == ext_len_)
+        return ext_;
+    uint64_t need = 0, wneed = 0, shift = 0;
+    int32_t v = nh;
+    for (const BatchElement *e : m_) {
+        if (shift > length)
+            break;
+        const uint32_t x = e->chain_extent(v, length - (uint32_t)shift);
+        const uint32_t wx = e->chain_write_extent(v, length - (uint32_t)shift);
+        need = x == 0xFFFFFFFFu ? (uint64_t)0xFFFFFFFFu : std::max<uint64_t>(need, shift + x);
+        wneed = wx == 0xFFFFFFFFu ? (uint64_t)0xFFFFFFFFu : std::max<uint64_t>(wneed, wx ? shift + wx : 0);
+        shift += e->strip();
+        if (e->nh_after() != -2)
+            v = e->nh_after();
+    }
+    ext_nh_ = nh;
+    ext_len_ = length;
+    ext_ = (uint32_t)std::min<uint64_t>(need, 0xFFFFFFFFu);
+    wext_ = (uint32_t)std::min<uint64_t>(wneed, 0xFFFFFFFFu);
+    return ext_;
+}
+
+int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
+{
+    if (!init_) {
+        init_ = true;
+        mm_.resize(m_.size());
+    }
+    if (resume_ >= 0) {
+        err_ = "the chain's failed flush must be retried (or the packets abandoned) first";
+        return CLK_EINVAL;
+    }
+    const uint32_t need = std::min(length, extent(nh_offset, length));
+    const size_t slot = (used_ + 15) & ~size_t(15);
+    if (slot + need + 64 > h_cap_ && pinned_grow(&h_arena_, &h_cap_, std::max(slot + need + 64, size_t(1) << 20), used_)) {
+        err_ = "out of pinned host memory";
+        return CLK_EINVAL;
+    }
+    stage_copy_bytes(h_arena_ + slot, data, need, length);
+    views0_.push_back(ChainView{data, token, slot, length, nh_offset, (uint16_t)anno});
+    staged_.push_back(need);
+    back_.push_back(std::min(need, wext_));
+    used_ = slot + need;
+    return views0_.size() >= m_[0]->batch_cap_ ? 1 : 0;
+}
+
+int Chain::push_burst(uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets, uint64_t first_token,
+                      uint32_t n)
+{
+    double t0 = now_s();
+    for (uint32_t k = 0; k < n; k++) {
+        int r = push(datas[k], lengths[k], nh_offsets ? nh_offsets[k] : -1, first_token + k, 0);
+        if (r < 0)
+            return r;
+        if (r == 1) {
+            stats_[0] += now_s() - t0;
+            if ((r = flush()) != 0)
+                return r;
+            t0 = now_s();
+        }
+    }
+    stats_[0] += now_s() - t0;
+    return CLK_SUCCESS;
+}
+
+int Chain::grow(size_t bytes, size_t n)
+{
+    if (d_cap_ < bytes) {
+        if (d_arena_)
+            (void)hipFree(d_arena_);
+        d_arena_ = nullptr;
+        const size_t c = std::max(bytes, d_cap_ * 2);
+        if (hipMalloc(&d_arena_, c) != hipSuccess)
+            return -1;
+        d_cap_ = c;
+    }
+    for (Member &M : mm_) {
+        for (void *&e : M.ev)
+            if (!e) {
+                hipEvent_t h = nullptr;
+                if (hipEventCreate(&h) != hipSuccess)
+                    return -1;
+                e = (void *)h;
+            }
+        if (M.cap >= n)
+            continue;
+        const size_t c = std::max(n, M.cap * 2);
+        size_t c1 = M.cap, c2 = M.cap, c3 = M.cap, c4 = M.cap, c5 = M.cap, c6 = M.cap;
+        if (pinned_grow(&M.h_off, &c1, c, 0) || pinned_grow(&M.h_len, &c2, c, 0) ||
+            pinned_grow(&M.h_codes, &c3, c, 0) || pinned_grow(&M.h_anno, &c4, c, 0) ||
+            pinned_grow(&M.h_aux8, &c5, c, 0) || pinned_grow(&M.h_sums, &c6, c, 0))
+            return -1;
+        for (void *q : {(void *)M.d_off, (void *)M.d_len, (void *)M.d_codes, (void *)M.d_anno, (void *)M.d_aux8,
+                        (void *)M.d_sums})
+            if (q)
+                (void)hipFree(q);
+        M.d_off = nullptr, M.d_len = nullptr, M.d_codes = nullptr, M.d_anno = nullptr, M.d_aux8 = nullptr;
+        M.d_sums = nullptr;
+        if (hipMalloc(&M.d_off, c * 8) != hipSuccess || hipMalloc(&M.d_len, c * 4) != hipSuccess ||
+            hipMalloc(&M.d_codes, c) != hipSuccess || hipMalloc(&M.d_anno, c) != hipSuccess ||
+            hipMalloc(&M.d_aux8, c) != hipSuccess || hipMalloc(&M.d_sums, c * 2) != hipSuccess)
+            return -1;
+        M.cap = c;
+    }
+    return 0;
+}
+
+// Member k over the packets that reach it (alive_): its descriptors
+// (chain_build: the class's span()), its kernel, its verdicts back, then its
+// routing (chain_route: the class's route()): output 0 goes on to member k+1
+// with the view the member's output has (strip(), nh_after(), the result's
+// length), anything else leaves the chain at member k.
+// *launched: the member's kernels were queued (a failure after that leaves
+// the device bytes rewritten by them).
+int Chain::run_member(size_t k, bool *launched)
+{
+    BatchElement *e = m_[k];
+    Member &M = mm_[k];
+    ChainWork &w = M.w;
+    hipStream_t s = (hipStream_t)clk_ctx_stream(e->ctx_);
+    w.views = &views_;
+    w.reached.assign(alive_.begin(), alive_.end());
+    w.next = &next_;
+    w.h_off = M.h_off, w.h_len = M.h_len, w.h_anno = M.h_anno;
+    w.h_codes = M.h_codes, w.h_sums = M.h_sums;
+    w.member = (int)k;
+    w.last = k + 1 == m_.size();
+    w.out = &out_;
+    w.done = &done_;
+    e->in_place_ = true;                             // the chain writes the packets back itself
+    double t0 = now_s();
+    e->chain_build(w);
+    e->in_place_ = false;
+    stats_[1] += now_s() - t0;
+    t0 = now_s();
+    M.ms = 0;
+    if (w.n) {
+        const size_t n = w.n;
+        hipError_t er;
+        if ((er = glue_checked(hipMemcpyAsync(M.d_off, M.h_off, n * 8, hipMemcpyHostToDevice, s))) != hipSuccess ||
+            (er = glue_checked(hipMemcpyAsync(M.d_len, M.h_len, n * 4, hipMemcpyHostToDevice, s))) != hipSuccess ||
+            (e->wants_anno() &&
+             (er = glue_checked(hipMemcpyAsync(M.d_anno, M.h_anno, n, hipMemcpyHostToDevice, s))) != hipSuccess)) {
+            err_ = e->name() + ": hipMemcpyAsync(descriptors): " + hipGetErrorString(er);
+            return CLK_EHIP;
+        }
+        (void)hipEventRecord((hipEvent_t)M.ev[0], s);
+        clk_batch b;
+        b.base = d_arena_;
+        b.off = M.d_off;
+        b.stride = 0;
+        b.len = M.d_len;
+        b.fixed_len = 0;
+        b.max_len = w.maxlen;
+        b.n = n;
+        e->d_anno_ = M.d_anno;
+        e->d_aux8_ = M.d_aux8;
+        e->err_.clear();
+        *launched = true;
+        int r = e->run(&b, M.d_codes, M.d_sums);
+        er = hipSuccess;
+        if (r == 0) {
+            (void)hipEventRecord((hipEvent_t)M.ev[1], s);
+            if ((er = glue_checked(hipMemcpyAsync(M.h_codes, M.d_codes, n, hipMemcpyDeviceToHost, s))) != hipSuccess ||
+                (e->wants_sums() &&
+                 (er = glue_checked(hipMemcpyAsync(M.h_sums, M.d_sums, n * 2, hipMemcpyDeviceToHost, s))) != hipSuccess) ||
+                (e->wants_arena_back() &&
+                 (er = glue_checked(hipMemcpyAsync(M.h_aux8, M.d_aux8, n, hipMemcpyDeviceToHost, s))) != hipSuccess) ||
+                (er = glue_checked(hipStreamSynchronize(s))) != hipSuccess)
+                r = CLK_EHIP;
+        }
+        if (r) {
+            (void)hipStreamSynchronize(s);
+            err_ = e->name() + ": " + (!e->err_.empty() ? e->err_
+                                        : er != hipSuccess ? std::string(hipGetErrorString(er))
+                                                           : std::string(clk_last_error(e->ctx_)));
+            return r;
+        }
+        (void)hipEventElapsedTime(&M.ms, (hipEvent_t)M.ev[0], (hipEvent_t)M.ev[1]);
+        if ((r = e->verify(M.h_codes, n)) != 0) {
+            err_ = e->name() + ": " + e->err_;
+            return r;
+        }
+    }
+    stats_[2] += now_s() - t0;
+    // route now (the next member's input is what this one passed)
+    t0 = now_s();
+    e->in_place_ = true;                             // the chain writes the packets back itself
+    e->h_aux8_ = M.h_aux8;
+    if (w.n) {
+        e->batches_++;
+        e->gpu_ns_ += (uint64_t)(M.ms * 1e6);
+    }
+    e->chain_route(w);
+    e->in_place_ = false;
+    if (!carry_.empty()) {                           // resumed: the packets it passed before it failed come first
+        next_.insert(next_.begin(), carry_.begin(), carry_.end());
+        carry_.clear();
+    }
+    alive_.swap(next_);
+    stats_[6] += now_s() - t0;
+    return CLK_SUCCESS;
+}
+
+// The rewritten bytes into the packets that have left the chain (all: every
+// packet of the batch), from one D2H of the device batch.
+int Chain::copy_back(bool all)
+{
+    bool any = false;
+    for (size_t i = 0; i < views0_.size() && !any; i++)
+        any = back_[i] && !copied_[i] && (all || done_[i]);
+    if (!any)
+        return CLK_SUCCESS;
+    hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
+    double t0 = now_s();
+    hipError_t er;
+    if (pinned_grow(&h_back_, &back_cap_, used_ + 64, 0) ||
+        (er = glue_checked(hipMemcpyAsync(h_back_, d_arena_, used_, hipMemcpyDeviceToHost, s))) != hipSuccess ||
+        (er = glue_checked(hipStreamSynchronize(s))) != hipSuccess) {
+        (void)hipStreamSynchronize(s);
+        err_ = "hipMemcpyAsync(packets back) failed";
+        return CLK_EHIP;
+    }
+    stats_[5] += now_s() - t0;
+    t0 = now_s();
+    for (size_t i = 0; i < views0_.size(); i++)
+        if (back_[i] && !copied_[i] && (all || done_[i])) {
+            std::memcpy(views0_[i].data, h_back_ + views0_[i].slot, back_[i]);
+            copied_[i] = 1;
+        }
+    stats_[7] += now_s() - t0;
+    return CLK_SUCCESS;
+}
+
+// Run the staged batch through the members and route it.  A member whose
+// step fails stops the flush there: the packets that left the chain before it
+// stay routed (their bytes copied back); the rest stay in the chain, and the
+// next flush resumes at that member (push() refuses packets until then).
+int Chain::flush()
+{
+    if (views0_.empty())
+        return CLK_SUCCESS;
+    err_.clear();
+    const size_t n = views0_.size();
+    hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
+    size_t k0 = 0;
+    if (resume_ >= 0) {
+        k0 = (size_t)resume_;
+    } else {
+        if (grow(used_ + 64, n)) {
+            err_ = "out of device / pinned memory";
+            return CLK_EHIP;
+        }
+        double t0 = now_s();
+        hipError_t er = glue_checked(hipMemcpyAsync(d_arena_, h_arena_, used_, hipMemcpyHostToDevice, s));
+        if (er != hipSuccess) {
+            (void)hipStreamSynchronize(s);
+            err_ = std::string("hipMemcpyAsync(packets): ") + hipGetErrorString(er);
+            return CLK_EHIP;
+        }
+        stats_[4] += now_s() - t0;
+        views_.assign(views0_.begin(), views0_.end());
+        alive_.resize(n);
+        for (size_t i = 0; i < n; i++)
+            alive_[i] = (uint32_t)i;
+        done_.assign(n, 0);
+        copied_.assign(n, 0);
+    }
+    int failed = CLK_SUCCESS;
+    std::string failed_why;
+    for (size_t k = k0; k < m_.size(); k++) {
+        if (alive_.empty())
+            break;
+        bool launched = false;
+        int r = run_member(k, &launched);
+        if (r == CLK_SUCCESS)
+            continue;
+        ChainWork &w = mm_[k].w;
+        if (launched && !m_[k]->idempotent()) {
+            // the member's kernel may have rewritten the device bytes: running
+            // it again would apply it twice (a second TTL decrement), so the
+            // packets it had not routed are killed, as a ZEROCOPY batch of such
+            // an element is; the ones it passed before that go on
+            BatchElement *e = m_[k];
+            for (size_t q = w.routed; q < w.reached.size(); q++) {
+                const uint32_t i = w.reached[q];
+                out_.push_back(ChainExit{views_[i].token, (int32_t)k, CLK_PORT_KILL, views_[i].length, 0});
+                done_[i] = 1;
+                e->lost_++;
+            }
+            alive_.swap(next_);
+            failed = r;
+            failed_why = err_ + " (its packets were killed, not retried)";
+            continue;
+        }
+        // the packets at member k that it had not routed yet stay in the
+        // chain (those it decided on the host before the failure are routed;
+        // the ones it passed resume at member k+1)
+        carry_.insert(carry_.end(), next_.begin(), next_.end());
+        alive_.assign(w.reached.begin() + (long)w.routed, w.reached.end());
+        resume_ = (int)k;
+        const std::string why = failed ? failed_why + "; " + err_ : err_;
+        (void)copy_back(false);
+        err_ = why;
+        return r;
+    }
+    int r = copy_back(true);
+    if (r) {
+        resume_ = (int)m_.size();                    // only the copy back is left
+        return r;
+    }
+    resume_ = -1;
+    views0_.clear();
+    staged_.clear();
+    back_.clear();
+    used_ = 0;
+    if (failed)
+        err_ = failed_why;
+    return failed;
+}
+
+uint64_t Chain::pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap)
+{
+    const size_t k = (size_t)std::min<uint64_t>(cap, out_.size() - head_);
+    for (size_t q = 0; q < k; q++) {
+        const ChainExit &x = out_[head_ + q];
+        if (tokens) tokens[q] = x.token;
+        if (members) members[q] = x.member;
+        if (ports) ports[q] = x.port;
+        if (lengths) lengths[q] = x.length;
+        if (aux) aux[q] = x.aux;
+    }
+    head_ += k;
+    if (head_ == out_.size())
+        out_.clear(), head_ = 0;
+    return k;
+}
+
+} // namespace host
+} // namespace clk
+
+// ---- C ABI (include/click_amd_elements.h) ------------------------------------
+
+struct clk_chain {
+    clk::host::Chain *c;
+};
+
+
+extern "C" {
+
+int clk_chain_create(clk_element *const *members, int n, clk_chain **out)
+{
+    if (!members || n < 1 || !out)
+        return clk_ctx_set_error_internal(nullptr, "clk_chain_create: bad arguments");
+    *out = nullptr;
+    std::vector<clk::host::BatchElement *> m;
+    for (int k = 0; k < n; k++) {
+        if (!members[k])
+            return clk_ctx_set_error_internal(nullptr, "clk_chain_create: null element");
+        m.push_back(clk::host::element_impl(members[k]));
+    }
+    clk::host::Chain *c = new (std::nothrow) clk::host::Chain(m);
+    if (!c)
+        return CLK_EINVAL;
+    std::string err;
+    int r = c->check(&err);
+    if (r) {
+        delete c;
+        clk_ctx_set_error_internal(nullptr, ("clk_chain_create: " + err).c_str());
+        return r;
+    }
+    clk_chain *w = new (std::nothrow) clk_chain{c};
+    if (!w) {
+        delete c;
+        return CLK_EINVAL;
+    }
+    *out = w;
+    return CLK_SUCCESS;
+}
+
+int clk_chain_destroy(clk_chain *w)
+{
+    if (w) {
+        delete w->c;
+        delete w;
+    }
+    return CLK_SUCCESS;
+}
+
+const char *clk_chain_last_error(clk_chain *w)
+{
+    return w ? w->c->last_error().c_str() : "null chain";
+}
+
+int clk_chain_push_anno(clk_chain *w, uint8_t *data, uint32_t length, int32_t nh_offset, uint32_t anno,
+                        uint64_t token)
+{
+    if (!w || (!data && length))
+        return CLK_EINVAL;
+    return w->c->push(data, length, nh_offset, token, anno);
+}
+
+int clk_chain_push_burst(clk_chain *w, uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets,
+                         uint64_t first_token, uint32_t n)
+{
+    if (!w || (n && (!datas || !lengths)))
+        return CLK_EINVAL;
+    return w->c->push_burst(datas, lengths, nh_offsets, first_token, n);
+}
+
+int clk_chain_flush(clk_chain *w)
+{
+    if (!w)
+        return CLK_EINVAL;
+    return w->c->flush();
+}
+
+int clk_chain_stats(clk_chain *w, double *sec, int n)
+{
+    if (!w || !sec)
+        return CLK_EINVAL;
+    return w->c->stats(sec, n);
+}
+
+uint64_t clk_chain_results(clk_chain *w, uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths,
+                           uint32_t *aux, uint64_t cap)
+{
+    if (!w)
+        return 0;
+    return w->c->pop(tokens, members, ports, lengths, aux, cap);
+}
+
+} // extern "C"

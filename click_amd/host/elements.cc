@@ -304,6 +304,22 @@ static inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint
     }
 }
 
+void stage_copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail)
+{
+    stage_copy(dst, src, n, avail);
+}
+
+void BatchElement::chain_build(ChainWork &w)
+{
+    chain_build_loop(w, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); },
+                     [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
+}
+
+void BatchElement::chain_route(ChainWork &w)
+{
+    chain_route_loop(w, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
+}
+
 template <class SpanF>
 inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token,
                                   uint32_t anno)
@@ -423,6 +439,11 @@ static hipError_t checked(hipError_t e)
     while (v > 0 && !g_fault_at.compare_exchange_weak(v, v - 1, std::memory_order_relaxed))
         ;
     return v == 1 ? hipErrorInvalidValue : e;
+}
+
+hipError_t glue_checked(hipError_t e)
+{
+    return checked(e);
 }
 
 // A launch step failed: drain what was queued on the stream so no copy or
@@ -1747,6 +1768,11 @@ struct clk_element {
     clk::host::BatchElement *e;
     clk_ctx *own_ctx;          // created for DEVICE when the caller passed no context
 };
+
+clk::host::BatchElement *clk::host::element_impl(clk_element *w)
+{
+    return w->e;
+}
 
 extern "C" {
 

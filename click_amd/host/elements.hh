@@ -19,6 +19,8 @@
 
 #include "../../include/click_amd_cksum.h"
 
+struct clk_element;          // include/click_amd_elements.h
+
 namespace clk {
 namespace host {
 
@@ -126,6 +128,39 @@ bool parse_int(const std::string &s, long *v);
 bool parse_ip(const std::string &s, uint32_t *saddr);       // raw network-order s_addr
 bool parse_prefix(const std::string &s, uint32_t *saddr, uint32_t *mask);
 
+// One member's share of a chain flush (class Chain, chain.cc).
+struct ChainView {           // a packet as a chain member sees it
+    uint8_t *data;
+    uint64_t token, slot;    // slot: the staging offset of data
+    uint32_t length;
+    int32_t nh;
+    uint16_t anno;
+};
+struct ChainExit {           // a result leaving the chain at `member`
+    uint64_t token;
+    int32_t member, port;
+    uint32_t length, aux;
+};
+struct ChainWork {
+    std::vector<ChainView> *views;            // per chain packet, updated as it passes members
+    std::vector<uint32_t> reached;            // the packets that reach this member, in push order
+    std::vector<int32_t> code;                // per reached packet: GPU index, or -1 - host code
+    std::vector<uint32_t> span_off;
+    std::vector<uint32_t> *next;              // chain_route(): the packets that pass, in order
+    std::vector<uint8_t> *done;               // per chain packet: has left the chain
+    size_t routed = 0;                        // reached packets chain_build() routed already
+    uint64_t *h_off = nullptr;                // the member's batch (pinned)
+    uint32_t *h_len = nullptr;
+    uint8_t *h_anno = nullptr;
+    const uint8_t *h_codes = nullptr;
+    const uint16_t *h_sums = nullptr;
+    size_t n = 0;
+    uint32_t maxlen = 0;
+    std::vector<ChainExit> *out = nullptr;
+    int member = 0;
+    bool last = false;
+};
+
 // The final classes' fast loops: push_burst() and route_stage() over the
 // class's own span() / route(), called qualified so they inline (no
 // virtual call per packet).
@@ -139,6 +174,16 @@ bool parse_prefix(const std::string &s, uint32_t *saddr, uint32_t *mask);
     void route_stage(Stage &g_) override                                                                        \
     {                                                                                                           \
         route_loop(g_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
+    }                                                                                                           \
+    void chain_build(ChainWork &w_) override                                                                    \
+    {                                                                                                           \
+        chain_build_loop(w_, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {                    \
+            return this->C::span(p, o, l, c);                                                                   \
+        }, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); });         \
+    }                                                                                                           \
+    void chain_route(ChainWork &w_) override                                                                    \
+    {                                                                                                           \
+        chain_route_loop(w_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
     }
 
 class BatchElement {
@@ -202,6 +247,34 @@ class BatchElement {
     // only when has_post_route_
     virtual void post_route(Pending &, int, ResultQueue &) {}
     bool has_pre_route_ = false, has_post_route_ = false;
+    // ---- chain mode (class Chain: consecutive elements on one staged batch)
+    // A packet route() sends to output 0 goes on to the next element of a
+    // chain with the result's length; the element may pull bytes off its
+    // front (IPInputCombo's Strip(14)) and set its network header offset
+    // (-2: unchanged).
+    virtual uint32_t strip() const { return 0; }
+    virtual int32_t nh_after() const { return -2; }
+    // the bytes from data() the element's kernel can read / write of a packet
+    // of `length` bytes whose network header is at nh (~0u: all of it)
+    virtual uint32_t chain_extent(int32_t nh, uint32_t length) const { (void)nh, (void)length; return 0xFFFFFFFFu; }
+    virtual uint32_t chain_write_extent(int32_t nh, uint32_t length) const
+    {
+        return writes() ? chain_extent(nh, length) : 0u;
+    }
+    // the element's kernel writes packet bytes (a chain copies them back)
+    virtual bool writes() const { return wants_sums() || wants_arena_back() || !idempotent(); }
+    // a chain's per-member passes (CLK_GLUE_LOOPS inlines the class's span /
+    // route into them): descriptors before the kernel, routing after it
+    virtual void chain_build(ChainWork &w);
+    virtual void chain_route(ChainWork &w);
+    template <class SpanF, class RouteF>
+    void chain_build_loop(ChainWork &w, SpanF &&span_f, RouteF &&route_f);
+    template <class RouteF>
+    void chain_route_loop(ChainWork &w, RouteF &&route_f);
+    template <class RouteF>
+    void chain_route_one(ChainWork &w, size_t q, Pending &p, int code, uint16_t sum, RouteF &&route_f);
+    ResultQueue chain_side_;          // a member's pre/post results while a chain routes
+    friend class Chain;
     // after the batch completed, before any packet is routed: nonzero fails
     // the flush (a kernel's internal fault report in the codes)
     virtual int verify(const uint8_t *, size_t) { return 0; }
@@ -339,6 +412,8 @@ class CheckIPHeader : public CheckElement {
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    int32_t nh_after() const override { return (int32_t)offset_; }
+    uint32_t chain_extent(int32_t, uint32_t) const override { return offset_ + 60; }
     const char *const *reason_texts() const override;
     int nreasons() const override { return 6; }
     std::string drop_message(const char *reason) const override;
@@ -370,6 +445,8 @@ class IPInputCombo : public CheckIPHeader {
 
   protected:
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    uint32_t strip() const override { return 14; }
+    int32_t nh_after() const override { return 0; }
 
   private:
     long color_ = 0;
@@ -387,6 +464,7 @@ class SetIPChecksum : public BatchElement {
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 60; }
     bool wants_sums() const override { return true; }
 
   private:
@@ -452,6 +530,7 @@ class DecIPTTL : public BatchElement {
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 20; }
     bool wants_sums() const override { return true; }
 
   private:
@@ -476,6 +555,7 @@ class IPGWOptions : public BatchElement {
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 64; }
     bool wants_arena_back() const override { return true; }
 
   private:
@@ -499,6 +579,7 @@ class FixIPSrc : public BatchElement {
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 64; }
     bool wants_arena_back() const override { return true; }
 
   private:
@@ -525,6 +606,7 @@ class IPOutputCombo : public BatchElement {
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void pre_route(Pending &p, ResultQueue &out) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 64; }
     bool wants_arena_back() const override { return true; }
     bool wants_anno() const override { return true; }
 
@@ -553,6 +635,11 @@ class IPFragmenter : public BatchElement {
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
+    uint32_t chain_extent(int32_t nh, uint32_t length) const override   // within the MTU: untouched (165-171)
+    {
+        const uint32_t h = nh > 0 ? (uint32_t)nh : 0u;
+        return h <= length && length - h <= mtu_ ? 0u : 0xFFFFFFFFu;
+    }
     int verify(const uint8_t *codes, size_t n) override;
     void post_route(Pending &p, int code, ResultQueue &out) override;
     bool wants_arena_back() const override { return true; }
@@ -578,7 +665,174 @@ class IPFragmenter : public BatchElement {
     uint64_t nfrag_ = 0;
 };
 
+// Descriptors of the packets that reach this member.  The leading packets
+// the member decides on the host (span() false) are routed right here, in
+// order, until the first one that needs the GPU (chain_route_loop() routes
+// the rest after the kernel): a member that decides every packet on the host
+// (IPGWOptions without options, FixIPSrc without the annotation,
+// IPFragmenter within the MTU) costs one pass.
+template <class SpanF, class RouteF>
+void BatchElement::chain_build_loop(ChainWork &w, SpanF &&span_f, RouteF &&route_f)
+{
+    const size_t m = w.reached.size();
+    w.code.resize(m);
+    w.span_off.resize(m);
+    w.n = 0;
+    w.maxlen = 0;
+    w.routed = 0;
+    w.next->clear();
+    const bool inline_ok = !has_pre_route_ && !has_post_route_;
+    for (size_t q = 0; q < m; q++) {
+        const ChainView &v = (*w.views)[w.reached[q]];
+        Pending p{v.data, v.token, v.slot, v.length, v.nh, 0, 0, 0, -1, v.anno};
+        uint32_t off = 0, len = 0;
+        int32_t hc = 0;
+        w.span_off[q] = 0;
+        if (!span_f(p, &off, &len, &hc)) {
+            w.code[q] = -1 - hc;                 // decided on the host
+            if (inline_ok && w.n == 0 && w.routed == q) {
+                p.host_code = (int16_t)hc;
+                chain_route_one(w, q, p, hc, 0, route_f);
+                w.routed = q + 1;
+            }
+            continue;
+        }
+        w.h_off[w.n] = v.slot + off;
+        w.h_len[w.n] = len;
+        w.h_anno[w.n] = (uint8_t)v.anno;
+        w.maxlen = std::max(w.maxlen, len);
+        w.span_off[q] = off;
+        w.code[q] = (int32_t)w.n++;
+    }
+}
+
+template <class RouteF>
+inline void BatchElement::chain_route_one(ChainWork &w, size_t q, Pending &p, int code, uint16_t sum, RouteF &&route_f)
+{
+    const uint32_t i = w.reached[q];
+    Result r{p.token, 0, p.length, 0};
+    packets_++;
+    route_f(p, code, sum, &r);
+    if (r.port == 0 && !w.last) {
+        ChainView &v = (*w.views)[i];
+        const uint32_t st = strip();
+        const int32_t nha = nh_after();
+        v.data += st;
+        v.slot += st;
+        v.length = r.length;
+        if (nha != -2)
+            v.nh = nha;
+        w.next->push_back(i);
+    } else {
+        w.out->push_back(ChainExit{r.token, w.member, r.port, r.length, r.aux});
+        (*w.done)[i] = 1;
+    }
+}
+
+// Route the packets that reached this member, in push order, from the first
+// one chain_build() left: output 0 goes on to the next member (its view moved
+// past this member), anything else -- and everything at the last member --
+// leaves the chain here.
+template <class RouteF>
+void BatchElement::chain_route_loop(ChainWork &w, RouteF &&route_f)
+{
+    const size_t m = w.reached.size();
+    const bool sums = wants_sums(), pre = has_pre_route_, post = has_post_route_;
+    uint64_t tok[64];
+    int32_t port[64];
+    uint32_t len[64], aux[64];
+    auto side = [&]() {
+        uint64_t got;
+        while ((got = chain_side_.pop(tok, port, len, aux, 64)) > 0)
+            for (uint64_t k = 0; k < got; k++)
+                w.out->push_back(ChainExit{tok[k], w.member, port[k], len[k], aux[k]});
+    };
+    for (size_t q = w.routed; q < m; q++) {
+        const int32_t c = w.code[q];
+        const int code = c >= 0 ? w.h_codes[c] : -1 - c;
+        const ChainView &v = (*w.views)[w.reached[q]];
+        Pending p{v.data, v.token, v.slot, v.length, v.nh, w.span_off[q], 0, c >= 0 ? (uint32_t)c : 0u,
+                  (int16_t)(c >= 0 ? -1 : code), v.anno};
+        if (pre) {
+            pre_route(p, chain_side_);
+            side();
+        }
+        chain_route_one(w, q, p, code, c >= 0 && sums ? w.h_sums[c] : 0, route_f);
+        if (post) {
+            post_route(p, code, chain_side_);
+            side();
+        }
+    }
+}
+
 BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::string &name, int noutputs);
+BatchElement *element_impl(::clk_element *w);
+hipError_t glue_checked(hipError_t e);                        // the glue's test fault hook       // the C ABI handle's element
+
+// A chain of elements in one thread, member k+1 connected to member k's
+// output 0 (chain.cc): each packet is staged once; a flush copies the batch
+// to HBM once, runs every member's kernel in order -- member k over the
+// packets members 0..k-1 passed on output 0 -- copies the rewritten bytes
+// back once, and routes each packet once, through the members' own
+// route() (counters, handlers, chatter as if each member had run it).  The
+// GPU analogue of click-xform's combos (ipinputcombo.cc:66-140,
+// ipoutputcombo.cc:44-205).
+class Chain {
+  public:
+    explicit Chain(const std::vector<BatchElement *> &members) : m_(members) {}
+    ~Chain();
+    int check(std::string *err) const;
+    int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno);
+    int push_burst(uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets, uint64_t first_token,
+                   uint32_t n);
+    int flush();
+    uint64_t pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap);
+    const std::string &last_error() const { return err_; }
+    size_t pending() const { return views0_.size(); }
+    // host seconds spent so far: staging (push), descriptors (build), the
+    // members' GPU round trips, next-member views, H2D of the batch, D2H of
+    // the rewritten bytes, routing, copy-back
+    int stats(double *sec, int n) const
+    {
+        for (int k = 0; k < n && k < 8; k++)
+            sec[k] = stats_[k];
+        return 8;
+    }
+
+  private:
+    struct Member {          // one member's batch buffers
+        uint64_t *h_off = nullptr, *d_off = nullptr;
+        uint32_t *h_len = nullptr, *d_len = nullptr;
+        uint8_t *h_codes = nullptr, *d_codes = nullptr, *h_anno = nullptr, *d_anno = nullptr;
+        uint8_t *h_aux8 = nullptr, *d_aux8 = nullptr;
+        uint16_t *h_sums = nullptr, *d_sums = nullptr;
+        size_t cap = 0;
+        void *ev[2] = {nullptr, nullptr};
+        float ms = 0;
+        ChainWork w;
+    };
+    int grow(size_t bytes, size_t n);
+    int run_member(size_t k, bool *launched);
+    int copy_back(bool all);
+    uint32_t extent(int32_t nh, uint32_t length);
+    std::vector<BatchElement *> m_;
+    std::vector<Member> mm_;
+    std::vector<ChainView> views0_, views_;   // as pushed; as they move through the members
+    std::vector<uint32_t> staged_, back_;     // bytes staged / written back per packet
+    std::vector<uint8_t> done_, copied_;      // per packet: left the chain; bytes copied back
+    int resume_ = -1;                         // a failed flush: the member it resumes at
+    std::vector<uint32_t> alive_, next_;
+    std::vector<uint32_t> carry_;             // a failed member's packets it had passed already
+    uint8_t *h_arena_ = nullptr, *h_back_ = nullptr, *d_arena_ = nullptr;
+    size_t h_cap_ = 0, back_cap_ = 0, d_cap_ = 0, used_ = 0;
+    std::vector<ChainExit> out_;
+    size_t head_ = 0;
+    double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int32_t ext_nh_ = -3;                     // extent() cache: the nh and length it was computed for
+    uint32_t ext_len_ = 0, ext_ = 0, wext_ = 0;
+    bool init_ = false;
+    std::string err_;
+};
 
 } // namespace host
 } // namespace clk

@@ -179,6 +179,47 @@ int clk_element_read_handler(clk_element *e, const char *handler, char *buf, siz
 /* Pop the click_chatter lines the element produced, '\n'-separated. */
 int clk_element_take_messages(clk_element *e, char *buf, size_t cap);
 
+/* ---- chains: consecutive elements on one device-resident batch ----------
+ * members[k+1] is connected to members[k]'s output 0, all in one thread and
+ * on one context, none ZEROCOPY; an element with extra results after its
+ * packet (IPFragmenter) only as the last member.  The members stay the
+ * caller's (configuration, handlers, counters: each counts what it routed,
+ * as if it had run alone); the chain never uses their own staging.  A packet
+ * pushed into the chain is staged once (the bytes any member reads); a flush
+ * copies the batch to the GPU once, runs member k's kernel over the packets
+ * members 0..k-1 passed on output 0, copies the rewritten bytes back once and
+ * routes each packet once, through every member it reaches, in order.  Each
+ * result names the member it leaves and that member's output (enum
+ * clk_port); a member's extra results (IPOutputCombo's clone before the
+ * packet, IPFragmenter's fragments after it) come with their member; new
+ * packets are taken with clk_element_take_packet(members[member], aux).
+ * The GPU analogue of click-xform's combos (ipinputcombo.cc:66-140,
+ * ipoutputcombo.cc:44-205): one gather, one H2D, one D2H and one routing
+ * pass per packet instead of one per element.  Results come member by
+ * member (each member's in push order, as its outputs see them).  A flush
+ * that fails at member k has routed what left the chain before k (their
+ * bytes written back); the packets at k stay in the chain and the next
+ * flush resumes there (push refuses packets until it has) -- except after
+ * the kernel of a member that is not idempotent (DecIPTTL, IPGWOptions,
+ * IPOutputCombo, IPFragmenter) was launched: its packets are then killed
+ * (results with CLK_PORT_KILL, counted by its "lost" handler), never run
+ * twice.                                                                   */
+typedef struct clk_chain clk_chain;
+int clk_chain_create(clk_element *const *members, int n, clk_chain **out);
+int clk_chain_destroy(clk_chain *c);
+const char *clk_chain_last_error(clk_chain *c);
+int clk_chain_push_anno(clk_chain *c, uint8_t *data, uint32_t length, int32_t nh_offset, uint32_t anno,
+                        uint64_t token);   /* 1: the batch is full, flush it */
+int clk_chain_push_burst(clk_chain *c, uint8_t *const *datas, const uint32_t *lengths,
+                         const int32_t *nh_offsets, uint64_t first_token, uint32_t n);
+int clk_chain_flush(clk_chain *c);
+uint64_t clk_chain_results(clk_chain *c, uint64_t *tokens, int32_t *members, int32_t *ports,
+                           uint32_t *lengths, uint32_t *aux, uint64_t cap);
+/* Host seconds the chain has spent, by phase: staging, descriptors, the
+ * members' GPU round trips, next-member views, H2D of the batch, D2H of the
+ * rewritten bytes, routing, copy-back into the packets.  Returns 8.       */
+int clk_chain_stats(clk_chain *c, double *sec, int n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,302 @@
+"""GPU tests of element chains (clk_chain_*, click_amd/host/chain.cc):
+consecutive elements on one staged, device-resident batch must route,
+rewrite and count exactly as the same elements run one after another (which
+tests/test_gpu_elements.py and test_gpu_output_elements.py pin to the
+oracle): the fake-iprouter forwarding path as separate elements and as the
+click-xform combos (iprouter-01), fuzzed frames with every drop reason, IP
+options, expiring TTLs, fragments, broadcast / painted annotations, a
+check-then-set pair over whole payloads, a failed flush resumed (or its
+packets killed after a rewriting member's kernel ran), and the chains the
+ABI refuses."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from tests import fuzz, oracle_lib
+
+pytestmark = pytest.mark.gpu
+
+MY_IP_TXT = "18.26.4.24"
+MY_IP = 0x18041A12
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import click_amd
+    c = click_amd.Context(0)
+    yield c
+    c.close()
+
+
+def framed(rng, a3, o3, c3, eth=14):
+    n = len(o3)
+    flen = (c3 + eth).astype(np.uint32)
+    foff = np.zeros(n, np.uint64)
+    pos = 0
+    for i in range(n):
+        pos += int(rng.integers(0, 8)) * 2
+        foff[i] = pos
+        pos += int(flen[i]) + 4
+    arena = np.zeros(pos + 64, np.uint8)
+    for i in range(n):
+        o = int(foff[i])
+        arena[o:o + eth] = rng.integers(0, 256, eth, dtype=np.uint8)
+        arena[o + eth:o + int(flen[i])] = a3[int(o3[i]):int(o3[i]) + int(c3[i])]
+    return arena, foff, flen
+
+
+def make(ctx, spec):
+    from click_amd.elements import Element
+    return [Element(ctx, cls, conf, name="m%d" % k, noutputs=nout) for k, (cls, conf, nout) in enumerate(spec)]
+
+
+def run_separate(ctx, spec, arena, foff, flen, nh0, anno):
+    """The members one after another, each flushed over what the one before
+    passed on output 0 (views as the Click adapters leave them: CheckIPHeader
+    sets the network header at OFFSET, IPInputCombo strips 14 bytes).
+    Returns the results in the chain's order and the elements."""
+    from click_amd.elements import AUX_CLONE
+    els = make(ctx, spec)
+    base = arena.ctypes.data
+    n = len(foff)
+    ptr = [base + int(foff[i]) for i in range(n)]
+    ln = [int(flen[i]) for i in range(n)]
+    nh = [nh0] * n
+    out = []                                    # member-major: each member's results in its own order
+    alive = list(range(n))
+    for k, e in enumerate(els):
+        for i in alive:
+            rc = e.lib.clk_element_push_anno(e.h, ctypes.c_void_p(ptr[i]), ln[i], nh[i], int(anno[i]), i)
+            assert rc >= 0
+            if rc == 1:
+                e.flush()
+        e.flush()
+        tok, port, length, aux = e.results(aux=True)
+        cls = spec[k][0]
+        passed = set()
+        nxt = []
+        seen = set()
+        for t, p, l_, a in zip(tok.tolist(), port.tolist(), length.tolist(), aux.tolist()):
+            primary = t not in seen and not (cls == "IPOutputCombo" and a == AUX_CLONE)
+            if primary:
+                seen.add(t)
+            if primary and p == 0 and k + 1 < len(els):
+                passed.add(t)
+                if cls in ("CheckIPHeader", "CheckIPHeader2"):
+                    nh[t] = int(e.read_handler("offset"))
+                if cls == "IPInputCombo":
+                    ptr[t] += 14
+                    nh[t] = 0
+                ln[t] = l_
+                nxt.append(t)
+                continue
+            out.append((t, k, p, l_, a))
+        alive = nxt
+    return out, els
+
+
+def run_chain(ctx, spec, arena, foff, flen, nh0, anno, batch_flush=None):
+    from click_amd.elements import Chain
+    els = make(ctx, spec)
+    ch = Chain(els)
+    base = arena.ctypes.data
+    for i in range(len(foff)):
+        if ch.push_anno(base + int(foff[i]), int(flen[i]), nh0, int(anno[i]), i) or \
+                (batch_flush and (i + 1) % batch_flush == 0):
+            ch.flush()
+    ch.flush()
+    tok, mem, port, length, aux = ch.results()
+    return list(zip(tok.tolist(), mem.tolist(), port.tolist(), length.tolist(), aux.tolist())), els, ch
+
+
+def compare_chain(ctx, spec, arena, foff, flen, nh0=-1, anno=None, batch_flush=None,
+                  handlers=("drops", "fragments", "packets", "lost")):
+    anno = np.zeros(len(foff), np.uint32) if anno is None else anno
+    a1, a2 = arena.copy(), arena.copy()
+    r1, e1 = run_separate(ctx, spec, a1, foff, flen, nh0, anno)
+    r2, e2, ch = run_chain(ctx, spec, a2, foff, flen, nh0, anno, batch_flush)
+    assert len(r1) == len(r2)
+    # each member's results in its own (push) order, as the elements one by
+    # one give them (a chain flush interleaves members batch by batch)
+    for k in range(len(spec)):
+        x1 = [x for x in r1 if x[1] == k]
+        x2 = [y for y in r2 if y[1] == k]
+        assert len(x1) == len(x2), (spec[k][0], len(x1), len(x2))
+        for x, y in zip(x1, x2):
+            if x[:4] != y[:4]:
+                raise AssertionError(("first difference", x, y))
+    assert np.array_equal(a1, a2), np.nonzero(a1 != a2)[0][:10]
+    for k in range(len(spec)):                  # new packets (fragments), byte for byte
+        for x, y in zip([x for x in r1 if x[1] == k], [y for y in r2 if y[1] == k]):
+            if spec[k][0] == "IPFragmenter" and x[4] != 0:
+                assert e1[k].take_packet(x[4]) == e2[k].take_packet(y[4])
+        for h in handlers:
+            assert e1[k].read_handler(h) == e2[k].read_handler(h), (spec[k][0], h)
+        assert e1[k].messages() == e2[k].messages(), spec[k][0]
+    ch.close()
+    for e in e1 + e2:
+        e.close()
+    return r2
+
+
+# fake-iprouter.click's forwarding path (bench.py C1_CHAINS)
+FAKE_IPROUTER = [("CheckIPHeader", "INTERFACES 18.26.4.1/24 18.26.7.1/24, OFFSET 14", 2),
+                 ("IPGWOptions", MY_IP_TXT, 2), ("FixIPSrc", MY_IP_TXT, 1), ("DecIPTTL", "", 2),
+                 ("IPFragmenter", "300", 2)]
+COMBOS = [("IPInputCombo", "1, INTERFACES 18.26.4.1/24 18.26.7.1/24", 1),
+          ("IPOutputCombo", "1, %s, 300" % MY_IP_TXT, 5)]
+
+
+def no_timestamps(arena, off, caplen):
+    """Timestamp options become Record Route ones: the TS value is the
+    wall clock at the flush (Timestamp::now(), ipgwoptions.cc:118-119), which
+    two runs cannot share; everything else about the option walk stays."""
+    for i in range(len(off)):
+        o, c = int(off[i]), int(caplen[i])
+        if c < 20:
+            continue
+        hl = int(arena[o] & 0xF) * 4
+        k = o + 20
+        while k < o + min(hl, c):
+            t = int(arena[k])
+            if t == 0:
+                break
+            if t == 1:
+                k += 1
+                continue
+            if k + 1 >= o + min(hl, c) or arena[k + 1] < 2:
+                break
+            if t == 68:
+                arena[k] = 7
+            k += int(arena[k + 1])
+        if hl <= c:
+            oracle_lib.batch("set_ip", arena[o:o + c], 1, fixed_len=c)
+
+
+def fake_frames(n):
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden_vectors.json")))["vectors"]
+    l3 = bytes.fromhex([v for v in g if v["name"] == "fake-iprouter-ip-check"][0]["l3"])
+    frame = np.frombuffer(bytes.fromhex("0000c0ae67ef0000000000000800") + l3, np.uint8)
+    arena = np.tile(frame, n)
+    return arena, np.arange(n, dtype=np.uint64) * len(frame), np.full(n, len(frame), np.uint32)
+
+
+@pytest.mark.parametrize("spec", [FAKE_IPROUTER, COMBOS], ids=["elements", "combos"])
+def test_fake_iprouter_chain(ctx, spec):
+    """iprouter-01's frames: every one forwarded on the last member's output
+    0, the same bytes as the elements one by one."""
+    arena, foff, flen = fake_frames(20000)
+    r = compare_chain(ctx, spec, arena, foff, flen)
+    assert all(m == len(spec) - 1 and p == 0 for _, m, p, _, _ in r)
+
+
+def fuzzed_frames(seed, n=3000):
+    rng = np.random.default_rng(seed)
+    a3, o3, c3, _ = fuzz.gw_batch(rng, n, MY_IP)
+    no_timestamps(a3, o3, c3)
+    arena, foff, flen = framed(rng, a3, o3, c3)
+    for i in range(0, n, 7):                    # TTLs 0-2: expired on DecIPTTL / IPOutputCombo
+        o = int(foff[i]) + 14
+        arena[o + 8] = i % 3
+        oracle_lib.batch("set_ip", arena[o:o + int(flen[i]) - 14], 1, fixed_len=int(flen[i]) - 14)
+    for i in range(3, n, 11):                   # a flipped bit: CheckIPHeader's output 1
+        arena[int(foff[i]) + 14 + 12] ^= 0x02
+    return rng, arena, foff, flen
+
+
+@pytest.mark.parametrize("batch_flush", [None, 333])
+def test_fuzzed_element_chain(ctx, batch_flush):
+    rng, arena, foff, flen = fuzzed_frames(5 + (batch_flush or 0))
+    anno = (rng.random(len(foff)) < 0.3).astype(np.uint32)        # FIX_IP_SRC on a third
+    spec = [("CheckIPHeader", "OFFSET 14, DETAILS true", 2), ("IPGWOptions", MY_IP_TXT + ", BATCH 700", 2),
+            ("FixIPSrc", MY_IP_TXT, 1), ("DecIPTTL", "", 2), ("IPFragmenter", "576, HONOR_DF true", 2)]
+    r = compare_chain(ctx, spec, arena, foff, flen, anno=anno, batch_flush=batch_flush)
+    seen = {(m, p) for _, m, p, _, _ in r}
+    assert {(0, 1), (1, 1), (3, 1), (4, 0)} <= seen, seen
+
+
+def test_fuzzed_combos_chain(ctx):
+    from click_amd.elements import ANNO_BCAST, anno_paint
+    rng, arena, foff, flen = fuzzed_frames(9)
+    n = len(foff)
+    anno = np.array([anno_paint(int(p)) for p in rng.integers(0, 3, n)], np.uint32) + \
+        (rng.random(n) < 0.05) * ANNO_BCAST + (rng.random(n) < 0.2).astype(np.uint32)
+    spec = [("IPInputCombo", "2", 1), ("IPOutputCombo", "1, %s, 120" % MY_IP_TXT, 5)]
+    r = compare_chain(ctx, spec, arena, foff, flen, anno=anno, handlers=("drops", "packets", "lost"))
+    assert {p for _, m, p, _, _ in r if m == 1} >= {-1, 0, 1, 2, 3, 4}
+
+
+def test_check_then_set_chain(ctx):
+    """CheckUDPHeader -> SetUDPChecksum over whole UDP payloads (L3 at
+    offset 0): the set runs on the packets the check passed."""
+    rng = np.random.default_rng(31)
+    a3, o3, c3, _ = fuzz.make_batch(rng, 2500, 17, max_total=1600)
+    spec = [("CheckUDPHeader", "", 2), ("SetUDPChecksum", "", 2)]
+    compare_chain(ctx, spec, a3, o3, c3, nh0=0)
+
+
+@pytest.mark.parametrize("nth", [1, 2, 4, 6, 8])
+def test_chain_failed_flush(ctx, nth):
+    """The nth checked HIP call of a chain flush fails (fake-iprouter chain:
+    1 the batch's H2D, 2 CheckIPHeader's descriptors, 4 its verdicts back,
+    6 DecIPTTL's descriptors, 8 its verdicts back).  Before any kernel of a
+    member that is not idempotent ran (1-6): nothing is routed, nothing
+    written, push() refuses packets, and the next flush resumes and routes
+    every packet exactly as a chain that never failed.  After DecIPTTL's
+    kernel (8): its packets are killed, never decremented twice."""
+    from click_amd import ClickAmdError
+    from click_amd.elements import Chain
+    arena, foff, flen = fake_frames(3000)
+    before = arena.copy()
+    els = make(ctx, FAKE_IPROUTER)
+    ch = Chain(els)
+    base = arena.ctypes.data
+    for i in range(len(foff)):
+        ch.push_anno(base + int(foff[i]), int(flen[i]), -1, 0, i)
+    hook = ctx.lib.clk_glue_inject_fault_internal
+    hook.argtypes, hook.restype = [ctypes.c_int], None
+    hook(nth)
+    try:
+        with pytest.raises(ClickAmdError):
+            ch.flush()
+    finally:
+        hook(0)
+    tok, mem, port, _, _ = ch.results()
+    if nth == 8:
+        assert len(tok) == 3000 and (mem == 3).all() and (port == -1).all()
+        assert "not retried" in ch.last_error()
+        assert els[3].read_handler("lost") == "3000"
+        ch.flush()
+        assert len(ch.results()[0]) == 0
+    else:
+        assert len(tok) == 0 and np.array_equal(arena, before)
+        if nth > 1:                              # a member failed: the chain holds its packets
+            with pytest.raises(ClickAmdError):
+                ch.push_anno(base, int(flen[0]), -1, 0, 99999)
+        ch.flush()
+        tok, mem, port, _, _ = ch.results()
+        assert len(tok) == 3000 and (mem == 4).all() and (port == 0).all()
+        ref = before.copy()                     # the same frames through a chain that never failed
+        run_chain(ctx, FAKE_IPROUTER, ref, foff, flen, -1, np.zeros(len(foff), np.uint32))
+        assert np.array_equal(arena, ref)
+    ch.close()
+
+
+def test_chain_refuses(ctx):
+    import click_amd
+    from click_amd import ClickAmdError
+    from click_amd.elements import Chain, Element
+    with pytest.raises(ClickAmdError, match="last element"):
+        Chain(make(ctx, [("IPFragmenter", "576", 2), ("DecIPTTL", "", 2)]))
+    with pytest.raises(ClickAmdError, match="ZEROCOPY"):
+        Chain([Element(ctx, "CheckIPHeader", "", noutputs=2), Element(ctx, "DecIPTTL", "ZEROCOPY true", noutputs=2)])
+    other = click_amd.Context(0)
+    with pytest.raises(ClickAmdError, match="one context"):
+        Chain([Element(ctx, "CheckIPHeader", "", noutputs=2), Element(other, "DecIPTTL", "", noutputs=2)])
+    other.close()
