@@ -813,6 +813,9 @@ def c1_frame():
     return bytes.fromhex("0000c0ae67ef0000000000000800") + l3          # fake-iprouter.click:42-44
 
 
+CHAIN_BATCH = 16384     # a chain's host passes over a batch that stays in L2
+
+
 def config1(ctx, n=C1_PACKETS, batch=65536):
     """Config 1 through the element glue on the GPU: every element of the
     chain takes all n frames by push_burst (C++ push() per packet, batches of
@@ -870,8 +873,9 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
     from click_amd.elements import Chain
     cbufs = [np.empty(n + 1, t) for t in (np.uint64, np.int32, np.int32, np.uint32, np.uint32)]
     cptrs = [b.ctypes.data_as(ctypes.c_void_p) for b in cbufs]
-    for name, chain in C1_CHAINS.items():
-        els = [Element(ctx, cls, ", ".join(x for x in (conf, "BATCH %d" % batch) if x), noutputs=nout)
+    for name, chain, cb in [(nm, ch_, b_) for nm, ch_ in C1_CHAINS.items() for b_ in (batch, CHAIN_BATCH)]:
+        name = name if cb == batch else "%s_%dk" % (name, cb >> 10)
+        els = [Element(ctx, cls, ", ".join(x for x in (conf, "BATCH %d" % cb) if x), noutputs=nout)
                for cls, conf, nout in chain]
         ch = Chain(els)
         for timed in (False, True):

@@ -625,8 +625,9 @@ void BatchElement::route_loop(Stage &g, RouteF &&route_f)
             k++;
         }
         Result r{p.token, 0, p.length, 0};
-        if (pre)
-            pre_route(p, results_);
+        Result pr;
+        if (pre && pre_route(p, &pr))
+            results_.push_back(pr);
         route_f(p, code, sum, &r);
         if (pre || post)
             results_.push_back(r);
@@ -1494,11 +1495,13 @@ int IPOutputCombo::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
     return clk_ip_output_combo(ctx_, b, &cfg, d_anno_, d_codes, d_aux8_, nullptr);
 }
 
-void IPOutputCombo::pre_route(Pending &p, ResultQueue &out)
+bool IPOutputCombo::pre_route(Pending &p, Result *r)
 {
     // PaintTee: a clone of the packet as it arrived goes to output 1 first (56-57)
-    if (!(p.anno & CLK_ANNO_BCAST) && (long)((p.anno >> 8) & 0xFF) == color_)
-        out.push_back(Result{p.token, noutputs_ >= 2 ? 1 : -1, p.length, CLK_AUX_CLONE});
+    if ((p.anno & CLK_ANNO_BCAST) || (long)((p.anno >> 8) & 0xFF) != color_)
+        return false;
+    *r = Result{p.token, noutputs_ >= 2 ? 1 : -1, p.length, CLK_AUX_CLONE};
+    return true;
 }
 
 void IPOutputCombo::route(Pending &p, int code, uint16_t, Result *r)

@@ -242,7 +242,8 @@ class BatchElement {
     virtual bool wants_anno() const { return false; }
     // called by flush() before route(): results() of the packet that precede
     // its own (IPOutputCombo's clone); only when has_pre_route_
-    virtual void pre_route(Pending &, ResultQueue &) {}
+    // (returns whether it made one, in *r)
+    virtual bool pre_route(Pending &, Result *) { return false; }
     // called after route(): results that follow the packet's own (fragments);
     // only when has_post_route_
     virtual void post_route(Pending &, int, ResultQueue &) {}
@@ -604,7 +605,7 @@ class IPOutputCombo : public BatchElement {
     bool idempotent() const override { return false; }
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
-    void pre_route(Pending &p, ResultQueue &out) override;
+    bool pre_route(Pending &p, Result *r) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
     uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 64; }
     bool wants_arena_back() const override { return true; }
@@ -753,10 +754,9 @@ void BatchElement::chain_route_loop(ChainWork &w, RouteF &&route_f)
         const ChainView &v = (*w.views)[w.reached[q]];
         Pending p{v.data, v.token, v.slot, v.length, v.nh, w.span_off[q], 0, c >= 0 ? (uint32_t)c : 0u,
                   (int16_t)(c >= 0 ? -1 : code), v.anno};
-        if (pre) {
-            pre_route(p, chain_side_);
-            side();
-        }
+        Result pr;
+        if (pre && pre_route(p, &pr))
+            w.out->push_back(ChainExit{pr.token, w.member, pr.port, pr.length, pr.aux});
         chain_route_one(w, q, p, code, c >= 0 && sums ? w.h_sums[c] : 0, route_f);
         if (post) {
             post_route(p, code, chain_side_);
