@@ -873,15 +873,19 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
     from click_amd.elements import Chain
     cbufs = [np.empty(n + 1, t) for t in (np.uint64, np.int32, np.int32, np.uint32, np.uint32)]
     cptrs = [b.ctypes.data_as(ctypes.c_void_p) for b in cbufs]
-    for name, chain, cb in [(nm, ch_, b_) for nm, ch_ in C1_CHAINS.items() for b_ in (batch, CHAIN_BATCH)]:
-        name = name if cb == batch else "%s_%dk" % (name, cb >> 10)
-        els = [Element(ctx, cls, ", ".join(x for x in (conf, "BATCH %d" % cb) if x), noutputs=nout)
+    for name, chain, cb, zc in [(nm, ch_, b_, z_) for nm, ch_ in C1_CHAINS.items()
+                                for b_, z_ in ((batch, False), (CHAIN_BATCH, False), (batch, True))]:
+        name = name + ("_zerocopy" if zc else "") + ("" if cb == batch else "_%dk" % (cb >> 10))
+        extra = "BATCH %d" % cb + (", ZEROCOPY true" if zc else "")
+        els = [Element(ctx, cls, ", ".join(x for x in (conf, extra) if x), noutputs=nout)
                for cls, conf, nout in chain]
         ch = Chain(els)
         for timed in (False, True):
             raw = np.empty(n * len(frame) + 8192, np.uint8)
             arena = raw[(-raw.ctypes.data) % 4096:][:n * len(frame)]
             arena[:] = np.tile(np.frombuffer(frame, np.uint8), n)
+            if zc:
+                ctx.host_register(arena)
             ptrs = np.uint64(arena.ctypes.data) + np.arange(n, dtype=np.uint64) * np.uint64(len(frame))
             lens = np.full(n, len(frame), np.uint32)
             t0 = time.perf_counter()
@@ -892,6 +896,8 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
             k = int(ch.lib.clk_chain_results(ch.h, *cptrs, n + 1))
             dt = time.perf_counter() - t0
             fwd = int(((cbufs[1][:k] == len(chain) - 1) & (cbufs[2][:k] == 0)).sum())
+            if zc:
+                ctx.host_unregister(arena)
         st = (ctypes.c_double * 8)()
         ch.lib.clk_chain_stats(ch.h, ctypes.cast(st, ctypes.c_void_p), 8)
         ch.close()

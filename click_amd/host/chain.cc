@@ -91,8 +91,8 @@ int Chain::check(std::string *err) const
             *err = e->name() + ": chain members must share one context (stream)";
             return CLK_EINVAL;
         }
-        if (e->zerocopy_) {
-            *err = e->name() + ": ZEROCOPY elements do not join a chain";
+        if (e->zerocopy_ != m_[0]->zerocopy_) {
+            *err = e->name() + ": the members of a chain are all ZEROCOPY or none";
             return CLK_EINVAL;
         }
         if (e->has_post_route_ && k + 1 != m_.size()) {
@@ -140,6 +140,35 @@ int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t toke
         err_ = "the chain's failed flush must be retried (or the packets abandoned) first";
         return CLK_EINVAL;
     }
+    if (m_[0]->zerocopy_) {
+        // ZEROCOPY: the kernels read and write the packets where they lie,
+        // in registered host memory (clk_host_register); one region per batch
+        const uint8_t *a = data;
+        const uint64_t gen = clk_host_generation_internal();
+        if (gen != zc_gen_ || !(a >= zc_last_ && a + (length ? length : 1) <= zc_last_ + zc_last_bytes_)) {
+            void *hs = nullptr, *db = nullptr;
+            size_t nb = 0;
+            if (clk_host_lookup(a, length ? length : 1, &hs, &nb, &db) != CLK_SUCCESS) {
+                err_ = "ZEROCOPY: packet memory is not registered (clk_host_register)";
+                return CLK_EINVAL;
+            }
+            zc_last_ = (const uint8_t *)hs;
+            zc_last_bytes_ = nb;
+            zc_last_dev_ = (uint8_t *)db;
+            zc_gen_ = gen;
+        }
+        if (!views0_.empty() && zc_host_ != zc_last_) {         // the batch's region ends here
+            int r = flush();
+            if (r)
+                return r;
+        }
+        zc_host_ = zc_last_;
+        zc_dev_ = zc_last_dev_;
+        views0_.push_back(ChainView{data, token, (uint64_t)(a - zc_host_), length, nh_offset, (uint16_t)anno});
+        staged_.push_back(0);
+        back_.push_back(0);
+        return views0_.size() >= m_[0]->batch_cap_ ? 1 : 0;
+    }
     const uint32_t need = std::min(length, extent(nh_offset, length));
     const size_t slot = (used_ + 15) & ~size_t(15);
     if (slot + need + 64 > h_cap_ && pinned_grow(&h_arena_, &h_cap_, std::max(slot + need + 64, size_t(1) << 20), used_)) {
@@ -175,7 +204,7 @@ int Chain::push_burst(uint8_t *const *datas, const uint32_t *lengths, const int3
 
 int Chain::grow(size_t bytes, size_t n)
 {
-    if (d_cap_ < bytes) {
+    if (bytes && d_cap_ < bytes) {
         if (d_arena_)
             (void)hipFree(d_arena_);
         d_arena_ = nullptr;
@@ -235,6 +264,7 @@ int Chain::run_member(size_t k, bool *launched)
     w.h_codes = M.h_codes, w.h_sums = M.h_sums;
     w.member = (int)k;
     w.last = k + 1 == m_.size();
+    w.report_passes = report_passes_;
     w.out = &out_;
     w.done = &done_;
     e->in_place_ = true;                             // the chain writes the packets back itself
@@ -256,7 +286,7 @@ int Chain::run_member(size_t k, bool *launched)
         }
         (void)hipEventRecord((hipEvent_t)M.ev[0], s);
         clk_batch b;
-        b.base = d_arena_;
+        b.base = m_[0]->zerocopy_ ? zc_dev_ : d_arena_;
         b.off = M.d_off;
         b.stride = 0;
         b.len = M.d_len;
@@ -356,6 +386,17 @@ int Chain::flush()
     size_t k0 = 0;
     if (resume_ >= 0) {
         k0 = (size_t)resume_;
+    } else if (m_[0]->zerocopy_) {
+        if (grow(0, n)) {
+            err_ = "out of device / pinned memory";
+            return CLK_EHIP;
+        }
+        views_.assign(views0_.begin(), views0_.end());
+        alive_.resize(n);
+        for (size_t i = 0; i < n; i++)
+            alive_[i] = (uint32_t)i;
+        done_.assign(n, 0);
+        copied_.assign(n, 0);
     } else {
         if (grow(used_ + 64, n)) {
             err_ = "out of device / pinned memory";
@@ -424,6 +465,7 @@ int Chain::flush()
     staged_.clear();
     back_.clear();
     used_ = 0;
+    zc_host_ = nullptr;
     if (failed)
         err_ = failed_why;
     return failed;
@@ -516,6 +558,14 @@ int clk_chain_push_burst(clk_chain *w, uint8_t *const *datas, const uint32_t *le
     if (!w || (n && (!datas || !lengths)))
         return CLK_EINVAL;
     return w->c->push_burst(datas, lengths, nh_offsets, first_token, n);
+}
+
+int clk_chain_report_passes(clk_chain *w, int on)
+{
+    if (!w)
+        return CLK_EINVAL;
+    w->c->report_passes(on != 0);
+    return CLK_SUCCESS;
 }
 
 int clk_chain_flush(clk_chain *w)

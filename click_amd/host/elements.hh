@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/click_amd_cksum.h"
+#include "../../include/click_amd_elements.h"
 
 struct clk_element;          // include/click_amd_elements.h
 
@@ -159,6 +160,7 @@ struct ChainWork {
     std::vector<ChainExit> *out = nullptr;
     int member = 0;
     bool last = false;
+    bool report_passes = false;               // a CLK_PORT_NEXT record for each packet passed on
 };
 
 // The final classes' fast loops: push_burst() and route_stage() over the
@@ -724,6 +726,8 @@ inline void BatchElement::chain_route_one(ChainWork &w, size_t q, Pending &p, in
         if (nha != -2)
             v.nh = nha;
         w.next->push_back(i);
+        if (w.report_passes)
+            w.out->push_back(ChainExit{r.token, w.member, CLK_PORT_NEXT, r.length, r.aux});
     } else {
         w.out->push_back(ChainExit{r.token, w.member, r.port, r.length, r.aux});
         (*w.done)[i] = 1;
@@ -789,6 +793,7 @@ class Chain {
     uint64_t pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap);
     const std::string &last_error() const { return err_; }
     size_t pending() const { return views0_.size(); }
+    void report_passes(bool on) { report_passes_ = on; }
     // host seconds spent so far: staging (push), descriptors (build), the
     // members' GPU round trips, next-member views, H2D of the batch, D2H of
     // the rewritten bytes, routing, copy-back
@@ -821,6 +826,12 @@ class Chain {
     std::vector<uint32_t> staged_, back_;     // bytes staged / written back per packet
     std::vector<uint8_t> done_, copied_;      // per packet: left the chain; bytes copied back
     int resume_ = -1;                         // a failed flush: the member it resumes at
+    const uint8_t *zc_host_ = nullptr;        // ZEROCOPY: the batch's registered region
+    uint8_t *zc_dev_ = nullptr;
+    const uint8_t *zc_last_ = nullptr;        // last region found (lookup cache)
+    size_t zc_last_bytes_ = 0;
+    uint8_t *zc_last_dev_ = nullptr;
+    uint64_t zc_gen_ = 0;
     std::vector<uint32_t> alive_, next_;
     std::vector<uint32_t> carry_;             // a failed member's packets it had passed already
     uint8_t *h_arena_ = nullptr, *h_back_ = nullptr, *d_arena_ = nullptr;
@@ -831,6 +842,7 @@ class Chain {
     int32_t ext_nh_ = -3;                     // extent() cache: the nh and length it was computed for
     uint32_t ext_len_ = 0, ext_ = 0, wext_ = 0;
     bool init_ = false;
+    bool report_passes_ = false;
     std::string err_;
 };
 

@@ -75,7 +75,9 @@ enum clk_port {
     CLK_PORT_OUT2 = 2,        /* IPOutputCombo: parameter problem           */
     CLK_PORT_OUT3 = 3,        /* IPOutputCombo: TTL expired                 */
     CLK_PORT_OUT4 = 4,        /* IPOutputCombo: longer than the MTU         */
-    CLK_PORT_KILL = -1        /* p->kill()                                   */
+    CLK_PORT_KILL = -1,       /* p->kill()                                   */
+    CLK_PORT_NEXT = 8         /* chains (clk_chain_report_passes): the packet
+                                 goes on to the next member                  */
 };
 
 /* name: the element's name in messages (Click's name(); NULL = class name);
@@ -213,6 +215,12 @@ int clk_chain_push_anno(clk_chain *c, uint8_t *data, uint32_t length, int32_t nh
 int clk_chain_push_burst(clk_chain *c, uint8_t *const *datas, const uint32_t *lengths,
                          const int32_t *nh_offsets, uint64_t first_token, uint32_t n);
 int clk_chain_flush(clk_chain *c);
+/* on != 0: every member also reports each packet it passes on to the next
+ * member (port CLK_PORT_NEXT, length as the next member sees it), in its
+ * place among the member's results -- so a host that applies each element's
+ * own side effects (the Click adapter: network header, trim, Strip,
+ * annotations) can apply them member by member.                           */
+int clk_chain_report_passes(clk_chain *c, int on);
 uint64_t clk_chain_results(clk_chain *c, uint64_t *tokens, int32_t *members, int32_t *ports,
                            uint32_t *lengths, uint32_t *aux, uint64_t cap);
 /* Host seconds the chain has spent, by phase: staging, descriptors, the

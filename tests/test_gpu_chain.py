@@ -288,13 +288,52 @@ def test_chain_failed_flush(ctx, nth):
     ch.close()
 
 
+@pytest.mark.parametrize("which", ["elements", "combos", "fuzzed"])
+def test_zerocopy_chain(ctx, which):
+    """ZEROCOPY chains: the members' kernels read and rewrite the packets in
+    registered host memory; routes, lengths, bytes and handlers equal the
+    staged elements one by one."""
+    from click_amd.elements import ANNO_BCAST, anno_paint
+    if which == "fuzzed":
+        rng, arena0, foff, flen = fuzzed_frames(77)
+        n = len(foff)
+        anno = np.array([anno_paint(int(p)) for p in rng.integers(0, 3, n)], np.uint32) + \
+            (rng.random(n) < 0.05) * ANNO_BCAST + (rng.random(n) < 0.2).astype(np.uint32)
+        spec = [("IPInputCombo", "2", 1), ("IPOutputCombo", "1, %s, 120" % MY_IP_TXT, 5)]
+    else:
+        arena0, foff, flen = fake_frames(20000)
+        anno = np.zeros(len(foff), np.uint32)
+        spec = FAKE_IPROUTER if which == "elements" else COMBOS
+    a1 = arena0.copy()
+    r1, e1 = run_separate(ctx, spec, a1, foff, flen, -1, anno)
+    raw = np.zeros(arena0.size + 8192, np.uint8)
+    a2 = raw[(-raw.ctypes.data) % 4096:][:arena0.size]
+    a2[:] = arena0
+    ctx.host_register(a2)
+    try:
+        zspec = [(c, ", ".join(x for x in (conf, "ZEROCOPY true") if x), k) for c, conf, k in spec]
+        r2, e2, ch = run_chain(ctx, zspec, a2, foff, flen, -1, anno)
+        for k in range(len(spec)):
+            x1 = [x[:4] for x in r1 if x[1] == k]
+            x2 = [y[:4] for y in r2 if y[1] == k]
+            assert x1 == x2, spec[k][0]
+            for h in ("drops", "packets", "lost"):
+                assert e1[k].read_handler(h) == e2[k].read_handler(h), (spec[k][0], h)
+        assert np.array_equal(a1, a2), np.nonzero(a1 != a2)[0][:10]
+        ch.close()
+        for e in e1 + e2:
+            e.close()
+    finally:
+        ctx.host_unregister(a2)
+
+
 def test_chain_refuses(ctx):
     import click_amd
     from click_amd import ClickAmdError
     from click_amd.elements import Chain, Element
     with pytest.raises(ClickAmdError, match="last element"):
         Chain(make(ctx, [("IPFragmenter", "576", 2), ("DecIPTTL", "", 2)]))
-    with pytest.raises(ClickAmdError, match="ZEROCOPY"):
+    with pytest.raises(ClickAmdError, match="all ZEROCOPY or none"):
         Chain([Element(ctx, "CheckIPHeader", "", noutputs=2), Element(ctx, "DecIPTTL", "ZEROCOPY true", noutputs=2)])
     other = click_amd.Context(0)
     with pytest.raises(ClickAmdError, match="one context"):

@@ -1,0 +1,10 @@
+# r04i: check of the tree -- every -m gpu test, smoke, the default bench, and
+# the driver's bench command under rocprofv3 --kernel-trace --stats
+set -o pipefail
+O=gpurun_out/r04i; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests > $O/gpu_tests.log 2>&1
+echo "tests rc=$?" >> $O/steps.txt
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 2
+timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.err || exit 3
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 10 > $O/bench_prof.json 2> $O/bench_prof.err || exit 4
