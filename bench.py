@@ -29,6 +29,7 @@ import argparse
 import ctypes
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -807,6 +808,21 @@ C1_CHAINS = {
 }
 
 
+def pull_legs(scale=1, timeout=300):
+    """Pull mode through the Click adapter's core (tests/native/pull_bench,
+    built by build()): Queue -> CheckIPHeader -> SetIPChecksum (C2, 64 B) and
+    Queue -> CheckUDPHeader -> SetUDPChecksum (C3, 1500 B) pulled on one
+    thread; Mpps and the per-pull() latency distribution.  None if the
+    program was not built."""
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "native", "bin", "pull_bench")
+    if not os.path.exists(exe):
+        return None
+    r = subprocess.run([exe, str(scale)], capture_output=True, text=True, timeout=timeout)
+    if r.returncode:
+        return {"error": (r.stderr or r.stdout)[-400:]}
+    return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+
+
 def c1_frame():
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden_vectors.json")))["vectors"]
     l3 = bytes.fromhex([v for v in g if v["name"] == "fake-iprouter-ip-check"][0]["l3"])
@@ -910,8 +926,8 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
                                        "results": round((t0 + dt - tc) * 1e3, 2)},
                                 # host ns per packet by phase, both runs (warm-up + timed)
                                 "ns_per_packet": {k: round(v * 1e9 / (2 * n), 1) for k, v in zip(
-                                    ("stage", "descriptors", "gpu_round_trips", "next_views", "h2d", "d2h_back",
-                                     "route", "copy_back"), list(st))}}
+                                    ("stage", "first_pass", "gpu_round_trips", "unused", "h2d", "d2h_back",
+                                     "route", "copy_back"), list(st)) if k != "unused"}}
     same = all(np.array_equal(arenas["elements"], arenas[k]) for k in arenas)
     return {"workload": "C1: conf/fake-iprouter.click forwarding path, %d x %d B frames, element glue on the GPU "
                         "(staged: push() gathers into pinned staging; _zerocopy: registered host arena)"
@@ -1087,8 +1103,9 @@ def main():
     if args.e2e:
         w = WORKLOADS[args.workload]
         res = [e2e(torch, ctx, args.workload, el) for el in w["elements"]]
+        pull = pull_legs() if rank == 0 else None
         if rank == 0:
-            print(json.dumps({"e2e": res}), flush=True)
+            print(json.dumps({"e2e": res, "pull": pull}), flush=True)
         ctx.close()
         return
     pk = args.packets or None

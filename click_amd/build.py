@@ -80,7 +80,8 @@ def build_examples(force=False):
     return out
 
 
-NATIVE_TESTS = ["hipcore_test"]
+NATIVE_TESTS = ["hipcore_test", "pull_bench"]
+NATIVE_ORACLE = {"hipcore_test"}          # the measurement programs never link the oracle
 
 
 def build_native_tests(force=False):
@@ -95,15 +96,20 @@ def build_native_tests(force=False):
     for name in NATIVE_TESTS:
         src = os.path.join(ndir, name + ".cc")
         exe = os.path.join(ndir, "bin", name)
-        deps = [src, lib, oracle, os.path.join(ROOT, "click_integration", "elements", "hip", "hipcore.hh")] + [
+        hip = os.path.join(ROOT, "click_integration", "elements", "hip")
+        deps = [src, lib, os.path.join(ndir, "harness.hh"), os.path.join(hip, "hipcore.hh"),
+                os.path.join(hip, "hipclasses.hh")] + [
             os.path.join(ROOT, "include", h) for h in ("click_amd_cksum.h", "click_amd_elements.h")]
+        orc = name in NATIVE_ORACLE
+        if orc:
+            deps.append(oracle)
         if force or _stale(exe, deps):
             subprocess.run(["g++", "-std=c++17", "-O2", "-g", "-Wall", "-Wextra", "-pthread",
-                            "-I" + os.path.join(ROOT, "include"), src,
-                            "-L" + PKG, "-lclick_amd_cksum", "-L" + os.path.join(ROOT, "oracle"), "-lcksum_oracle",
-                            "-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib",
-                            "-Wl,-rpath,$ORIGIN/../../../click_amd", "-Wl,-rpath,$ORIGIN/../../../oracle",
-                            "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
+                            "-I" + os.path.join(ROOT, "include"), src, "-L" + PKG, "-lclick_amd_cksum"] +
+                           (["-L" + os.path.join(ROOT, "oracle"), "-lcksum_oracle",
+                             "-Wl,-rpath,$ORIGIN/../../../oracle"] if orc else []) +
+                           ["-L/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib",
+                            "-Wl,-rpath,$ORIGIN/../../../click_amd", "-Wl,-rpath,/opt/rocm/lib", "-o", exe], check=True)
         out.append(exe)
     return out
 

@@ -6,15 +6,16 @@
 // ipoutputcombo.cc:44-205).  Here a chain of glue elements in one thread --
 // member k+1 connected to member k's output 0 -- shares one staged batch:
 //   push     each packet's bytes are gathered once (the most any member reads);
-//   flush    one H2D of the batch; member k's kernel runs over the packets
-//            members 0..k-1 passed on output 0 (its descriptors built on the
-//            host from the members' verdicts, BatchElement::passes()); one D2H
-//            of the rewritten bytes; then each packet is routed once, through
-//            each member's own route() in order (counters, handlers, chatter
-//            exactly as if the member had run it alone), and leaves the chain
-//            at the member and output where the reference would push it.
-// A flush that fails at any step routes nothing: the batch stays staged and
-// the next flush runs it again from the bytes as staged.
+//   flush    one H2D of the batch; every packet enters member 0 and goes on
+//            at once through the members that decide it on the host (span()
+//            false); member k's kernel then runs over the packets that reached
+//            it and wait for the GPU, and routing its verdicts sends each one
+//            on to member k+1 (the next kernel's descriptors) or out of the
+//            chain at member k -- each member's own route() (counters,
+//            handlers, chatter as if it had run alone), in push order per
+//            member; one D2H of the rewritten bytes at the end.
+// A member's GPU step that fails leaves the packets it had not routed in the
+// chain; the next flush builds its batch again and resumes there.
 #include "elements.hh"
 #include "../../include/click_amd_elements.h"
 #include "../csrc/internal.hh"
@@ -34,8 +35,6 @@ static inline double now_s()
 {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-
-void stage_copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail);
 
 template <typename T>
 static int pinned_grow(T **p, size_t *cap, size_t need, size_t keep)
@@ -175,7 +174,7 @@ int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t toke
         err_ = "out of pinned host memory";
         return CLK_EINVAL;
     }
-    stage_copy_bytes(h_arena_ + slot, data, need, length);
+    stage_copy(h_arena_ + slot, data, need, length);
     views0_.push_back(ChainView{data, token, slot, length, nh_offset, (uint16_t)anno});
     staged_.push_back(need);
     back_.push_back(std::min(need, wext_));
@@ -244,33 +243,68 @@ int Chain::grow(size_t bytes, size_t n)
     return 0;
 }
 
-// Member k over the packets that reach it (alive_): its descriptors
-// (chain_build: the class's span()), its kernel, its verdicts back, then its
-// routing (chain_route: the class's route()): output 0 goes on to member k+1
-// with the view the member's output has (strip(), nh_after(), the result's
-// length), anything else leaves the chain at member k.
-// *launched: the member's kernels were queued (a failure after that leaves
-// the device bytes rewritten by them).
+// Member k's per-flush work state.
+void Chain::setup(size_t k)
+{
+    BatchElement *e = m_[k];
+    Member &M = mm_[k];
+    ChainWork &w = M.w;
+    w.views = &views_;
+    w.done = &done_;
+    w.out = &out_;
+    w.h_off = M.h_off, w.h_len = M.h_len, w.h_anno = M.h_anno;
+    w.h_codes = M.h_codes;
+    w.h_sums = e->wants_sums() ? M.h_sums : nullptr;
+    w.member = (int)k;
+    w.strip = e->strip();
+    w.nh_after = e->nh_after();
+    w.last = k + 1 == m_.size();
+    w.inline_ok = !e->has_pre_route_ && !e->has_post_route_;
+    w.report_passes = report_passes_;
+    e->h_aux8_ = M.h_aux8;
+}
+
+// Packet i reaches member k: its descriptor there, or its host decision.  A
+// host decision is routed at once while the member has routed every packet
+// before it (none of them waits for the GPU), so results stay in push order
+// at every member; a packet passed on goes straight to the next member.  A
+// member that decides every packet on the host (IPGWOptions without options,
+// FixIPSrc without the annotation, IPFragmenter within the MTU) so costs no
+// pass of its own.
+void Chain::advance(uint32_t i, size_t k)
+{
+    for (;;) {
+        BatchElement *e = m_[k];
+        ChainWork &w = mm_[k].w;
+        const size_t q = w.reached.size();
+        if (!e->chain_span(w, i) || !w.inline_ok || w.n != 0 || w.routed != q)
+            return;
+        w.routed = q + 1;
+        if (!e->chain_route(w, q))
+            return;
+        k++;
+    }
+}
+
+// Member k's GPU step over the packets that reached it and are not routed
+// yet -- descriptors up, its kernel, its verdicts back -- then their routing
+// (the class's route()): output 0 goes on to member k+1, anything else leaves
+// the chain at member k.  *launched: the member's kernels were queued (a
+// failure after that leaves the device bytes rewritten by them).
 int Chain::run_member(size_t k, bool *launched)
 {
     BatchElement *e = m_[k];
     Member &M = mm_[k];
     ChainWork &w = M.w;
     hipStream_t s = (hipStream_t)clk_ctx_stream(e->ctx_);
-    w.views = &views_;
-    w.reached.assign(alive_.begin(), alive_.end());
-    w.next = &next_;
-    w.h_off = M.h_off, w.h_len = M.h_len, w.h_anno = M.h_anno;
-    w.h_codes = M.h_codes, w.h_sums = M.h_sums;
-    w.member = (int)k;
-    w.last = k + 1 == m_.size();
-    w.report_passes = report_passes_;
-    w.out = &out_;
-    w.done = &done_;
-    e->in_place_ = true;                             // the chain writes the packets back itself
     double t0 = now_s();
-    e->chain_build(w);
-    e->in_place_ = false;
+    if (M.rebuild) {                                 // resumed: a new batch of the packets left
+        M.rebuild = false;
+        std::vector<uint32_t> left(w.reached.begin() + (long)w.routed, w.reached.end());
+        w.reset();
+        for (uint32_t i : left)
+            advance(i, k);
+    }
     stats_[1] += now_s() - t0;
     t0 = now_s();
     M.ms = 0;
@@ -321,23 +355,17 @@ int Chain::run_member(size_t k, bool *launched)
             err_ = e->name() + ": " + e->err_;
             return r;
         }
-    }
-    stats_[2] += now_s() - t0;
-    // route now (the next member's input is what this one passed)
-    t0 = now_s();
-    e->in_place_ = true;                             // the chain writes the packets back itself
-    e->h_aux8_ = M.h_aux8;
-    if (w.n) {
         e->batches_++;
         e->gpu_ns_ += (uint64_t)(M.ms * 1e6);
     }
-    e->chain_route(w);
-    e->in_place_ = false;
-    if (!carry_.empty()) {                           // resumed: the packets it passed before it failed come first
-        next_.insert(next_.begin(), carry_.begin(), carry_.end());
-        carry_.clear();
+    stats_[2] += now_s() - t0;
+    t0 = now_s();
+    const bool more = k + 1 < m_.size();
+    for (size_t q = w.routed; q < w.reached.size(); q++) {
+        w.routed = q + 1;
+        if (e->chain_route(w, q) && more)
+            advance(w.reached[q], k + 1);
     }
-    alive_.swap(next_);
     stats_[6] += now_s() - t0;
     return CLK_SUCCESS;
 }
@@ -383,50 +411,52 @@ int Chain::flush()
     err_.clear();
     const size_t n = views0_.size();
     hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
+    struct InPlace {         // routing: the chain writes the packets back itself
+        std::vector<BatchElement *> &m;
+        explicit InPlace(std::vector<BatchElement *> &v) : m(v) { for (BatchElement *e : m) e->in_place_ = true; }
+        ~InPlace() { for (BatchElement *e : m) e->in_place_ = false; }
+    } in_place(m_);
     size_t k0 = 0;
     if (resume_ >= 0) {
         k0 = (size_t)resume_;
-    } else if (m_[0]->zerocopy_) {
-        if (grow(0, n)) {
+    } else {
+        if (grow(m_[0]->zerocopy_ ? 0 : used_ + 64, n)) {
             err_ = "out of device / pinned memory";
             return CLK_EHIP;
         }
+        if (!m_[0]->zerocopy_) {
+            double t0 = now_s();
+            hipError_t er = glue_checked(hipMemcpyAsync(d_arena_, h_arena_, used_, hipMemcpyHostToDevice, s));
+            if (er != hipSuccess) {
+                (void)hipStreamSynchronize(s);
+                err_ = std::string("hipMemcpyAsync(packets): ") + hipGetErrorString(er);
+                return CLK_EHIP;
+            }
+            stats_[4] += now_s() - t0;
+        }
         views_.assign(views0_.begin(), views0_.end());
-        alive_.resize(n);
-        for (size_t i = 0; i < n; i++)
-            alive_[i] = (uint32_t)i;
         done_.assign(n, 0);
         copied_.assign(n, 0);
-    } else {
-        if (grow(used_ + 64, n)) {
-            err_ = "out of device / pinned memory";
-            return CLK_EHIP;
+        for (size_t k = 0; k < m_.size(); k++) {
+            setup(k);
+            mm_[k].w.reset();
+            mm_[k].rebuild = false;
         }
         double t0 = now_s();
-        hipError_t er = glue_checked(hipMemcpyAsync(d_arena_, h_arena_, used_, hipMemcpyHostToDevice, s));
-        if (er != hipSuccess) {
-            (void)hipStreamSynchronize(s);
-            err_ = std::string("hipMemcpyAsync(packets): ") + hipGetErrorString(er);
-            return CLK_EHIP;
-        }
-        stats_[4] += now_s() - t0;
-        views_.assign(views0_.begin(), views0_.end());
-        alive_.resize(n);
         for (size_t i = 0; i < n; i++)
-            alive_[i] = (uint32_t)i;
-        done_.assign(n, 0);
-        copied_.assign(n, 0);
+            advance((uint32_t)i, 0);
+        stats_[1] += now_s() - t0;
     }
     int failed = CLK_SUCCESS;
     std::string failed_why;
     for (size_t k = k0; k < m_.size(); k++) {
-        if (alive_.empty())
-            break;
+        ChainWork &w = mm_[k].w;
+        if (w.routed == w.reached.size())
+            continue;
         bool launched = false;
         int r = run_member(k, &launched);
         if (r == CLK_SUCCESS)
             continue;
-        ChainWork &w = mm_[k].w;
         if (launched && !m_[k]->idempotent()) {
             // the member's kernel may have rewritten the device bytes: running
             // it again would apply it twice (a second TTL decrement), so the
@@ -439,16 +469,16 @@ int Chain::flush()
                 done_[i] = 1;
                 e->lost_++;
             }
-            alive_.swap(next_);
+            w.routed = w.reached.size();
             failed = r;
             failed_why = err_ + " (its packets were killed, not retried)";
             continue;
         }
-        // the packets at member k that it had not routed yet stay in the
-        // chain (those it decided on the host before the failure are routed;
-        // the ones it passed resume at member k+1)
-        carry_.insert(carry_.end(), next_.begin(), next_.end());
-        alive_.assign(w.reached.begin() + (long)w.routed, w.reached.end());
+        // the packets at member k that it had not routed stay in the chain
+        // (the ones it routed before the failure -- host decisions -- are
+        // routed, and the ones those passed are at the next members already);
+        // the next flush builds member k's batch of them again
+        mm_[k].rebuild = true;
         resume_ = (int)k;
         const std::string why = failed ? failed_why + "; " + err_ : err_;
         (void)copy_back(false);

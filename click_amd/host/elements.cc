@@ -281,43 +281,14 @@ int BatchElement::grow_dev(Stage &g, size_t bytes, size_t n)
     return 0;
 }
 
-// Copy n staged bytes.  Headers (n <= 64) move as whole 16 B pieces when
-// the packet has them (avail: bytes readable from src): fixed-size moves
-// instead of a variable-length memcpy call.  The bytes copied past n stay
-// inside the 64 B of slack every staging slot is grown with and are
-// overwritten by the next packet's slot.
-static inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail)
+bool BatchElement::chain_span(ChainWork &w, uint32_t i)
 {
-    if (n == 0)
-        return;
-    const uint64_t q = ((uint64_t)n + 15) >> 4;
-    if (q <= 4 && 16 * q <= avail) {
-        std::memcpy(dst, src, 16);
-        if (q > 1)
-            std::memcpy(dst + 16, src + 16, 16);
-        if (q > 2)
-            std::memcpy(dst + 32, src + 32, 16);
-        if (q > 3)
-            std::memcpy(dst + 48, src + 48, 16);
-    } else {
-        std::memcpy(dst, src, n);
-    }
+    return chain_span_one(w, i, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); });
 }
 
-void stage_copy_bytes(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail)
+bool BatchElement::chain_route(ChainWork &w, size_t q)
 {
-    stage_copy(dst, src, n, avail);
-}
-
-void BatchElement::chain_build(ChainWork &w)
-{
-    chain_build_loop(w, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); },
-                     [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
-}
-
-void BatchElement::chain_route(ChainWork &w)
-{
-    chain_route_loop(w, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
+    return chain_route_at(w, q, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
 }
 
 template <class SpanF>

@@ -129,6 +129,24 @@ bool parse_int(const std::string &s, long *v);
 bool parse_ip(const std::string &s, uint32_t *saddr);       // raw network-order s_addr
 bool parse_prefix(const std::string &s, uint32_t *saddr, uint32_t *mask);
 
+// Copy n staged bytes.  Spans up to 128 B move as whole 16 B pieces when
+// the packet has them (avail: bytes readable from src): fixed-size moves
+// instead of a variable-length memcpy call.  The bytes copied past n stay
+// inside the 64 B of slack every staging slot is grown with and are
+// overwritten by the next packet's slot.
+inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail)
+{
+    if (n == 0)
+        return;
+    const uint64_t q = ((uint64_t)n + 15) >> 4;
+    if (q <= 8 && 16 * q <= avail) {
+        for (uint64_t k = 0; k < q; k++)
+            std::memcpy(dst + 16 * k, src + 16 * k, 16);
+    } else {
+        std::memcpy(dst, src, n);
+    }
+}
+
 // One member's share of a chain flush (class Chain, chain.cc).
 struct ChainView {           // a packet as a chain member sees it
     uint8_t *data;
@@ -144,23 +162,34 @@ struct ChainExit {           // a result leaving the chain at `member`
 };
 struct ChainWork {
     std::vector<ChainView> *views;            // per chain packet, updated as it passes members
-    std::vector<uint32_t> reached;            // the packets that reach this member, in push order
+    std::vector<uint32_t> reached;            // the packets that reached this member, in push order
     std::vector<int32_t> code;                // per reached packet: GPU index, or -1 - host code
     std::vector<uint32_t> span_off;
-    std::vector<uint32_t> *next;              // chain_route(): the packets that pass, in order
     std::vector<uint8_t> *done;               // per chain packet: has left the chain
-    size_t routed = 0;                        // reached packets chain_build() routed already
+    size_t routed = 0;                        // reached packets routed so far
     uint64_t *h_off = nullptr;                // the member's batch (pinned)
     uint32_t *h_len = nullptr;
     uint8_t *h_anno = nullptr;
     const uint8_t *h_codes = nullptr;
     const uint16_t *h_sums = nullptr;
-    size_t n = 0;
+    size_t n = 0;                             // packets in the member's GPU batch
     uint32_t maxlen = 0;
     std::vector<ChainExit> *out = nullptr;
     int member = 0;
+    uint32_t strip = 0;                       // the member's strip() / nh_after()
+    int32_t nh_after = -2;
     bool last = false;
+    bool inline_ok = false;                   // no pre/post results: a host decision may route at once
     bool report_passes = false;               // a CLK_PORT_NEXT record for each packet passed on
+    void reset()
+    {
+        reached.clear();
+        code.clear();
+        span_off.clear();
+        routed = 0;
+        n = 0;
+        maxlen = 0;
+    }
 };
 
 // The final classes' fast loops: push_burst() and route_stage() over the
@@ -177,15 +206,15 @@ struct ChainWork {
     {                                                                                                           \
         route_loop(g_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
     }                                                                                                           \
-    void chain_build(ChainWork &w_) override                                                                    \
+    bool chain_span(ChainWork &w_, uint32_t i_) override                                                        \
     {                                                                                                           \
-        chain_build_loop(w_, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {                    \
+        return chain_span_one(w_, i_, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {           \
             return this->C::span(p, o, l, c);                                                                   \
-        }, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); });         \
+        });                                                                                                     \
     }                                                                                                           \
-    void chain_route(ChainWork &w_) override                                                                    \
+    bool chain_route(ChainWork &w_, size_t q_) override                                                         \
     {                                                                                                           \
-        chain_route_loop(w_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
+        return chain_route_at(w_, q_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
     }
 
 class BatchElement {
@@ -266,16 +295,17 @@ class BatchElement {
     }
     // the element's kernel writes packet bytes (a chain copies them back)
     virtual bool writes() const { return wants_sums() || wants_arena_back() || !idempotent(); }
-    // a chain's per-member passes (CLK_GLUE_LOOPS inlines the class's span /
-    // route into them): descriptors before the kernel, routing after it
-    virtual void chain_build(ChainWork &w);
-    virtual void chain_route(ChainWork &w);
-    template <class SpanF, class RouteF>
-    void chain_build_loop(ChainWork &w, SpanF &&span_f, RouteF &&route_f);
+    // a chain's per-packet steps (CLK_GLUE_LOOPS inlines the class's span /
+    // route into them).  chain_span(): packet i reaches the member -- its
+    // descriptor, or its host decision; returns true for a host decision.
+    // chain_route(): route reached packet q; returns true when it goes on to
+    // the next member (its view moved past this one).
+    virtual bool chain_span(ChainWork &w, uint32_t i);
+    virtual bool chain_route(ChainWork &w, size_t q);
+    template <class SpanF>
+    bool chain_span_one(ChainWork &w, uint32_t i, SpanF &&span_f);
     template <class RouteF>
-    void chain_route_loop(ChainWork &w, RouteF &&route_f);
-    template <class RouteF>
-    void chain_route_one(ChainWork &w, size_t q, Pending &p, int code, uint16_t sum, RouteF &&route_f);
+    bool chain_route_at(ChainWork &w, size_t q, RouteF &&route_f);
     ResultQueue chain_side_;          // a member's pre/post results while a chain routes
     friend class Chain;
     // after the batch completed, before any packet is routed: nonzero fails
@@ -668,105 +698,67 @@ class IPFragmenter : public BatchElement {
     uint64_t nfrag_ = 0;
 };
 
-// Descriptors of the packets that reach this member.  The leading packets
-// the member decides on the host (span() false) are routed right here, in
-// order, until the first one that needs the GPU (chain_route_loop() routes
-// the rest after the kernel): a member that decides every packet on the host
-// (IPGWOptions without options, FixIPSrc without the annotation,
-// IPFragmenter within the MTU) costs one pass.
-template <class SpanF, class RouteF>
-void BatchElement::chain_build_loop(ChainWork &w, SpanF &&span_f, RouteF &&route_f)
+template <class SpanF>
+inline bool BatchElement::chain_span_one(ChainWork &w, uint32_t i, SpanF &&span_f)
 {
-    const size_t m = w.reached.size();
-    w.code.resize(m);
-    w.span_off.resize(m);
-    w.n = 0;
-    w.maxlen = 0;
-    w.routed = 0;
-    w.next->clear();
-    const bool inline_ok = !has_pre_route_ && !has_post_route_;
-    for (size_t q = 0; q < m; q++) {
-        const ChainView &v = (*w.views)[w.reached[q]];
-        Pending p{v.data, v.token, v.slot, v.length, v.nh, 0, 0, 0, -1, v.anno};
-        uint32_t off = 0, len = 0;
-        int32_t hc = 0;
-        w.span_off[q] = 0;
-        if (!span_f(p, &off, &len, &hc)) {
-            w.code[q] = -1 - hc;                 // decided on the host
-            if (inline_ok && w.n == 0 && w.routed == q) {
-                p.host_code = (int16_t)hc;
-                chain_route_one(w, q, p, hc, 0, route_f);
-                w.routed = q + 1;
-            }
-            continue;
-        }
-        w.h_off[w.n] = v.slot + off;
-        w.h_len[w.n] = len;
-        w.h_anno[w.n] = (uint8_t)v.anno;
-        w.maxlen = std::max(w.maxlen, len);
-        w.span_off[q] = off;
-        w.code[q] = (int32_t)w.n++;
+    const ChainView &v = (*w.views)[i];
+    Pending p{v.data, v.token, v.slot, v.length, v.nh, 0, 0, 0, -1, v.anno};
+    uint32_t off = 0, len = 0;
+    int32_t hc = 0;
+    w.reached.push_back(i);
+    if (!span_f(p, &off, &len, &hc)) {
+        w.code.push_back(-1 - hc);
+        w.span_off.push_back(0);
+        return true;
     }
+    w.h_off[w.n] = v.slot + off;
+    w.h_len[w.n] = len;
+    w.h_anno[w.n] = (uint8_t)v.anno;
+    w.maxlen = std::max(w.maxlen, len);
+    w.span_off.push_back(off);
+    w.code.push_back((int32_t)w.n++);
+    return false;
 }
 
 template <class RouteF>
-inline void BatchElement::chain_route_one(ChainWork &w, size_t q, Pending &p, int code, uint16_t sum, RouteF &&route_f)
+inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_f)
 {
     const uint32_t i = w.reached[q];
+    const int32_t c = w.code[q];
+    const int code = c >= 0 ? w.h_codes[c] : -1 - c;
+    ChainView &v = (*w.views)[i];
+    Pending p{v.data, v.token, v.slot, v.length, v.nh, w.span_off[q], 0, c >= 0 ? (uint32_t)c : 0u,
+              (int16_t)(c >= 0 ? -1 : code), v.anno};
+    Result pr;
+    if (has_pre_route_ && pre_route(p, &pr))
+        w.out->push_back(ChainExit{pr.token, w.member, pr.port, pr.length, pr.aux});
     Result r{p.token, 0, p.length, 0};
     packets_++;
-    route_f(p, code, sum, &r);
-    if (r.port == 0 && !w.last) {
-        ChainView &v = (*w.views)[i];
-        const uint32_t st = strip();
-        const int32_t nha = nh_after();
-        v.data += st;
-        v.slot += st;
+    route_f(p, code, c >= 0 && w.h_sums ? w.h_sums[c] : 0, &r);
+    const bool pass = r.port == 0 && !w.last;
+    if (pass) {
+        v.data += w.strip;
+        v.slot += w.strip;
         v.length = r.length;
-        if (nha != -2)
-            v.nh = nha;
-        w.next->push_back(i);
+        if (w.nh_after != -2)
+            v.nh = w.nh_after;
         if (w.report_passes)
             w.out->push_back(ChainExit{r.token, w.member, CLK_PORT_NEXT, r.length, r.aux});
     } else {
         w.out->push_back(ChainExit{r.token, w.member, r.port, r.length, r.aux});
         (*w.done)[i] = 1;
     }
-}
-
-// Route the packets that reached this member, in push order, from the first
-// one chain_build() left: output 0 goes on to the next member (its view moved
-// past this member), anything else -- and everything at the last member --
-// leaves the chain here.
-template <class RouteF>
-void BatchElement::chain_route_loop(ChainWork &w, RouteF &&route_f)
-{
-    const size_t m = w.reached.size();
-    const bool sums = wants_sums(), pre = has_pre_route_, post = has_post_route_;
-    uint64_t tok[64];
-    int32_t port[64];
-    uint32_t len[64], aux[64];
-    auto side = [&]() {
+    if (has_post_route_) {                    // results that follow the packet's own (fragments)
+        post_route(p, code, chain_side_);
+        uint64_t tok[64];
+        int32_t port[64];
+        uint32_t len[64], aux[64];
         uint64_t got;
         while ((got = chain_side_.pop(tok, port, len, aux, 64)) > 0)
             for (uint64_t k = 0; k < got; k++)
                 w.out->push_back(ChainExit{tok[k], w.member, port[k], len[k], aux[k]});
-    };
-    for (size_t q = w.routed; q < m; q++) {
-        const int32_t c = w.code[q];
-        const int code = c >= 0 ? w.h_codes[c] : -1 - c;
-        const ChainView &v = (*w.views)[w.reached[q]];
-        Pending p{v.data, v.token, v.slot, v.length, v.nh, w.span_off[q], 0, c >= 0 ? (uint32_t)c : 0u,
-                  (int16_t)(c >= 0 ? -1 : code), v.anno};
-        Result pr;
-        if (pre && pre_route(p, &pr))
-            w.out->push_back(ChainExit{pr.token, w.member, pr.port, pr.length, pr.aux});
-        chain_route_one(w, q, p, code, c >= 0 && sums ? w.h_sums[c] : 0, route_f);
-        if (post) {
-            post_route(p, code, chain_side_);
-            side();
-        }
     }
+    return pass;
 }
 
 BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::string &name, int noutputs);
@@ -814,9 +806,12 @@ class Chain {
         size_t cap = 0;
         void *ev[2] = {nullptr, nullptr};
         float ms = 0;
+        bool rebuild = false;                 // resumed: rebuild the batch of the packets not routed
         ChainWork w;
     };
     int grow(size_t bytes, size_t n);
+    void setup(size_t k);
+    void advance(uint32_t i, size_t k);
     int run_member(size_t k, bool *launched);
     int copy_back(bool all);
     uint32_t extent(int32_t nh, uint32_t length);
@@ -832,8 +827,6 @@ class Chain {
     size_t zc_last_bytes_ = 0;
     uint8_t *zc_last_dev_ = nullptr;
     uint64_t zc_gen_ = 0;
-    std::vector<uint32_t> alive_, next_;
-    std::vector<uint32_t> carry_;             // a failed member's packets it had passed already
     uint8_t *h_arena_ = nullptr, *h_back_ = nullptr, *d_arena_ = nullptr;
     size_t h_cap_ = 0, back_cap_ = 0, d_cap_ = 0, used_ = 0;
     std::vector<ChainExit> out_;

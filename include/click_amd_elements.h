@@ -183,7 +183,7 @@ int clk_element_take_messages(clk_element *e, char *buf, size_t cap);
 
 /* ---- chains: consecutive elements on one device-resident batch ----------
  * members[k+1] is connected to members[k]'s output 0, all in one thread and
- * on one context, none ZEROCOPY; an element with extra results after its
+ * on one context, all ZEROCOPY or none; an element with extra results after its
  * packet (IPFragmenter) only as the last member.  The members stay the
  * caller's (configuration, handlers, counters: each counts what it routed,
  * as if it had run alone); the chain never uses their own staging.  A packet
@@ -197,8 +197,11 @@ int clk_element_take_messages(clk_element *e, char *buf, size_t cap);
  * packets are taken with clk_element_take_packet(members[member], aux).
  * The GPU analogue of click-xform's combos (ipinputcombo.cc:66-140,
  * ipoutputcombo.cc:44-205): one gather, one H2D, one D2H and one routing
- * pass per packet instead of one per element.  Results come member by
- * member (each member's in push order, as its outputs see them).  A flush
+ * pass per packet instead of one per element.  Each member's results come
+ * in push order, as its outputs see them, and a packet's results at member
+ * k before those at k+1; results of different members may interleave (a
+ * packet a member decides on the host goes on to the next member at once,
+ * while that member has no packet before it waiting for the GPU).  A flush
  * that fails at member k has routed what left the chain before k (their
  * bytes written back); the packets at k stay in the chain and the next
  * flush resumes there (push refuses packets until it has) -- except after
@@ -223,9 +226,12 @@ int clk_chain_flush(clk_chain *c);
 int clk_chain_report_passes(clk_chain *c, int on);
 uint64_t clk_chain_results(clk_chain *c, uint64_t *tokens, int32_t *members, int32_t *ports,
                            uint32_t *lengths, uint32_t *aux, uint64_t cap);
-/* Host seconds the chain has spent, by phase: staging, descriptors, the
- * members' GPU round trips, next-member views, H2D of the batch, D2H of the
- * rewritten bytes, routing, copy-back into the packets.  Returns 8.       */
+/* Host seconds the chain has spent, by phase: staging (push), the first
+ * pass (every packet into member 0, and through the members that decide it
+ * on the host), the members' GPU round trips, (unused), H2D of the batch,
+ * D2H of the rewritten bytes, routing after each GPU step (with the next
+ * members' descriptors and host decisions), copy-back into the packets.
+ * Returns 8.                                                               */
 int clk_chain_stats(clk_chain *c, double *sec, int n);
 
 #ifdef __cplusplus

@@ -1,0 +1,236 @@
+// -*- c-basic-offset: 4 -*-
+// Native harness (not product code) shared by tests/native/hipcore_test.cc
+// and tests/native/pull_bench.cc: a packet type, the packet-operations trait
+// over it, a lock, and a test "element" (Host<C>) that drives the Click
+// adapter's core (click_integration/elements/hip/hipcore.hh) with element
+// class C's shipped logic (hipclasses.hh) and records its outputs.
+//
+// The test packet models what the classes depend on in Click's Packet:
+// buffers shared by clones until uniqueify() copies them, data()/length()
+// moved by pull()/take(), a network header offset, and an annotation area
+// (paint, dst, ICMP parameter problem, FIX_IP_SRC, packet type, and an id
+// the test traces packets by) that copy_annotations() copies.
+#ifndef CLICK_AMD_TESTS_NATIVE_HARNESS_HH
+#define CLICK_AMD_TESTS_NATIVE_HARNESS_HH
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "click_amd_elements.h"
+#include "../../click_integration/elements/hip/hipcore.hh"
+#include "../../click_integration/elements/hip/hipclasses.hh"
+
+namespace {
+
+struct TAnno {
+    long id = 0;
+    uint32_t paint = 0, dst = 0, prob = 0;
+    bool fix_src = false, bcast = false;
+};
+
+struct TPacket {
+    std::shared_ptr<std::vector<uint8_t> > buf;
+    size_t off = 0, len = 0;
+    long nh = -1;                    // absolute offset of the network header in buf
+    TAnno a;
+};
+
+std::atomic<long> g_live{0};
+std::atomic<long> g_kills{0};        // packets killed (by the core or a class)
+std::atomic<int> g_uniq_fail{0};     // the n-th uniqueify() that must copy fails
+
+TPacket *make(const uint8_t *bytes, size_t len, long id, size_t headroom = 0)
+{
+    TPacket *p = new TPacket;
+    p->buf = std::make_shared<std::vector<uint8_t> >(headroom + len);
+    if (len && bytes)
+        std::memcpy(p->buf->data() + headroom, bytes, len);
+    p->off = headroom;
+    p->len = len;
+    p->a.id = id;
+    g_live++;
+    return p;
+}
+
+// The packet operations trait (hipclasses.hh) over TPacket, as
+// ClickPacketOps is over Click's Packet.
+struct TOps {
+    static TPacket *uniqueify(TPacket *p)
+    {
+        if (p->buf.use_count() > 1) {
+            int v = g_uniq_fail.load();
+            if (v > 0 && g_uniq_fail.fetch_sub(1) == 1) {
+                kill(p);                 // Packet::uniqueify kills on failure
+                return nullptr;
+            }
+            p->buf = std::make_shared<std::vector<uint8_t> >(*p->buf);
+        }
+        return p;
+    }
+    static TPacket *clone(TPacket *p)
+    {
+        TPacket *q = new TPacket(*p);
+        g_live++;
+        return q;
+    }
+    static void kill(TPacket *p)
+    {
+        g_kills++;
+        g_live--;
+        delete p;
+    }
+    static uint8_t *data(TPacket *p) { return p->buf->data() + p->off; }
+    static uint32_t length(TPacket *p) { return (uint32_t)p->len; }
+    static bool has_network_header(TPacket *p) { return p->nh >= 0; }
+    static const uint8_t *network_header(TPacket *p) { return p->buf->data() + p->nh; }
+    static int32_t network_header_offset(TPacket *p) { return (int32_t)(p->nh - (long)p->off); }
+    static int network_length(TPacket *p) { return (int)((long)(p->off + p->len) - p->nh); }
+    static void set_ip_header(TPacket *p, const uint8_t *ip, uint32_t) { p->nh = ip - p->buf->data(); }
+    static void take(TPacket *p, uint32_t n) { p->len -= n; }
+    static void pull(TPacket *p, uint32_t n) { p->off += n, p->len -= n; }
+    static void set_dst_ip_anno(TPacket *p, uint32_t a) { p->a.dst = a; }
+    static uint32_t paint(TPacket *p) { return p->a.paint; }
+    static void set_paint(TPacket *p, uint32_t c) { p->a.paint = c; }
+    static bool fix_ip_src(TPacket *p) { return p->a.fix_src; }
+    static void clear_fix_ip_src(TPacket *p) { p->a.fix_src = false; }
+    static void set_icmp_paramprob(TPacket *p, uint32_t v) { p->a.prob = v; }
+    static bool broadcast_or_multicast(TPacket *p) { return p->a.bcast; }
+    static void copy_annotations(TPacket *to, TPacket *from) { to->a = from->a; }
+    static TPacket *make(uint32_t headroom, uint32_t len) { return ::make(nullptr, len, -1, headroom); }
+};
+
+struct TLock {
+    std::mutex m;
+    void acquire() { m.lock(); }
+    void release() { m.unlock(); }
+};
+
+typedef hipcore::State<TPacket, TLock> St;
+template <class C> class Host;
+
+// The test's "element": HIPBatchElement's host interface, with the outputs
+// recorded (and the thread that pushed each), around class C's shipped logic.
+template <class C>
+class Host {
+  public:
+    typedef hipcore::Core<TPacket, Host<C>, TLock> Core;
+    C cls;
+    Core core;
+    std::vector<St> st;
+    std::mutex out_mu;
+    std::vector<std::vector<TPacket *> > out;          // per output port, in push order
+    std::vector<std::vector<std::thread::id> > out_thread;
+    std::atomic<int> runcount{0};
+    std::deque<TPacket *> input;                        // pull context source
+    std::function<TPacket *()> upstream;                // or another element's pull()
+    std::vector<std::string> chat, msgs;        // (under out_mu: states on several threads)
+    std::atomic<int> wakes{0};
+    void (*on_out0)(Host &, TPacket *) = nullptr;       // re-entrancy probe
+
+    Host(const char *glue_class, const std::string &conf, int noutputs, int nstates = 1)
+        : st(nstates), out(5), out_thread(5)
+    {
+        for (int k = 0; k < nstates; k++) {
+            st[k].id = k;
+            if (clk_ctx_create(0, &st[k].ctx) != CLK_SUCCESS ||
+                clk_element_create(st[k].ctx, glue_class, conf.c_str(), glue_class, noutputs, &st[k].e) !=
+                    CLK_SUCCESS) {
+                std::fprintf(stderr, "create %s(%s): %s\n", glue_class, conf.c_str(), clk_last_error(st[k].ctx));
+                std::exit(3);
+            }
+        }
+        char buf[64];
+        clk_element_read_handler(st[0].e, "batch", buf, sizeof buf);
+        core.set_batch((uint32_t)std::strtoul(buf, nullptr, 10));
+    }
+    ~Host()
+    {
+        for (St &t : st)
+            core.cleanup(*this, t);
+        for (auto &v : out)
+            for (TPacket *p : v)
+                TOps::kill(p);
+    }
+
+    // ---- the core's host interface (as HIPBatchElement / HIPClassElement) -----
+    TPacket *prepare(TPacket *p, uint32_t *anno, TPacket **extra) { return cls.prepare(p, anno, extra); }
+    int32_t nh_offset(TPacket *p) { return cls.nh_offset(p); }
+    bool primary(int32_t port, uint32_t aux) { return cls.primary(port, aux); }
+    TPacket *make_packet(clk_element *e, uint32_t key) { return cls.make_packet(e, key); }
+    int finish(St &t, hipcore::Routed<TPacket> &r, TPacket **o) { return cls.finish(t, r, o); }
+    void end_of_batch(St &t) { cls.end_of_batch(t); }
+    uint8_t *data(TPacket *p) { return TOps::data(p); }
+    uint32_t length(TPacket *p) { return TOps::length(p); }
+    void output_push(int port, TPacket *p)
+    {
+        {
+            std::lock_guard<std::mutex> g(out_mu);
+            out[(size_t)port].push_back(p);
+            out_thread[(size_t)port].push_back(std::this_thread::get_id());
+        }
+        if (port == 0 && on_out0)
+            on_out0(*this, p);
+    }
+    TPacket *input_pull()
+    {
+        if (upstream)
+            return upstream();
+        if (input.empty())
+            return nullptr;
+        TPacket *p = input.front();
+        input.pop_front();
+        return p;
+    }
+    void kill(TPacket *p) { TOps::kill(p); }
+    void adjust_runcount(int d) { runcount += d; }
+    uint64_t now_ns()
+    {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    void wake(St &) { wakes++; }
+    void chatter(const char *s)
+    {
+        std::lock_guard<std::mutex> g(out_mu);
+        chat.push_back(s);
+    }
+    void message(const char *s)
+    {
+        std::lock_guard<std::mutex> g(out_mu);
+        msgs.push_back(s);
+    }
+
+    void push(TPacket *p, int state = 0) { core.push(*this, st[(size_t)state], p); }
+    TPacket *pull(int state = 0) { return core.pull(*this, st[(size_t)state]); }
+    void timer(int state = 0) { core.timer(*this, st[(size_t)state]); }
+    bool poll(int state = 0) { return core.poll(*this, st[(size_t)state]); }
+    bool armed(int state = 0) { return core.armed(st[(size_t)state]); }
+    std::string handler(const char *h, int state = 0)
+    {
+        char buf[256];
+        clk_element_read_handler(st[(size_t)state].e, h, buf, sizeof buf);
+        return buf;
+    }
+};
+
+typedef hipcore::Plain<TPacket, TOps> PlainC;
+typedef hipcore::CheckIPHeaderClass<TPacket, TOps> CheckIPC;
+typedef hipcore::IPInputComboClass<TPacket, TOps> InputComboC;
+typedef hipcore::SetChecksumClass<TPacket, TOps> SetC;
+typedef hipcore::DecIPTTLClass<TPacket, TOps> DecTTLC;
+typedef hipcore::IPGWOptionsClass<TPacket, TOps> GWOptC;
+typedef hipcore::FixIPSrcClass<TPacket, TOps> FixSrcC;
+typedef hipcore::IPOutputComboClass<TPacket, TOps> OutComboC;
+typedef hipcore::IPFragmenterClass<TPacket, TOps> FragC;
+
+}   // namespace
+#endif
