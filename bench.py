@@ -803,7 +803,7 @@ C1_CHAINS = {
     "elements": [("CheckIPHeader", "INTERFACES 18.26.4.1/24 18.26.7.1/24, OFFSET 14", 2),
                  ("IPGWOptions", "18.26.4.24", 2), ("FixIPSrc", "18.26.4.24", 1),
                  ("DecIPTTL", "", 2), ("IPFragmenter", "300", 2)],
-    "combos": [("IPInputCombo", "1, INTERFACES 18.26.4.1/24 18.26.7.1/24", 1),
+    "combos": [("IPInputCombo", "2, INTERFACES 18.26.4.1/24 18.26.7.1/24", 1),
                ("IPOutputCombo", "1, 18.26.4.24, 300", 5)],
 }
 

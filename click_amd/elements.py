@@ -232,6 +232,10 @@ class Chain:
             err.rc = rc
             raise err
 
+    def abandon(self):
+        """Kill every packet still in the chain (clk_chain_abandon); returns the count."""
+        return int(self.lib.clk_chain_abandon(self.h))
+
     def results(self, cap=1 << 20):
         """(tokens, members, ports, lengths, aux) of every routed result, in order."""
         out = []

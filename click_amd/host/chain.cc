@@ -377,8 +377,10 @@ int Chain::copy_back(bool all)
     bool any = false;
     for (size_t i = 0; i < views0_.size() && !any; i++)
         any = back_[i] && !copied_[i] && (all || done_[i]);
-    if (!any)
+    if (!any) {
+        pub_ = out_.size();
         return CLK_SUCCESS;
+    }
     hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
     double t0 = now_s();
     hipError_t er;
@@ -397,6 +399,7 @@ int Chain::copy_back(bool all)
             copied_[i] = 1;
         }
     stats_[7] += now_s() - t0;
+    pub_ = out_.size();                              // every result so far has its bytes
     return CLK_SUCCESS;
 }
 
@@ -465,7 +468,7 @@ int Chain::flush()
             BatchElement *e = m_[k];
             for (size_t q = w.routed; q < w.reached.size(); q++) {
                 const uint32_t i = w.reached[q];
-                out_.push_back(ChainExit{views_[i].token, (int32_t)k, CLK_PORT_KILL, views_[i].length, 0});
+                out_.push_back(ChainExit{views_[i].token, (int32_t)k, CLK_PORT_KILL, views_[i].length, 0, i});
                 done_[i] = 1;
                 e->lost_++;
             }
@@ -501,9 +504,58 @@ int Chain::flush()
     return failed;
 }
 
+// A GPU that keeps failing: every packet still in the chain -- staged, or
+// waiting at the member a failed flush stopped at -- leaves it killed at the
+// member it has reached (counted by that member's "lost" handler), and a
+// packet routed out whose bytes never came back is killed rather than
+// delivered with stale bytes.  Returns the packets killed.
+uint64_t Chain::abandon()
+{
+    uint64_t k = 0;
+    if (resume_ >= 0) {
+        (void)copy_back(false);                      // one more try for the bytes of the routed ones
+        for (size_t j = 0; j < mm_.size(); j++) {
+            ChainWork &w = mm_[j].w;
+            for (size_t q = w.routed; q < w.reached.size(); q++) {
+                const uint32_t i = w.reached[q];
+                if (done_[i])
+                    continue;
+                out_.push_back(ChainExit{views_[i].token, (int32_t)j, CLK_PORT_KILL, views_[i].length, 0, i});
+                done_[i] = 1;
+                m_[j]->lost_++;
+                k++;
+            }
+            w.routed = w.reached.size();
+            mm_[j].rebuild = false;
+        }
+        for (size_t r = pub_; r < out_.size(); r++) {
+            ChainExit &x = out_[r];
+            if (x.idx != ~0u && x.port != CLK_PORT_KILL && x.port != CLK_PORT_NEXT && back_[x.idx] && !copied_[x.idx]) {
+                x.port = CLK_PORT_KILL;
+                m_[(size_t)x.member]->lost_++;
+                k++;
+            }
+        }
+        resume_ = -1;
+    } else {
+        for (size_t i = 0; i < views0_.size(); i++) {
+            out_.push_back(ChainExit{views0_[i].token, 0, CLK_PORT_KILL, views0_[i].length, 0, (uint32_t)i});
+            m_[0]->lost_++;
+            k++;
+        }
+    }
+    pub_ = out_.size();
+    views0_.clear();
+    staged_.clear();
+    back_.clear();
+    used_ = 0;
+    zc_host_ = nullptr;
+    return k;
+}
+
 uint64_t Chain::pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap)
 {
-    const size_t k = (size_t)std::min<uint64_t>(cap, out_.size() - head_);
+    const size_t k = (size_t)std::min<uint64_t>(cap, pub_ - head_);
     for (size_t q = 0; q < k; q++) {
         const ChainExit &x = out_[head_ + q];
         if (tokens) tokens[q] = x.token;
@@ -514,7 +566,7 @@ uint64_t Chain::pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t
     }
     head_ += k;
     if (head_ == out_.size())
-        out_.clear(), head_ = 0;
+        out_.clear(), head_ = 0, pub_ = 0;
     return k;
 }
 
@@ -596,6 +648,11 @@ int clk_chain_report_passes(clk_chain *w, int on)
         return CLK_EINVAL;
     w->c->report_passes(on != 0);
     return CLK_SUCCESS;
+}
+
+uint64_t clk_chain_abandon(clk_chain *w)
+{
+    return w ? w->c->abandon() : 0;
 }
 
 int clk_chain_flush(clk_chain *w)

@@ -992,6 +992,7 @@ void IPInputCombo::route(Pending &p, int code, uint16_t, Result *r)
         r->port = -1;
         return;
     }
+    p.anno = (uint16_t)((p.anno & ~0xFF00u) | CLK_ANNO_PAINT(color_));   // Paint(COLOR), 71: what a chain's next member sees
     // after Strip(14): set_ip_header, shorten to ip_len (125-130)
     const uint32_t plen = p.length - 14;
     const uint32_t len = be16(p.data + 14 + 2);
@@ -1405,8 +1406,10 @@ int FixIPSrc::run(const clk_batch *b, uint8_t *, uint16_t *)
 
 void FixIPSrc::route(Pending &p, int, uint16_t, Result *r)
 {
-    if (p.host_code < 0)
+    if (p.host_code < 0) {
         write_back(p, p.span_len);
+        p.anno &= (uint16_t)~CLK_ANNO_FIX_IP_SRC;           // SET_FIX_IP_SRC_ANNO(p, 0), 50
+    }
     r->port = 0;
 }
 
@@ -1487,6 +1490,7 @@ void IPOutputCombo::route(Pending &p, int code, uint16_t, Result *r)
         return;
     }
     write_back(p, p.span_len);
+    p.anno &= (uint16_t)~CLK_ANNO_FIX_IP_SRC;               // 169-170 (staged packets only reach here)
     if (code == 2)
         r->aux = h_aux8_[p.index];
     r->port = out(code == 0 && p.length > mtu_ ? 4 : code);

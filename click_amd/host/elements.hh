@@ -159,6 +159,7 @@ struct ChainExit {           // a result leaving the chain at `member`
     uint64_t token;
     int32_t member, port;
     uint32_t length, aux;
+    uint32_t idx;            // the packet's place in the batch (~0u: a clone / new packet)
 };
 struct ChainWork {
     std::vector<ChainView> *views;            // per chain packet, updated as it passes members
@@ -731,7 +732,7 @@ inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_
               (int16_t)(c >= 0 ? -1 : code), v.anno};
     Result pr;
     if (has_pre_route_ && pre_route(p, &pr))
-        w.out->push_back(ChainExit{pr.token, w.member, pr.port, pr.length, pr.aux});
+        w.out->push_back(ChainExit{pr.token, w.member, pr.port, pr.length, pr.aux, ~0u});
     Result r{p.token, 0, p.length, 0};
     packets_++;
     route_f(p, code, c >= 0 && w.h_sums ? w.h_sums[c] : 0, &r);
@@ -742,10 +743,11 @@ inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_
         v.length = r.length;
         if (w.nh_after != -2)
             v.nh = w.nh_after;
+        v.anno = p.anno;                      // the annotations the member set / cleared
         if (w.report_passes)
-            w.out->push_back(ChainExit{r.token, w.member, CLK_PORT_NEXT, r.length, r.aux});
+            w.out->push_back(ChainExit{r.token, w.member, CLK_PORT_NEXT, r.length, r.aux, i});
     } else {
-        w.out->push_back(ChainExit{r.token, w.member, r.port, r.length, r.aux});
+        w.out->push_back(ChainExit{r.token, w.member, r.port, r.length, r.aux, i});
         (*w.done)[i] = 1;
     }
     if (has_post_route_) {                    // results that follow the packet's own (fragments)
@@ -756,7 +758,7 @@ inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_
         uint64_t got;
         while ((got = chain_side_.pop(tok, port, len, aux, 64)) > 0)
             for (uint64_t k = 0; k < got; k++)
-                w.out->push_back(ChainExit{tok[k], w.member, port[k], len[k], aux[k]});
+                w.out->push_back(ChainExit{tok[k], w.member, port[k], len[k], aux[k], ~0u});
     }
     return pass;
 }
@@ -782,6 +784,7 @@ class Chain {
     int push_burst(uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets, uint64_t first_token,
                    uint32_t n);
     int flush();
+    uint64_t abandon();
     uint64_t pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap);
     const std::string &last_error() const { return err_; }
     size_t pending() const { return views0_.size(); }
@@ -831,6 +834,7 @@ class Chain {
     size_t h_cap_ = 0, back_cap_ = 0, d_cap_ = 0, used_ = 0;
     std::vector<ChainExit> out_;
     size_t head_ = 0;
+    size_t pub_ = 0;                          // out_[head_, pub_): results whose bytes are back
     double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int32_t ext_nh_ = -3;                     // extent() cache: the nh and length it was computed for
     uint32_t ext_len_ = 0, ext_ = 0, wext_ = 0;

@@ -42,13 +42,25 @@
  * (clk_element_abandon: every held packet killed, counted by the glue's
  * "lost" handler) and the runcount released, so the router can stop.
  *
- * Host interface (all called on the thread that drives the core):
- *   the class hooks of hipclasses.hh -- prepare(), nh_offset(), primary(),
- *        make_packet(), finish(), end_of_batch() -- which the host forwards
- *        to the element class's shipped logic (the Click adapter and the
- *        native test instantiate the same classes)
+ * Chains: a state whose `chain` is set runs its element and the GPU-backed
+ * elements after it on output 0 as one clk_chain (include/
+ * click_amd_elements.h): one staged batch, one flush, results tagged with
+ * the member they leave (mem[k] is member k's glue element on the state's
+ * context).  A packet passed from member k to k+1 comes as a pass record
+ * (CLK_PORT_NEXT): member k's finish() applies its side effects (network
+ * header, trim, Strip, annotations) and nothing is pushed; a result leaving
+ * at member k is finished by member k and pushed on member k's output.  The
+ * host's prepare() readies a packet for the whole chain (writable if any
+ * member writes, the annotations every member reads).
+ *
+ * Host interface (all called on the thread that drives the core; m is the
+ * chain member, 0 without a chain):
+ *   the class hooks of hipclasses.hh -- prepare(), nh_offset(), primary(m,..),
+ *        make_packet(m,..), finish(m,..), end_of_batch(m,..) -- which the
+ *        host forwards to the element class's shipped logic (the Click
+ *        adapter and the native test instantiate the same classes)
  *   uint8_t *data(P *p); uint32_t length(P *p)
- *   void output_push(int port, P *p)             checked_output_push
+ *   void output_push(int m, int port, P *p)      member m's checked_output_push
  *   P *input_pull()                              input(0).pull(0)
  *   void kill(P *p)
  *   void adjust_runcount(int delta)
@@ -56,7 +68,7 @@
  *   void wake(S &t)                              make sure poll(t) runs on t's
  *        thread soon (Click: the state's Task, moved to that RouterThread)
  *   void chatter(const char *text)               the adapter's own messages
- *   void message(const char *line)               the element's chatter lines from the glue
+ *   void message(int m, const char *line)        member m's chatter lines from the glue
  *
  * Latency flush on the state's own thread: a state that holds packets has a
  * deadline (LATENCY after its batch started); poll(t), run by the thread's
@@ -76,6 +88,7 @@
 #include <stdint.h>
 #include <string.h>
 #include <deque>
+#include <string>
 #include <vector>
 #include "click_amd_elements.h"
 
@@ -96,12 +109,16 @@ template <class P> struct Routed {
     uint32_t anno;
     int32_t port;
     uint32_t len, aux;
+    int member;     // chains: the member whose result it is (0: the state's own element)
+    bool pass;      // chains: p went on to the next member (its finish() applies, no push)
     bool end;       // not a result: the end of a batch (host end_of_batch)
 };
 
 template <class P, class L> struct State {
     clk_ctx *ctx;
     clk_element *e;
+    clk_chain *chain;             // set: e heads a chain -- mem[k] is member k's glue element
+    std::vector<clk_element *> mem;   // on ctx (mem[0] == e; the others are the state's own)
     int id;                       // the thread (Click: the RouterThread id)
     std::deque<Held<P> > held;    // held[k] has token base + k
     uint64_t base, next;
@@ -116,7 +133,7 @@ template <class P, class L> struct State {
     P *last_primary;              // route(): the packet of the last primary result
     P *frag_parent;               // host use (IPFragmenter's first-fragment parent)
     L lock;
-    State() : ctx(0), e(0), id(0), base(0), next(0), counted(false), fails(0), draining(false), armed(false),
+    State() : ctx(0), e(0), chain(0), id(0), base(0), next(0), counted(false), fails(0), draining(false), armed(false),
               deadline(0), push_errors(0), last_primary(0), frag_parent(0) { }
 };
 
@@ -225,6 +242,8 @@ template <class P, class Host, class L> class Core {
         t.held.clear();
         for (size_t i = 0; i < t.outbox.size(); i++) {
             R &r = t.outbox[i];
+            if (r.pass)                  // the packet is still held (killed above)
+                continue;
             if (r.p) h.kill(r.p);
             if (r.extra) h.kill(r.extra);
             if (r.made) h.kill(r.made);
@@ -243,6 +262,13 @@ template <class P, class Host, class L> class Core {
             t.counted = false;
             h.adjust_runcount(-1);
         }
+        if (t.chain) {
+            clk_chain_destroy(t.chain);
+            t.chain = 0;
+        }
+        for (size_t m = 1; m < t.mem.size(); m++)
+            clk_element_destroy(t.mem[m]);
+        t.mem.clear();
         if (t.e) {
             clk_element_destroy(t.e);
             t.e = 0;
@@ -301,7 +327,8 @@ template <class P, class Host, class L> class Core {
             t.counted = true;
             arm(h, t);
         }
-        int r = clk_element_push_anno(t.e, h.data(p), h.length(p), h.nh_offset(p), anno, t.next);
+        int r = t.chain ? clk_chain_push_anno(t.chain, h.data(p), h.length(p), h.nh_offset(p), anno, t.next)
+                        : clk_element_push_anno(t.e, h.data(p), h.length(p), h.nh_offset(p), anno, t.next);
         if (r < 0) {                     // not staged
             t.held.pop_back();
             h.kill(p);
@@ -316,7 +343,7 @@ template <class P, class Host, class L> class Core {
             } else if (t.push_errors++ == 0 || (t.push_errors & 0xFFFF) == 0) {
                 char buf[640];           // per-packet errors, once per 65536
                 snprintf(buf, sizeof(buf), "%llu packet(s) not staged: %s", (unsigned long long) t.push_errors,
-                         clk_element_last_error(t.e));
+                         last_error(t).c_str());
                 h.chatter(buf);
             }
             release_if_idle(h, t);
@@ -344,13 +371,14 @@ template <class P, class Host, class L> class Core {
         t.fails++;
         char buf[640];
         if (t.fails >= _max_retries) {
-            uint64_t k = clk_element_abandon(t.e);
+            const std::string why = last_error(t);
+            uint64_t k = t.chain ? clk_chain_abandon(t.chain) : clk_element_abandon(t.e);
             snprintf(buf, sizeof(buf), "GPU batch failed %u times, %llu packets killed: %s", t.fails,
-                     (unsigned long long) k, clk_element_last_error(t.e));
+                     (unsigned long long) k, why.c_str());
             t.fails = 0;
         } else
             snprintf(buf, sizeof(buf), "GPU batch failed (retry %u of %u): %s", t.fails, _max_retries - 1,
-                     clk_element_last_error(t.e));
+                     last_error(t).c_str());
         h.chatter(buf);
     }
 
@@ -360,7 +388,8 @@ template <class P, class Host, class L> class Core {
     {
         if (!t.e)
             return;
-        int r = wait ? clk_element_flush(t.e) : clk_element_flush_async(t.e);
+        // a chain runs its members one after another on the batch: synchronous
+        int r = t.chain ? clk_chain_flush(t.chain) : wait ? clk_element_flush(t.e) : clk_element_flush_async(t.e);
         if (r != CLK_SUCCESS)            // nothing of the failed batch was routed; it stays staged
             failed_flush(h, t);
         else
@@ -382,20 +411,32 @@ template <class P, class Host, class L> class Core {
         }
     }
 
+    static std::string last_error(S &t)
+    {
+        return t.chain ? clk_chain_last_error(t.chain) : clk_element_last_error(t.e);
+    }
+
     // Move the glue's results into the outbox (locked).
     void route(Host &h, S &t)
     {
         enum { CAP = 256 };
         uint64_t tok[CAP];
-        int32_t port[CAP];
+        int32_t mem[CAP], port[CAP];
         uint32_t len[CAP], aux[CAP];
         uint64_t n;
         bool any = false;
-        while ((n = clk_element_results_aux(t.e, tok, port, len, aux, CAP)) > 0) {
+        for (;;) {
+            if (t.chain)
+                n = clk_chain_results(t.chain, tok, mem, port, len, aux, CAP);
+            else if ((n = clk_element_results_aux(t.e, tok, port, len, aux, CAP)) > 0)
+                memset(mem, 0, sizeof(int32_t) * (size_t) n);
+            if (!n)
+                break;
             any = true;
             for (uint64_t i = 0; i < n; i++) {
                 R r;
                 memset(&r, 0, sizeof(r));
+                r.member = mem[i];
                 r.port = port[i];
                 r.len = len[i];
                 r.aux = aux[i];
@@ -403,7 +444,12 @@ template <class P, class Host, class L> class Core {
                 Held<P> *e = have ? &t.held[(size_t) (tok[i] - t.base)] : 0;
                 if (e)
                     r.anno = e->anno;
-                if (h.primary(port[i], aux[i])) {
+                if (port[i] == CLK_PORT_NEXT) {  // chains: on to the next member, still held
+                    r.pass = true;
+                    r.port = CLK_PORT_OUT0;
+                    r.p = e ? e->p : 0;
+                    t.last_primary = r.p;
+                } else if (h.primary(r.member, port[i], aux[i])) {
                     if (e) {
                         r.p = e->p;
                         e->p = 0;
@@ -419,7 +465,7 @@ template <class P, class Host, class L> class Core {
                         e->extra = 0;
                     }
                 } else {                 // a new packet made by the element
-                    r.made = h.make_packet(t.e, aux[i]);
+                    r.made = h.make_packet(r.member, t.chain ? t.mem[(size_t) r.member] : t.e, aux[i]);
                     r.parent = t.last_primary;
                 }
                 t.outbox.push_back(r);
@@ -437,16 +483,18 @@ template <class P, class Host, class L> class Core {
             end.end = true;
             t.outbox.push_back(end);
         }
-        // the element's click_chatter lines (e.g. the first drop's reason)
+        // the elements' click_chatter lines (e.g. the first drop's reason)
         char buf[8192];
-        if (clk_element_take_messages(t.e, buf, sizeof(buf)) > 0)
-            for (char *s = buf, *e; *s; s = e) {
-                if (!(e = strchr(s, '\n')))
-                    e = s + strlen(s);
-                else
-                    *e++ = 0;
-                h.message(s);
-            }
+        const size_t nm = t.chain ? t.mem.size() : 1;
+        for (size_t m = 0; m < nm; m++)
+            if (clk_element_take_messages(t.chain ? t.mem[m] : t.e, buf, sizeof(buf)) > 0)
+                for (char *s = buf, *e; *s; s = e) {
+                    if (!(e = strchr(s, '\n')))
+                        e = s + strlen(s);
+                    else
+                        *e++ = 0;
+                    h.message((int) m, s);
+                }
     }
 
     // Deliver the outbox in order, without the lock.  Re-entrant calls on
@@ -467,19 +515,21 @@ template <class P, class Host, class L> class Core {
             for (size_t i = 0; i < work.size(); i++) {
                 R &r = work[i];
                 if (r.end) {
-                    h.end_of_batch(t);
+                    const size_t nm = t.chain ? t.mem.size() : 1;
+                    for (size_t m = 0; m < nm; m++)
+                        h.end_of_batch((int) m, t);
                     continue;
                 }
                 P *out = 0;
-                int port = h.finish(t, r, &out);
-                if (port < 0 || !out)
+                int port = h.finish(r.member, t, r, &out);
+                if (r.pass || port < 0 || !out)  // a pass: the member's side effects only
                     continue;
-                if (pull_ctx && port == 0) {
+                if (pull_ctx && port == 0 && r.member + 1 == (int) (t.chain ? t.mem.size() : 1)) {
                     t.lock.acquire();
                     t.ready.push_back(out);
                     t.lock.release();
                 } else
-                    h.output_push(port, out);
+                    h.output_push(r.member, port, out);
             }
             work.clear();
             t.lock.acquire();

@@ -218,6 +218,13 @@ int clk_chain_push_anno(clk_chain *c, uint8_t *data, uint32_t length, int32_t nh
 int clk_chain_push_burst(clk_chain *c, uint8_t *const *datas, const uint32_t *lengths,
                          const int32_t *nh_offsets, uint64_t first_token, uint32_t n);
 int clk_chain_flush(clk_chain *c);
+/* A GPU that keeps failing: every packet still in the chain (staged, or at
+ * the member a failed flush stopped at) becomes a CLK_PORT_KILL result at
+ * the member it has reached, counted by that member's "lost" handler; so
+ * does a packet routed out whose rewritten bytes could not be copied back
+ * (results are only handed out once their bytes are back).  Returns the
+ * packets killed.                                                          */
+uint64_t clk_chain_abandon(clk_chain *c);
 /* on != 0: every member also reports each packet it passes on to the next
  * member (port CLK_PORT_NEXT, length as the next member sees it), in its
  * place among the member's results -- so a host that applies each element's

@@ -164,13 +164,13 @@ class Host {
     // ---- the core's host interface (as HIPBatchElement / HIPClassElement) -----
     TPacket *prepare(TPacket *p, uint32_t *anno, TPacket **extra) { return cls.prepare(p, anno, extra); }
     int32_t nh_offset(TPacket *p) { return cls.nh_offset(p); }
-    bool primary(int32_t port, uint32_t aux) { return cls.primary(port, aux); }
-    TPacket *make_packet(clk_element *e, uint32_t key) { return cls.make_packet(e, key); }
-    int finish(St &t, hipcore::Routed<TPacket> &r, TPacket **o) { return cls.finish(t, r, o); }
-    void end_of_batch(St &t) { cls.end_of_batch(t); }
+    bool primary(int, int32_t port, uint32_t aux) { return cls.primary(port, aux); }
+    TPacket *make_packet(int, clk_element *e, uint32_t key) { return cls.make_packet(e, key); }
+    int finish(int, St &t, hipcore::Routed<TPacket> &r, TPacket **o) { return cls.finish(t, r, o); }
+    void end_of_batch(int, St &t) { cls.end_of_batch(t); }
     uint8_t *data(TPacket *p) { return TOps::data(p); }
     uint32_t length(TPacket *p) { return TOps::length(p); }
-    void output_push(int port, TPacket *p)
+    void output_push(int, int port, TPacket *p)
     {
         {
             std::lock_guard<std::mutex> g(out_mu);
@@ -203,7 +203,7 @@ class Host {
         std::lock_guard<std::mutex> g(out_mu);
         chat.push_back(s);
     }
-    void message(const char *s)
+    void message(int, const char *s)
     {
         std::lock_guard<std::mutex> g(out_mu);
         msgs.push_back(s);
@@ -231,6 +231,123 @@ typedef hipcore::IPGWOptionsClass<TPacket, TOps> GWOptC;
 typedef hipcore::FixIPSrcClass<TPacket, TOps> FixSrcC;
 typedef hipcore::IPOutputComboClass<TPacket, TOps> OutComboC;
 typedef hipcore::IPFragmenterClass<TPacket, TOps> FragC;
+
+// A chain of elements in one thread (hipcore.hh chains): the core's state
+// heads the chain, member k is class logic of its own with outputs the test
+// records; prepare() readies a packet for the whole chain, as the Click
+// adapter's head does (writable if any member writes, the annotations any
+// member reads).
+struct MemberBase {
+    std::vector<std::vector<TPacket *> > out = std::vector<std::vector<TPacket *> >(5);
+    std::string glue, conf;
+    int noutputs = 2;
+    virtual ~MemberBase() {}
+    virtual TPacket *prepare(TPacket *p, uint32_t *anno, TPacket **extra) = 0;
+    virtual int32_t nh_offset(TPacket *p) = 0;
+    virtual bool primary(int32_t port, uint32_t aux) = 0;
+    virtual TPacket *make_packet(clk_element *e, uint32_t key) = 0;
+    virtual int finish(St &t, hipcore::Routed<TPacket> &r, TPacket **o) = 0;
+    virtual void end_of_batch(St &t) = 0;
+    virtual bool may_write() const = 0;
+};
+
+template <class C> struct Member : MemberBase {
+    C cls;
+    Member(const char *g, const std::string &c, int nout) { glue = g, conf = c, noutputs = nout; }
+    TPacket *prepare(TPacket *p, uint32_t *anno, TPacket **extra) override { return cls.prepare(p, anno, extra); }
+    int32_t nh_offset(TPacket *p) override { return cls.nh_offset(p); }
+    bool primary(int32_t port, uint32_t aux) override { return cls.primary(port, aux); }
+    TPacket *make_packet(clk_element *e, uint32_t key) override { return cls.make_packet(e, key); }
+    int finish(St &t, hipcore::Routed<TPacket> &r, TPacket **o) override { return cls.finish(t, r, o); }
+    void end_of_batch(St &t) override { cls.end_of_batch(t); }
+    bool may_write() const override { return C::may_write != 0; }
+};
+
+class ChainHost {
+  public:
+    typedef hipcore::Core<TPacket, ChainHost, TLock> Core;
+    std::vector<MemberBase *> m;                        // not owned
+    Core core;
+    St st;
+    std::atomic<int> runcount{0};
+    std::vector<std::string> chat, msgs;
+
+    explicit ChainHost(const std::vector<MemberBase *> &members) : m(members)
+    {
+        if (clk_ctx_create(0, &st.ctx) != CLK_SUCCESS) {
+            std::fprintf(stderr, "ctx: %s\n", clk_last_error(0));
+            std::exit(3);
+        }
+        for (MemberBase *x : m) {
+            clk_element *e = nullptr;
+            if (clk_element_create(st.ctx, x->glue.c_str(), x->conf.c_str(), x->glue.c_str(), x->noutputs, &e) !=
+                CLK_SUCCESS) {
+                std::fprintf(stderr, "create %s(%s): %s\n", x->glue.c_str(), x->conf.c_str(), clk_last_error(st.ctx));
+                std::exit(3);
+            }
+            st.mem.push_back(e);
+        }
+        st.e = st.mem[0];
+        if (clk_chain_create(st.mem.data(), (int)st.mem.size(), &st.chain) != CLK_SUCCESS) {
+            std::fprintf(stderr, "chain: %s\n", clk_last_error(0));
+            std::exit(3);
+        }
+        clk_chain_report_passes(st.chain, 1);
+        char buf[64];
+        clk_element_read_handler(st.e, "batch", buf, sizeof buf);
+        core.set_batch((uint32_t)std::strtoul(buf, nullptr, 10));
+    }
+    ~ChainHost()
+    {
+        core.cleanup(*this, st);
+        for (MemberBase *x : m)
+            for (auto &v : x->out)
+                for (TPacket *p : v)
+                    TOps::kill(p);
+    }
+
+    TPacket *prepare(TPacket *p, uint32_t *anno, TPacket **extra)
+    {
+        if (!(p = m[0]->prepare(p, anno, extra)))
+            return nullptr;
+        bool w = false;
+        for (size_t k = 1; k < m.size(); k++)
+            w = w || m[k]->may_write();
+        if (w && !(p = TOps::uniqueify(p)))
+            return nullptr;
+        *anno |= (TOps::fix_ip_src(p) ? CLK_ANNO_FIX_IP_SRC : 0u) | (TOps::broadcast_or_multicast(p) ? CLK_ANNO_BCAST : 0u) |
+                 CLK_ANNO_PAINT(TOps::paint(p));
+        return p;
+    }
+    int32_t nh_offset(TPacket *p) { return m[0]->nh_offset(p); }
+    bool primary(int k, int32_t port, uint32_t aux) { return m[(size_t)k]->primary(port, aux); }
+    TPacket *make_packet(int k, clk_element *e, uint32_t key) { return m[(size_t)k]->make_packet(e, key); }
+    int finish(int k, St &t, hipcore::Routed<TPacket> &r, TPacket **o) { return m[(size_t)k]->finish(t, r, o); }
+    void end_of_batch(int k, St &t) { m[(size_t)k]->end_of_batch(t); }
+    uint8_t *data(TPacket *p) { return TOps::data(p); }
+    uint32_t length(TPacket *p) { return TOps::length(p); }
+    void output_push(int k, int port, TPacket *p) { m[(size_t)k]->out[(size_t)port].push_back(p); }
+    TPacket *input_pull() { return nullptr; }
+    void kill(TPacket *p) { TOps::kill(p); }
+    void adjust_runcount(int d) { runcount += d; }
+    uint64_t now_ns()
+    {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    void wake(St &) {}
+    void chatter(const char *s) { chat.push_back(s); }
+    void message(int k, const char *s) { msgs.push_back(std::to_string(k) + ": " + s); }
+
+    void push(TPacket *p) { core.push(*this, st, p); }
+    void timer() { core.timer(*this, st); }
+    std::string handler(int k, const char *h)
+    {
+        char buf[256];
+        clk_element_read_handler(st.mem[(size_t)k], h, buf, sizeof buf);
+        return buf;
+    }
+};
 
 }   // namespace
 #endif

@@ -837,6 +837,105 @@ void cleanup_partial()
     report("cleanup_kills_held_packets_pushes_nothing", ok);
 }
 
+// 12. a chain (hipcore chains): CheckIPHeader -> IPGWOptions -> FixIPSrc ->
+//     DecIPTTL -> IPFragmenter run by one state as a clk_chain, against the
+//     same classes as five separate elements, each pushed what the one before
+//     put out on output 0.  Every member's every output: the same packets in
+//     the same order, byte for byte, with the same length, network header and
+//     annotations; the members' handlers agree.
+bool same_packet(const TPacket *a, const TPacket *b)
+{
+    return a->a.id == b->a.id && a->len == b->len && (a->nh - (long)a->off) == (b->nh - (long)b->off) &&
+           a->a.dst == b->a.dst && a->a.fix_src == b->a.fix_src && a->a.prob == b->a.prob &&
+           a->a.paint == b->a.paint && std::memcmp(a->buf->data() + a->off, b->buf->data() + b->off, a->len) == 0;
+}
+
+void chain_vs_elements(uint32_t batch, uint32_t flush_every)
+{
+    bool ok = true;
+    const int n = 2500;
+    const std::string B = "BATCH " + std::to_string(batch);
+    Member<CheckIPC> c0("CheckIPHeader", "DETAILS true, " + B, 2);
+    Member<GWOptC> c1("IPGWOptions", std::string(MY_IP_TXT) + ", " + B, 2);
+    Member<FixSrcC> c2("FixIPSrc", std::string(MY_IP_TXT) + ", " + B, 1);
+    Member<DecTTLC> c3("DecIPTTL", B, 2);
+    Member<FragC> c4("IPFragmenter", "576, " + B, 2);
+    c4.cls.mtu = 576;
+    ChainHost ch({&c0, &c1, &c2, &c3, &c4});
+    Host<CheckIPC> h0("CheckIPHeader", "DETAILS true, " + B, 2);
+    Host<GWOptC> h1("IPGWOptions", std::string(MY_IP_TXT) + ", " + B, 2);
+    Host<FixSrcC> h2("FixIPSrc", std::string(MY_IP_TXT) + ", " + B, 1);
+    Host<DecTTLC> h3("DecIPTTL", B, 2);
+    Host<FragC> h4("IPFragmenter", "576, " + B, 2);
+    h4.cls.mtu = 576;
+    for (int i = 0; i < n; i++) {
+        std::vector<uint8_t> b = ip_bytes(40 + (uint32_t)(i * 53) % 1400, i);
+        if (i % 7 == 3)
+            b = with_options(b, 1 + i % 4);
+        if (i % 11 == 5) {                           // TTL 0-2: DecIPTTL's output 1
+            b[8] = (uint8_t)(i % 3);
+            oracle_set_ip_checksum(b.data(), (uint32_t)b.size());
+        }
+        if (i % 9 == 1) {                            // DF: IPFragmenter's output 1 when too long
+            b[6] |= 0x40;
+            oracle_set_ip_checksum(b.data(), (uint32_t)b.size());
+        }
+        if (i % 13 == 6)
+            b[12] ^= 1;                              // a bad checksum: CheckIPHeader's output 1
+        for (int run = 0; run < 2; run++) {
+            TPacket *p = make(b.data(), b.size(), i);
+            p->a.fix_src = i % 4 == 0;
+            p->a.paint = (uint32_t)(i % 3);
+            if (run == 0) {
+                ch.push(p);
+                if (flush_every && (i + 1) % flush_every == 0)
+                    ch.timer();
+            } else
+                h0.push(p);
+        }
+    }
+    ch.timer();
+    h0.timer();
+    // the separate elements: each takes what the one before put out on output 0
+    auto feed = [](std::vector<TPacket *> &from, auto &to) {
+        for (TPacket *p : from)
+            to.push(p);
+        from.clear();
+        to.timer();
+    };
+    feed(h0.out[0], h1);
+    feed(h1.out[0], h2);
+    feed(h2.out[0], h3);
+    feed(h3.out[0], h4);
+    std::vector<std::vector<std::vector<TPacket *> > *> sep = {&h0.out, &h1.out, &h2.out, &h3.out, &h4.out};
+    size_t total = 0;
+    for (size_t k = 0; k < 5; k++)
+        for (size_t q = 0; q < 5; q++) {
+            const std::vector<TPacket *> &x = ch.m[k]->out[q], &y = (*sep[k])[q];
+            CHECK(x.size() == y.size());
+            for (size_t j = 0; j < x.size() && j < y.size(); j++)
+                if (!same_packet(x[j], y[j])) {
+                    std::printf("  member %zu port %zu #%zu: id %ld / %ld\n", k, q, j, x[j]->a.id, y[j]->a.id);
+                    CHECK(same_packet(x[j], y[j]));
+                    break;
+                }
+            total += x.size();
+        }
+    CHECK(!ch.m[0]->out[1].empty() && !ch.m[3]->out[1].empty() && !ch.m[4]->out[1].empty());
+    CHECK(ch.m[4]->out[0].size() > (size_t)n / 2);
+    const char *hs[] = {"drops", "drop_details", "packets", "fragments"};
+    CHECK(ch.handler(0, "drops") == h0.handler("drops") && ch.handler(0, "drop_details") == h0.handler("drop_details"));
+    CHECK(ch.handler(1, "drops") == h1.handler("drops") && ch.handler(3, "drops") == h3.handler("drops"));
+    CHECK(ch.handler(4, "fragments") == h4.handler("fragments") && ch.handler(4, "drops") == h4.handler("drops"));
+    for (const char *h : hs)
+        CHECK(ch.handler(2, h) == h2.handler(h));
+    CHECK(ch.runcount == 0 && h0.runcount == 0);
+    CHECK(total > (size_t)n);
+    std::string label = "chain_of_five_matches_separate_elements_batch_" + std::to_string(batch) +
+                        (flush_every ? "_flush_" + std::to_string(flush_every) : std::string());
+    report(label.c_str(), ok);
+}
+
 }   // namespace
 
 int main()
@@ -863,6 +962,9 @@ int main()
     reentrant_push();
     threads();
     cleanup_partial();
+    chain_vs_elements(65536, 0);
+    chain_vs_elements(300, 0);
+    chain_vs_elements(1000, 777);
     std::printf("live packets at exit: %ld\n", (long)g_live);
     return g_fail ? 1 : 0;
 }

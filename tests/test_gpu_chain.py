@@ -66,11 +66,12 @@ def run_separate(ctx, spec, arena, foff, flen, nh0, anno):
     ptr = [base + int(foff[i]) for i in range(n)]
     ln = [int(flen[i]) for i in range(n)]
     nh = [nh0] * n
+    anno = [int(a) for a in anno]
     out = []                                    # member-major: each member's results in its own order
     alive = list(range(n))
     for k, e in enumerate(els):
         for i in alive:
-            rc = e.lib.clk_element_push_anno(e.h, ctypes.c_void_p(ptr[i]), ln[i], nh[i], int(anno[i]), i)
+            rc = e.lib.clk_element_push_anno(e.h, ctypes.c_void_p(ptr[i]), ln[i], nh[i], anno[i], i)
             assert rc >= 0
             if rc == 1:
                 e.flush()
@@ -91,6 +92,10 @@ def run_separate(ctx, spec, arena, foff, flen, nh0, anno):
                 if cls == "IPInputCombo":
                     ptr[t] += 14
                     nh[t] = 0
+                    color = int(spec[k][1].split(",")[0])
+                    anno[t] = (anno[t] & ~0xFF00) | ((color & 0xFF) << 8)    # Paint(COLOR)
+                if cls == "FixIPSrc" and anno[t] & 1 and 0 <= nh[t] < ln[t]:
+                    anno[t] &= ~1                                           # the fixed source clears FIX_IP_SRC
                 ln[t] = l_
                 nxt.append(t)
                 continue
@@ -147,7 +152,7 @@ def compare_chain(ctx, spec, arena, foff, flen, nh0=-1, anno=None, batch_flush=N
 FAKE_IPROUTER = [("CheckIPHeader", "INTERFACES 18.26.4.1/24 18.26.7.1/24, OFFSET 14", 2),
                  ("IPGWOptions", MY_IP_TXT, 2), ("FixIPSrc", MY_IP_TXT, 1), ("DecIPTTL", "", 2),
                  ("IPFragmenter", "300", 2)]
-COMBOS = [("IPInputCombo", "1, INTERFACES 18.26.4.1/24 18.26.7.1/24", 1),
+COMBOS = [("IPInputCombo", "2, INTERFACES 18.26.4.1/24 18.26.7.1/24", 1),
           ("IPOutputCombo", "1, %s, 300" % MY_IP_TXT, 5)]
 
 
@@ -227,7 +232,7 @@ def test_fuzzed_combos_chain(ctx):
     n = len(foff)
     anno = np.array([anno_paint(int(p)) for p in rng.integers(0, 3, n)], np.uint32) + \
         (rng.random(n) < 0.05) * ANNO_BCAST + (rng.random(n) < 0.2).astype(np.uint32)
-    spec = [("IPInputCombo", "2", 1), ("IPOutputCombo", "1, %s, 120" % MY_IP_TXT, 5)]
+    spec = [("IPInputCombo", "1", 1), ("IPOutputCombo", "1, %s, 120" % MY_IP_TXT, 5)]
     r = compare_chain(ctx, spec, arena, foff, flen, anno=anno, handlers=("drops", "packets", "lost"))
     assert {p for _, m, p, _, _ in r if m == 1} >= {-1, 0, 1, 2, 3, 4}
 
@@ -241,15 +246,17 @@ def test_check_then_set_chain(ctx):
     compare_chain(ctx, spec, a3, o3, c3, nh0=0)
 
 
-@pytest.mark.parametrize("nth", [1, 2, 4, 6, 8])
+@pytest.mark.parametrize("nth", [1, 2, 4, 6, 8, 11])
 def test_chain_failed_flush(ctx, nth):
     """The nth checked HIP call of a chain flush fails (fake-iprouter chain:
     1 the batch's H2D, 2 CheckIPHeader's descriptors, 4 its verdicts back,
-    6 DecIPTTL's descriptors, 8 its verdicts back).  Before any kernel of a
-    member that is not idempotent ran (1-6): nothing is routed, nothing
-    written, push() refuses packets, and the next flush resumes and routes
-    every packet exactly as a chain that never failed.  After DecIPTTL's
-    kernel (8): its packets are killed, never decremented twice."""
+    6 DecIPTTL's descriptors, 8 its verdicts back, 11 the rewritten bytes
+    back).  Before any kernel of a member that is not idempotent ran (1-6):
+    nothing is routed, nothing written, push() refuses packets, and the next
+    flush resumes and routes every packet exactly as a chain that never
+    failed.  After DecIPTTL's kernel (8): its packets are killed, never
+    decremented twice.  The copy back (11): no result is handed out before
+    its bytes are back; the next flush copies them and hands them all out."""
     from click_amd import ClickAmdError
     from click_amd.elements import Chain
     arena, foff, flen = fake_frames(3000)
@@ -299,7 +306,7 @@ def test_zerocopy_chain(ctx, which):
         n = len(foff)
         anno = np.array([anno_paint(int(p)) for p in rng.integers(0, 3, n)], np.uint32) + \
             (rng.random(n) < 0.05) * ANNO_BCAST + (rng.random(n) < 0.2).astype(np.uint32)
-        spec = [("IPInputCombo", "2", 1), ("IPOutputCombo", "1, %s, 120" % MY_IP_TXT, 5)]
+        spec = [("IPInputCombo", "1", 1), ("IPOutputCombo", "1, %s, 120" % MY_IP_TXT, 5)]
     else:
         arena0, foff, flen = fake_frames(20000)
         anno = np.zeros(len(foff), np.uint32)
@@ -339,3 +346,40 @@ def test_chain_refuses(ctx):
     with pytest.raises(ClickAmdError, match="one context"):
         Chain([Element(ctx, "CheckIPHeader", "", noutputs=2), Element(other, "DecIPTTL", "", noutputs=2)])
     other.close()
+
+
+def test_chain_abandon(ctx):
+    """A chain whose flush keeps failing gives its packets up
+    (clk_chain_abandon): each is killed at the member it reached and counted
+    by that member's "lost" handler; the chain then takes packets again."""
+    from click_amd import ClickAmdError
+    from click_amd.elements import Chain
+    arena, foff, flen = fake_frames(2000)
+    before = arena.copy()
+    els = make(ctx, FAKE_IPROUTER)
+    ch = Chain(els)
+    base = arena.ctypes.data
+    for i in range(len(foff)):
+        ch.push_anno(base + int(foff[i]), int(flen[i]), -1, 0, i)
+    hook = ctx.lib.clk_glue_inject_fault_internal
+    hook.argtypes, hook.restype = [ctypes.c_int], None
+    hook(6)                                     # DecIPTTL's descriptors: the packets wait at member 3
+    try:
+        with pytest.raises(ClickAmdError):
+            ch.flush()
+    finally:
+        hook(0)
+    assert ch.abandon() == 2000
+    tok, mem, port, _, _ = ch.results()
+    assert len(tok) == 2000 and (mem == 3).all() and (port == -1).all()
+    assert np.array_equal(arena, before)
+    assert els[3].read_handler("lost") == "2000" and els[0].read_handler("lost") == "0"
+    assert ch.abandon() == 0
+    for i in range(len(foff)):                  # the chain works again
+        ch.push_anno(base + int(foff[i]), int(flen[i]), -1, 0, i)
+    ch.flush()
+    tok, mem, port, _, _ = ch.results()
+    assert len(tok) == 2000 and (mem == 4).all() and (port == 0).all()
+    ch.close()
+    for e in els:
+        e.close()

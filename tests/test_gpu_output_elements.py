@@ -215,7 +215,8 @@ def test_fake_iprouter_through_the_glue(ctx):
     """iprouter-01: the forwarding path of conf/fake-iprouter.click through
     the element glue, once as Strip(14) + CheckIPHeader(INTERFACES ...) ->
     IPGWOptions -> FixIPSrc -> DecIPTTL -> IPFragmenter(300) and once as
-    IPInputCombo -> IPOutputCombo(1, 18.26.4.24, 300): all 60,000 frames
+    IPInputCombo(2, ...) -> IPOutputCombo(1, 18.26.4.24, 300) (xform-ip-01:282,285;
+    painted 2, not redirected by the colour-1 PaintTee): all 60,000 frames
     forwarded on port 0, identical bytes both ways."""
     import json
     import os
@@ -229,7 +230,7 @@ def test_fake_iprouter_through_the_glue(ctx):
         arena = np.tile(np.frombuffer(frame, np.uint8), n).copy()
         foff = np.arange(n, dtype=np.uint64) * len(frame)
         flen = np.full(n, len(frame), np.uint32)
-        chain = ([("IPInputCombo", "1, INTERFACES 18.26.4.1/24 18.26.7.1/24", 1, 14),
+        chain = ([("IPInputCombo", "2, INTERFACES 18.26.4.1/24 18.26.7.1/24", 1, 14),
                   ("IPOutputCombo", "1, 18.26.4.24, 300", 5, 14)] if combo else
                  [("CheckIPHeader", "INTERFACES 18.26.4.1/24 18.26.7.1/24, OFFSET 14", 2, 14),
                   ("IPGWOptions", "18.26.4.24", 2, 14), ("FixIPSrc", "18.26.4.24", 1, 14),
