@@ -12,6 +12,7 @@
 #include <click/error.hh>
 #include <click/glue.hh>
 #include <click/router.hh>
+#include <click/routervisitor.hh>
 #include <click/straccum.hh>
 #include <stdlib.h>
 #include <string.h>
@@ -19,13 +20,15 @@
 CLICK_DECLS
 
 HIPBatchElement::HIPBatchElement()
-    : _device(-1), _latency_ms(1), _retries(3), _pt(0), _tasks(0), _npt(0), _gate(0)
+    : _device(-1), _latency_ms(1), _retries(3), _pt(0), _tasks(0), _npt(0), _gate(0), _chain_conf(true),
+      _chain_tried(0)
 {
 }
 
 HIPBatchElement::~HIPBatchElement()
 {
     delete[] _pt;
+    delete[] _chain_tried;
     if (_tasks) {
 	for (int k = 0; k < _npt; k++)
 	    _tasks[k].~Task();
@@ -44,6 +47,7 @@ HIPBatchElement::configure(Vector<String> &conf, ErrorHandler *errh)
 	.read("LATENCY", _latency_ms)
 	.read("DEVICE", _device)
 	.read("RETRIES", _retries)
+	.read("CHAIN", _chain_conf)
 	.consume() < 0)
 	return -1;
     _glue_conf = cp_unargvec(conf);
@@ -113,7 +117,136 @@ HIPBatchElement::initialize(ErrorHandler *errh)
     char buf[64];			// BATCH, parsed by the glue
     clk_element_read_handler(_pt[home].e, "batch", buf, sizeof(buf));
     _core.set_batch(strtoul(buf, 0, 10));
+    // a chain head collects the members down output 0 (the connections and
+    // every element's configuration exist now; the states set their chains
+    // up on first use, when every member is initialized)
+    _chain_tried = new bool[_npt];
+    for (int k = 0; k < _npt; k++)
+	_chain_tried[k] = false;
+    _chain.clear();
+    _chain.push_back(this);
+    if (_chain_conf && !chain_member())
+	for (HIPBatchElement *x = this, *y; !x->cls_chain_last() && (y = x->chain_next()); x = y)
+	    _chain.push_back(y);
     return 0;
+}
+
+void *
+HIPBatchElement::cast(const char *n)
+{
+    if (strcmp(n, "HIPBatchElement") == 0)
+	return this;
+    return Element::cast(n);
+}
+
+namespace {
+// the output ports connected to one input port
+struct UpstreamPorts : public RouterVisitor {
+    int n;
+    Element *first;
+    UpstreamPorts() : n(0), first(0) { }
+    bool visit(Element *e, bool isoutput, int, Element *, int, int distance) {
+	if (isoutput && distance == 1 && n++ == 0)
+	    first = e;
+	return false;
+    }
+};
+}
+
+// The GPU-backed element this one's output 0 pushes into, if it can join
+// this one's chain: its input 0, fed by nothing else, CHAIN true, the same
+// DEVICE, not an element that only starts chains.
+HIPBatchElement *
+HIPBatchElement::chain_next()
+{
+    if (!_chain_conf || noutputs() < 1 || !output_is_push(0) || output(0).port() != 0)
+	return 0;
+    Element *e = output(0).element();
+    HIPBatchElement *y = e ? static_cast<HIPBatchElement *>(e->cast("HIPBatchElement")) : 0;
+    if (!y || y == this || !y->_chain_conf || y->_device != _device || y->cls_chain_head_only())
+	return 0;
+    UpstreamPorts up;
+    router()->visit_upstream(y, 0, &up);
+    return up.n == 1 && up.first == this ? y : 0;
+}
+
+// A member of the chain of the element before it (which runs it)
+bool
+HIPBatchElement::chain_member()
+{
+    if (ninputs() < 1 || !input_is_push(0))
+	return false;
+    UpstreamPorts up;
+    router()->visit_upstream(this, 0, &up);
+    HIPBatchElement *u = up.n == 1 && up.first ? static_cast<HIPBatchElement *>(up.first->cast("HIPBatchElement")) : 0;
+    return u && !u->cls_chain_last() && u->chain_next() == this;
+}
+
+// State t runs the chain (under t's lock): each member's glue element on t's
+// context, counted in the member's handlers.  If the glue refuses the chain
+// the elements stay separate (output 0 pushes into the next one).
+void
+HIPBatchElement::ensure_chain(PerThread &t)
+{
+    _chain_tried[t.id] = true;
+    if (_chain.size() < 2 || !t.e || t.chain)
+	return;
+    t.mem.push_back(t.e);
+    for (int m = 1; m < _chain.size(); m++) {
+	HIPBatchElement *y = _chain[m];
+	clk_element *me = 0;
+	if (clk_element_create(t.ctx, y->glue_class(), y->_glue_conf.c_str(), y->name().c_str(),
+			       y->noutputs(), &me) != CLK_SUCCESS)
+	    break;
+	if (y->_gate)
+	    clk_element_share_messages(me, y->_gate);
+	t.mem.push_back(me);
+    }
+    if (t.mem.size() == (size_t) _chain.size()
+	&& clk_chain_create(t.mem.data(), (int) t.mem.size(), &t.chain) == CLK_SUCCESS) {
+	clk_chain_report_passes(t.chain, 1);
+	for (int m = 1; m < _chain.size(); m++) {
+	    _chain[m]->_borrow_lock.acquire();
+	    _chain[m]->_borrowed.push_back(t.mem[m]);
+	    _chain[m]->_borrow_lock.release();
+	}
+	return;
+    }
+    click_chatter("%p{element}: running separately from the elements after it: %s", this,
+		  t.mem.size() == (size_t) _chain.size() ? clk_last_error(0) : clk_last_error(t.ctx));
+    for (size_t m = 1; m < t.mem.size(); m++)
+	clk_element_destroy(t.mem[m]);
+    t.mem.clear();
+    t.chain = 0;
+}
+
+// The annotations the members after the head read (CLK_ANNO_*), staged with
+// the packet: FixIPSrc's and IPOutputCombo's FIX_IP_SRC, IPOutputCombo's
+// paint and packet type
+uint32_t
+HIPBatchElement::chain_anno(Packet *p) const
+{
+    return (ClickPacketOps::fix_ip_src(p) ? CLK_ANNO_FIX_IP_SRC : 0u)
+	| (ClickPacketOps::broadcast_or_multicast(p) ? CLK_ANNO_BCAST : 0u)
+	| CLK_ANNO_PAINT(ClickPacketOps::paint(p));
+}
+
+Packet *
+HIPBatchElement::prepare(Packet *p, uint32_t *anno, Packet **extra)
+{
+    if (!(p = cls_prepare(p, anno, extra)))
+	return 0;
+    if (_chain.size() > 1) {
+	// readied for every member: writable if any may write (where the
+	// reference makes it writable only in the element that writes it)
+	bool w = false;
+	for (int m = 1; m < _chain.size(); m++)
+	    w = w || _chain[m]->cls_may_write();
+	if (w && !(p = p->uniqueify()))
+	    return 0;
+	*anno |= chain_anno(p);
+    }
+    return p;
 }
 
 HIPBatchElement::PerThread &
@@ -132,7 +265,13 @@ HIPBatchElement::state()
 void
 HIPBatchElement::push(int, Packet *p)
 {
-    _core.push(*this, state(), p);
+    PerThread &t = state();
+    if (!_chain_tried[t.id]) {
+	t.lock.acquire();
+	ensure_chain(t);
+	t.lock.release();
+    }
+    _core.push(*this, t, p);
 }
 
 Packet *
@@ -166,7 +305,7 @@ HIPBatchElement::chatter(const char *text)
 }
 
 void
-HIPBatchElement::message(const char *line)
+HIPBatchElement::message(int, const char *line)
 {
     click_chatter("%s", line);		// already worded as the reference element's
 }
@@ -175,9 +314,22 @@ void
 HIPBatchElement::cleanup(CleanupStage)
 {
     // nothing is pushed downstream: held, routed-but-undelivered and ready
-    // packets are killed, the glue elements and contexts destroyed
-    for (int k = 0; k < _npt; k++)
+    // packets are killed, the glue elements and contexts destroyed (the
+    // members' copies taken out of their handler sums first)
+    for (int k = 0; k < _npt; k++) {
+	for (size_t m = 1; m < _pt[k].mem.size() && (int) m < _chain.size(); m++) {
+	    HIPBatchElement *y = _chain[m];
+	    y->_borrow_lock.acquire();
+	    for (int i = 0; i < y->_borrowed.size(); i++)
+		if (y->_borrowed[i] == _pt[k].mem[m]) {
+		    y->_borrowed[i] = y->_borrowed.back();
+		    y->_borrowed.pop_back();
+		    break;
+		}
+	    y->_borrow_lock.release();
+	}
 	_core.cleanup(*this, _pt[k]);
+    }
 }
 
 String
@@ -199,14 +351,21 @@ HIPBatchElement::read_handler(Element *e, void *thunk)
 {
     HIPBatchElement *he = static_cast<HIPBatchElement *>(e);
     const char *hname = static_cast<const char *>(thunk);
+    // this element's glue elements: its states' and its copies in chains
+    Vector<clk_element *> els;
+    for (int k = 0; k < he->_npt; k++)
+	if (he->_pt[k].e)
+	    els.push_back(he->_pt[k].e);
+    he->_borrow_lock.acquire();
+    for (int i = 0; i < he->_borrowed.size(); i++)
+	els.push_back(he->_borrowed[i]);
+    he->_borrow_lock.release();
     if (strcmp(hname, "drop_details") == 0) {
 	Vector<unsigned long long> sum;
 	Vector<String> text;
-	for (int k = 0; k < he->_npt; k++) {
-	    if (!he->_pt[k].e)
-		continue;
+	for (int k = 0; k < els.size(); k++) {
 	    char buf[4096];
-	    clk_element_read_handler(he->_pt[k].e, hname, buf, sizeof(buf));
+	    clk_element_read_handler(els[k], hname, buf, sizeof(buf));
 	    int line = 0;
 	    for (char *s = buf, *nl; *s; s = nl, line++) {
 		if (!(nl = strchr(s, '\n')))
@@ -229,12 +388,11 @@ HIPBatchElement::read_handler(Element *e, void *thunk)
     if (strcmp(hname, "device") == 0 || strcmp(hname, "color") == 0 || strcmp(hname, "active") == 0)
 	return he->glue_handler(hname);
     unsigned long long total = 0;
-    for (int k = 0; k < he->_npt; k++)
-	if (he->_pt[k].e) {
-	    char buf[64];
-	    clk_element_read_handler(he->_pt[k].e, hname, buf, sizeof(buf));
-	    total += strtoull(buf, 0, 10);
-	}
+    for (int k = 0; k < els.size(); k++) {
+	char buf[64];
+	clk_element_read_handler(els[k], hname, buf, sizeof(buf));
+	total += strtoull(buf, 0, 10);
+    }
     return String(total);
 }
 

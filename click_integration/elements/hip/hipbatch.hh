@@ -71,6 +71,8 @@ struct ClickPacketOps {
  *                 glue validates it: CLK_ENODEV for a GPU that is not there)
  *   RETRIES  n    failed flushes of a batch before its packets are killed
  *                 (default 3)
+ *   CHAIN    bool join the GPU-backed elements after this one into one batch
+ *                 (default true; see Chains below)
  * Glue keywords passed through: BATCH, ZEROCOPY, and the element's own.
  *
  * Threads (click -j N): one hipcore::State (context, glue element, held
@@ -85,6 +87,20 @@ struct ClickPacketOps {
  * The element classes' own logic (what the reference element does around
  * its checksum) is hipclasses.hh's, instantiated with ClickPacketOps;
  * HIPClassElement<C> forwards the core's hooks to it.
+ *
+ * Chains (the GPU analogue of click-xform's combos): when this element's
+ * output 0 pushes into a GPU-backed element's input 0 that nothing else
+ * pushes into, on the same DEVICE, both with CHAIN true, the second joins
+ * the first one's batch -- and so on down output 0 (an IPFragmenter ends a
+ * chain, an IPOutputCombo only starts one: its PaintTee clones the packet
+ * as it arrives).  The head's thread states run the members as one
+ * clk_chain: a packet is staged once, each member's kernel runs over what
+ * the members before it passed, and each result is finished by the member
+ * it leaves (its class logic) and pushed on that member's output.  The
+ * head makes a packet writable when any member may write it, and stages
+ * the annotations every member reads.  The members' handlers count what
+ * they did in the chains too.  A chain that cannot be created (e.g. ZEROCOPY
+ * on some members only) is left as separate elements, with one message.
  */
 class HIPBatchElement : public Element { public:
 
@@ -103,25 +119,37 @@ class HIPBatchElement : public Element { public:
     void push(int port, Packet *p);
     Packet *pull(int port);
 
-    // ---- the core's host interface (hipcore.hh) ------------------------------
-    // the class hooks (hipclasses.hh): the plain check elements' here,
+    void *cast(const char *n);
+
+    // ---- the class hooks (hipclasses.hh): the plain check elements' here,
     // HIPClassElement<C> forwards them to its class
-    virtual Packet *prepare(Packet *p, uint32_t *anno, Packet **extra)	{ return _plain.prepare(p, anno, extra); }
-    virtual int32_t nh_offset(Packet *p)	{ return _plain.nh_offset(p); }
-    virtual bool primary(int32_t port, uint32_t aux) const	{ return _plain.primary(port, aux); }
-    virtual Packet *make_packet(clk_element *e, uint32_t key)	{ return _plain.make_packet(e, key); }
-    virtual int finish(PerThread &t, Routed &r, Packet **out)	{ return _plain.finish(t, r, out); }
-    virtual void end_of_batch(PerThread &t)	{ _plain.end_of_batch(t); }
+    virtual Packet *cls_prepare(Packet *p, uint32_t *anno, Packet **extra)	{ return _plain.prepare(p, anno, extra); }
+    virtual int32_t cls_nh_offset(Packet *p)	{ return _plain.nh_offset(p); }
+    virtual bool cls_primary(int32_t port, uint32_t aux) const	{ return _plain.primary(port, aux); }
+    virtual Packet *cls_make_packet(clk_element *e, uint32_t key)	{ return _plain.make_packet(e, key); }
+    virtual int cls_finish(PerThread &t, Routed &r, Packet **out)	{ return _plain.finish(t, r, out); }
+    virtual void cls_end_of_batch(PerThread &t)	{ _plain.end_of_batch(t); }
+    virtual bool cls_may_write() const		{ return false; }
+    virtual bool cls_chain_last() const		{ return false; }
+    virtual bool cls_chain_head_only() const	{ return false; }
+
+    // ---- the core's host interface (hipcore.hh); m: the chain member ---------
+    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
+    int32_t nh_offset(Packet *p)		{ return cls_nh_offset(p); }
+    bool primary(int m, int32_t port, uint32_t aux) const	{ return _chain[m]->cls_primary(port, aux); }
+    Packet *make_packet(int m, clk_element *e, uint32_t key)	{ return _chain[m]->cls_make_packet(e, key); }
+    int finish(int m, PerThread &t, Routed &r, Packet **out)	{ return _chain[m]->cls_finish(t, r, out); }
+    void end_of_batch(int m, PerThread &t)	{ _chain[m]->cls_end_of_batch(t); }
     uint8_t *data(Packet *p)		{ return ClickPacketOps::data(p); }
     uint32_t length(Packet *p)		{ return p->length(); }
-    void output_push(int port, Packet *p)	{ checked_output_push(port, p); }
+    void output_push(int m, int port, Packet *p)	{ _chain[m]->checked_output_push(port, p); }
     Packet *input_pull()			{ return input(0).pull(); }
     void kill(Packet *p)			{ p->kill(); }
     void adjust_runcount(int delta);
     uint64_t now_ns()			{ return Timestamp::now_steady().nsecval(); }
     void wake(PerThread &t)		{ _tasks[t.id].reschedule(); }
     void chatter(const char *text);
-    void message(const char *line);
+    void message(int m, const char *line);
     bool run_task(Task *task);
 
   protected:
@@ -143,6 +171,11 @@ class HIPBatchElement : public Element { public:
     Task *_tasks;			// one per state, on its RouterThread
     int _npt;
     clk_element *_gate;		// whose once-only chatter the thread elements share
+    bool _chain_conf;		// CHAIN
+    Vector<HIPBatchElement *> _chain;	// [0] this; then the members this head runs
+    bool *_chain_tried;		// per state: its chain was set up (or refused)
+    Vector<clk_element *> _borrowed;	// this element's glue copies in chains of heads before it
+    Spinlock _borrow_lock;
     hipcore::Core<Packet, HIPBatchElement, Spinlock> _core;
     hipcore::Plain<Packet, ClickPacketOps> _plain;
 
@@ -150,6 +183,10 @@ class HIPBatchElement : public Element { public:
 
     PerThread &state();
     int ensure(PerThread &t, ErrorHandler *errh);
+    void ensure_chain(PerThread &t);
+    HIPBatchElement *chain_next();
+    bool chain_member();
+    uint32_t chain_anno(Packet *p) const;
     static String read_handler(Element *e, void *thunk) CLICK_COLD;
 
 };
@@ -160,12 +197,15 @@ class HIPBatchElement : public Element { public:
  */
 template <class C>
 class HIPClassElement : public HIPBatchElement { public:
-    Packet *prepare(Packet *p, uint32_t *anno, Packet **extra)	{ return _cls.prepare(p, anno, extra); }
-    int32_t nh_offset(Packet *p)	{ return _cls.nh_offset(p); }
-    bool primary(int32_t port, uint32_t aux) const	{ return _cls.primary(port, aux); }
-    Packet *make_packet(clk_element *e, uint32_t key)	{ return _cls.make_packet(e, key); }
-    int finish(PerThread &t, Routed &r, Packet **out)	{ return _cls.finish(t, r, out); }
-    void end_of_batch(PerThread &t)	{ _cls.end_of_batch(t); }
+    Packet *cls_prepare(Packet *p, uint32_t *anno, Packet **extra)	{ return _cls.prepare(p, anno, extra); }
+    int32_t cls_nh_offset(Packet *p)	{ return _cls.nh_offset(p); }
+    bool cls_primary(int32_t port, uint32_t aux) const	{ return _cls.primary(port, aux); }
+    Packet *cls_make_packet(clk_element *e, uint32_t key)	{ return _cls.make_packet(e, key); }
+    int cls_finish(PerThread &t, Routed &r, Packet **out)	{ return _cls.finish(t, r, out); }
+    void cls_end_of_batch(PerThread &t)	{ _cls.end_of_batch(t); }
+    bool cls_may_write() const		{ return C::may_write != 0; }
+    bool cls_chain_last() const		{ return C::chain_last != 0; }
+    bool cls_chain_head_only() const	{ return C::chain_head_only != 0; }
   protected:
     C _cls;
 };
