@@ -109,15 +109,13 @@ uint32_t Chain::extent(int32_t nh, uint32_t length)
 {
     if (nh == ext_nh_ && length == ext_len_)
         return ext_;
-    uint64_t need = 0, wneed = 0, shift = 0;
+    uint64_t need = 0, shift = 0;
     int32_t v = nh;
     for (const BatchElement *e : m_) {
         if (shift > length)
             break;
         const uint32_t x = e->chain_extent(v, length - (uint32_t)shift);
-        const uint32_t wx = e->chain_write_extent(v, length - (uint32_t)shift);
         need = x == 0xFFFFFFFFu ? (uint64_t)0xFFFFFFFFu : std::max<uint64_t>(need, shift + x);
-        wneed = wx == 0xFFFFFFFFu ? (uint64_t)0xFFFFFFFFu : std::max<uint64_t>(wneed, wx ? shift + wx : 0);
         shift += e->strip();
         if (e->nh_after() != -2)
             v = e->nh_after();
@@ -125,7 +123,6 @@ uint32_t Chain::extent(int32_t nh, uint32_t length)
     ext_nh_ = nh;
     ext_len_ = length;
     ext_ = (uint32_t)std::min<uint64_t>(need, 0xFFFFFFFFu);
-    wext_ = (uint32_t)std::min<uint64_t>(wneed, 0xFFFFFFFFu);
     return ext_;
 }
 
@@ -177,7 +174,7 @@ int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t toke
     stage_copy(h_arena_ + slot, data, need, length);
     views0_.push_back(ChainView{data, token, slot, length, nh_offset, (uint16_t)anno});
     staged_.push_back(need);
-    back_.push_back(std::min(need, wext_));
+    back_.push_back(0);                              // grown by each member whose kernel may rewrite it
     used_ = slot + need;
     return views0_.size() >= m_[0]->batch_cap_ ? 1 : 0;
 }
@@ -249,9 +246,21 @@ void Chain::setup(size_t k)
     BatchElement *e = m_[k];
     Member &M = mm_[k];
     ChainWork &w = M.w;
+    const size_t n = views0_.size();
+    if (M.reached.size() < n) {
+        M.reached.resize(n);
+        M.code.resize(n);
+        M.span_off.resize(n);
+    }
+    w.reached = M.reached.data(), w.code = M.code.data(), w.span_off = M.span_off.data();
     w.views = &views_;
     w.done = &done_;
     w.out = &out_;
+    w.back = e->zerocopy_ ? nullptr : back_.data();
+    w.staged = staged_.data();
+    w.views0 = views0_.data();
+    w.wext = e->chain_write_past_nh();
+    e->chain_pass(&w.pass, &w.pass_param);
     w.h_off = M.h_off, w.h_len = M.h_len, w.h_anno = M.h_anno;
     w.h_codes = M.h_codes;
     w.h_sums = e->wants_sums() ? M.h_sums : nullptr;
@@ -273,14 +282,20 @@ void Chain::setup(size_t k)
 // pass of its own.
 void Chain::advance(uint32_t i, size_t k)
 {
+    const ChainView &v = views_[i];
     for (;;) {
-        BatchElement *e = m_[k];
         ChainWork &w = mm_[k].w;
-        const size_t q = w.reached.size();
-        if (!e->chain_span(w, i) || !w.inline_ok || w.n != 0 || w.routed != q)
-            return;
-        w.routed = q + 1;
-        if (!e->chain_route(w, q))
+        if (w.routed == w.nreached && w.passes(v)) {  // passes unchanged: counted, not asked
+            m_[k]->packets_++;
+            if (w.last) {
+                out_.push_back(ChainExit{v.token, (int32_t)k, 0, v.length, 0, i});
+                done_[i] = 1;
+                return;
+            }
+            k++;
+            continue;
+        }
+        if (m_[k]->chain_step(w, i) != 1)
             return;
         k++;
     }
@@ -300,7 +315,7 @@ int Chain::run_member(size_t k, bool *launched)
     double t0 = now_s();
     if (M.rebuild) {                                 // resumed: a new batch of the packets left
         M.rebuild = false;
-        std::vector<uint32_t> left(w.reached.begin() + (long)w.routed, w.reached.end());
+        std::vector<uint32_t> left(w.reached + w.routed, w.reached + w.nreached);
         w.reset();
         for (uint32_t i : left)
             advance(i, k);
@@ -361,7 +376,7 @@ int Chain::run_member(size_t k, bool *launched)
     stats_[2] += now_s() - t0;
     t0 = now_s();
     const bool more = k + 1 < m_.size();
-    for (size_t q = w.routed; q < w.reached.size(); q++) {
+    for (size_t q = w.routed; q < w.nreached; q++) {
         w.routed = q + 1;
         if (e->chain_route(w, q) && more)
             advance(w.reached[q], k + 1);
@@ -454,7 +469,7 @@ int Chain::flush()
     std::string failed_why;
     for (size_t k = k0; k < m_.size(); k++) {
         ChainWork &w = mm_[k].w;
-        if (w.routed == w.reached.size())
+        if (w.routed == w.nreached)
             continue;
         bool launched = false;
         int r = run_member(k, &launched);
@@ -466,13 +481,13 @@ int Chain::flush()
             // packets it had not routed are killed, as a ZEROCOPY batch of such
             // an element is; the ones it passed before that go on
             BatchElement *e = m_[k];
-            for (size_t q = w.routed; q < w.reached.size(); q++) {
+            for (size_t q = w.routed; q < w.nreached; q++) {
                 const uint32_t i = w.reached[q];
                 out_.push_back(ChainExit{views_[i].token, (int32_t)k, CLK_PORT_KILL, views_[i].length, 0, i});
                 done_[i] = 1;
                 e->lost_++;
             }
-            w.routed = w.reached.size();
+            w.routed = w.nreached;
             failed = r;
             failed_why = err_ + " (its packets were killed, not retried)";
             continue;
@@ -516,7 +531,7 @@ uint64_t Chain::abandon()
         (void)copy_back(false);                      // one more try for the bytes of the routed ones
         for (size_t j = 0; j < mm_.size(); j++) {
             ChainWork &w = mm_[j].w;
-            for (size_t q = w.routed; q < w.reached.size(); q++) {
+            for (size_t q = w.routed; q < w.nreached; q++) {
                 const uint32_t i = w.reached[q];
                 if (done_[i])
                     continue;
@@ -525,7 +540,7 @@ uint64_t Chain::abandon()
                 m_[j]->lost_++;
                 k++;
             }
-            w.routed = w.reached.size();
+            w.routed = w.nreached;
             mm_[j].rebuild = false;
         }
         for (size_t r = pub_; r < out_.size(); r++) {

@@ -281,9 +281,10 @@ int BatchElement::grow_dev(Stage &g, size_t bytes, size_t n)
     return 0;
 }
 
-bool BatchElement::chain_span(ChainWork &w, uint32_t i)
+int BatchElement::chain_step(ChainWork &w, uint32_t i)
 {
-    return chain_span_one(w, i, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); });
+    return chain_step_one(w, i, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); },
+                          [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
 }
 
 bool BatchElement::chain_route(ChainWork &w, size_t q)

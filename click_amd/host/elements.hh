@@ -161,12 +161,23 @@ struct ChainExit {           // a result leaving the chain at `member`
     uint32_t length, aux;
     uint32_t idx;            // the packet's place in the batch (~0u: a clone / new packet)
 };
+// A member's decision a chain can take without asking it: the packets its
+// span() decides on the host and its route() then passes on unchanged
+// (no write, no annotation, no result of its own but the count).
+enum ChainPass {
+    CHAIN_PASS_NONE = 0,
+    CHAIN_PASS_NO_OPTIONS,   // IPGWOptions: no header, or ip_hl <= 5
+    CHAIN_PASS_NO_FIX,       // FixIPSrc: no FIX_IP_SRC annotation, or no header
+    CHAIN_PASS_WITHIN,       // IPFragmenter: network length <= param (MTU), or no header
+    CHAIN_PASS_TTL,          // DecIPTTL: param == 0 (ACTIVE false), or no header
+};
 struct ChainWork {
     std::vector<ChainView> *views;            // per chain packet, updated as it passes members
-    std::vector<uint32_t> reached;            // the packets that reached this member, in push order
-    std::vector<int32_t> code;                // per reached packet: GPU index, or -1 - host code
-    std::vector<uint32_t> span_off;
     std::vector<uint8_t> *done;               // per chain packet: has left the chain
+    uint32_t *reached = nullptr;              // the packets that reached this member, in push order
+    int32_t *code = nullptr;                  // per reached packet: GPU index, or -1 - host code
+    uint32_t *span_off = nullptr;
+    size_t nreached = 0;
     size_t routed = 0;                        // reached packets routed so far
     uint64_t *h_off = nullptr;                // the member's batch (pinned)
     uint32_t *h_len = nullptr;
@@ -176,20 +187,45 @@ struct ChainWork {
     size_t n = 0;                             // packets in the member's GPU batch
     uint32_t maxlen = 0;
     std::vector<ChainExit> *out = nullptr;
+    // staged batches: per packet, the bytes to copy back (grown by each
+    // member that rewrites it: shift + its write extent), its first slot
+    uint32_t *back = nullptr;
+    const uint32_t *staged = nullptr;
+    const ChainView *views0 = nullptr;
+    uint32_t wext = 0;                        // the member's write extent past nh (~0u: all; 0: none)
     int member = 0;
     uint32_t strip = 0;                       // the member's strip() / nh_after()
     int32_t nh_after = -2;
+    uint8_t pass = CHAIN_PASS_NONE;           // ChainPass, with pass_param
+    uint32_t pass_param = 0;
     bool last = false;
     bool inline_ok = false;                   // no pre/post results: a host decision may route at once
     bool report_passes = false;               // a CLK_PORT_NEXT record for each packet passed on
     void reset()
     {
-        reached.clear();
-        code.clear();
-        span_off.clear();
+        nreached = 0;
         routed = 0;
         n = 0;
         maxlen = 0;
+    }
+    // the packet passes this member unchanged, decided without the member
+    bool passes(const ChainView &v) const
+    {
+        const bool nohdr = v.nh < 0 || (uint32_t)v.nh >= v.length;
+        switch (pass) {
+        case CHAIN_PASS_NO_OPTIONS:
+            return nohdr || v.length - (uint32_t)v.nh < 20 || (v.data[v.nh] & 0xF) <= 5;
+        case CHAIN_PASS_NO_FIX:
+            return nohdr || !(v.anno & CLK_ANNO_FIX_IP_SRC);
+        case CHAIN_PASS_WITHIN: {
+            const uint32_t nh = v.nh >= 0 ? (uint32_t)v.nh : 0u;
+            return nh > v.length || (int)(v.length - nh) <= (int)pass_param;
+        }
+        case CHAIN_PASS_TTL:
+            return pass_param == 0 || v.nh < 0 || (uint32_t)v.nh > v.length;
+        default:
+            return false;
+        }
     }
 };
 
@@ -207,11 +243,11 @@ struct ChainWork {
     {                                                                                                           \
         route_loop(g_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
     }                                                                                                           \
-    bool chain_span(ChainWork &w_, uint32_t i_) override                                                        \
+    int chain_step(ChainWork &w_, uint32_t i_) override                                                         \
     {                                                                                                           \
-        return chain_span_one(w_, i_, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {           \
+        return chain_step_one(w_, i_, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {           \
             return this->C::span(p, o, l, c);                                                                   \
-        });                                                                                                     \
+        }, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); });         \
     }                                                                                                           \
     bool chain_route(ChainWork &w_, size_t q_) override                                                         \
     {                                                                                                           \
@@ -290,23 +326,26 @@ class BatchElement {
     // the bytes from data() the element's kernel can read / write of a packet
     // of `length` bytes whose network header is at nh (~0u: all of it)
     virtual uint32_t chain_extent(int32_t nh, uint32_t length) const { (void)nh, (void)length; return 0xFFFFFFFFu; }
-    virtual uint32_t chain_write_extent(int32_t nh, uint32_t length) const
-    {
-        return writes() ? chain_extent(nh, length) : 0u;
-    }
     // the element's kernel writes packet bytes (a chain copies them back)
     virtual bool writes() const { return wants_sums() || wants_arena_back() || !idempotent(); }
     // a chain's per-packet steps (CLK_GLUE_LOOPS inlines the class's span /
-    // route into them).  chain_span(): packet i reaches the member -- its
-    // descriptor, or its host decision; returns true for a host decision.
-    // chain_route(): route reached packet q; returns true when it goes on to
-    // the next member (its view moved past this one).
-    virtual bool chain_span(ChainWork &w, uint32_t i);
+    // route into them).  chain_step(): packet i reaches the member -- its
+    // descriptor (0: it waits for the GPU), or its host decision, routed at
+    // once while no packet before it waits (1: passed on, 2: left the
+    // chain).  chain_route(): route reached packet q after the member's
+    // kernel; true when it goes on to the next member.
+    virtual int chain_step(ChainWork &w, uint32_t i);
     virtual bool chain_route(ChainWork &w, size_t q);
-    template <class SpanF>
-    bool chain_span_one(ChainWork &w, uint32_t i, SpanF &&span_f);
+    // the decision the chain may take for the member (ChainPass)
+    virtual void chain_pass(uint8_t *kind, uint32_t *param) const { *kind = CHAIN_PASS_NONE, *param = 0; }
+    // the bytes past the network header the kernel may write (~0u: any)
+    virtual uint32_t chain_write_past_nh() const { return writes() ? 0xFFFFFFFFu : 0u; }
+    template <class SpanF, class RouteF>
+    int chain_step_one(ChainWork &w, uint32_t i, SpanF &&span_f, RouteF &&route_f);
     template <class RouteF>
     bool chain_route_at(ChainWork &w, size_t q, RouteF &&route_f);
+    template <class RouteF>
+    bool chain_route_pending(ChainWork &w, uint32_t i, Pending &p, int code, uint16_t sum, RouteF &&route_f);
     ResultQueue chain_side_;          // a member's pre/post results while a chain routes
     friend class Chain;
     // after the batch completed, before any packet is routed: nonzero fails
@@ -499,6 +538,7 @@ class SetIPChecksum : public BatchElement {
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
     uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 60; }
+    uint32_t chain_write_past_nh() const override { return 60; }
     bool wants_sums() const override { return true; }
 
   private:
@@ -565,6 +605,8 @@ class DecIPTTL : public BatchElement {
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
     uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 20; }
+    uint32_t chain_write_past_nh() const override { return 20; }
+    void chain_pass(uint8_t *k, uint32_t *a) const override { *k = CHAIN_PASS_TTL, *a = active_ ? 1u : 0u; }
     bool wants_sums() const override { return true; }
 
   private:
@@ -590,6 +632,8 @@ class IPGWOptions : public BatchElement {
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
     uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 64; }
+    uint32_t chain_write_past_nh() const override { return 64; }
+    void chain_pass(uint8_t *k, uint32_t *a) const override { *k = CHAIN_PASS_NO_OPTIONS, *a = 0; }
     bool wants_arena_back() const override { return true; }
 
   private:
@@ -614,6 +658,8 @@ class FixIPSrc : public BatchElement {
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
     uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 64; }
+    uint32_t chain_write_past_nh() const override { return 64; }
+    void chain_pass(uint8_t *k, uint32_t *a) const override { *k = CHAIN_PASS_NO_FIX, *a = 0; }
     bool wants_arena_back() const override { return true; }
 
   private:
@@ -641,6 +687,7 @@ class IPOutputCombo : public BatchElement {
     bool pre_route(Pending &p, Result *r) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
     uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 64; }
+    uint32_t chain_write_past_nh() const override { return 64; }
     bool wants_arena_back() const override { return true; }
     bool wants_anno() const override { return true; }
 
@@ -674,6 +721,7 @@ class IPFragmenter : public BatchElement {
         const uint32_t h = nh > 0 ? (uint32_t)nh : 0u;
         return h <= length && length - h <= mtu_ ? 0u : 0xFFFFFFFFu;
     }
+    void chain_pass(uint8_t *k, uint32_t *a) const override { *k = CHAIN_PASS_WITHIN, *a = mtu_; }
     int verify(const uint8_t *codes, size_t n) override;
     void post_route(Pending &p, int code, ResultQueue &out) override;
     bool wants_arena_back() const override { return true; }
@@ -699,43 +747,50 @@ class IPFragmenter : public BatchElement {
     uint64_t nfrag_ = 0;
 };
 
-template <class SpanF>
-inline bool BatchElement::chain_span_one(ChainWork &w, uint32_t i, SpanF &&span_f)
+template <class SpanF, class RouteF>
+inline int BatchElement::chain_step_one(ChainWork &w, uint32_t i, SpanF &&span_f, RouteF &&route_f)
 {
     const ChainView &v = (*w.views)[i];
     Pending p{v.data, v.token, v.slot, v.length, v.nh, 0, 0, 0, -1, v.anno};
     uint32_t off = 0, len = 0;
     int32_t hc = 0;
-    w.reached.push_back(i);
+    const size_t q = w.nreached++;
+    w.reached[q] = i;
     if (!span_f(p, &off, &len, &hc)) {
-        w.code.push_back(-1 - hc);
-        w.span_off.push_back(0);
-        return true;
+        w.code[q] = -1 - hc;
+        w.span_off[q] = 0;
+        if (!w.inline_ok || w.routed != q)
+            return 0;
+        w.routed = q + 1;
+        p.host_code = (int16_t)hc;
+        return chain_route_pending(w, i, p, hc, 0, route_f) ? 1 : 2;
     }
     w.h_off[w.n] = v.slot + off;
     w.h_len[w.n] = len;
     w.h_anno[w.n] = (uint8_t)v.anno;
     w.maxlen = std::max(w.maxlen, len);
-    w.span_off.push_back(off);
-    w.code.push_back((int32_t)w.n++);
-    return false;
+    w.span_off[q] = off;
+    w.code[q] = (int32_t)w.n++;
+    if (w.wext && w.back) {                  // the bytes this member's kernel may rewrite, to copy back
+        const uint64_t shift = v.slot - w.views0[i].slot;
+        const uint64_t e = w.wext == 0xFFFFFFFFu ? (uint64_t)0xFFFFFFFFu
+                                                 : shift + (v.nh > 0 ? (uint32_t)v.nh : 0u) + w.wext;
+        w.back[i] = (uint32_t)std::max<uint64_t>(w.back[i], std::min<uint64_t>(e, w.staged[i]));
+    }
+    return 0;
 }
 
 template <class RouteF>
-inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_f)
+inline bool BatchElement::chain_route_pending(ChainWork &w, uint32_t i, Pending &p, int code, uint16_t sum,
+                                              RouteF &&route_f)
 {
-    const uint32_t i = w.reached[q];
-    const int32_t c = w.code[q];
-    const int code = c >= 0 ? w.h_codes[c] : -1 - c;
     ChainView &v = (*w.views)[i];
-    Pending p{v.data, v.token, v.slot, v.length, v.nh, w.span_off[q], 0, c >= 0 ? (uint32_t)c : 0u,
-              (int16_t)(c >= 0 ? -1 : code), v.anno};
     Result pr;
     if (has_pre_route_ && pre_route(p, &pr))
         w.out->push_back(ChainExit{pr.token, w.member, pr.port, pr.length, pr.aux, ~0u});
     Result r{p.token, 0, p.length, 0};
     packets_++;
-    route_f(p, code, c >= 0 && w.h_sums ? w.h_sums[c] : 0, &r);
+    route_f(p, code, sum, &r);
     const bool pass = r.port == 0 && !w.last;
     if (pass) {
         v.data += w.strip;
@@ -761,6 +816,18 @@ inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_
                 w.out->push_back(ChainExit{tok[k], w.member, port[k], len[k], aux[k], ~0u});
     }
     return pass;
+}
+
+template <class RouteF>
+inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_f)
+{
+    const uint32_t i = w.reached[q];
+    const int32_t c = w.code[q];
+    const int code = c >= 0 ? w.h_codes[c] : -1 - c;
+    const ChainView &v = (*w.views)[i];
+    Pending p{v.data, v.token, v.slot, v.length, v.nh, w.span_off[q], 0, c >= 0 ? (uint32_t)c : 0u,
+              (int16_t)(c >= 0 ? -1 : code), v.anno};
+    return chain_route_pending(w, i, p, code, c >= 0 && w.h_sums ? w.h_sums[c] : 0, route_f);
 }
 
 BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::string &name, int noutputs);
@@ -810,6 +877,8 @@ class Chain {
         void *ev[2] = {nullptr, nullptr};
         float ms = 0;
         bool rebuild = false;                 // resumed: rebuild the batch of the packets not routed
+        std::vector<uint32_t> reached, span_off;
+        std::vector<int32_t> code;
         ChainWork w;
     };
     int grow(size_t bytes, size_t n);
@@ -837,7 +906,7 @@ class Chain {
     size_t pub_ = 0;                          // out_[head_, pub_): results whose bytes are back
     double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int32_t ext_nh_ = -3;                     // extent() cache: the nh and length it was computed for
-    uint32_t ext_len_ = 0, ext_ = 0, wext_ = 0;
+    uint32_t ext_len_ = 0, ext_ = 0;
     bool init_ = false;
     bool report_passes_ = false;
     std::string err_;

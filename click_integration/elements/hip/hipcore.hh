@@ -286,12 +286,22 @@ template <class P, class Host, class L> class Core {
     // delivered (its output-0 packets to the ready queue).
     void refill_and_launch(Host &h, S &t)
     {
+        // pulled in groups without the lock (input 0 is another element),
+        // each group staged under one lock
+        enum { GROUP = 64 };
+        P *grp[GROUP];
         uint32_t k = 0;
-        P *q;
-        while (k < _batch && (q = h.input_pull()) != 0) {
+        bool dry = false;
+        while (k < _batch && !dry) {
+            uint32_t g = 0;
+            const uint32_t want = _batch - k < (uint32_t) GROUP ? _batch - k : (uint32_t) GROUP;
+            while (g < want && (grp[g] = h.input_pull()) != 0)
+                g++;
+            dry = g < want;
             t.lock.acquire();
-            if (stage(h, t, q, false))
-                k++;
+            for (uint32_t j = 0; j < g; j++)
+                if (stage(h, t, grp[j], false))
+                    k++;
             t.lock.release();
         }
         t.lock.acquire();
@@ -503,6 +513,7 @@ template <class P, class Host, class L> class Core {
     void drain(Host &h, S &t, bool pull_ctx)
     {
         std::vector<R> work;
+        std::vector<P *> ready;                 // pull context: output-0 packets, queued under one lock
         t.lock.acquire();
         if (t.draining) {
             t.lock.release();
@@ -524,15 +535,15 @@ template <class P, class Host, class L> class Core {
                 int port = h.finish(r.member, t, r, &out);
                 if (r.pass || port < 0 || !out)  // a pass: the member's side effects only
                     continue;
-                if (pull_ctx && port == 0 && r.member + 1 == (int) (t.chain ? t.mem.size() : 1)) {
-                    t.lock.acquire();
-                    t.ready.push_back(out);
-                    t.lock.release();
-                } else
+                if (pull_ctx && port == 0 && r.member + 1 == (int) (t.chain ? t.mem.size() : 1))
+                    ready.push_back(out);
+                else
                     h.output_push(r.member, port, out);
             }
             work.clear();
             t.lock.acquire();
+            t.ready.insert(t.ready.end(), ready.begin(), ready.end());
+            ready.clear();
         }
         t.draining = false;
         t.lock.release();

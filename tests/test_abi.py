@@ -189,4 +189,4 @@ def test_click_adapters_keep_the_reference_processing():
         m = re.search(r"processing\(\) const\s*\{ return (\w+); \}", body)
         assert (m.group(1) if m else base) == proc, n
     cc = open(os.path.join(hip, "hipbatch.cc")).read()
-    assert "_core.pull(*this, state())" in cc and "_core.push(*this, state(), p)" in cc
+    assert "_core.pull(*this, state())" in cc and "_core.push(*this, t, p)" in cc and "PerThread &t = state();" in cc
