@@ -58,6 +58,8 @@ Chain::~Chain()
 {
     if (init_)
         (void)clk_ctx_sync(m_[0]->ctx_);
+    for (BatchElement *e : m_)
+        e->in_place_ = false;
     for (void *q : {(void *)h_arena_, (void *)h_back_})
         if (q)
             (void)hipHostFree(q);
@@ -126,16 +128,61 @@ uint32_t Chain::extent(int32_t nh, uint32_t length)
     return ext_;
 }
 
-int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
+// A new batch: every member's work state reset, the per-packet arrays
+// reserved for BATCH packets (member 0's).
+int Chain::begin_batch()
 {
     if (!init_) {
         init_ = true;
         mm_.resize(m_.size());
     }
-    if (resume_ >= 0) {
+    const size_t cap = std::max<size_t>(m_[0]->batch_cap_, 1);
+    if (grow_members(cap, 0))
+        return -1;
+    views_.clear();
+    done_.clear();
+    copied_.clear();
+    for (auto *v : {&views0_, &views_})
+        v->reserve(mcap_);
+    for (auto *v : {&staged_, &back_})
+        v->reserve(mcap_);
+    done_.reserve(mcap_);
+    copied_.reserve(mcap_);
+    for (size_t k = 0; k < m_.size(); k++) {
+        setup(k);
+        mm_[k].w.reset();
+        mm_[k].rebuild = false;
+        m_[k]->in_place_ = true;                      // the chain writes the packets back itself
+    }
+    h2d_done_ = false;
+    return 0;
+}
+
+// The batch outgrew its arrays (a caller that pushes past a full batch)
+int Chain::grow_batch()
+{
+    const size_t c = mcap_ * 2;
+    if (grow_members(c, 1))
+        return -1;
+    for (auto *v : {&views0_, &views_})
+        v->reserve(c);
+    for (auto *v : {&staged_, &back_})
+        v->reserve(c);
+    done_.reserve(c);
+    copied_.reserve(c);
+    for (size_t k = 0; k < m_.size(); k++)
+        setup(k);                                    // the arrays moved
+    return 0;
+}
+
+int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
+{
+    if (failed_) {
         err_ = "the chain's failed flush must be retried (or the packets abandoned) first";
         return CLK_EINVAL;
     }
+    uint64_t slot = 0;
+    uint32_t need = 0;
     if (m_[0]->zerocopy_) {
         // ZEROCOPY: the kernels read and write the packets where they lie,
         // in registered host memory (clk_host_register); one region per batch
@@ -158,24 +205,41 @@ int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t toke
             if (r)
                 return r;
         }
+        if (views0_.empty() && begin_batch()) {
+            err_ = "out of device / pinned memory";
+            return CLK_EINVAL;
+        }
         zc_host_ = zc_last_;
         zc_dev_ = zc_last_dev_;
-        views0_.push_back(ChainView{data, token, (uint64_t)(a - zc_host_), length, nh_offset, (uint16_t)anno});
-        staged_.push_back(0);
-        back_.push_back(0);
-        return views0_.size() >= m_[0]->batch_cap_ ? 1 : 0;
+        slot = (uint64_t)(a - zc_host_);
+    } else {
+        if (views0_.empty() && begin_batch()) {
+            err_ = "out of device / pinned memory";
+            return CLK_EINVAL;
+        }
+        need = std::min(length, extent(nh_offset, length));
+        slot = (used_ + 15) & ~size_t(15);
+        if (slot + need + 64 > h_cap_ &&
+            pinned_grow(&h_arena_, &h_cap_, std::max<size_t>(slot + need + 64, size_t(1) << 20), used_)) {
+            err_ = "out of pinned host memory";
+            return CLK_EINVAL;
+        }
+        stage_copy(h_arena_ + slot, data, need, length);
+        used_ = slot + need;
     }
-    const uint32_t need = std::min(length, extent(nh_offset, length));
-    const size_t slot = (used_ + 15) & ~size_t(15);
-    if (slot + need + 64 > h_cap_ && pinned_grow(&h_arena_, &h_cap_, std::max(slot + need + 64, size_t(1) << 20), used_)) {
-        err_ = "out of pinned host memory";
+    if (views0_.size() == mcap_ && grow_batch()) {
+        err_ = "out of device / pinned memory";
         return CLK_EINVAL;
     }
-    stage_copy(h_arena_ + slot, data, need, length);
-    views0_.push_back(ChainView{data, token, slot, length, nh_offset, (uint16_t)anno});
+    const ChainView v{data, token, slot, length, nh_offset, (uint16_t)anno};
+    const uint32_t i = (uint32_t)views0_.size();
+    views0_.push_back(v);
+    views_.push_back(v);
     staged_.push_back(need);
     back_.push_back(0);                              // grown by each member whose kernel may rewrite it
-    used_ = slot + need;
+    done_.push_back(0);
+    copied_.push_back(0);
+    advance(i, 0);                                   // into member 0, and on through host decisions
     return views0_.size() >= m_[0]->batch_cap_ ? 1 : 0;
 }
 
@@ -184,6 +248,8 @@ int Chain::push_burst(uint8_t *const *datas, const uint32_t *lengths, const int3
 {
     double t0 = now_s();
     for (uint32_t k = 0; k < n; k++) {
+        if (k + 8 < n)                               // the packet 8 ahead, while this one is staged
+            __builtin_prefetch(datas[k + 8]);
         int r = push(datas[k], lengths[k], nh_offsets ? nh_offsets[k] : -1, first_token + k, 0);
         if (r < 0)
             return r;
@@ -198,17 +264,10 @@ int Chain::push_burst(uint8_t *const *datas, const uint32_t *lengths, const int3
     return CLK_SUCCESS;
 }
 
-int Chain::grow(size_t bytes, size_t n)
+// Member buffers for c packets (pinned descriptors / verdicts, device
+// copies, events, work arrays); keep: the descriptors filled so far survive.
+int Chain::grow_members(size_t c, int keep)
 {
-    if (bytes && d_cap_ < bytes) {
-        if (d_arena_)
-            (void)hipFree(d_arena_);
-        d_arena_ = nullptr;
-        const size_t c = std::max(bytes, d_cap_ * 2);
-        if (hipMalloc(&d_arena_, c) != hipSuccess)
-            return -1;
-        d_cap_ = c;
-    }
     for (Member &M : mm_) {
         for (void *&e : M.ev)
             if (!e) {
@@ -217,41 +276,41 @@ int Chain::grow(size_t bytes, size_t n)
                     return -1;
                 e = (void *)h;
             }
-        if (M.cap >= n)
-            continue;
-        const size_t c = std::max(n, M.cap * 2);
-        size_t c1 = M.cap, c2 = M.cap, c3 = M.cap, c4 = M.cap, c5 = M.cap, c6 = M.cap;
-        if (pinned_grow(&M.h_off, &c1, c, 0) || pinned_grow(&M.h_len, &c2, c, 0) ||
-            pinned_grow(&M.h_codes, &c3, c, 0) || pinned_grow(&M.h_anno, &c4, c, 0) ||
-            pinned_grow(&M.h_aux8, &c5, c, 0) || pinned_grow(&M.h_sums, &c6, c, 0))
-            return -1;
-        for (void *q : {(void *)M.d_off, (void *)M.d_len, (void *)M.d_codes, (void *)M.d_anno, (void *)M.d_aux8,
-                        (void *)M.d_sums})
-            if (q)
-                (void)hipFree(q);
-        M.d_off = nullptr, M.d_len = nullptr, M.d_codes = nullptr, M.d_anno = nullptr, M.d_aux8 = nullptr;
-        M.d_sums = nullptr;
-        if (hipMalloc(&M.d_off, c * 8) != hipSuccess || hipMalloc(&M.d_len, c * 4) != hipSuccess ||
-            hipMalloc(&M.d_codes, c) != hipSuccess || hipMalloc(&M.d_anno, c) != hipSuccess ||
-            hipMalloc(&M.d_aux8, c) != hipSuccess || hipMalloc(&M.d_sums, c * 2) != hipSuccess)
-            return -1;
-        M.cap = c;
+        if (M.cap < c) {
+            const size_t kn = keep ? M.w.n : 0;
+            size_t c1 = M.cap, c2 = M.cap, c3 = M.cap, c4 = M.cap, c5 = M.cap, c6 = M.cap;
+            if (pinned_grow(&M.h_off, &c1, c, kn) || pinned_grow(&M.h_len, &c2, c, kn) ||
+                pinned_grow(&M.h_codes, &c3, c, 0) || pinned_grow(&M.h_anno, &c4, c, kn) ||
+                pinned_grow(&M.h_aux8, &c5, c, 0) || pinned_grow(&M.h_sums, &c6, c, 0))
+                return -1;
+            for (void *q : {(void *)M.d_off, (void *)M.d_len, (void *)M.d_codes, (void *)M.d_anno, (void *)M.d_aux8,
+                            (void *)M.d_sums})
+                if (q)
+                    (void)hipFree(q);
+            M.d_off = nullptr, M.d_len = nullptr, M.d_codes = nullptr, M.d_anno = nullptr, M.d_aux8 = nullptr;
+            M.d_sums = nullptr;
+            if (hipMalloc(&M.d_off, c * 8) != hipSuccess || hipMalloc(&M.d_len, c * 4) != hipSuccess ||
+                hipMalloc(&M.d_codes, c) != hipSuccess || hipMalloc(&M.d_anno, c) != hipSuccess ||
+                hipMalloc(&M.d_aux8, c) != hipSuccess || hipMalloc(&M.d_sums, c * 2) != hipSuccess)
+                return -1;
+            M.cap = c;
+        }
+        if (M.reached.size() < c) {
+            M.reached.resize(c);
+            M.code.resize(c);
+            M.span_off.resize(c);
+        }
     }
+    mcap_ = std::max(mcap_, c);
     return 0;
 }
 
-// Member k's per-flush work state.
+// Member k's work state: where its arrays are, what it is.
 void Chain::setup(size_t k)
 {
     BatchElement *e = m_[k];
     Member &M = mm_[k];
     ChainWork &w = M.w;
-    const size_t n = views0_.size();
-    if (M.reached.size() < n) {
-        M.reached.resize(n);
-        M.code.resize(n);
-        M.span_off.resize(n);
-    }
     w.reached = M.reached.data(), w.code = M.code.data(), w.span_off = M.span_off.data();
     w.views = &views_;
     w.done = &done_;
@@ -279,13 +338,14 @@ void Chain::setup(size_t k)
 // at every member; a packet passed on goes straight to the next member.  A
 // member that decides every packet on the host (IPGWOptions without options,
 // FixIPSrc without the annotation, IPFragmenter within the MTU) so costs no
-// pass of its own.
+// pass of its own; the ones that pass such a member unchanged are not even
+// asked (ChainWork::passes).
 void Chain::advance(uint32_t i, size_t k)
 {
     const ChainView &v = views_[i];
     for (;;) {
         ChainWork &w = mm_[k].w;
-        if (w.routed == w.nreached && w.passes(v)) {  // passes unchanged: counted, not asked
+        if (w.routed == w.nreached && w.passes(v)) {
             m_[k]->packets_++;
             if (w.last) {
                 out_.push_back(ChainExit{v.token, (int32_t)k, 0, v.length, 0, i});
@@ -303,9 +363,10 @@ void Chain::advance(uint32_t i, size_t k)
 
 // Member k's GPU step over the packets that reached it and are not routed
 // yet -- descriptors up, its kernel, its verdicts back -- then their routing
-// (the class's route()): output 0 goes on to member k+1, anything else leaves
-// the chain at member k.  *launched: the member's kernels were queued (a
-// failure after that leaves the device bytes rewritten by them).
+// (the class's route(), chain_route_all): output 0 goes on to member k+1,
+// anything else leaves the chain at member k.  *launched: the member's
+// kernels were queued (a failure after that leaves the device bytes
+// rewritten by them).
 int Chain::run_member(size_t k, bool *launched)
 {
     BatchElement *e = m_[k];
@@ -313,7 +374,7 @@ int Chain::run_member(size_t k, bool *launched)
     ChainWork &w = M.w;
     hipStream_t s = (hipStream_t)clk_ctx_stream(e->ctx_);
     double t0 = now_s();
-    if (M.rebuild) {                                 // resumed: a new batch of the packets left
+    if (M.rebuild) {                                 // after a failure: a new batch of the packets left
         M.rebuild = false;
         std::vector<uint32_t> left(w.reached + w.routed, w.reached + w.nreached);
         w.reset();
@@ -375,12 +436,8 @@ int Chain::run_member(size_t k, bool *launched)
     }
     stats_[2] += now_s() - t0;
     t0 = now_s();
-    const bool more = k + 1 < m_.size();
-    for (size_t q = w.routed; q < w.nreached; q++) {
-        w.routed = q + 1;
-        if (e->chain_route(w, q) && more)
-            advance(w.reached[q], k + 1);
-    }
+    e->h_aux8_ = M.h_aux8;
+    e->chain_route_all(w, *this, k);
     stats_[6] += now_s() - t0;
     return CLK_SUCCESS;
 }
@@ -427,47 +484,35 @@ int Chain::flush()
     if (views0_.empty())
         return CLK_SUCCESS;
     err_.clear();
-    const size_t n = views0_.size();
     hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
-    struct InPlace {         // routing: the chain writes the packets back itself
-        std::vector<BatchElement *> &m;
-        explicit InPlace(std::vector<BatchElement *> &v) : m(v) { for (BatchElement *e : m) e->in_place_ = true; }
-        ~InPlace() { for (BatchElement *e : m) e->in_place_ = false; }
-    } in_place(m_);
-    size_t k0 = 0;
-    if (resume_ >= 0) {
-        k0 = (size_t)resume_;
-    } else {
-        if (grow(m_[0]->zerocopy_ ? 0 : used_ + 64, n)) {
-            err_ = "out of device / pinned memory";
-            return CLK_EHIP;
-        }
-        if (!m_[0]->zerocopy_) {
-            double t0 = now_s();
-            hipError_t er = glue_checked(hipMemcpyAsync(d_arena_, h_arena_, used_, hipMemcpyHostToDevice, s));
-            if (er != hipSuccess) {
-                (void)hipStreamSynchronize(s);
-                err_ = std::string("hipMemcpyAsync(packets): ") + hipGetErrorString(er);
+    if (!h2d_done_ && !m_[0]->zerocopy_) {
+        if (d_cap_ < used_ + 64) {
+            if (d_arena_)
+                (void)hipFree(d_arena_);
+            d_arena_ = nullptr;
+            const size_t c = std::max(used_ + 64, d_cap_ * 2);
+            d_cap_ = 0;
+            if (hipMalloc(&d_arena_, c) != hipSuccess) {
+                failed_ = true;
+                err_ = "out of device memory";
                 return CLK_EHIP;
             }
-            stats_[4] += now_s() - t0;
-        }
-        views_.assign(views0_.begin(), views0_.end());
-        done_.assign(n, 0);
-        copied_.assign(n, 0);
-        for (size_t k = 0; k < m_.size(); k++) {
-            setup(k);
-            mm_[k].w.reset();
-            mm_[k].rebuild = false;
+            d_cap_ = c;
         }
         double t0 = now_s();
-        for (size_t i = 0; i < n; i++)
-            advance((uint32_t)i, 0);
-        stats_[1] += now_s() - t0;
+        hipError_t er = glue_checked(hipMemcpyAsync(d_arena_, h_arena_, used_, hipMemcpyHostToDevice, s));
+        if (er != hipSuccess) {
+            (void)hipStreamSynchronize(s);
+            failed_ = true;
+            err_ = std::string("hipMemcpyAsync(packets): ") + hipGetErrorString(er);
+            return CLK_EHIP;
+        }
+        stats_[4] += now_s() - t0;
     }
+    h2d_done_ = true;
     int failed = CLK_SUCCESS;
     std::string failed_why;
-    for (size_t k = k0; k < m_.size(); k++) {
+    for (size_t k = 0; k < m_.size(); k++) {
         ChainWork &w = mm_[k].w;
         if (w.routed == w.nreached)
             continue;
@@ -497,7 +542,7 @@ int Chain::flush()
         // routed, and the ones those passed are at the next members already);
         // the next flush builds member k's batch of them again
         mm_[k].rebuild = true;
-        resume_ = (int)k;
+        failed_ = true;
         const std::string why = failed ? failed_why + "; " + err_ : err_;
         (void)copy_back(false);
         err_ = why;
@@ -505,18 +550,28 @@ int Chain::flush()
     }
     int r = copy_back(true);
     if (r) {
-        resume_ = (int)m_.size();                    // only the copy back is left
+        failed_ = true;                              // only the copy back is left
         return r;
     }
-    resume_ = -1;
-    views0_.clear();
-    staged_.clear();
-    back_.clear();
-    used_ = 0;
-    zc_host_ = nullptr;
+    end_batch();
     if (failed)
         err_ = failed_why;
     return failed;
+}
+
+void Chain::end_batch()
+{
+    failed_ = false;
+    views0_.clear();
+    views_.clear();
+    staged_.clear();
+    back_.clear();
+    done_.clear();
+    copied_.clear();
+    used_ = 0;
+    zc_host_ = nullptr;
+    for (BatchElement *e : m_)
+        e->in_place_ = false;
 }
 
 // A GPU that keeps failing: every packet still in the chain -- staged, or
@@ -527,44 +582,34 @@ int Chain::flush()
 uint64_t Chain::abandon()
 {
     uint64_t k = 0;
-    if (resume_ >= 0) {
+    if (views0_.empty())
+        return 0;
+    if (h2d_done_)
         (void)copy_back(false);                      // one more try for the bytes of the routed ones
-        for (size_t j = 0; j < mm_.size(); j++) {
-            ChainWork &w = mm_[j].w;
-            for (size_t q = w.routed; q < w.nreached; q++) {
-                const uint32_t i = w.reached[q];
-                if (done_[i])
-                    continue;
-                out_.push_back(ChainExit{views_[i].token, (int32_t)j, CLK_PORT_KILL, views_[i].length, 0, i});
-                done_[i] = 1;
-                m_[j]->lost_++;
-                k++;
-            }
-            w.routed = w.nreached;
-            mm_[j].rebuild = false;
+    for (size_t j = 0; j < mm_.size(); j++) {
+        ChainWork &w = mm_[j].w;
+        for (size_t q = w.routed; q < w.nreached; q++) {
+            const uint32_t i = w.reached[q];
+            if (done_[i])
+                continue;
+            out_.push_back(ChainExit{views_[i].token, (int32_t)j, CLK_PORT_KILL, views_[i].length, 0, i});
+            done_[i] = 1;
+            m_[j]->lost_++;
+            k++;
         }
-        for (size_t r = pub_; r < out_.size(); r++) {
-            ChainExit &x = out_[r];
-            if (x.idx != ~0u && x.port != CLK_PORT_KILL && x.port != CLK_PORT_NEXT && back_[x.idx] && !copied_[x.idx]) {
-                x.port = CLK_PORT_KILL;
-                m_[(size_t)x.member]->lost_++;
-                k++;
-            }
-        }
-        resume_ = -1;
-    } else {
-        for (size_t i = 0; i < views0_.size(); i++) {
-            out_.push_back(ChainExit{views0_[i].token, 0, CLK_PORT_KILL, views0_[i].length, 0, (uint32_t)i});
-            m_[0]->lost_++;
+        w.routed = w.nreached;
+        mm_[j].rebuild = false;
+    }
+    for (size_t r = pub_; r < out_.size(); r++) {
+        ChainExit &x = out_[r];
+        if (x.idx != ~0u && x.port != CLK_PORT_KILL && x.port != CLK_PORT_NEXT && back_[x.idx] && !copied_[x.idx]) {
+            x.port = CLK_PORT_KILL;
+            m_[(size_t)x.member]->lost_++;
             k++;
         }
     }
     pub_ = out_.size();
-    views0_.clear();
-    staged_.clear();
-    back_.clear();
-    used_ = 0;
-    zc_host_ = nullptr;
+    end_batch();
     return k;
 }
 

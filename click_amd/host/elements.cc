@@ -287,9 +287,9 @@ int BatchElement::chain_step(ChainWork &w, uint32_t i)
                           [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
 }
 
-bool BatchElement::chain_route(ChainWork &w, size_t q)
+void BatchElement::chain_route_all(ChainWork &w, Chain &c, size_t k)
 {
-    return chain_route_at(w, q, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
+    chain_route_loop(w, c, k, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
 }
 
 template <class SpanF>

@@ -249,10 +249,12 @@ struct ChainWork {
             return this->C::span(p, o, l, c);                                                                   \
         }, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); });         \
     }                                                                                                           \
-    bool chain_route(ChainWork &w_, size_t q_) override                                                         \
+    void chain_route_all(ChainWork &w_, Chain &c_, size_t k_) override                                        \
     {                                                                                                           \
-        return chain_route_at(w_, q_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
+        chain_route_loop(w_, c_, k_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
     }
+
+class Chain;
 
 class BatchElement {
   public:
@@ -332,10 +334,11 @@ class BatchElement {
     // route into them).  chain_step(): packet i reaches the member -- its
     // descriptor (0: it waits for the GPU), or its host decision, routed at
     // once while no packet before it waits (1: passed on, 2: left the
-    // chain).  chain_route(): route reached packet q after the member's
-    // kernel; true when it goes on to the next member.
+    // chain).  chain_route_all(): route the packets waiting at member k
+    // after its kernel, each one passed on going into member k+1
+    // (Chain::advance).
     virtual int chain_step(ChainWork &w, uint32_t i);
-    virtual bool chain_route(ChainWork &w, size_t q);
+    virtual void chain_route_all(ChainWork &w, Chain &c, size_t k);
     // the decision the chain may take for the member (ChainPass)
     virtual void chain_pass(uint8_t *kind, uint32_t *param) const { *kind = CHAIN_PASS_NONE, *param = 0; }
     // the bytes past the network header the kernel may write (~0u: any)
@@ -344,6 +347,8 @@ class BatchElement {
     int chain_step_one(ChainWork &w, uint32_t i, SpanF &&span_f, RouteF &&route_f);
     template <class RouteF>
     bool chain_route_at(ChainWork &w, size_t q, RouteF &&route_f);
+    template <class RouteF>
+    void chain_route_loop(ChainWork &w, Chain &c, size_t k, RouteF &&route_f);
     template <class RouteF>
     bool chain_route_pending(ChainWork &w, uint32_t i, Pending &p, int code, uint16_t sum, RouteF &&route_f);
     ResultQueue chain_side_;          // a member's pre/post results while a chain routes
@@ -852,6 +857,8 @@ class Chain {
                    uint32_t n);
     int flush();
     uint64_t abandon();
+    // packet i reaches member k (and goes on through host decisions)
+    void advance(uint32_t i, size_t k);
     uint64_t pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap);
     const std::string &last_error() const { return err_; }
     size_t pending() const { return views0_.size(); }
@@ -881,9 +888,11 @@ class Chain {
         std::vector<int32_t> code;
         ChainWork w;
     };
-    int grow(size_t bytes, size_t n);
+    int begin_batch();
+    int grow_batch();
+    int grow_members(size_t c, int keep);
+    void end_batch();
     void setup(size_t k);
-    void advance(uint32_t i, size_t k);
     int run_member(size_t k, bool *launched);
     int copy_back(bool all);
     uint32_t extent(int32_t nh, uint32_t length);
@@ -892,7 +901,9 @@ class Chain {
     std::vector<ChainView> views0_, views_;   // as pushed; as they move through the members
     std::vector<uint32_t> staged_, back_;     // bytes staged / written back per packet
     std::vector<uint8_t> done_, copied_;      // per packet: left the chain; bytes copied back
-    int resume_ = -1;                         // a failed flush: the member it resumes at
+    bool failed_ = false;                     // a flush failed: the batch must be flushed (or abandoned)
+    bool h2d_done_ = false;                   // the staged batch is on the device
+    size_t mcap_ = 0;                         // packets the per-packet arrays hold
     const uint8_t *zc_host_ = nullptr;        // ZEROCOPY: the batch's registered region
     uint8_t *zc_dev_ = nullptr;
     const uint8_t *zc_last_ = nullptr;        // last region found (lookup cache)
@@ -911,6 +922,16 @@ class Chain {
     bool report_passes_ = false;
     std::string err_;
 };
+
+template <class RouteF>
+void BatchElement::chain_route_loop(ChainWork &w, Chain &c, size_t k, RouteF &&route_f)
+{
+    for (size_t q = w.routed; q < w.nreached; q++) {
+        w.routed = q + 1;
+        if (chain_route_at(w, q, route_f) && !w.last)
+            c.advance(w.reached[q], k + 1);
+    }
+}
 
 } // namespace host
 } // namespace clk
