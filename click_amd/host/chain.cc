@@ -155,7 +155,42 @@ int Chain::begin_batch()
         m_[k]->in_place_ = true;                      // the chain writes the packets back itself
     }
     h2d_done_ = false;
+    sent_ = 0;
+    sent_ok_ = true;
     return 0;
+}
+
+// Staged bytes go to the device while the batch fills (one async copy per
+// H2D_CHUNK), so the flush waits only for the tail.  A copy that fails is
+// sent again, whole, by the flush.
+int Chain::device_arena(size_t bytes)
+{
+    if (d_cap_ >= bytes)
+        return 0;
+    hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
+    (void)hipStreamSynchronize(s);
+    if (d_arena_)
+        (void)hipFree(d_arena_);
+    d_arena_ = nullptr;
+    d_cap_ = 0;
+    sent_ = 0;                                       // what was sent is gone with the old arena
+    const size_t c = std::max(bytes, h_cap_);
+    if (hipMalloc(&d_arena_, c) != hipSuccess)
+        return -1;
+    d_cap_ = c;
+    return 0;
+}
+
+void Chain::send_chunk()
+{
+    if (!sent_ok_ || device_arena(used_ + 64))
+        return;
+    hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
+    if (glue_checked(hipMemcpyAsync(d_arena_ + sent_, h_arena_ + sent_, used_ - sent_, hipMemcpyHostToDevice, s)) !=
+        hipSuccess)
+        sent_ok_ = false;
+    else
+        sent_ = used_;
 }
 
 // The batch outgrew its arrays (a caller that pushes past a full batch)
@@ -219,13 +254,18 @@ int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t toke
         }
         need = std::min(length, extent(nh_offset, length));
         slot = (used_ + 15) & ~size_t(15);
-        if (slot + need + 64 > h_cap_ &&
-            pinned_grow(&h_arena_, &h_cap_, std::max<size_t>(slot + need + 64, size_t(1) << 20), used_)) {
-            err_ = "out of pinned host memory";
-            return CLK_EINVAL;
+        if (slot + need + 64 > h_cap_) {
+            if (sent_)                               // copies from the old arena may be in flight
+                (void)hipStreamSynchronize((hipStream_t)clk_ctx_stream(m_[0]->ctx_));
+            if (pinned_grow(&h_arena_, &h_cap_, std::max<size_t>(slot + need + 64, size_t(1) << 20), used_)) {
+                err_ = "out of pinned host memory";
+                return CLK_EINVAL;
+            }
         }
         stage_copy(h_arena_ + slot, data, need, length);
         used_ = slot + need;
+        if (used_ - sent_ >= H2D_CHUNK)
+            send_chunk();
     }
     if (views0_.size() == mcap_ && grow_batch()) {
         err_ = "out of device / pinned memory";
@@ -486,27 +526,24 @@ int Chain::flush()
     err_.clear();
     hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
     if (!h2d_done_ && !m_[0]->zerocopy_) {
-        if (d_cap_ < used_ + 64) {
-            if (d_arena_)
-                (void)hipFree(d_arena_);
-            d_arena_ = nullptr;
-            const size_t c = std::max(used_ + 64, d_cap_ * 2);
-            d_cap_ = 0;
-            if (hipMalloc(&d_arena_, c) != hipSuccess) {
-                failed_ = true;
-                err_ = "out of device memory";
-                return CLK_EHIP;
-            }
-            d_cap_ = c;
+        if (device_arena(used_ + 64)) {
+            failed_ = true;
+            err_ = "out of device memory";
+            return CLK_EHIP;
         }
+        if (!sent_ok_)
+            sent_ = 0, sent_ok_ = true;
         double t0 = now_s();
-        hipError_t er = glue_checked(hipMemcpyAsync(d_arena_, h_arena_, used_, hipMemcpyHostToDevice, s));
+        hipError_t er = glue_checked(hipMemcpyAsync(d_arena_ + sent_, h_arena_ + sent_, used_ - sent_,
+                                                    hipMemcpyHostToDevice, s));
         if (er != hipSuccess) {
             (void)hipStreamSynchronize(s);
             failed_ = true;
+            sent_ = 0;
             err_ = std::string("hipMemcpyAsync(packets): ") + hipGetErrorString(er);
             return CLK_EHIP;
         }
+        sent_ = used_;
         stats_[4] += now_s() - t0;
     }
     h2d_done_ = true;

@@ -890,6 +890,9 @@ class Chain {
     };
     int begin_batch();
     int grow_batch();
+    int device_arena(size_t bytes);
+    void send_chunk();
+    static constexpr size_t H2D_CHUNK = size_t(1) << 20;
     int grow_members(size_t c, int keep);
     void end_batch();
     void setup(size_t k);
@@ -903,6 +906,8 @@ class Chain {
     std::vector<uint8_t> done_, copied_;      // per packet: left the chain; bytes copied back
     bool failed_ = false;                     // a flush failed: the batch must be flushed (or abandoned)
     bool h2d_done_ = false;                   // the staged batch is on the device
+    size_t sent_ = 0;                         // staged bytes already copied to the device this batch
+    bool sent_ok_ = true;
     size_t mcap_ = 0;                         // packets the per-packet arrays hold
     const uint8_t *zc_host_ = nullptr;        // ZEROCOPY: the batch's registered region
     uint8_t *zc_dev_ = nullptr;
@@ -928,6 +933,8 @@ void BatchElement::chain_route_loop(ChainWork &w, Chain &c, size_t k, RouteF &&r
 {
     for (size_t q = w.routed; q < w.nreached; q++) {
         w.routed = q + 1;
+        if (q + 8 < w.nreached)              // the packet route() reads 8 ahead
+            __builtin_prefetch((*w.views)[w.reached[q + 8]].data);
         if (chain_route_at(w, q, route_f) && !w.last)
             c.advance(w.reached[q], k + 1);
     }
