@@ -49,10 +49,11 @@ std::vector<uint8_t> udp_packet(uint32_t L)
 }
 
 template <class CA, class CB>
-void leg(const char *name, const char *ga, const char *gb, uint32_t L, int n)
+void leg(const char *name, const char *ga, const char *gb, uint32_t L, int n, uint32_t batch)
 {
-    Host<CA> a(ga, "", 2);
-    Host<CB> b(gb, "", 2);
+    const std::string conf = "BATCH " + std::to_string(batch);
+    Host<CA> a(ga, conf, 2);
+    Host<CB> b(gb, conf, 2);
     b.upstream = [&a]() { return a.pull(); };
     const std::vector<uint8_t> x = udp_packet(L);
     auto fill = [&](int k) {
@@ -92,11 +93,11 @@ void leg(const char *name, const char *ga, const char *gb, uint32_t L, int n)
     size_t slow = 0;
     for (uint32_t t : v)
         slow += t > 10000;
-    std::printf("{\"leg\": \"%s\", \"graph\": \"Queue -> %s -> %s -> pull\", \"bytes\": %u, \"packets\": %d, "
+    std::printf("{\"leg\": \"%s\", \"graph\": \"Queue -> %s -> %s -> pull\", \"batch\": %u, \"bytes\": %u, \"packets\": %d, "
                 "\"delivered\": %zu, \"dropped\": %zu, \"seconds\": %.4f, \"mpps\": %.2f, "
                 "\"pull_ns\": {\"p50\": %u, \"p99\": %u, \"p999\": %u, \"max\": %u}, \"pulls_over_10us\": %zu, "
                 "\"batches\": [%llu, %llu]}\n",
-                name, ga, gb, L, n, got.size(), a.out[1].size() + b.out[1].size(), sec,
+                name, ga, gb, batch, L, n, got.size(), a.out[1].size() + b.out[1].size(), sec,
                 (double)got.size() / sec / 1e6, pct(0.5), pct(0.99), pct(0.999), v.empty() ? 0u : v.back(), slow,
                 std::stoull(a.handler("batches")) - std::stoull(b0), std::stoull(b.handler("batches")) - std::stoull(b1));
     std::fflush(stdout);
@@ -113,7 +114,11 @@ int main(int argc, char **argv)
         return 0;
     }
     const int scale = argc > 1 ? std::max(1, std::atoi(argv[1])) : 1;
-    leg<CheckIPC, SetC>("pull_c2", "CheckIPHeader", "SetIPChecksum", 64, 2000000 / scale);
-    leg<PlainC, SetC>("pull_c3", "CheckUDPHeader", "SetUDPChecksum", 1500, 1000000 / scale);
+    // BATCH bounds the longest pull (one refill stages a batch and routes
+    // the one before): the default and a small one
+    for (uint32_t batch : {65536u, 4096u}) {
+        leg<CheckIPC, SetC>("pull_c2", "CheckIPHeader", "SetIPChecksum", 64, 2000000 / scale, batch);
+        leg<PlainC, SetC>("pull_c3", "CheckUDPHeader", "SetUDPChecksum", 1500, 1000000 / scale, batch);
+    }
     return 0;
 }
