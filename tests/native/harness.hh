@@ -132,6 +132,7 @@ class Host {
     std::atomic<int> runcount{0};
     std::deque<TPacket *> input;                        // pull context source
     std::function<TPacket *()> upstream;                // or another element's pull()
+    std::function<void(TPacket *)> downstream;          // output 0 pushes into another element
     std::vector<std::string> chat, msgs;        // (under out_mu: states on several threads)
     std::atomic<int> wakes{0};
     void (*on_out0)(Host &, TPacket *) = nullptr;       // re-entrancy probe
@@ -172,6 +173,10 @@ class Host {
     uint32_t length(TPacket *p) { return TOps::length(p); }
     void output_push(int, int port, TPacket *p)
     {
+        if (port == 0 && downstream) {                  // output 0 connected to another element
+            downstream(p);
+            return;
+        }
         {
             std::lock_guard<std::mutex> g(out_mu);
             out[(size_t)port].push_back(p);

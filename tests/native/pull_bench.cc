@@ -1,5 +1,6 @@
-// Pull-mode measurement (not a test, not product code; bench.py --e2e runs
-// it): the Click adapter's core in pull context on one thread, through the
+// Adapter-core measurement (not a test, not product code; bench.py --e2e
+// runs it): config 1 pushed through five elements or one chain, and the
+// Click adapter's core in pull context on one thread, through the
 // native harness (harness.hh), Queue -> X -> Y -> pulled downstream (as
 // ToDevice pulls), with the packets already in the queue.  Prints one JSON
 // line per leg (after an untimed warm-up drain of n/4 packets): Mpps over
@@ -105,6 +106,97 @@ void leg(const char *name, const char *ga, const char *gb, uint32_t L, int n, ui
         TOps::kill(p);
 }
 
+// Push context, config 1 (fake-iprouter's forwarding path: 114 B frames,
+// CheckIPHeader OFFSET 14 -> IPGWOptions -> FixIPSrc -> DecIPTTL ->
+// IPFragmenter), through the adapter core: five elements, each output 0
+// pushing into the next, or one chain (hipcore chains, as the Click adapter
+// forms it).  The frames are made before the clock starts; all are pushed,
+// then the latency timer's flush runs.
+std::vector<uint8_t> c1_frame()
+{
+    std::vector<uint8_t> f(14, 0);
+    f[12] = 0x08;
+    const std::vector<uint8_t> ip = udp_packet(100);
+    f.insert(f.end(), ip.begin(), ip.end());
+    return f;
+}
+
+void push_c1(int n, bool chained)
+{
+    const std::string B = "BATCH 65536";
+    const std::vector<uint8_t> f = c1_frame();
+    std::vector<TPacket *> in((size_t)n);
+    auto fill = [&]() {
+        for (int i = 0; i < n; i++)
+            in[(size_t)i] = make(f.data(), f.size(), i);
+    };
+    double sec = 0;
+    size_t out0 = 0;
+    if (chained) {
+        Member<CheckIPC> c0("CheckIPHeader", "OFFSET 14, " + B, 2);
+        c0.cls.offset = 14;
+        Member<GWOptC> c1("IPGWOptions", "10.0.0.2, " + B, 2);
+        Member<FixSrcC> c2("FixIPSrc", "10.0.0.2, " + B, 1);
+        Member<DecTTLC> c3("DecIPTTL", B, 2);
+        Member<FragC> c4("IPFragmenter", "1500, " + B, 2);
+        c4.cls.mtu = 1500;
+        ChainHost ch({&c0, &c1, &c2, &c3, &c4});
+        for (int run = 0; run < 2; run++) {            // the first run warms up
+            fill();
+            const auto t0 = std::chrono::steady_clock::now();
+            for (TPacket *p : in)
+                ch.push(p);
+            ch.timer();
+            sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            out0 = c4.out[0].size();
+            for (auto *m : ch.m)
+                for (auto &v : m->out) {
+                    for (TPacket *p : v)
+                        TOps::kill(p);
+                    v.clear();
+                }
+        }
+    } else {
+        Host<CheckIPC> h0("CheckIPHeader", "OFFSET 14, " + B, 2);
+        h0.cls.offset = 14;
+        Host<GWOptC> h1("IPGWOptions", "10.0.0.2, " + B, 2);
+        Host<FixSrcC> h2("FixIPSrc", "10.0.0.2, " + B, 1);
+        Host<DecTTLC> h3("DecIPTTL", B, 2);
+        Host<FragC> h4("IPFragmenter", "1500, " + B, 2);
+        h4.cls.mtu = 1500;
+        h0.downstream = [&](TPacket *p) { h1.push(p); };
+        h1.downstream = [&](TPacket *p) { h2.push(p); };
+        h2.downstream = [&](TPacket *p) { h3.push(p); };
+        h3.downstream = [&](TPacket *p) { h4.push(p); };
+        for (int run = 0; run < 2; run++) {
+            fill();
+            const auto t0 = std::chrono::steady_clock::now();
+            for (TPacket *p : in)
+                h0.push(p);
+            h0.timer();
+            h1.timer();
+            h2.timer();
+            h3.timer();
+            h4.timer();
+            sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            out0 = h4.out[0].size();
+            for (auto *h : std::initializer_list<std::vector<std::vector<TPacket *> > *>{&h0.out, &h1.out, &h2.out,
+                                                                                         &h3.out, &h4.out})
+                for (auto &v : *h) {
+                    for (TPacket *p : v)
+                        TOps::kill(p);
+                    v.clear();
+                }
+        }
+    }
+    std::printf("{\"leg\": \"push_c1_%s\", \"graph\": \"CheckIPHeader(14) -> IPGWOptions -> FixIPSrc -> DecIPTTL -> "
+                "IPFragmenter(1500), %s\", \"bytes\": %zu, \"packets\": %d, \"forwarded\": %zu, \"seconds\": %.4f, "
+                "\"mpps\": %.2f}\n",
+                chained ? "chain" : "elements", chained ? "one chain" : "five elements", f.size(), n, out0, sec,
+                (double)n / sec / 1e6);
+    std::fflush(stdout);
+}
+
 }   // namespace
 
 int main(int argc, char **argv)
@@ -116,6 +208,8 @@ int main(int argc, char **argv)
     const int scale = argc > 1 ? std::max(1, std::atoi(argv[1])) : 1;
     // BATCH bounds the longest pull (one refill stages a batch and routes
     // the one before): the default and a small one
+    push_c1(600000 / scale, false);
+    push_c1(600000 / scale, true);
     for (uint32_t batch : {65536u, 4096u}) {
         leg<CheckIPC, SetC>("pull_c2", "CheckIPHeader", "SetIPChecksum", 64, 2000000 / scale, batch);
         leg<PlainC, SetC>("pull_c3", "CheckUDPHeader", "SetUDPChecksum", 1500, 1000000 / scale, batch);
