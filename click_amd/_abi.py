@@ -179,7 +179,7 @@ SIGNATURES = {
     "clk_chain_push_burst": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_uint64, ctypes.c_uint32]),
     "clk_chain_flush": (ctypes.c_int, [_P]),
     "clk_chain_abandon": (ctypes.c_uint64, [_P]),
-    "clk_chain_report_passes": (ctypes.c_int, [_P, ctypes.c_int]),
+    "clk_chain_report_passes": (ctypes.c_int, [_P, ctypes.c_uint64]),
     "clk_chain_results": (ctypes.c_uint64, [_P, _P, _P, _P, _P, _P, ctypes.c_uint64]),
     "clk_chain_stats": (ctypes.c_int, [_P, _P, ctypes.c_int]),
 }

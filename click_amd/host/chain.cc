@@ -368,7 +368,7 @@ void Chain::setup(size_t k)
     w.nh_after = e->nh_after();
     w.last = k + 1 == m_.size();
     w.inline_ok = !e->has_pre_route_ && !e->has_post_route_;
-    w.report_passes = report_passes_;
+    w.report_passes = k < 64 && (report_passes_ >> k & 1);
     e->h_aux8_ = M.h_aux8;
 }
 
@@ -739,11 +739,11 @@ int clk_chain_push_burst(clk_chain *w, uint8_t *const *datas, const uint32_t *le
     return w->c->push_burst(datas, lengths, nh_offsets, first_token, n);
 }
 
-int clk_chain_report_passes(clk_chain *w, int on)
+int clk_chain_report_passes(clk_chain *w, uint64_t members)
 {
     if (!w)
         return CLK_EINVAL;
-    w->c->report_passes(on != 0);
+    w->c->report_passes(members);
     return CLK_SUCCESS;
 }
 

@@ -862,7 +862,7 @@ class Chain {
     uint64_t pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap);
     const std::string &last_error() const { return err_; }
     size_t pending() const { return views0_.size(); }
-    void report_passes(bool on) { report_passes_ = on; }
+    void report_passes(uint64_t members) { report_passes_ = members; }
     // host seconds spent so far: staging (push), descriptors (build), the
     // members' GPU round trips, next-member views, H2D of the batch, D2H of
     // the rewritten bytes, routing, copy-back
@@ -924,7 +924,7 @@ class Chain {
     int32_t ext_nh_ = -3;                     // extent() cache: the nh and length it was computed for
     uint32_t ext_len_ = 0, ext_ = 0;
     bool init_ = false;
-    bool report_passes_ = false;
+    uint64_t report_passes_ = 0;              // bit k: member k reports its passes
     std::string err_;
 };
 

@@ -14,6 +14,7 @@
 #include <click/router.hh>
 #include <click/routervisitor.hh>
 #include <click/straccum.hh>
+#include <ctype.h>
 #include <stdlib.h>
 #include <string.h>
 #include <new>
@@ -50,6 +51,17 @@ HIPBatchElement::configure(Vector<String> &conf, ErrorHandler *errh)
 	.read("CHAIN", _chain_conf)
 	.consume() < 0)
 	return -1;
+    // BATCH: the glue's (65536, sized for the device batch) unless given;
+    // the adapter's default is smaller, so a batch's packets stay in the
+    // host caches between staging and delivery (config 1
+    // through the core, 2.8 Mpps at 65536, 4.4 at 8192)
+    bool batch = false;
+    for (int i = 0; i < conf.size(); i++) {
+	String w = cp_uncomment(conf[i]);
+	batch = batch || (w.length() >= 5 && strncmp(w.data(), "BATCH", 5) == 0 && (w.length() == 5 || isspace((unsigned char) w[5])));
+    }
+    if (!batch)
+	conf.push_back(String("BATCH ") + String((int) ADAPTER_BATCH));
     _glue_conf = cp_unargvec(conf);
     _core.set_latency(_latency_ms);
     _core.set_max_retries(_retries);
@@ -204,7 +216,11 @@ HIPBatchElement::ensure_chain(PerThread &t)
     }
     if (t.mem.size() == (size_t) _chain.size()
 	&& clk_chain_create(t.mem.data(), (int) t.mem.size(), &t.chain) == CLK_SUCCESS) {
-	clk_chain_report_passes(t.chain, 1);
+	uint64_t report = 0;		// the members whose finish() changes a packet they pass on
+	for (int m = 0; m < _chain.size() && m < 64; m++)
+	    if (_chain[m]->cls_pass_effects())
+		report |= uint64_t(1) << m;
+	clk_chain_report_passes(t.chain, report);
 	for (int m = 1; m < _chain.size(); m++) {
 	    _chain[m]->_borrow_lock.acquire();
 	    _chain[m]->_borrowed.push_back(t.mem[m]);

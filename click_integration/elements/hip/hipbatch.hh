@@ -73,7 +73,8 @@ struct ClickPacketOps {
  *                 (default 3)
  *   CHAIN    bool join the GPU-backed elements after this one into one batch
  *                 (default true; see Chains below)
- * Glue keywords passed through: BATCH, ZEROCOPY, and the element's own.
+ * Glue keywords passed through: BATCH (default here ADAPTER_BATCH = 8192,
+ * where the glue's own default is 65536), ZEROCOPY, and the element's own.
  *
  * Threads (click -j N): one hipcore::State (context, glue element, held
  * packets, lock) per RouterThread, chosen by click_current_cpu_id()
@@ -104,6 +105,8 @@ struct ClickPacketOps {
  */
 class HIPBatchElement : public Element { public:
 
+    enum { ADAPTER_BATCH = 8192 };
+
     typedef hipcore::State<Packet, Spinlock> PerThread;
     typedef hipcore::Routed<Packet> Routed;
 
@@ -132,6 +135,7 @@ class HIPBatchElement : public Element { public:
     virtual bool cls_may_write() const		{ return false; }
     virtual bool cls_chain_last() const		{ return false; }
     virtual bool cls_chain_head_only() const	{ return false; }
+    virtual bool cls_pass_effects() const	{ return false; }
 
     // ---- the core's host interface (hipcore.hh); m: the chain member ---------
     Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
@@ -206,6 +210,7 @@ class HIPClassElement : public HIPBatchElement { public:
     bool cls_may_write() const		{ return C::may_write != 0; }
     bool cls_chain_last() const		{ return C::chain_last != 0; }
     bool cls_chain_head_only() const	{ return C::chain_head_only != 0; }
+    bool cls_pass_effects() const	{ return C::pass_effects != 0; }
   protected:
     C _cls;
 };

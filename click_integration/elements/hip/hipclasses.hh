@@ -42,13 +42,16 @@
  *                              returns the output port of *out, -1 for none
  *   end_of_batch(t)            after a batch's results
  *
- * And three traits for chains (hipcore.hh; the adapter forms them):
+ * And four traits for chains (hipcore.hh; the adapter forms them):
  *   may_write        the element may rewrite a packet's bytes (a chain makes
  *                    the packet writable at its head)
  *   chain_last       extra results after a packet (fragments): only the last
  *                    member of a chain
  *   chain_head_only  its prepare() clones the packet as it arrives
  *                    (PaintTee): only the first member
+ *   pass_effects     its finish() changes a packet it passes on (network
+ *                    header, trim, Strip, annotations): the chain reports
+ *                    those passes (clk_chain_report_passes)
  */
 #include <stdint.h>
 #include <string.h>
@@ -60,7 +63,7 @@ namespace hipcore {
 // The glue's drop(): output 1 if it exists, killed otherwise (the port comes
 // routed; checkipheader.cc:143-159, checked_output_push).
 template <class P, class O> struct Plain {
-    enum { may_write = 0, chain_last = 0, chain_head_only = 0 };
+    enum { may_write = 0, chain_last = 0, chain_head_only = 0, pass_effects = 0 };
     P *prepare(P *p, uint32_t *anno, P **extra) { (void) anno, (void) extra; return p; }
     int32_t nh_offset(P *p) const { return O::has_network_header(p) ? O::network_header_offset(p) : -1; }
     bool primary(int32_t port, uint32_t aux) const { (void) port, (void) aux; return true; }
@@ -100,6 +103,7 @@ template <class P, class O> struct Plain {
 // packet gets its network header set, is trimmed to ip_len, and carries
 // ip_dst as its destination annotation (213-223).
 template <class P, class O> struct CheckIPHeaderClass : Plain<P, O> {
+    enum { may_write = 0, chain_last = 0, chain_head_only = 0, pass_effects = 1 };
     uint32_t offset = 0;            // OFFSET (the glue parsed it)
     template <class S> int finish(S &t, Routed<P> &r, P **out)
     {
@@ -122,6 +126,7 @@ template <class P, class O> struct CheckIPHeaderClass : Plain<P, O> {
 // IPInputCombo (ipinputcombo.cc:66-140): Paint (71), Strip(14) (74), the
 // CheckIPHeader steps (125-132); a bad packet is killed (134-139).
 template <class P, class O> struct IPInputComboClass : Plain<P, O> {
+    enum { may_write = 0, chain_last = 0, chain_head_only = 0, pass_effects = 1 };
     uint32_t color = 0;             // COLOR
     int32_t nh_offset(P *p) const { (void) p; return 14; }   // the header sits behind the 14 bytes Strip removes
     template <class S> int finish(S &t, Routed<P> &r, P **out)
@@ -152,13 +157,13 @@ template <class P, class O> struct IPInputComboClass : Plain<P, O> {
 // (setipchecksum.cc:77, setudpchecksum.cc:40, settcpchecksum.cc:47); the
 // results route as the glue decided (output 1: SetUDPChecksum's fragments).
 template <class P, class O> struct SetChecksumClass : Plain<P, O> {
-    enum { may_write = 1, chain_last = 0, chain_head_only = 0 };
+    enum { may_write = 1, chain_last = 0, chain_head_only = 0, pass_effects = 0 };
     P *prepare(P *p, uint32_t *anno, P **extra) { (void) anno, (void) extra; return O::uniqueify(p); }
 };
 
 // DecIPTTL (decipttl.cc:45-77): writable only when the TTL is decremented.
 template <class P, class O> struct DecIPTTLClass : Plain<P, O> {
-    enum { may_write = 1, chain_last = 0, chain_head_only = 0 };
+    enum { may_write = 1, chain_last = 0, chain_head_only = 0, pass_effects = 0 };
     P *prepare(P *p, uint32_t *anno, P **extra)
     {
         (void) anno, (void) extra;
@@ -172,7 +177,7 @@ template <class P, class O> struct DecIPTTLClass : Plain<P, O> {
 // writable (167-169); a parameter problem goes to output 1 with its pointer
 // as the ICMP annotation (161-165).
 template <class P, class O> struct IPGWOptionsClass : Plain<P, O> {
-    enum { may_write = 1, chain_last = 0, chain_head_only = 0 };
+    enum { may_write = 1, chain_last = 0, chain_head_only = 0, pass_effects = 0 };
     P *prepare(P *p, uint32_t *anno, P **extra)
     {
         (void) anno, (void) extra;
@@ -192,7 +197,7 @@ template <class P, class O> struct IPGWOptionsClass : Plain<P, O> {
 // FixIPSrc (fixipsrc.cc:52-72): a packet with the annotation is made
 // writable, rewritten by the glue, and its annotation cleared (59).
 template <class P, class O> struct FixIPSrcClass : Plain<P, O> {
-    enum { may_write = 1, chain_last = 0, chain_head_only = 0 };
+    enum { may_write = 1, chain_last = 0, chain_head_only = 0, pass_effects = 1 };
     P *prepare(P *p, uint32_t *anno, P **extra)
     {
         (void) extra;
@@ -213,7 +218,7 @@ template <class P, class O> struct FixIPSrcClass : Plain<P, O> {
 
 // IPOutputCombo (ipoutputcombo.cc:44-205), ports 0-4.
 template <class P, class O> struct IPOutputComboClass : Plain<P, O> {
-    enum { may_write = 1, chain_last = 0, chain_head_only = 1 };
+    enum { may_write = 1, chain_last = 0, chain_head_only = 1, pass_effects = 1 };
     uint32_t color = 0;             // COLOR
     P *prepare(P *p, uint32_t *anno, P **extra)
     {
@@ -264,7 +269,7 @@ template <class P, class O> struct IPOutputComboClass : Plain<P, O> {
 
 // IPFragmenter (ipfragmenter.cc:88-171).
 template <class P, class O> struct IPFragmenterClass : Plain<P, O> {
-    enum { may_write = 1, chain_last = 1, chain_head_only = 0 };
+    enum { may_write = 1, chain_last = 1, chain_head_only = 0, pass_effects = 0 };
     uint32_t mtu = 0, headroom = 0; // MTU / HEADROOM
     P *prepare(P *p, uint32_t *anno, P **extra)
     {

@@ -100,6 +100,41 @@ template <class P> struct Held {
     uint32_t anno;  // the CLK_ANNO_* bits it was staged with
 };
 
+// The packets a state holds, by token: a ring over a power-of-two vector
+// (held[k] is token base + k), grown by doubling.
+template <class T> class HeldRing {
+  public:
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    T &operator[](size_t k) { return v_[(h_ + k) & (v_.size() - 1)]; }
+    T &front() { return v_[h_]; }
+    void push_back(const T &x)
+    {
+        if (n_ == v_.size())
+            grow();
+        v_[(h_ + n_++) & (v_.size() - 1)] = x;
+    }
+    void pop_back() { n_--; }
+    void pop_front()
+    {
+        h_ = (h_ + 1) & (v_.size() - 1);
+        n_--;
+    }
+    void clear() { h_ = n_ = 0; }
+
+  private:
+    void grow()
+    {
+        std::vector<T> w(v_.empty() ? 1024 : v_.size() * 2);
+        for (size_t k = 0; k < n_; k++)
+            w[k] = (*this)[k];
+        v_.swap(w);
+        h_ = 0;
+    }
+    std::vector<T> v_;
+    size_t h_ = 0, n_ = 0;
+};
+
 // One result, handed to the host's finish() after the lock is released.
 template <class P> struct Routed {
     P *p;           // the held packet (its primary result), 0 otherwise
@@ -120,20 +155,24 @@ template <class P, class L> struct State {
     clk_chain *chain;             // set: e heads a chain -- mem[k] is member k's glue element
     std::vector<clk_element *> mem;   // on ctx (mem[0] == e; the others are the state's own)
     int id;                       // the thread (Click: the RouterThread id)
-    std::deque<Held<P> > held;    // held[k] has token base + k
+    HeldRing<Held<P> > held;      // held[k] has token base + k
     uint64_t base, next;
     bool counted;                 // holds a runcount reference
     unsigned fails;               // consecutive failed flushes
     bool draining;                // a delivery loop is running on this state
+    bool unrouted;                // the glue may hold results route() has not taken
+    bool routed_any;              // results taken since the last end-of-batch mark
     bool armed;                   // the latency deadline is set
     uint64_t deadline;            // now_ns() at which poll() flushes
     uint64_t push_errors;         // packets push() could not stage (chatter is rate-limited)
     std::vector<Routed<P> > outbox;
+    std::vector<Routed<P> > spare;    // delivery storage kept between batches
     std::deque<P *> ready;        // pull context: output-0 packets ready to hand out
     P *last_primary;              // route(): the packet of the last primary result
     P *frag_parent;               // host use (IPFragmenter's first-fragment parent)
     L lock;
-    State() : ctx(0), e(0), chain(0), id(0), base(0), next(0), counted(false), fails(0), draining(false), armed(false),
+    State() : ctx(0), e(0), chain(0), id(0), base(0), next(0), counted(false), fails(0), draining(false),
+              unrouted(false), routed_any(false), armed(false),
               deadline(0), push_errors(0), last_primary(0), frag_parent(0) { }
 };
 
@@ -154,8 +193,11 @@ template <class P, class Host, class L> class Core {
     {
         t.lock.acquire();
         stage(h, t, p, true);
+        // most pushes only stage: deliver when there is something to
+        const bool deliver = (!t.outbox.empty() || t.unrouted) && !t.draining;
         t.lock.release();
-        drain(h, t, false);
+        if (deliver)
+            drain(h, t, false);
     }
 
     // run state t's partial batch now and route everything (the deadline
@@ -349,7 +391,7 @@ template <class P, class Host, class L> class Core {
                 // the next packet's memory region starts): the staged batch
                 // counts a failed flush, as a timer flush would
                 failed_flush(h, t);
-                route(h, t);
+                t.unrouted = true;
             } else if (t.push_errors++ == 0 || (t.push_errors & 0xFFFF) == 0) {
                 char buf[640];           // per-packet errors, once per 65536
                 snprintf(buf, sizeof(buf), "%llu packet(s) not staged: %s", (unsigned long long) t.push_errors,
@@ -404,8 +446,7 @@ template <class P, class Host, class L> class Core {
             failed_flush(h, t);
         else
             t.fails = 0;
-        route(h, t);
-        release_if_idle(h, t);
+        t.unrouted = true;               // drain() takes the results, a chunk at a time
         if (t.counted)                   // a new deadline for what is still held
             arm(h, t);
     }
@@ -426,7 +467,11 @@ template <class P, class Host, class L> class Core {
         return t.chain ? clk_chain_last_error(t.chain) : clk_element_last_error(t.e);
     }
 
-    // Move the glue's results into the outbox (locked).
+    // Move up to one chunk of the glue's results into the outbox (locked):
+    // drain() delivers them before it takes the next, so the results stay in
+    // cache between here and their delivery.  Once the glue has none left:
+    // the end of the batch, the elements' chatter, and the runcount released
+    // if nothing is held.
     void route(Host &h, S &t)
     {
         enum { CAP = 256 };
@@ -434,15 +479,13 @@ template <class P, class Host, class L> class Core {
         int32_t mem[CAP], port[CAP];
         uint32_t len[CAP], aux[CAP];
         uint64_t n;
-        bool any = false;
-        for (;;) {
+        {
             if (t.chain)
                 n = clk_chain_results(t.chain, tok, mem, port, len, aux, CAP);
             else if ((n = clk_element_results_aux(t.e, tok, port, len, aux, CAP)) > 0)
                 memset(mem, 0, sizeof(int32_t) * (size_t) n);
-            if (!n)
-                break;
-            any = true;
+            if (n)
+                t.routed_any = true;
             for (uint64_t i = 0; i < n; i++) {
                 R r;
                 memset(&r, 0, sizeof(r));
@@ -484,15 +527,18 @@ template <class P, class Host, class L> class Core {
                 t.held.pop_front();
                 t.base++;
             }
-            if (n < CAP)
-                break;
         }
-        if (any) {
+        if (n == CAP)
+            return;                      // more to come
+        t.unrouted = false;
+        if (t.routed_any) {
+            t.routed_any = false;
             R end;
             memset(&end, 0, sizeof(end));
             end.end = true;
             t.outbox.push_back(end);
         }
+        release_if_idle(h, t);
         // the elements' click_chatter lines (e.g. the first drop's reason)
         char buf[8192];
         const size_t nm = t.chain ? t.mem.size() : 1;
@@ -512,7 +558,6 @@ template <class P, class Host, class L> class Core {
     // append: the running loop delivers their results after these.
     void drain(Host &h, S &t, bool pull_ctx)
     {
-        std::vector<R> work;
         std::vector<P *> ready;                 // pull context: output-0 packets, queued under one lock
         t.lock.acquire();
         if (t.draining) {
@@ -520,7 +565,13 @@ template <class P, class Host, class L> class Core {
             return;
         }
         t.draining = true;
-        while (!t.outbox.empty()) {
+        std::vector<R> work;
+        work.swap(t.spare);                     // a delivered outbox's storage, reused
+        for (;;) {
+            if (t.outbox.empty() && t.unrouted && t.e)
+                route(h, t);
+            if (t.outbox.empty())
+                break;
             work.swap(t.outbox);
             t.lock.release();
             for (size_t i = 0; i < work.size(); i++) {
@@ -542,9 +593,12 @@ template <class P, class Host, class L> class Core {
             }
             work.clear();
             t.lock.acquire();
+            if (t.outbox.empty())
+                t.outbox.swap(work);             // the next chunk goes into this storage
             t.ready.insert(t.ready.end(), ready.begin(), ready.end());
             ready.clear();
         }
+        t.spare.swap(work);
         t.draining = false;
         t.lock.release();
     }

@@ -225,12 +225,14 @@ int clk_chain_flush(clk_chain *c);
  * (results are only handed out once their bytes are back).  Returns the
  * packets killed.                                                          */
 uint64_t clk_chain_abandon(clk_chain *c);
-/* on != 0: every member also reports each packet it passes on to the next
- * member (port CLK_PORT_NEXT, length as the next member sees it), in its
- * place among the member's results -- so a host that applies each element's
+/* Bit k of `members` set: member k also reports each packet it passes on to
+ * the next member (port CLK_PORT_NEXT, length as the next member sees it),
+ * in its place among its results -- so a host that applies each element's
  * own side effects (the Click adapter: network header, trim, Strip,
- * annotations) can apply them member by member.                           */
-int clk_chain_report_passes(clk_chain *c, int on);
+ * annotations) can apply them member by member; ~0: every member.  A
+ * packet a pass rule lets through a member unchanged (the member decides it
+ * on the host and changes nothing) is not reported.                        */
+int clk_chain_report_passes(clk_chain *c, uint64_t members);
 uint64_t clk_chain_results(clk_chain *c, uint64_t *tokens, int32_t *members, int32_t *ports,
                            uint32_t *lengths, uint32_t *aux, uint64_t cap);
 /* Host seconds the chain has spent, by phase: staging (push), the first

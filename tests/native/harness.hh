@@ -39,6 +39,7 @@ struct TAnno {
 
 struct TPacket {
     std::shared_ptr<std::vector<uint8_t> > buf;
+    uint8_t *raw = nullptr;          // buf->data(), kept in the packet as Click's Packet keeps its buffer
     size_t off = 0, len = 0;
     long nh = -1;                    // absolute offset of the network header in buf
     TAnno a;
@@ -52,8 +53,9 @@ TPacket *make(const uint8_t *bytes, size_t len, long id, size_t headroom = 0)
 {
     TPacket *p = new TPacket;
     p->buf = std::make_shared<std::vector<uint8_t> >(headroom + len);
+    p->raw = p->buf->data();
     if (len && bytes)
-        std::memcpy(p->buf->data() + headroom, bytes, len);
+        std::memcpy(p->raw + headroom, bytes, len);
     p->off = headroom;
     p->len = len;
     p->a.id = id;
@@ -73,6 +75,7 @@ struct TOps {
                 return nullptr;
             }
             p->buf = std::make_shared<std::vector<uint8_t> >(*p->buf);
+            p->raw = p->buf->data();
         }
         return p;
     }
@@ -88,13 +91,13 @@ struct TOps {
         g_live--;
         delete p;
     }
-    static uint8_t *data(TPacket *p) { return p->buf->data() + p->off; }
+    static uint8_t *data(TPacket *p) { return p->raw + p->off; }
     static uint32_t length(TPacket *p) { return (uint32_t)p->len; }
     static bool has_network_header(TPacket *p) { return p->nh >= 0; }
-    static const uint8_t *network_header(TPacket *p) { return p->buf->data() + p->nh; }
+    static const uint8_t *network_header(TPacket *p) { return p->raw + p->nh; }
     static int32_t network_header_offset(TPacket *p) { return (int32_t)(p->nh - (long)p->off); }
     static int network_length(TPacket *p) { return (int)((long)(p->off + p->len) - p->nh); }
-    static void set_ip_header(TPacket *p, const uint8_t *ip, uint32_t) { p->nh = ip - p->buf->data(); }
+    static void set_ip_header(TPacket *p, const uint8_t *ip, uint32_t) { p->nh = ip - p->raw; }
     static void take(TPacket *p, uint32_t n) { p->len -= n; }
     static void pull(TPacket *p, uint32_t n) { p->off += n, p->len -= n; }
     static void set_dst_ip_anno(TPacket *p, uint32_t a) { p->a.dst = a; }
@@ -108,10 +111,19 @@ struct TOps {
     static TPacket *make(uint32_t headroom, uint32_t len) { return ::make(nullptr, len, -1, headroom); }
 };
 
+// A test-and-set spinlock, as Click's Spinlock (the state lock), and the
+// same as a BasicLockable for the outputs the test records.
 struct TLock {
-    std::mutex m;
-    void acquire() { m.lock(); }
-    void release() { m.unlock(); }
+    std::atomic<bool> f{false};
+    void acquire()
+    {
+        while (f.exchange(true, std::memory_order_acquire))
+            while (f.load(std::memory_order_relaxed))
+                std::this_thread::yield();
+    }
+    void release() { f.store(false, std::memory_order_release); }
+    void lock() { acquire(); }
+    void unlock() { release(); }
 };
 
 typedef hipcore::State<TPacket, TLock> St;
@@ -126,7 +138,7 @@ class Host {
     C cls;
     Core core;
     std::vector<St> st;
-    std::mutex out_mu;
+    TLock out_mu;
     std::vector<std::vector<TPacket *> > out;          // per output port, in push order
     std::vector<std::vector<std::thread::id> > out_thread;
     std::atomic<int> runcount{0};
@@ -178,7 +190,7 @@ class Host {
             return;
         }
         {
-            std::lock_guard<std::mutex> g(out_mu);
+            std::lock_guard<TLock> g(out_mu);
             out[(size_t)port].push_back(p);
             out_thread[(size_t)port].push_back(std::this_thread::get_id());
         }
@@ -205,12 +217,12 @@ class Host {
     void wake(St &) { wakes++; }
     void chatter(const char *s)
     {
-        std::lock_guard<std::mutex> g(out_mu);
+        std::lock_guard<TLock> g(out_mu);
         chat.push_back(s);
     }
     void message(int, const char *s)
     {
-        std::lock_guard<std::mutex> g(out_mu);
+        std::lock_guard<TLock> g(out_mu);
         msgs.push_back(s);
     }
 
@@ -254,6 +266,7 @@ struct MemberBase {
     virtual int finish(St &t, hipcore::Routed<TPacket> &r, TPacket **o) = 0;
     virtual void end_of_batch(St &t) = 0;
     virtual bool may_write() const = 0;
+    virtual bool pass_effects() const = 0;
 };
 
 template <class C> struct Member : MemberBase {
@@ -266,6 +279,7 @@ template <class C> struct Member : MemberBase {
     int finish(St &t, hipcore::Routed<TPacket> &r, TPacket **o) override { return cls.finish(t, r, o); }
     void end_of_batch(St &t) override { cls.end_of_batch(t); }
     bool may_write() const override { return C::may_write != 0; }
+    bool pass_effects() const override { return C::pass_effects != 0; }
 };
 
 class ChainHost {
@@ -297,7 +311,11 @@ class ChainHost {
             std::fprintf(stderr, "chain: %s\n", clk_last_error(0));
             std::exit(3);
         }
-        clk_chain_report_passes(st.chain, 1);
+        uint64_t report = 0;                            // the members whose passes change the packet
+        for (size_t k = 0; k < m.size(); k++)
+            if (m[k]->pass_effects())
+                report |= uint64_t(1) << k;
+        clk_chain_report_passes(st.chain, report);
         char buf[64];
         clk_element_read_handler(st.e, "batch", buf, sizeof buf);
         core.set_batch((uint32_t)std::strtoul(buf, nullptr, 10));

@@ -746,6 +746,7 @@ void reentrant_push()
         if (p->a.id < 40) {
             TPacket *q = TOps::clone(p);
             q->buf = std::make_shared<std::vector<uint8_t> >(*p->buf);
+            q->raw = q->buf->data();
             q->a.id = p->a.id + 100000;
             hh.push(q);
         }

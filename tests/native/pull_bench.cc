@@ -121,9 +121,9 @@ std::vector<uint8_t> c1_frame()
     return f;
 }
 
-void push_c1(int n, bool chained)
+void push_c1(int n, bool chained, uint32_t batch)
 {
-    const std::string B = "BATCH 65536";
+    const std::string B = "BATCH " + std::to_string(batch);
     const std::vector<uint8_t> f = c1_frame();
     std::vector<TPacket *> in((size_t)n);
     auto fill = [&]() {
@@ -190,9 +190,9 @@ void push_c1(int n, bool chained)
         }
     }
     std::printf("{\"leg\": \"push_c1_%s\", \"graph\": \"CheckIPHeader(14) -> IPGWOptions -> FixIPSrc -> DecIPTTL -> "
-                "IPFragmenter(1500), %s\", \"bytes\": %zu, \"packets\": %d, \"forwarded\": %zu, \"seconds\": %.4f, "
-                "\"mpps\": %.2f}\n",
-                chained ? "chain" : "elements", chained ? "one chain" : "five elements", f.size(), n, out0, sec,
+                "IPFragmenter(1500), %s\", \"batch\": %u, \"bytes\": %zu, \"packets\": %d, \"forwarded\": %zu, "
+                "\"seconds\": %.4f, \"mpps\": %.2f}\n",
+                chained ? "chain" : "elements", chained ? "one chain" : "five elements", batch, f.size(), n, out0, sec,
                 (double)n / sec / 1e6);
     std::fflush(stdout);
 }
@@ -208,8 +208,10 @@ int main(int argc, char **argv)
     const int scale = argc > 1 ? std::max(1, std::atoi(argv[1])) : 1;
     // BATCH bounds the longest pull (one refill stages a batch and routes
     // the one before): the default and a small one
-    push_c1(600000 / scale, false);
-    push_c1(600000 / scale, true);
+    for (uint32_t batch : {65536u, 8192u}) {
+        push_c1(600000 / scale, false, batch);
+        push_c1(600000 / scale, true, batch);
+    }
     for (uint32_t batch : {65536u, 4096u}) {
         leg<CheckIPC, SetC>("pull_c2", "CheckIPHeader", "SetIPChecksum", 64, 2000000 / scale, batch);
         leg<PlainC, SetC>("pull_c3", "CheckUDPHeader", "SetUDPChecksum", 1500, 1000000 / scale, batch);
