@@ -152,7 +152,11 @@ int Chain::begin_batch()
         setup(k);
         mm_[k].w.reset();
         mm_[k].rebuild = false;
-        m_[k]->in_place_ = true;                      // the chain writes the packets back itself
+        // the chain copies the members' rewritten bytes back, except a staged
+        // member whose verdict carries its whole rewrite (DecIPTTL, the Set
+        // elements: the new checksum): its route() writes those few bytes
+        // into the packet itself, and nothing of it is copied back
+        m_[k]->in_place_ = !host_writes(m_[k]);
     }
     h2d_done_ = false;
     sent_ = 0;
@@ -345,6 +349,12 @@ int Chain::grow_members(size_t c, int keep)
     return 0;
 }
 
+// A staged member whose route() applies its rewrite from the verdict alone
+bool Chain::host_writes(const BatchElement *e)
+{
+    return !e->zerocopy_ && e->wants_sums() && !e->wants_arena_back();
+}
+
 // Member k's work state: where its arrays are, what it is.
 void Chain::setup(size_t k)
 {
@@ -358,7 +368,7 @@ void Chain::setup(size_t k)
     w.back = e->zerocopy_ ? nullptr : back_.data();
     w.staged = staged_.data();
     w.views0 = views0_.data();
-    w.wext = e->chain_write_past_nh();
+    w.wext = host_writes(e) ? 0u : e->chain_write_past_nh();
     e->chain_pass(&w.pass, &w.pass_param);
     w.h_off = M.h_off, w.h_len = M.h_len, w.h_anno = M.h_anno;
     w.h_codes = M.h_codes;

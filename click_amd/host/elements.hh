@@ -890,6 +890,7 @@ class Chain {
     };
     int begin_batch();
     int grow_batch();
+    static bool host_writes(const BatchElement *e);
     int device_arena(size_t bytes);
     void send_chunk();
     static constexpr size_t H2D_CHUNK = size_t(1) << 20;

@@ -246,17 +246,15 @@ def test_check_then_set_chain(ctx):
     compare_chain(ctx, spec, a3, o3, c3, nh0=0)
 
 
-@pytest.mark.parametrize("nth", [1, 2, 4, 6, 8, 11])
+@pytest.mark.parametrize("nth", [1, 2, 4, 6, 8])
 def test_chain_failed_flush(ctx, nth):
     """The nth checked HIP call of a chain flush fails (fake-iprouter chain:
     1 the batch's H2D, 2 CheckIPHeader's descriptors, 4 its verdicts back,
-    6 DecIPTTL's descriptors, 8 its verdicts back, 11 the rewritten bytes
-    back).  Before any kernel of a member that is not idempotent ran (1-6):
-    nothing is routed, nothing written, push() refuses packets, and the next
-    flush resumes and routes every packet exactly as a chain that never
-    failed.  After DecIPTTL's kernel (8): its packets are killed, never
-    decremented twice.  The copy back (11): no result is handed out before
-    its bytes are back; the next flush copies them and hands them all out."""
+    6 DecIPTTL's descriptors, 8 its verdicts back).  Before any kernel of a
+    member that is not idempotent ran (1-6): nothing is routed, nothing
+    written, push() refuses packets, and the next flush resumes and routes
+    every packet exactly as a chain that never failed.  After DecIPTTL's
+    kernel (8): its packets are killed, never decremented twice."""
     from click_amd import ClickAmdError
     from click_amd.elements import Chain
     arena, foff, flen = fake_frames(3000)
@@ -380,6 +378,45 @@ def test_chain_abandon(ctx):
     ch.flush()
     tok, mem, port, _, _ = ch.results()
     assert len(tok) == 2000 and (mem == 4).all() and (port == 0).all()
+    ch.close()
+    for e in els:
+        e.close()
+
+
+def test_chain_copy_back_failure(ctx):
+    """The rewritten bytes' copy back fails (every frame carries FIX_IP_SRC,
+    so FixIPSrc rewrites each on the GPU: calls 1 H2D, 2-5 CheckIPHeader,
+    6-10 FixIPSrc, 11-15 DecIPTTL, 16 the bytes back).  No result is handed
+    out before its bytes are back; push() refuses packets; the next flush
+    copies them and hands every packet out, bytes as a chain that never
+    failed."""
+    from click_amd import ClickAmdError
+    from click_amd.elements import Chain
+    arena, foff, flen = fake_frames(3000)
+    before = arena.copy()
+    els = make(ctx, FAKE_IPROUTER)
+    ch = Chain(els)
+    base = arena.ctypes.data
+    for i in range(len(foff)):
+        ch.push_anno(base + int(foff[i]), int(flen[i]), -1, 1, i)
+    hook = ctx.lib.clk_glue_inject_fault_internal
+    hook.argtypes, hook.restype = [ctypes.c_int], None
+    hook(16)
+    try:
+        with pytest.raises(ClickAmdError):
+            ch.flush()
+    finally:
+        hook(0)
+    tok, mem, port, _, _ = ch.results()
+    assert len(tok) == 0
+    with pytest.raises(ClickAmdError):
+        ch.push_anno(base, int(flen[0]), -1, 1, 99999)
+    ch.flush()
+    tok, mem, port, _, _ = ch.results()
+    assert len(tok) == 3000 and (mem == 4).all() and (port == 0).all()
+    ref = before.copy()
+    run_chain(ctx, FAKE_IPROUTER, ref, foff, flen, -1, np.ones(len(foff), np.uint32))
+    assert np.array_equal(arena, ref) and not np.array_equal(arena, before)
     ch.close()
     for e in els:
         e.close()
