@@ -59,7 +59,7 @@ Chain::~Chain()
     if (init_)
         (void)clk_ctx_sync(m_[0]->ctx_);
     for (BatchElement *e : m_)
-        e->in_place_ = false;
+        e->in_place_ = false, e->chain_ = false;
     for (void *q : {(void *)h_arena_, (void *)h_back_})
         if (q)
             (void)hipHostFree(q);
@@ -157,6 +157,7 @@ int Chain::begin_batch()
         // elements: the new checksum): its route() writes those few bytes
         // into the packet itself, and nothing of it is copied back
         m_[k]->in_place_ = !host_writes(m_[k]);
+        m_[k]->chain_ = true;
     }
     h2d_done_ = false;
     sent_ = 0;
@@ -352,7 +353,7 @@ int Chain::grow_members(size_t c, int keep)
 // A staged member whose route() applies its rewrite from the verdict alone
 bool Chain::host_writes(const BatchElement *e)
 {
-    return !e->zerocopy_ && e->wants_sums() && !e->wants_arena_back();
+    return !e->zerocopy_ && e->chain_host_rewrite() != CHAIN_HOST_NONE;
 }
 
 // Member k's work state: where its arrays are, what it is.
@@ -368,7 +369,9 @@ void Chain::setup(size_t k)
     w.back = e->zerocopy_ ? nullptr : back_.data();
     w.staged = staged_.data();
     w.views0 = views0_.data();
-    w.wext = host_writes(e) ? 0u : e->chain_write_past_nh();
+    const uint8_t hr = e->zerocopy_ ? (uint8_t)CHAIN_HOST_NONE : e->chain_host_rewrite();
+    w.wext = hr == CHAIN_HOST_ALL ? 0u : e->chain_write_past_nh();
+    w.wext_unless_simple = hr == CHAIN_HOST_SIMPLE;
     e->chain_pass(&w.pass, &w.pass_param);
     w.h_off = M.h_off, w.h_len = M.h_len, w.h_anno = M.h_anno;
     w.h_codes = M.h_codes;
@@ -618,7 +621,7 @@ void Chain::end_batch()
     used_ = 0;
     zc_host_ = nullptr;
     for (BatchElement *e : m_)
-        e->in_place_ = false;
+        e->in_place_ = false, e->chain_ = false;
 }
 
 // A GPU that keeps failing: every packet still in the chain -- staged, or

@@ -678,7 +678,7 @@ uint64_t BatchElement::pop_results(uint64_t *tokens, int32_t *ports, uint32_t *l
 
 void BatchElement::write_back(const Pending &p, uint32_t nbytes) const
 {
-    if (in_place_)                       // zero-copy: the kernel wrote the packet itself
+    if (in_place_ || chain_)             // zero-copy: the kernel wrote the packet itself; a chain copies back
         return;
     std::memcpy(p.data + p.span_off, (wants_arena_back() ? rt_->h_back : rt_->h_arena) + p.slot,
                 std::min(std::min(nbytes, p.span_len), stage_cap_));   // the staged bytes only
@@ -1463,11 +1463,11 @@ bool IPOutputCombo::span(const Pending &p, uint32_t *off, uint32_t *len, int32_t
     return true;
 }
 
-int IPOutputCombo::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
+int IPOutputCombo::run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums)
 {
     // the staged span is the header only: the MTU test is the host's (194)
     clk_ip_out_cfg cfg{my_ip_, ts_now(), nullptr, 0, 0xFFFFFFFFu};
-    return clk_ip_output_combo(ctx_, b, &cfg, d_anno_, d_codes, d_aux8_, nullptr);
+    return clk_ip_output_combo(ctx_, b, &cfg, d_anno_, d_codes, d_aux8_, zerocopy_ ? nullptr : d_sums);
 }
 
 bool IPOutputCombo::pre_route(Pending &p, Result *r)
@@ -1479,7 +1479,7 @@ bool IPOutputCombo::pre_route(Pending &p, Result *r)
     return true;
 }
 
-void IPOutputCombo::route(Pending &p, int code, uint16_t, Result *r)
+void IPOutputCombo::route(Pending &p, int code, uint16_t sum, Result *r)
 {
     if (code == 255) {
         r->port = -1;
@@ -1490,7 +1490,17 @@ void IPOutputCombo::route(Pending &p, int code, uint16_t, Result *r)
         r->port = out(p.length > mtu_ ? 4 : 0);
         return;
     }
-    write_back(p, p.span_len);
+    if (!in_place_ && simple_rewrite(p.data + p.span_off, p.span_len, p.anno)) {
+        // no option walk, no FixIPSrc: the kernel changed the TTL and the
+        // checksum only (DecIPTTL's step, 182-191), and the verdict carries
+        // the checksum
+        if (code == 0) {
+            uint8_t *iph = p.data + p.span_off;
+            iph[8]--;
+            std::memcpy(iph + 10, &sum, 2);
+        }
+    } else
+        write_back(p, p.span_len);
     p.anno &= (uint16_t)~CLK_ANNO_FIX_IP_SRC;               // 169-170 (staged packets only reach here)
     if (code == 2)
         r->aux = h_aux8_[p.index];

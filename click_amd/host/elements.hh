@@ -164,6 +164,12 @@ struct ChainExit {           // a result leaving the chain at `member`
 // A member's decision a chain can take without asking it: the packets its
 // span() decides on the host and its route() then passes on unchanged
 // (no write, no annotation, no result of its own but the count).
+// How a staged chain member's rewrite reaches the packet.
+enum ChainHostRewrite {
+    CHAIN_HOST_NONE = 0,     // copied back (write extent past nh)
+    CHAIN_HOST_ALL,          // route() writes it from the verdict (DecIPTTL, the Set elements)
+    CHAIN_HOST_SIMPLE,       // route() writes it for simple packets, the rest copied back (IPOutputCombo)
+};
 enum ChainPass {
     CHAIN_PASS_NONE = 0,
     CHAIN_PASS_NO_OPTIONS,   // IPGWOptions: no header, or ip_hl <= 5
@@ -193,6 +199,7 @@ struct ChainWork {
     const uint32_t *staged = nullptr;
     const ChainView *views0 = nullptr;
     uint32_t wext = 0;                        // the member's write extent past nh (~0u: all; 0: none)
+    bool wext_unless_simple = false;          // CHAIN_HOST_SIMPLE: only packets that are not simple
     int member = 0;
     uint32_t strip = 0;                       // the member's strip() / nh_after()
     int32_t nh_after = -2;
@@ -343,6 +350,13 @@ class BatchElement {
     virtual void chain_pass(uint8_t *kind, uint32_t *param) const { *kind = CHAIN_PASS_NONE, *param = 0; }
     // the bytes past the network header the kernel may write (~0u: any)
     virtual uint32_t chain_write_past_nh() const { return writes() ? 0xFFFFFFFFu : 0u; }
+    // in a staged chain, route() writes the member's rewrite into the packet
+    // from its verdict (ChainHostRewrite) instead of the chain copying it back
+    virtual uint8_t chain_host_rewrite() const
+    {
+        return wants_sums() && !wants_arena_back() ? CHAIN_HOST_ALL : CHAIN_HOST_NONE;
+    }
+    bool chain_ = false;             // a chain runs the element (it copies the rewritten bytes back)
     template <class SpanF, class RouteF>
     int chain_step_one(ChainWork &w, uint32_t i, SpanF &&span_f, RouteF &&route_f);
     template <class RouteF>
@@ -695,6 +709,17 @@ class IPOutputCombo : public BatchElement {
     uint32_t chain_write_past_nh() const override { return 64; }
     bool wants_arena_back() const override { return true; }
     bool wants_anno() const override { return true; }
+    bool wants_sums() const override { return !zerocopy_; }   // the checksum route() writes (staged)
+    uint8_t chain_host_rewrite() const override { return CHAIN_HOST_SIMPLE; }
+  public:
+    // a packet whose combo rewrite is the TTL and the checksum alone: no
+    // FIX_IP_SRC annotation, no options walked (ip_out_kernel's condition)
+    static bool simple_rewrite(const uint8_t *iph, uint32_t span_len, uint32_t anno)
+    {
+        const uint32_t hl = (uint32_t)(iph[0] & 0xF) << 2;
+        return !(anno & CLK_ANNO_FIX_IP_SRC) && !(hl > 20 && hl <= span_len);
+    }
+  protected:
 
   private:
     long color_ = 0;
@@ -776,7 +801,8 @@ inline int BatchElement::chain_step_one(ChainWork &w, uint32_t i, SpanF &&span_f
     w.maxlen = std::max(w.maxlen, len);
     w.span_off[q] = off;
     w.code[q] = (int32_t)w.n++;
-    if (w.wext && w.back) {                  // the bytes this member's kernel may rewrite, to copy back
+    if (w.wext && w.back &&                  // the bytes this member's kernel may rewrite, to copy back
+        !(w.wext_unless_simple && IPOutputCombo::simple_rewrite(v.data + off, len, v.anno))) {
         const uint64_t shift = v.slot - w.views0[i].slot;
         const uint64_t e = w.wext == 0xFFFFFFFFu ? (uint64_t)0xFFFFFFFFu
                                                  : shift + (v.nh > 0 ? (uint32_t)v.nh : 0u) + w.wext;

@@ -953,11 +953,12 @@ int main()
     pull_two_elements();
     fragmenter();
     // the n-th checked HIP call of the first flush fails: the packets H2D
-    // (4), a verdict D2H (SetUDPChecksum 9, IPOutputCombo 10), the packets
-    // back D2H (IPOutputCombo 11); -1: the completion wait
+    // (4), a verdict D2H (SetUDPChecksum 9, IPOutputCombo 10), IPOutputCombo's
+    // checksums D2H (11), the packets back D2H (IPOutputCombo 12); -1: the
+    // completion wait
     for (int nth : {4, 9, -1})
         failed_flush_retry<SetC>("SetUDPChecksum", "", nth);
-    for (int nth : {4, 10, 11, -1})
+    for (int nth : {4, 10, 11, 12, -1})
         failed_flush_retry<OutComboC>("IPOutputCombo", "1, 18.26.4.24, 1500", nth);
     retry_limit();
     reentrant_push();

@@ -119,9 +119,10 @@ def udp_600(n):
 
 
 # nth: the n-th checked HIP call of the flush fails (4: the packets' H2D,
-# before any kernel); -1: the completion wait, after the kernel ran and the
+# before any kernel; IPOutputCombo 11 its checksums back, 12 the rewritten
+# arena back); -1: the completion wait, after the kernel ran and the
 # rewritten arena was copied back
-@pytest.mark.parametrize("cls,conf,nth", [("IPOutputCombo", "1, 18.26.4.24, 1500", k) for k in (4, 11, -1)] +
+@pytest.mark.parametrize("cls,conf,nth", [("IPOutputCombo", "1, 18.26.4.24, 1500", k) for k in (4, 11, 12, -1)] +
                          [("IPFragmenter", "576", k) for k in (4, -1)] +
                          [("DecIPTTL", "", k) for k in (4, -1)])
 def test_rewriting_element_retry_is_exact(ctx, cls, conf, nth):
