@@ -926,7 +926,7 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
                                        "results": round((t0 + dt - tc) * 1e3, 2)},
                                 # host ns per packet by phase, both runs (warm-up + timed)
                                 "ns_per_packet": {k: round(v * 1e9 / (2 * n), 1) for k, v in zip(
-                                    ("stage", "first_pass", "gpu_round_trips", "unused", "h2d", "d2h_back",
+                                    ("push", "rebuild", "gpu_round_trips", "unused", "h2d", "d2h_back",
                                      "route", "copy_back"), list(st)) if k != "unused"}}
     same = all(np.array_equal(arenas["elements"], arenas[k]) for k in arenas)
     return {"workload": "C1: conf/fake-iprouter.click forwarding path, %d x %d B frames, element glue on the GPU "

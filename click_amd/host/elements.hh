@@ -889,9 +889,8 @@ class Chain {
     const std::string &last_error() const { return err_; }
     size_t pending() const { return views0_.size(); }
     void report_passes(uint64_t members) { report_passes_ = members; }
-    // host seconds spent so far: staging (push), descriptors (build), the
-    // members' GPU round trips, next-member views, H2D of the batch, D2H of
-    // the rewritten bytes, routing, copy-back
+    // host seconds spent so far, by phase (include/click_amd_elements.h,
+    // clk_chain_stats)
     int stats(double *sec, int n) const
     {
         for (int k = 0; k < n && k < 8; k++)

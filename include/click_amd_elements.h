@@ -235,12 +235,13 @@ uint64_t clk_chain_abandon(clk_chain *c);
 int clk_chain_report_passes(clk_chain *c, uint64_t members);
 uint64_t clk_chain_results(clk_chain *c, uint64_t *tokens, int32_t *members, int32_t *ports,
                            uint32_t *lengths, uint32_t *aux, uint64_t cap);
-/* Host seconds the chain has spent, by phase: staging (push), the first
- * pass (every packet into member 0, and through the members that decide it
- * on the host), the members' GPU round trips, (unused), H2D of the batch,
- * D2H of the rewritten bytes, routing after each GPU step (with the next
- * members' descriptors and host decisions), copy-back into the packets.
- * Returns 8.                                                               */
+/* Host seconds the chain has spent, by phase: push (staging, and the packet
+ * into member 0 and on through the members that decide it on the host),
+ * rebuilding the batch of a member a failed flush stopped at, the members'
+ * GPU round trips, (unused), the flush's H2D of the batch (pieces go while
+ * it fills), D2H of the rewritten bytes, routing after each GPU step (with
+ * the next members' descriptors and host decisions), copy-back into the
+ * packets.  Returns 8.                                                     */
 int clk_chain_stats(clk_chain *c, double *sec, int n);
 
 #ifdef __cplusplus
