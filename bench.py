@@ -928,6 +928,38 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
                                 "ns_per_packet": {k: round(v * 1e9 / (2 * n), 1) for k, v in zip(
                                     ("push", "rebuild", "gpu_round_trips", "unused", "h2d", "d2h_back",
                                      "route", "copy_back"), list(st)) if k != "unused"}}
+    # as the Click adapter forms fake-iprouter.click's graph (lines 91-106):
+    # CheckIPHeader alone (StaticIPLookup follows it), then gio -> FixIPSrc ->
+    # dt -> fr on one chain (each fed only by the one before, output 0)
+    spec = C1_CHAINS["elements"]
+    head = Element(ctx, spec[0][0], spec[0][1] + ", BATCH %d" % batch, noutputs=spec[0][2])
+    tail = [Element(ctx, cls, ", ".join(x for x in (conf, "BATCH %d" % batch) if x), noutputs=nout)
+            for cls, conf, nout in spec[1:]]
+    ch = Chain(tail)
+    for timed in (False, True):
+        raw = np.empty(n * len(frame) + 8192, np.uint8)
+        arena = raw[(-raw.ctypes.data) % 4096:][:n * len(frame)]
+        arena[:] = np.tile(np.frombuffer(frame, np.uint8), n)
+        ptrs = np.uint64(arena.ctypes.data) + np.arange(n, dtype=np.uint64) * np.uint64(len(frame))
+        lens = np.full(n, len(frame), np.uint32)
+        nhs = np.full(n, 14, np.int32)
+        t0 = time.perf_counter()
+        head.push_burst(ptrs, lens, nhs, first_token=0)
+        head.flush()
+        tok, port, ln = head.results(bufs=rbufs)
+        keep = port == 0
+        sel = tok[keep].astype(np.int64)
+        ch.push_burst(ptrs[sel], ln[keep].astype(np.uint32), nhs[sel], first_token=0)
+        ch.flush()
+        k = int(ch.lib.clk_chain_results(ch.h, *cptrs, n + 1))
+        dt = time.perf_counter() - t0
+        fwd = int(((cbufs[1][:k] == len(tail) - 1) & (cbufs[2][:k] == 0)).sum())
+    ch.close()
+    for e in [head] + tail:
+        e.close()
+    arenas["elements_as_click_forms"] = arena
+    out["elements_as_click_forms"] = {"chain": [spec[0][0], "[" + ", ".join(c[0] for c in spec[1:]) + "]"],
+                                      "forwarded": fwd, "wall_s": round(dt, 4), "mpps": round(n / dt / 1e6, 2)}
     same = all(np.array_equal(arenas["elements"], arenas[k]) for k in arenas)
     return {"workload": "C1: conf/fake-iprouter.click forwarding path, %d x %d B frames, element glue on the GPU "
                         "(staged: push() gathers into pinned staging; _zerocopy: registered host arena)"
