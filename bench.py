@@ -1090,6 +1090,8 @@ def main():
     ap.add_argument("--no-frag", action="store_true", help="skip the IPFragmenter measurement (C3)")
     ap.add_argument("--skip", default="", help="comma list of side configurations to skip: c4,c5")
     ap.add_argument("--e2e", action="store_true", help="measure the host-resident end-to-end rates instead")
+    ap.add_argument("--scatter-bytes", type=int, default=1 << 30,
+                    help="N > 1: bytes rank 0 sends each rank for the root-scatter measurement (0: skip)")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the host-oracle digest of each element's results (SURVEY §8(e)(1))")
     args = ap.parse_args()
@@ -1162,6 +1164,22 @@ def main():
     if rank == 0 and world == 1 and not args.no_c1:
         c1 = config1(ctx)
 
+    # an input that starts on one GPU would first be scattered;
+    # measured on a sample after the timed regions, never part of `value`
+    rsc = None
+    if dist is not None and world > 1 and args.scatter_bytes > 0:
+        from click_amd import shard
+        r_ = shard.root_scatter(torch, dist, coll_dev, args.scatter_bytes)
+        if r_:
+            t_, b_ = r_
+            w_ = WORKLOADS[args.workload]
+            per_rank = (pk or w_["n"]) * (w_["stride"] or 354)       # C4: the IMIX mean
+            rsc = {"sample_bytes_per_rank": args.scatter_bytes, "seconds": round(t_, 5),
+                   "GBps_out_of_rank0": round(b_ / t_ / 1e9, 1),
+                   "whole_shards_s": {args.workload: round(per_rank * (world - 1) * t_ / b_, 3),
+                                      "c5": round((16 << 20) * 9024 * (world - 1) * t_ / b_, 3)},
+                   "note": "rank 0 sends each other rank its piece (grouped send/recv over RCCL); "
+                           "an input that starts on one GPU, not the device-resident value"}
     comm = comm_info(torch, dist, dev)         # a collective: every rank joins
     if rank == 0:
         w = WORKLOADS[args.workload]
@@ -1184,6 +1202,8 @@ def main():
             "elements": {e: summarize(r, args.steps, args.workload) for e, r in main_res.items()},
             "comm": comm,
         }
+        if rsc:
+            line["root_scatter"] = rsc
         if c2:
             line["c2_64b"] = {"workload": WORKLOADS["c2"]["desc"],
                               "elements": {e: summarize(r, args.steps, "c2") for e, r in c2.items()}}

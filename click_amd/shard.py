@@ -180,3 +180,41 @@ def gather_results(torch, dist, device, values, root=0):
         for req in dist.batch_isend_irecv(ops):
             req.wait()
     return torch.cat(parts).view(values.dtype) if rank == root else None
+
+
+def root_scatter(torch, dist, device, sample_bytes, reps=3, root=0):
+    """an input that originates on one GPU (a single NIC) must
+    first reach the other ranks.  `root` sends `sample_bytes` to every other
+    rank in one grouped send/recv (RCCL point-to-point over xGMI: one piece
+    per link), timed between barriers, `reps` times after one untimed round;
+    returns (seconds of the slowest rank's median round, bytes root sent per
+    round), the same on every rank, or None without a process group of two
+    or more.  Kept out of the device-resident metric: the caller reports it
+    beside the time the whole shards would take at that rate."""
+    if dist is None or dist.get_world_size() < 2:
+        return None
+    import time
+    rank, world = dist.get_rank(), dist.get_world_size()
+    sync = (lambda: torch.cuda.synchronize()) if str(device).startswith("cuda") else (lambda: None)
+    if rank == root:
+        buf = torch.empty(sample_bytes * (world - 1), dtype=torch.uint8, device=device)
+        peers = [r for r in range(world) if r != root]
+        ops = [dist.P2POp(dist.isend, buf[k * sample_bytes:(k + 1) * sample_bytes], r) for k, r in enumerate(peers)]
+    else:
+        buf = torch.empty(sample_bytes, dtype=torch.uint8, device=device)
+        ops = [dist.P2POp(dist.irecv, buf, root)]
+    times = []
+    for it in range(reps + 1):
+        sync()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+        sync()
+        dt = time.perf_counter() - t0
+        if it:
+            times.append(dt)
+    times.sort()
+    t = torch.tensor([times[len(times) // 2]], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item()), sample_bytes * (world - 1)

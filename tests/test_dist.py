@@ -59,8 +59,9 @@ def worker(rank, world, port, q, n_imix):
     clo, chi = shard.balanced_cuts(torch, dist, "cpu", rank * n_imix, imix_block(rank * n_imix, n_imix))
     # unequal shard sizes gather too (the C4 shards)
     g2 = shard.gather_results(torch, dist, "cpu", torch.arange(clo, chi, dtype=torch.int64).to(torch.int16))
+    rs = shard.root_scatter(torch, dist, "cpu", 1 << 16, reps=2)
     q.put((rank, lo, hi, wall, kms, total, None if allsums is None else allsums.numpy(), extra, per_rank,
-           (clo, chi), None if g2 is None else g2.numpy()))
+           (clo, chi), None if g2 is None else g2.numpy(), rs))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -106,6 +107,9 @@ def test_sharded_digest_matches_single_process(world):
     sizes = [int(lens[a:b].sum()) for a, b in cuts]
     assert max(abs(s - lens.sum() / world) for s in sizes) <= 1500
     assert out[0][10] is not None and np.array_equal(out[0][10], np.arange(world * n_imix).astype(np.int16))
+    # root scatter: the same (max-over-ranks) time everywhere, root's bytes
+    rs = [o[11] for o in out]
+    assert all(r is not None and r == rs[0] for r in rs) and rs[0][1] == (1 << 16) * (world - 1) and rs[0][0] > 0
 
 
 def test_shard_by_bytes_balances_imix():

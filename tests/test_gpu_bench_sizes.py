@@ -126,7 +126,7 @@ def run_bench(gpus, packets, skip="c4,c5", extra_env=None):
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--packets", str(packets),
            "--steps", "2", "--warmup", "1", "--no-c2", "--no-c1", "--no-cpu", "--no-peak", "--no-frag",
-           "--skip", skip]
+           "--skip", skip, "--scatter-bytes", str(1 << 20)]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -151,6 +151,9 @@ def test_bench_two_ranks_match_one(torch):
     one = run_bench(1, 2 * n, skip="c5")
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1
     assert two["config"]["packets_per_gpu"] == n
+    # the root-scatter sample (an input starting on one GPU), N > 1 only
+    rs = two["root_scatter"]
+    assert rs["sample_bytes_per_rank"] == 1 << 20 and rs["seconds"] > 0 and "root_scatter" not in one
     for sect, elements in ((None, ("CheckUDPHeader", "SetUDPChecksum")),
                            ("c4_imix", ("CheckUDPHeader", "SetUDPChecksum"))):
         t_el = two["elements"] if sect is None else two[sect]["elements"]
