@@ -1055,6 +1055,12 @@ def bench_summary(line):
     if c1:
         out["C1 mpps"] = {k: c1[k]["mpps"] for k in c1 if isinstance(c1[k], dict) and "mpps" in c1[k]}
         out["C1 ok"] = c1.get("ok")
+    rs = line.get("root_scatter")
+    if rs:
+        out["root scatter GB/s"] = rs["GBps_out_of_rank0"]
+    comm = line.get("comm")
+    if comm:
+        out["ranks"] = [comm.get("backend"), comm.get("world_size")]
     return out
 
 
