@@ -586,7 +586,11 @@ void BatchElement::route_loop(Stage &g, RouteF &&route_f)
     size_t k = 0;
     const bool sums = wants_sums(), pre = has_pre_route_, post = has_post_route_;
     results_.reserve_more(g.pend.size());
-    for (Pending &p : g.pend) {
+    const size_t np = g.pend.size();
+    for (size_t q = 0; q < np; q++) {
+        Pending &p = g.pend[q];
+        if (q + 8 < np)                      // the packet route() may read, 8 ahead
+            __builtin_prefetch(g.pend[q + 8].data + g.pend[q + 8].span_off);
         int code;
         uint16_t sum = 0;
         if (p.host_code >= 0) {
