@@ -420,3 +420,15 @@ def test_chain_copy_back_failure(ctx):
     ch.close()
     for e in els:
         e.close()
+
+
+def test_ttl_then_set_chain(ctx):
+    """CheckIPHeader -> DecIPTTL -> SetIPChecksum: two members whose
+    verdicts carry their rewrites (the TTL and checksum written into the
+    packet by route(), nothing copied back for them), one after the other on
+    the same bytes -- equal to the elements one by one, byte for byte."""
+    rng, arena, foff, flen = fuzzed_frames(21)
+    spec = [("CheckIPHeader", "OFFSET 14", 2), ("DecIPTTL", "", 2), ("SetIPChecksum", "", 1)]
+    r = compare_chain(ctx, spec, arena, foff, flen)
+    seen = {(m, p) for _, m, p, _, _ in r}
+    assert {(0, 1), (1, 1), (2, 0)} <= seen, seen
