@@ -22,7 +22,7 @@ CLICK_DECLS
 
 HIPBatchElement::HIPBatchElement()
     : _device(-1), _latency_ms(1), _retries(3), _pt(0), _tasks(0), _npt(0), _gate(0), _chain_conf(true),
-      _chain_tried(0)
+      _chain_writes(false), _chain_tried(0)
 {
 }
 
@@ -140,6 +140,9 @@ HIPBatchElement::initialize(ErrorHandler *errh)
     if (_chain_conf && !chain_member())
 	for (HIPBatchElement *x = this, *y; !x->cls_chain_last() && (y = x->chain_next()); x = y)
 	    _chain.push_back(y);
+    _chain_writes = false;
+    for (int m = 1; m < _chain.size(); m++)
+	_chain_writes = _chain_writes || _chain[m]->cls_may_write();
     return 0;
 }
 
@@ -255,10 +258,7 @@ HIPBatchElement::prepare(Packet *p, uint32_t *anno, Packet **extra)
     if (_chain.size() > 1) {
 	// readied for every member: writable if any may write (where the
 	// reference makes it writable only in the element that writes it)
-	bool w = false;
-	for (int m = 1; m < _chain.size(); m++)
-	    w = w || _chain[m]->cls_may_write();
-	if (w && !(p = p->uniqueify()))
+	if (_chain_writes && !(p = p->uniqueify()))
 	    return 0;
 	*anno |= chain_anno(p);
     }

@@ -176,6 +176,7 @@ class HIPBatchElement : public Element { public:
     int _npt;
     clk_element *_gate;		// whose once-only chatter the thread elements share
     bool _chain_conf;		// CHAIN
+    bool _chain_writes;		// a member after this head may write packets
     Vector<HIPBatchElement *> _chain;	// [0] this; then the members this head runs
     bool *_chain_tried;		// per state: its chain was set up (or refused)
     Vector<clk_element *> _borrowed;	// this element's glue copies in chains of heads before it
