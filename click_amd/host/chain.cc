@@ -54,12 +54,40 @@ static int pinned_grow(T **p, size_t *cap, size_t need, size_t keep)
     return 0;
 }
 
+void Chain::attach()
+{
+    for (BatchElement *e : m_)
+        e->chains_.push_back(this);
+}
+
+// A member element is destroyed while the chain lives (the caller's order,
+// or a garbage collector's): the chain lets go of every member and refuses
+// all further work; its own destructor then touches no member.
+void Chain::member_gone(BatchElement *gone)
+{
+    if (!dead_ && init_)
+        (void)clk_ctx_sync(gone->ctx_);
+    for (BatchElement *e : m_) {
+        auto &v = e->chains_;
+        v.erase(std::remove(v.begin(), v.end(), this), v.end());
+        if (e != gone)
+            e->in_place_ = false, e->chain_ = false;
+    }
+    dead_ = true;
+    err_ = "a member element was destroyed";
+}
+
 Chain::~Chain()
 {
-    if (init_)
-        (void)clk_ctx_sync(m_[0]->ctx_);
-    for (BatchElement *e : m_)
-        e->in_place_ = false, e->chain_ = false;
+    if (!dead_) {
+        if (init_)
+            (void)clk_ctx_sync(m_[0]->ctx_);
+        for (BatchElement *e : m_) {
+            e->in_place_ = false, e->chain_ = false;
+            auto &v = e->chains_;
+            v.erase(std::remove(v.begin(), v.end(), this), v.end());
+        }
+    }
     for (void *q : {(void *)h_arena_, (void *)h_back_})
         if (q)
             (void)hipHostFree(q);
@@ -217,6 +245,8 @@ int Chain::grow_batch()
 
 int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
 {
+    if (dead_)
+        return CLK_EINVAL;
     if (failed_) {
         err_ = "the chain's failed flush must be retried (or the packets abandoned) first";
         return CLK_EINVAL;
@@ -344,6 +374,7 @@ int Chain::grow_members(size_t c, int keep)
             M.reached.resize(c);
             M.code.resize(c);
             M.span_off.resize(c);
+            M.span_len.resize(c);
         }
     }
     mcap_ = std::max(mcap_, c);
@@ -363,6 +394,7 @@ void Chain::setup(size_t k)
     Member &M = mm_[k];
     ChainWork &w = M.w;
     w.reached = M.reached.data(), w.code = M.code.data(), w.span_off = M.span_off.data();
+    w.span_len = M.span_len.data();
     w.views = &views_;
     w.done = &done_;
     w.out = &out_;
@@ -534,6 +566,8 @@ int Chain::copy_back(bool all)
 // next flush resumes at that member (push() refuses packets until then).
 int Chain::flush()
 {
+    if (dead_)
+        return views0_.empty() ? CLK_SUCCESS : CLK_EINVAL;
     if (views0_.empty())
         return CLK_SUCCESS;
     err_.clear();
@@ -632,7 +666,7 @@ void Chain::end_batch()
 uint64_t Chain::abandon()
 {
     uint64_t k = 0;
-    if (views0_.empty())
+    if (views0_.empty() || dead_)
         return 0;
     if (h2d_done_)
         (void)copy_back(false);                      // one more try for the bytes of the routed ones
@@ -718,6 +752,7 @@ int clk_chain_create(clk_element *const *members, int n, clk_chain **out)
         delete c;
         return CLK_EINVAL;
     }
+    c->attach();
     *out = w;
     return CLK_SUCCESS;
 }

@@ -192,6 +192,8 @@ void BatchElement::free_stage(Stage &g)
 
 BatchElement::~BatchElement()
 {
+    while (!chains_.empty())                 // a chain that outlives its member stops using it
+        chains_.back()->member_gone(this);
     for (Stage &g : st_) {
         if (g.inflight)
             (void)hipEventSynchronize((hipEvent_t)g.ev[2]);
@@ -1496,9 +1498,9 @@ void IPOutputCombo::route(Pending &p, int code, uint16_t sum, Result *r)
     }
     if (!in_place_ && simple_rewrite(p.data + p.span_off, p.span_len, p.anno)) {
         // no option walk, no FixIPSrc: the kernel changed the TTL and the
-        // checksum only (DecIPTTL's step, 182-191), and the verdict carries
-        // the checksum
-        if (code == 0) {
+        // checksum only (DecIPTTL's step, 182-191; a header shorter than 20 B
+        // it leaves alone), and the verdict carries the checksum
+        if (code == 0 && p.span_len >= 20) {
             uint8_t *iph = p.data + p.span_off;
             iph[8]--;
             std::memcpy(iph + 10, &sum, 2);

@@ -182,7 +182,8 @@ struct ChainWork {
     std::vector<uint8_t> *done;               // per chain packet: has left the chain
     uint32_t *reached = nullptr;              // the packets that reached this member, in push order
     int32_t *code = nullptr;                  // per reached packet: GPU index, or -1 - host code
-    uint32_t *span_off = nullptr;
+    uint32_t *span_off = nullptr;             // per reached packet with a descriptor: its span
+    uint32_t *span_len = nullptr;
     size_t nreached = 0;
     size_t routed = 0;                        // reached packets routed so far
     uint64_t *h_off = nullptr;                // the member's batch (pinned)
@@ -357,6 +358,7 @@ class BatchElement {
         return wants_sums() && !wants_arena_back() ? CHAIN_HOST_ALL : CHAIN_HOST_NONE;
     }
     bool chain_ = false;             // a chain runs the element (it copies the rewritten bytes back)
+    std::vector<Chain *> chains_;    // the chains the element is a member of (detached when it goes)
     template <class SpanF, class RouteF>
     int chain_step_one(ChainWork &w, uint32_t i, SpanF &&span_f, RouteF &&route_f);
     template <class RouteF>
@@ -789,6 +791,7 @@ inline int BatchElement::chain_step_one(ChainWork &w, uint32_t i, SpanF &&span_f
     if (!span_f(p, &off, &len, &hc)) {
         w.code[q] = -1 - hc;
         w.span_off[q] = 0;
+        w.span_len[q] = 0;
         if (!w.inline_ok || w.routed != q)
             return 0;
         w.routed = q + 1;
@@ -800,6 +803,7 @@ inline int BatchElement::chain_step_one(ChainWork &w, uint32_t i, SpanF &&span_f
     w.h_anno[w.n] = (uint8_t)v.anno;
     w.maxlen = std::max(w.maxlen, len);
     w.span_off[q] = off;
+    w.span_len[q] = len;
     w.code[q] = (int32_t)w.n++;
     if (w.wext && w.back &&                  // the bytes this member's kernel may rewrite, to copy back
         !(w.wext_unless_simple && IPOutputCombo::simple_rewrite(v.data + off, len, v.anno))) {
@@ -856,7 +860,7 @@ inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_
     const int32_t c = w.code[q];
     const int code = c >= 0 ? w.h_codes[c] : -1 - c;
     const ChainView &v = (*w.views)[i];
-    Pending p{v.data, v.token, v.slot, v.length, v.nh, w.span_off[q], 0, c >= 0 ? (uint32_t)c : 0u,
+    Pending p{v.data, v.token, v.slot, v.length, v.nh, w.span_off[q], w.span_len[q], c >= 0 ? (uint32_t)c : 0u,
               (int16_t)(c >= 0 ? -1 : code), v.anno};
     return chain_route_pending(w, i, p, code, c >= 0 && w.h_sums ? w.h_sums[c] : 0, route_f);
 }
@@ -877,6 +881,8 @@ class Chain {
   public:
     explicit Chain(const std::vector<BatchElement *> &members) : m_(members) {}
     ~Chain();
+    void attach();                            // registered with its members
+    void member_gone(BatchElement *e);        // a member is being destroyed: the chain is dead
     int check(std::string *err) const;
     int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno);
     int push_burst(uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets, uint64_t first_token,
@@ -909,7 +915,7 @@ class Chain {
         void *ev[2] = {nullptr, nullptr};
         float ms = 0;
         bool rebuild = false;                 // resumed: rebuild the batch of the packets not routed
-        std::vector<uint32_t> reached, span_off;
+        std::vector<uint32_t> reached, span_off, span_len;
         std::vector<int32_t> code;
         ChainWork w;
     };
@@ -931,6 +937,7 @@ class Chain {
     std::vector<uint32_t> staged_, back_;     // bytes staged / written back per packet
     std::vector<uint8_t> done_, copied_;      // per packet: left the chain; bytes copied back
     bool failed_ = false;                     // a flush failed: the batch must be flushed (or abandoned)
+    bool dead_ = false;                       // a member was destroyed first: nothing runs any more
     bool h2d_done_ = false;                   // the staged batch is on the device
     size_t sent_ = 0;                         // staged bytes already copied to the device this batch
     bool sent_ok_ = true;

@@ -432,3 +432,29 @@ def test_ttl_then_set_chain(ctx):
     r = compare_chain(ctx, spec, arena, foff, flen)
     seen = {(m, p) for _, m, p, _, _ in r}
     assert {(0, 1), (1, 1), (2, 0)} <= seen, seen
+
+
+def test_member_destroyed_before_chain(ctx):
+    """A member element destroyed while its chain lives (a caller's order, or
+    a garbage collector's): the chain lets go of every member, refuses
+    further work, and is then destroyed without touching them."""
+    from click_amd import ClickAmdError
+    from click_amd.elements import Chain
+    arena, foff, flen = fake_frames(100)
+    els = make(ctx, FAKE_IPROUTER)
+    ch = Chain(els)
+    base = arena.ctypes.data
+    for i in range(len(foff)):
+        ch.push_anno(base + int(foff[i]), int(flen[i]), -1, 0, i)
+    els[2].close()
+    with pytest.raises(ClickAmdError):
+        ch.push_anno(base, int(flen[0]), -1, 0, 999)
+    assert "destroyed" in ch.last_error()
+    ch.close()
+    for e in els:
+        e.close()
+    ch2 = Chain(make(ctx, FAKE_IPROUTER))       # the context and the library are fine
+    ch2.push_anno(base, int(flen[0]), -1, 0, 0)
+    ch2.flush()
+    assert len(ch2.results()[0]) == 1
+    ch2.close()
