@@ -27,6 +27,9 @@ struct clk_ctx {
     int scatter_blocks;  // grid cap of field_scatter_kernel: fewer, longer-lived waves
                          // (C3 scatter 0.57 vs 0.67 ms at 16K vs 64K blocks)
     uint64_t stream_min; // len[] batches of >= stream_min packets run by the packet-stream kernel
+    int set_chunks;      // two-phase Set: packet ranges whose scatter overlaps the next range's compute
+    hipStream_t side;    // the scatters' stream (created on first use)
+    hipEvent_t ev_pass, ev_side;
     void *scratch;       // two-phase work array (grown on demand)
     size_t scratch_bytes;
     uint32_t *dev_flags;   // device word kernels report internal faults in (fragmenter look-back timeout)
@@ -93,6 +96,18 @@ int ensure_scratch(clk_ctx *ctx, size_t bytes)
     return CLK_SUCCESS;
 }
 
+// The side stream and events of the chunked two-phase Set (first use).
+int ensure_side(clk_ctx *ctx)
+{
+    hipError_t e = hipSuccess;
+    if (!ctx->side && (e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking)) != hipSuccess)
+        return hip_fail(ctx, e, "hipStreamCreateWithFlags(side)");
+    for (hipEvent_t *ev : {&ctx->ev_pass, &ctx->ev_side})
+        if (!*ev && (e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(ctx, e, "hipEventCreateWithFlags");
+    return CLK_SUCCESS;
+}
+
 int check_batch(clk_ctx *ctx, const clk_batch *b, const char *fn)
 {
     if (!b)
@@ -113,6 +128,20 @@ clk::BatchArgs args_of(const clk_batch *b)
     a.len = b->len;
     a.fixed_len = b->fixed_len;
     a.n = b->n;
+    return a;
+}
+
+// packets [i0, i0 + m) of a batch
+clk::BatchArgs sub_args(const clk_batch *b, uint64_t i0, uint64_t m)
+{
+    clk::BatchArgs a = args_of(b);
+    if (a.off)
+        a.off += i0;
+    else
+        a.base += i0 * a.stride;
+    if (a.len)
+        a.len += i0;
+    a.n = m;
     return a;
 }
 
@@ -253,12 +282,38 @@ int launch_l4(clk_ctx *ctx, const clk_batch *b, int fixoff, uint8_t *code, uint1
                                ctx->cur, args_of(b), fixoff, code, sum, work);
     } else {
         const int g = pick_group(ctx, b);
-        uint64_t threads = b->n * (uint64_t)g;
-        if (CLK_L4_RUNS && (!SET || g >= CLK_L4_RUNS_SET_G)) {   // a workgroup per run
-            const uint64_t run = 256 / g < 64 ? 64 : 256 / g;        // as l4_kernel's RB
-            threads = (b->n + run - 1) / run * BLOCK;
+        auto compute = [&](const clk::BatchArgs &a, uint8_t *c_, uint16_t *s_, uint32_t *w_) {
+            uint64_t threads = a.n * (uint64_t)g;
+            if (CLK_L4_RUNS && (!SET || g >= CLK_L4_RUNS_SET_G)) {   // a workgroup per run
+                const uint64_t run = 256 / g < 64 ? 64 : 256 / g;    // as l4_kernel's RB
+                threads = (a.n + run - 1) / run * BLOCK;
+            }
+            launch_l4_dispatch<PROTO, SET>(ctx, a, grid_for(ctx, threads), fixoff, c_, s_, w_, g);
+        };
+        const uint64_t per = work && ctx->set_chunks > 1
+                                 ? (((b->n + ctx->set_chunks - 1) / ctx->set_chunks + 255) & ~uint64_t(255))
+                                 : b->n;
+        if (per < b->n) {
+            // the two-phase Set in packet ranges: each range's scatter (2 B
+            // writes, read-modify-write bound) runs on the side stream while
+            // the next range's compute pass (read bound) runs on this one
+            if ((r = ensure_side(ctx))) return r;
+            constexpr int FIELD = PROTO == clk::UDP ? 6 : 16;
+            for (uint64_t i0 = 0; i0 < b->n; i0 += per) {
+                const clk::BatchArgs a = sub_args(b, i0, std::min(per, b->n - i0));
+                compute(a, code + i0, sum ? sum + i0 : nullptr, work + i0);
+                (void)hipEventRecord(ctx->ev_pass, ctx->cur);
+                (void)hipStreamWaitEvent(ctx->side, ctx->ev_pass, 0);
+                hipLaunchKernelGGL((clk::field_scatter_kernel<FIELD>),
+                                   dim3(std::min<unsigned>(grid_for(ctx, a.n), (unsigned)ctx->scatter_blocks)),
+                                   dim3(BLOCK), 0, ctx->side, a, (const uint32_t *)(work + i0), code + i0,
+                                   sum ? sum + i0 : nullptr);
+            }
+            (void)hipEventRecord(ctx->ev_side, ctx->side);
+            (void)hipStreamWaitEvent(ctx->cur, ctx->ev_side, 0);
+            return check_launch(ctx, fn);
         }
-        launch_l4_dispatch<PROTO, SET>(ctx, args_of(b), grid_for(ctx, threads), fixoff, code, sum, work, g);
+        compute(args_of(b), code, sum, work);
     }
     if (work) {
         constexpr int FIELD = PROTO == clk::UDP ? 6 : 16;
@@ -322,6 +377,9 @@ int clk_ctx_create(int device, clk_ctx **out)
     c->scratch = nullptr;
     c->scratch_bytes = 0;
     c->set_mode = -1;
+    c->set_chunks = 1;
+    c->side = nullptr;
+    c->ev_pass = c->ev_side = nullptr;
     c->scatter_blocks = 16384;
     c->stream_min = 65536;
     c->force_group = 0;
@@ -349,6 +407,13 @@ int clk_ctx_destroy(clk_ctx *ctx)
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->cur);
     (void)hipStreamDestroy(ctx->own);
+    if (ctx->side) {
+        (void)hipStreamSynchronize(ctx->side);
+        (void)hipStreamDestroy(ctx->side);
+    }
+    for (hipEvent_t e : {ctx->ev_pass, ctx->ev_side})
+        if (e)
+            (void)hipEventDestroy(e);
     if (ctx->scratch)
         (void)hipFree(ctx->scratch);
     if (ctx->dev_flags)
@@ -396,6 +461,10 @@ int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value)
     case CLK_TUNE_STREAM_MIN:
         if (value < 1) break;
         ctx->stream_min = (uint64_t)value;
+        return CLK_SUCCESS;
+    case CLK_TUNE_SET_CHUNKS:
+        if (value < 1 || value > 64) break;
+        ctx->set_chunks = (int)value;
         return CLK_SUCCESS;
     case CLK_TUNE_GROUP:
         if (!(value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16 || value == 32 ||

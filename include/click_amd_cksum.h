@@ -108,8 +108,11 @@ enum clk_tune_knob {
     CLK_TUNE_SET_MODE = 3,            /* -1 auto, 0 fused Set, 1 two-phase Set           */
     CLK_TUNE_STREAM_MIN = 4,          /* len[] batches of >= this many packets run by the
                                          packet-stream kernel (65536)                     */
-    CLK_TUNE_GROUP = 5                /* lanes per packet of the fixed-geometry kernels:
+    CLK_TUNE_GROUP = 5,               /* lanes per packet of the fixed-geometry kernels:
                                          0 (by max_len), 1, 2, 4, ..., 64                 */
+    CLK_TUNE_SET_CHUNKS = 6           /* two-phase Set in this many packet ranges, each
+                                         range's scatter on a side stream overlapping the
+                                         next range's compute pass (1: one of each)       */
 };
 int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value);
 /* Last error text for `ctx` (or for the calling thread when ctx == NULL). */

@@ -339,6 +339,26 @@ def test_dec_ttl_full_size(torch, ctx):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("chunks", [2, 5, 64])
+def test_chunked_two_phase_set_bit_exact(torch, chunks):
+    """The two-phase Set in packet ranges (set_chunks: each range's scatter
+    on a side stream, overlapping the next range's compute pass) equals the
+    oracle on fuzzed off/len batches, on fixed-stride batches, and on
+    batches smaller than one range."""
+    import click_amd
+    c = click_amd.Context(0).tune(set_mode=1, set_chunks=chunks)
+    rng = np.random.default_rng(chunks)
+    for proto in (17, 6):
+        arena, off, caplen, ml = fuzz.make_batch(rng, 3000, proto, max_total=1600)
+        compare(torch, c, OPS_L4[proto][1], arena, len(off), off=off, length=caplen, max_len=ml, arg=1)
+    for n in (4096 + 77, 100):
+        L, stride = 1500, 1536
+        arena = np.zeros(n * stride, np.uint8)
+        oracle_lib.gen(arena, n, stride=stride, fixed_len=L)
+        compare(torch, c, "set_udp", arena, n, stride=stride, fixed_len=L)
+    c.close()
+
+
 @pytest.mark.parametrize("mode", [0, 1])
 def test_set_modes_bit_exact(torch, mode):
     """Fused (mode 0) and two-phase (mode 1, compute then scatter) Set

@@ -79,6 +79,10 @@ VARIANTS = {
     "oldset": (["-DCLK_DENSE_SET=0", "-DCLK_SKV=2", "-DCLK_SWPE=8"], {}),
     "dsetk5": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=5", "-DCLK_SWPE=4"], {}),
     "dsetk6w3": (["-DCLK_DENSE_SET=1", "-DCLK_SKV=6", "-DCLK_SWPE=3"], {}),
+    "ch2": ([], {"set_chunks": 2}),
+    "ch4": ([], {"set_chunks": 4}),
+    "ch8": ([], {"set_chunks": 8}),
+    "ch16": ([], {"set_chunks": 16}),
 }
 
 
