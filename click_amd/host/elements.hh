@@ -870,13 +870,15 @@ BatchElement *element_impl(::clk_element *w);
 hipError_t glue_checked(hipError_t e);                        // the glue's test fault hook       // the C ABI handle's element
 
 // A chain of elements in one thread, member k+1 connected to member k's
-// output 0 (chain.cc): each packet is staged once; a flush copies the batch
-// to HBM once, runs every member's kernel in order -- member k over the
-// packets members 0..k-1 passed on output 0 -- copies the rewritten bytes
-// back once, and routes each packet once, through the members' own
-// route() (counters, handlers, chatter as if each member had run it).  The
-// GPU analogue of click-xform's combos (ipinputcombo.cc:66-140,
-// ipoutputcombo.cc:44-205).
+// output 0 (chain.cc): each packet is staged once and enters member 0 at
+// push (going on at once through members that decide it on the host); a
+// flush copies the batch to HBM once, runs every member's kernel in order --
+// member k over the packets members 0..k-1 passed on output 0 -- routing each
+// member's verdicts through its own route() (counters, handlers, chatter as
+// if it had run alone) before the next member's kernel, and copies the
+// rewritten bytes back once (a member whose verdict carries its rewrite
+// writes it from route() instead).  The GPU analogue of click-xform's combos
+// (ipinputcombo.cc:66-140, ipoutputcombo.cc:44-205).
 class Chain {
   public:
     explicit Chain(const std::vector<BatchElement *> &members) : m_(members) {}
