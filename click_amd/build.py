@@ -98,7 +98,7 @@ def build_native_tests(force=False):
         exe = os.path.join(ndir, "bin", name)
         hip = os.path.join(ROOT, "click_integration", "elements", "hip")
         deps = [src, lib, os.path.join(ndir, "harness.hh"), os.path.join(hip, "hipcore.hh"),
-                os.path.join(hip, "hipclasses.hh")] + [
+                os.path.join(hip, "hipclasses.hh"), os.path.join(hip, "hipchain.hh")] + [
             os.path.join(ROOT, "include", h) for h in ("click_amd_cksum.h", "click_amd_elements.h")]
         orc = name in NATIVE_ORACLE
         if orc:

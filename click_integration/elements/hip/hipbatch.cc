@@ -20,6 +20,50 @@
 #include <new>
 CLICK_DECLS
 
+namespace {
+// the output ports connected to one input port
+struct UpstreamPorts : public RouterVisitor {
+    int n;
+    Element *first;
+    UpstreamPorts() : n(0), first(0) { }
+    bool visit(Element *e, bool isoutput, int, Element *, int, int distance) {
+	if (isoutput && distance == 1 && n++ == 0)
+	    first = e;
+	return false;
+    }
+};
+
+HIPBatchElement *
+gpu_backed(Element *e)
+{
+    return e ? static_cast<HIPBatchElement *>(e->cast("HIPBatchElement")) : 0;
+}
+}
+
+// hipchain.hh's graph trait over the router's connections: the chain rules
+// themselves are hipchain.hh's (tested natively)
+struct HIPChainGraph {
+    typedef HIPBatchElement *Node;
+    Node push_next(Node x) const {
+	if (x->noutputs() < 1 || !x->output_is_push(0) || x->output(0).port() != 0)
+	    return 0;
+	return gpu_backed(x->output(0).element());
+    }
+    Node sole_upstream(Node y) const {
+	if (y->ninputs() < 1 || !y->input_is_push(0))
+	    return 0;
+	UpstreamPorts up;
+	y->router()->visit_upstream(y, 0, &up);
+	return up.n == 1 ? gpu_backed(up.first) : 0;
+    }
+    bool chain_conf(Node x) const	{ return x->_chain_conf; }
+    int device(Node x) const		{ return x->_device; }
+    bool may_write(Node x) const	{ return x->cls_may_write(); }
+    bool chain_last(Node x) const	{ return x->cls_chain_last(); }
+    bool chain_head_only(Node x) const	{ return x->cls_chain_head_only(); }
+    bool pass_effects(Node x) const	{ return x->cls_pass_effects(); }
+};
+
 HIPBatchElement::HIPBatchElement()
     : _device(-1), _latency_ms(1), _retries(3), _pt(0), _tasks(0), _npt(0), _gate(0), _chain_conf(true),
       _chain_writes(false), _chain_tried(0)
@@ -135,14 +179,9 @@ HIPBatchElement::initialize(ErrorHandler *errh)
     _chain_tried = new bool[_npt];
     for (int k = 0; k < _npt; k++)
 	_chain_tried[k] = false;
-    _chain.clear();
-    _chain.push_back(this);
-    if (_chain_conf && !chain_member())
-	for (HIPBatchElement *x = this, *y; !x->cls_chain_last() && (y = x->chain_next()); x = y)
-	    _chain.push_back(y);
-    _chain_writes = false;
-    for (int m = 1; m < _chain.size(); m++)
-	_chain_writes = _chain_writes || _chain[m]->cls_may_write();
+    HIPChainGraph g;
+    hipcore::form_chain(g, this, _chain);
+    _chain_writes = hipcore::chain_writes(g, _chain);
     return 0;
 }
 
@@ -152,49 +191,6 @@ HIPBatchElement::cast(const char *n)
     if (strcmp(n, "HIPBatchElement") == 0)
 	return this;
     return Element::cast(n);
-}
-
-namespace {
-// the output ports connected to one input port
-struct UpstreamPorts : public RouterVisitor {
-    int n;
-    Element *first;
-    UpstreamPorts() : n(0), first(0) { }
-    bool visit(Element *e, bool isoutput, int, Element *, int, int distance) {
-	if (isoutput && distance == 1 && n++ == 0)
-	    first = e;
-	return false;
-    }
-};
-}
-
-// The GPU-backed element this one's output 0 pushes into, if it can join
-// this one's chain: its input 0, fed by nothing else, CHAIN true, the same
-// DEVICE, not an element that only starts chains.
-HIPBatchElement *
-HIPBatchElement::chain_next()
-{
-    if (!_chain_conf || noutputs() < 1 || !output_is_push(0) || output(0).port() != 0)
-	return 0;
-    Element *e = output(0).element();
-    HIPBatchElement *y = e ? static_cast<HIPBatchElement *>(e->cast("HIPBatchElement")) : 0;
-    if (!y || y == this || !y->_chain_conf || y->_device != _device || y->cls_chain_head_only())
-	return 0;
-    UpstreamPorts up;
-    router()->visit_upstream(y, 0, &up);
-    return up.n == 1 && up.first == this ? y : 0;
-}
-
-// A member of the chain of the element before it (which runs it)
-bool
-HIPBatchElement::chain_member()
-{
-    if (ninputs() < 1 || !input_is_push(0))
-	return false;
-    UpstreamPorts up;
-    router()->visit_upstream(this, 0, &up);
-    HIPBatchElement *u = up.n == 1 && up.first ? static_cast<HIPBatchElement *>(up.first->cast("HIPBatchElement")) : 0;
-    return u && !u->cls_chain_last() && u->chain_next() == this;
 }
 
 // State t runs the chain (under t's lock): each member's glue element on t's
@@ -219,11 +215,8 @@ HIPBatchElement::ensure_chain(PerThread &t)
     }
     if (t.mem.size() == (size_t) _chain.size()
 	&& clk_chain_create(t.mem.data(), (int) t.mem.size(), &t.chain) == CLK_SUCCESS) {
-	uint64_t report = 0;		// the members whose finish() changes a packet they pass on
-	for (int m = 0; m < _chain.size() && m < 64; m++)
-	    if (_chain[m]->cls_pass_effects())
-		report |= uint64_t(1) << m;
-	clk_chain_report_passes(t.chain, report);
+	HIPChainGraph g;
+	clk_chain_report_passes(t.chain, hipcore::chain_report(g, _chain));
 	for (int m = 1; m < _chain.size(); m++) {
 	    _chain[m]->_borrow_lock.acquire();
 	    _chain[m]->_borrowed.push_back(t.mem[m]);
@@ -239,29 +232,13 @@ HIPBatchElement::ensure_chain(PerThread &t)
     t.chain = 0;
 }
 
-// The annotations the members after the head read (CLK_ANNO_*), staged with
-// the packet: FixIPSrc's and IPOutputCombo's FIX_IP_SRC, IPOutputCombo's
-// paint and packet type
-uint32_t
-HIPBatchElement::chain_anno(Packet *p) const
-{
-    return (ClickPacketOps::fix_ip_src(p) ? CLK_ANNO_FIX_IP_SRC : 0u)
-	| (ClickPacketOps::broadcast_or_multicast(p) ? CLK_ANNO_BCAST : 0u)
-	| CLK_ANNO_PAINT(ClickPacketOps::paint(p));
-}
-
 Packet *
 HIPBatchElement::prepare(Packet *p, uint32_t *anno, Packet **extra)
 {
     if (!(p = cls_prepare(p, anno, extra)))
 	return 0;
-    if (_chain.size() > 1) {
-	// readied for every member: writable if any may write (where the
-	// reference makes it writable only in the element that writes it)
-	if (_chain_writes && !(p = p->uniqueify()))
-	    return 0;
-	*anno |= chain_anno(p);
-    }
+    if (_chain.size() > 1)		// readied for every member
+	p = hipcore::chain_ready<Packet, ClickPacketOps>(p, _chain_writes, anno);
     return p;
 }
 

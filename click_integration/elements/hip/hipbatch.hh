@@ -9,6 +9,7 @@
 #include "click_amd_elements.h"
 #include "hipcore.hh"
 #include "hipclasses.hh"
+#include "hipchain.hh"
 CLICK_DECLS
 
 /*
@@ -102,6 +103,7 @@ struct ClickPacketOps {
  * the annotations every member reads.  The members' handlers count what
  * they did in the chains too.  A chain that cannot be created (e.g. ZEROCOPY
  * on some members only) is left as separate elements, with one message.
+ * The rules are hipchain.hh's (HIPChainGraph answers its graph questions).
  */
 class HIPBatchElement : public Element { public:
 
@@ -189,10 +191,9 @@ class HIPBatchElement : public Element { public:
     PerThread &state();
     int ensure(PerThread &t, ErrorHandler *errh);
     void ensure_chain(PerThread &t);
-    HIPBatchElement *chain_next();
-    bool chain_member();
-    uint32_t chain_anno(Packet *p) const;
     static String read_handler(Element *e, void *thunk) CLICK_COLD;
+
+    friend struct HIPChainGraph;
 
 };
 

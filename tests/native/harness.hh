@@ -28,6 +28,7 @@
 #include "click_amd_elements.h"
 #include "../../click_integration/elements/hip/hipcore.hh"
 #include "../../click_integration/elements/hip/hipclasses.hh"
+#include "../../click_integration/elements/hip/hipchain.hh"
 
 namespace {
 
@@ -285,7 +286,13 @@ template <class C> struct Member : MemberBase {
 class ChainHost {
   public:
     typedef hipcore::Core<TPacket, ChainHost, TLock> Core;
+    struct Traits {                                     // the members' class traits, for hipchain.hh
+        typedef MemberBase *Node;
+        bool may_write(Node x) const { return x->may_write(); }
+        bool pass_effects(Node x) const { return x->pass_effects(); }
+    };
     std::vector<MemberBase *> m;                        // not owned
+    bool writes = false;                                // a member after the head may write
     Core core;
     St st;
     std::atomic<int> runcount{0};
@@ -311,11 +318,9 @@ class ChainHost {
             std::fprintf(stderr, "chain: %s\n", clk_last_error(0));
             std::exit(3);
         }
-        uint64_t report = 0;                            // the members whose passes change the packet
-        for (size_t k = 0; k < m.size(); k++)
-            if (m[k]->pass_effects())
-                report |= uint64_t(1) << k;
-        clk_chain_report_passes(st.chain, report);
+        Traits g;                                       // the adapter's chain rules (hipchain.hh)
+        writes = hipcore::chain_writes(g, m);
+        clk_chain_report_passes(st.chain, hipcore::chain_report(g, m));
         char buf[64];
         clk_element_read_handler(st.e, "batch", buf, sizeof buf);
         core.set_batch((uint32_t)std::strtoul(buf, nullptr, 10));
@@ -333,14 +338,7 @@ class ChainHost {
     {
         if (!(p = m[0]->prepare(p, anno, extra)))
             return nullptr;
-        bool w = false;
-        for (size_t k = 1; k < m.size(); k++)
-            w = w || m[k]->may_write();
-        if (w && !(p = TOps::uniqueify(p)))
-            return nullptr;
-        *anno |= (TOps::fix_ip_src(p) ? CLK_ANNO_FIX_IP_SRC : 0u) | (TOps::broadcast_or_multicast(p) ? CLK_ANNO_BCAST : 0u) |
-                 CLK_ANNO_PAINT(TOps::paint(p));
-        return p;
+        return hipcore::chain_ready<TPacket, TOps>(p, writes, anno);
     }
     int32_t nh_offset(TPacket *p) { return m[0]->nh_offset(p); }
     bool primary(int k, int32_t port, uint32_t aux) { return m[(size_t)k]->primary(port, aux); }
