@@ -830,6 +830,12 @@ def c1_frame():
 
 
 CHAIN_BATCH = 16384     # a chain's host passes over a batch that stays in L2
+C1_RUNS = 5             # timed runs per leg (after one warm-up); the median is reported
+
+
+def c1_median(walls):
+    """The median of a config-1 leg's timed runs (wall seconds)."""
+    return sorted(walls)[len(walls) // 2]
 
 
 def config1(ctx, n=C1_PACKETS, batch=65536):
@@ -837,8 +843,9 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
     chain takes all n frames by push_burst (C++ push() per packet, batches of
     `batch` double-buffered), flushes and routes them; the next element takes
     the survivors.  One untimed warm-up run on a copy allocates the staging
-    buffers.  Asserts all n forwarded on port 0 and identical bytes both
-    ways (OUTA == OUTB)."""
+    buffers; then C1_RUNS timed runs, each on fresh frames, and the median
+    run is reported (`mpps`; every run in `runs_mpps`).  Asserts all n
+    forwarded on port 0 and identical bytes both ways (OUTA == OUTB)."""
     import numpy as np
     from click_amd.elements import Element, ResultBuffers
     frame = c1_frame()
@@ -849,7 +856,8 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
     for name, chain, zc in runs:
         extra = "BATCH %d" % batch + (", ZEROCOPY true" if zc else "")
         els = [Element(ctx, cls, ", ".join(x for x in (conf, extra) if x), noutputs=nout) for cls, conf, nout in chain]
-        for timed in (False, True):
+        walls, runs = [], []
+        for run in range(1 + C1_RUNS):
             raw = np.empty(n * len(frame) + 8192, np.uint8)          # page-aligned, registrable
             arena = raw[(-raw.ctypes.data) % 4096:][:n * len(frame)]
             arena[:] = np.tile(np.frombuffer(frame, np.uint8), n)
@@ -876,11 +884,16 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
             dt = time.perf_counter() - t0
             if zc:
                 ctx.host_unregister(arena)
+            if run:
+                walls.append(dt)
+                runs.append(parts)
         for e in els:
             e.close()
+        dt = c1_median(walls)
+        parts = runs[walls.index(dt)]
         arenas[name] = arena
         out[name] = {"chain": [c[0] for c in chain], "forwarded": fwd, "wall_s": round(dt, 4),
-                     "mpps": round(n / dt / 1e6, 2),
+                     "mpps": round(n / dt / 1e6, 2), "runs_mpps": [round(n / w / 1e6, 2) for w in walls],
                      "per_element_ms": {c[0]: {"push": round(a * 1e3, 2), "flush": round(b * 1e3, 2),
                                                "results": round(r * 1e3, 2)} for c, (a, b, r) in zip(chain, parts)}}
     # the same chains on one device-resident batch (clk_chain_*: one gather,
@@ -896,7 +909,8 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
         els = [Element(ctx, cls, ", ".join(x for x in (conf, extra) if x), noutputs=nout)
                for cls, conf, nout in chain]
         ch = Chain(els)
-        for timed in (False, True):
+        walls, phases = [], []
+        for run in range(1 + C1_RUNS):
             raw = np.empty(n * len(frame) + 8192, np.uint8)
             arena = raw[(-raw.ctypes.data) % 4096:][:n * len(frame)]
             arena[:] = np.tile(np.frombuffer(frame, np.uint8), n)
@@ -914,6 +928,11 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
             fwd = int(((cbufs[1][:k] == len(chain) - 1) & (cbufs[2][:k] == 0)).sum())
             if zc:
                 ctx.host_unregister(arena)
+            if run:
+                walls.append(dt)
+                phases.append((tb - t0, tc - tb, t0 + dt - tc))
+        dt = c1_median(walls)
+        ph = phases[walls.index(dt)]
         st = (ctypes.c_double * 8)()
         ch.lib.clk_chain_stats(ch.h, ctypes.cast(st, ctypes.c_void_p), 8)
         ch.close()
@@ -921,11 +940,11 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
             e.close()
         arenas[name + "_chain"] = arena
         out[name + "_chain"] = {"chain": [c[0] for c in chain], "forwarded": fwd, "wall_s": round(dt, 4),
-                                "mpps": round(n / dt / 1e6, 2),
-                                "ms": {"push": round((tb - t0) * 1e3, 2), "flush": round((tc - tb) * 1e3, 2),
-                                       "results": round((t0 + dt - tc) * 1e3, 2)},
-                                # host ns per packet by phase, both runs (warm-up + timed)
-                                "ns_per_packet": {k: round(v * 1e9 / (2 * n), 1) for k, v in zip(
+                                "mpps": round(n / dt / 1e6, 2), "runs_mpps": [round(n / w / 1e6, 2) for w in walls],
+                                "ms": {"push": round(ph[0] * 1e3, 2), "flush": round(ph[1] * 1e3, 2),
+                                       "results": round(ph[2] * 1e3, 2)},
+                                # host ns per packet by phase, over all runs (warm-up + timed)
+                                "ns_per_packet": {k: round(v * 1e9 / ((1 + C1_RUNS) * n), 1) for k, v in zip(
                                     ("push", "rebuild", "gpu_round_trips", "unused", "h2d", "d2h_back",
                                      "route", "copy_back"), list(st)) if k != "unused"}}
     # as the Click adapter forms fake-iprouter.click's graph (lines 91-106):
@@ -936,7 +955,8 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
     tail = [Element(ctx, cls, ", ".join(x for x in (conf, "BATCH %d" % batch) if x), noutputs=nout)
             for cls, conf, nout in spec[1:]]
     ch = Chain(tail)
-    for timed in (False, True):
+    walls = []
+    for run in range(1 + C1_RUNS):
         raw = np.empty(n * len(frame) + 8192, np.uint8)
         arena = raw[(-raw.ctypes.data) % 4096:][:n * len(frame)]
         arena[:] = np.tile(np.frombuffer(frame, np.uint8), n)
@@ -954,16 +974,20 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
         k = int(ch.lib.clk_chain_results(ch.h, *cptrs, n + 1))
         dt = time.perf_counter() - t0
         fwd = int(((cbufs[1][:k] == len(tail) - 1) & (cbufs[2][:k] == 0)).sum())
+        if run:
+            walls.append(dt)
+    dt = c1_median(walls)
     ch.close()
     for e in [head] + tail:
         e.close()
     arenas["elements_as_click_forms"] = arena
     out["elements_as_click_forms"] = {"chain": [spec[0][0], "[" + ", ".join(c[0] for c in spec[1:]) + "]"],
-                                      "forwarded": fwd, "wall_s": round(dt, 4), "mpps": round(n / dt / 1e6, 2)}
+                                      "forwarded": fwd, "wall_s": round(dt, 4), "mpps": round(n / dt / 1e6, 2),
+                                      "runs_mpps": [round(n / w / 1e6, 2) for w in walls]}
     same = all(np.array_equal(arenas["elements"], arenas[k]) for k in arenas)
     return {"workload": "C1: conf/fake-iprouter.click forwarding path, %d x %d B frames, element glue on the GPU "
-                        "(staged: push() gathers into pinned staging; _zerocopy: registered host arena)"
-                        % (n, len(frame)),
+                        "(staged: push() gathers into pinned staging; _zerocopy: registered host arena); "
+                        "median of %d timed runs" % (n, len(frame), C1_RUNS),
             "packets": n, "expect_forwarded": n, "outa_eq_outb": same,
             "ok": same and all(v["forwarded"] == n for v in out.values()), **out}
 
@@ -972,13 +996,14 @@ def config1_cpu(n=C1_PACKETS):
     """The same chains on one host thread through the oracle restatement
     (the byte-touching elements only; Click's scheduler, Classifier and
     queues are not part of it): CheckIPHeader + IPGWOptions + FixIPSrc +
-    DecIPTTL + IPFragmenter(300), and IPInputCombo + IPOutputCombo."""
+    DecIPTTL + IPFragmenter(300), and IPInputCombo + IPOutputCombo; the
+    median of C1_RUNS runs, each on fresh frames, as the GPU legs."""
     import numpy as np
     from tests import oracle_lib
     frame = c1_frame()
     fl = len(frame)
-    res = {}
-    for name in ("elements", "combos"):
+    res, walls = {}, {}
+    for name, run in [(nm, r) for nm in ("elements", "combos") for r in range(C1_RUNS)]:
         arena = np.tile(np.frombuffer(frame, np.uint8), n)
         l3 = arena[14:]
         t0 = time.perf_counter()
@@ -994,9 +1019,11 @@ def config1_cpu(n=C1_PACKETS):
             port, _, _ = oracle_lib.ip_out_batch("ip_output_combo", l3, n, stride=fl, fixed_len=fl - 14,
                                                  my_ip=0x18041A12, mtu=300)
             fwd = int(((codes == 0) & (port == 0)).sum())
-        dt = time.perf_counter() - t0
-        res[name] = {"forwarded": fwd, "wall_s": round(dt, 4), "mpps": round(n / dt / 1e6, 2)}
-    return {"threads": 1, "kind": "port", **res,
+        walls.setdefault(name, []).append(time.perf_counter() - t0)
+        dt = c1_median(walls[name])
+        res[name] = {"forwarded": fwd, "wall_s": round(dt, 4), "mpps": round(n / dt / 1e6, 2),
+                     "runs_mpps": [round(n / w / 1e6, 2) for w in walls[name]]}
+    return {"threads": 1, "kind": "port", "runs": C1_RUNS, **res,
             "note": "oracle restatement of the byte-touching elements, one host thread; the reference's own "
                     "`click -t conf/fake-iprouter.click` (Click runtime included) measured 4.3-6.7 Mpps on the "
                     "survey VM (BASELINE.md §3)"}

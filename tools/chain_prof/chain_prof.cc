@@ -1,0 +1,91 @@
+// chain_prof.cc -- tools only (never shipped, not a test): config 1's
+// five-element chain (bench.py C1_CHAINS["elements"]) through the chain C
+// ABI from C++, as bench.py's elements_chain leg runs it, so the host glue
+// can be profiled with gprof (tools/chain_prof/run.sh builds the glue's host
+// files into this executable with -pg).  Prints the median Mpps of the timed
+// runs and clk_chain_stats.
+//   chain_prof FRAME_HEX [RUNS] [BATCH]
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+#include "click_amd_cksum.h"
+#include "click_amd_elements.h"
+
+int main(int argc, char **argv)
+{
+    if (argc < 2)
+        return 2;
+    std::vector<uint8_t> frame;
+    for (const char *h = argv[1]; h[0] && h[1]; h += 2)
+        frame.push_back((uint8_t)std::strtoul(std::string(h, 2).c_str(), nullptr, 16));
+    const int runs = argc > 2 ? std::atoi(argv[2]) : 5;
+    const std::string B = ", BATCH " + std::string(argc > 3 ? argv[3] : "65536");
+    const uint32_t n = 600000, L = (uint32_t)frame.size();
+    clk_ctx *ctx = nullptr;
+    if (clk_ctx_create(0, &ctx) != CLK_SUCCESS) {
+        std::printf("{\"skip\": \"no GPU\"}\n");
+        return 0;
+    }
+    struct Spec { const char *cls, *conf; int nout; };
+    const Spec spec[] = {{"CheckIPHeader", "INTERFACES 18.26.4.1/24 18.26.7.1/24, OFFSET 14", 2},
+                         {"IPGWOptions", "18.26.4.24", 2}, {"FixIPSrc", "18.26.4.24", 1},
+                         {"DecIPTTL", "", 2}, {"IPFragmenter", "300", 2}};
+    std::vector<clk_element *> els;
+    for (const Spec &s : spec) {
+        clk_element *e = nullptr;
+        std::string conf = std::string(s.conf) + (s.conf[0] ? B : B.substr(2));
+        if (clk_element_create(ctx, s.cls, conf.c_str(), s.cls, s.nout, &e) != CLK_SUCCESS) {
+            std::fprintf(stderr, "%s: %s\n", s.cls, clk_last_error(ctx));
+            return 3;
+        }
+        els.push_back(e);
+    }
+    clk_chain *c = nullptr;
+    if (clk_chain_create(els.data(), (int)els.size(), &c) != CLK_SUCCESS)
+        return 3;
+    std::vector<uint64_t> tok(n + 1);
+    std::vector<int32_t> mem(n + 1), port(n + 1);
+    std::vector<uint32_t> len(n + 1), aux(n + 1), lens(n, L);
+    std::vector<uint8_t *> ptrs(n);
+    std::vector<double> mpps;
+    uint64_t fwd = 0;
+    for (int r = 0; r <= runs; r++) {               // run 0 warms up
+        std::vector<uint8_t> arena((size_t)n * L);
+        for (uint32_t i = 0; i < n; i++) {
+            std::copy(frame.begin(), frame.end(), arena.begin() + (size_t)i * L);
+            ptrs[i] = arena.data() + (size_t)i * L;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        if (clk_chain_push_burst(c, ptrs.data(), lens.data(), nullptr, 0, n) != CLK_SUCCESS ||
+            clk_chain_flush(c) != CLK_SUCCESS) {
+            std::fprintf(stderr, "chain: %s\n", clk_chain_last_error(c));
+            return 4;
+        }
+        const uint64_t k = clk_chain_results(c, tok.data(), mem.data(), port.data(), len.data(), aux.data(), n + 1);
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        fwd = 0;
+        for (uint64_t j = 0; j < k; j++)
+            fwd += mem[j] == 4 && port[j] == 0;
+        if (r)
+            mpps.push_back(n / s / 1e6);
+    }
+    std::vector<double> sorted = mpps;
+    std::sort(sorted.begin(), sorted.end());
+    double st[8] = {0};
+    clk_chain_stats(c, st, 8);
+    std::printf("{\"leg\": \"elements_chain\", \"forwarded\": %llu, \"mpps\": %.2f, \"runs_mpps\": [",
+                (unsigned long long)fwd, sorted[sorted.size() / 2]);
+    for (size_t k = 0; k < mpps.size(); k++)
+        std::printf("%s%.2f", k ? ", " : "", mpps[k]);
+    const double per = 1e9 / ((runs + 1) * (double)n);
+    std::printf("], \"ns_per_packet\": {\"push\": %.1f, \"gpu\": %.1f, \"h2d\": %.1f, \"route\": %.1f, \"copy_back\": %.1f}}\n",
+                st[0] * per, st[2] * per, st[4] * per, st[6] * per, st[7] * per);
+    clk_chain_destroy(c);
+    for (clk_element *e : els)
+        clk_element_destroy(e);
+    clk_ctx_destroy(ctx);
+    return 0;
+}
