@@ -43,6 +43,8 @@ struct TPacket {
     uint8_t *raw = nullptr;          // buf->data(), kept in the packet as Click's Packet keeps its buffer
     size_t off = 0, len = 0;
     long nh = -1;                    // absolute offset of the network header in buf
+    bool cloned = false;             // a clone of it was made, or it is one: uniqueify() asks the
+                                     // buffer's count (Click keeps that count in the Packet itself)
     TAnno a;
 };
 
@@ -69,7 +71,7 @@ TPacket *make(const uint8_t *bytes, size_t len, long id, size_t headroom = 0)
 struct TOps {
     static TPacket *uniqueify(TPacket *p)
     {
-        if (p->buf.use_count() > 1) {
+        if (p->cloned && p->buf.use_count() > 1) {
             int v = g_uniq_fail.load();
             if (v > 0 && g_uniq_fail.fetch_sub(1) == 1) {
                 kill(p);                 // Packet::uniqueify kills on failure
@@ -77,11 +79,13 @@ struct TOps {
             }
             p->buf = std::make_shared<std::vector<uint8_t> >(*p->buf);
             p->raw = p->buf->data();
+            p->cloned = false;
         }
         return p;
     }
     static TPacket *clone(TPacket *p)
     {
+        p->cloned = true;
         TPacket *q = new TPacket(*p);
         g_live++;
         return q;

@@ -8,10 +8,14 @@
 // distribution (most pulls hand out a ready packet; a refill launches the
 // next batch and routes the one before, hipcore.hh).
 //   pull_bench [SCALE]     packet counts divided by SCALE
+//   pull_bench SCALE chain REPS   the push_c1 chain leg only, REPS times
+//                                 (BATCH 8192, the Click adapter's default)
 #include <algorithm>
 #include "harness.hh"
 
 namespace {
+
+const uint32_t ADAPTER_BATCH = 8192;                    // hipbatch.hh HIPBatchElement::ADAPTER_BATCH
 
 uint16_t fold_sum(const uint8_t *b, uint32_t n, uint32_t acc)   // RFC 1071 over n bytes
 {
@@ -206,6 +210,11 @@ int main(int argc, char **argv)
         return 0;
     }
     const int scale = argc > 1 ? std::max(1, std::atoi(argv[1])) : 1;
+    if (argc > 3 && std::string(argv[2]) == "chain") {   // profiling (tools/core_profile): the chain leg only
+        for (int r = std::atoi(argv[3]); r > 0; r--)
+            push_c1(600000 / scale, true, ADAPTER_BATCH);
+        return 0;
+    }
     // BATCH bounds the longest pull (one refill stages a batch and routes
     // the one before): the default and a small one
     for (uint32_t batch : {65536u, 8192u}) {

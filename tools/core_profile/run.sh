@@ -1,9 +1,29 @@
 #!/bin/bash
-# The adapter core's own per-packet cost on the CPU (no GPU): the
-# measurement program over the null glue, optionally with gprof (-pg).
+# The adapter core's own per-packet cost (tools only).
+#   run.sh [SCALE]      on the CPU (no GPU): the measurement program
+#                       (tests/native/pull_bench.cc) over the null glue,
+#                       with gprof when PG=1
+#   run.sh gprof_build  here: pull_bench over the real glue library, linked
+#                       with -pg (gprof's PC sampling of the core's code; the
+#                       library's own time is not sampled)
+#   run.sh gprof_run    on the GPU box: its chain leg REPS times, flat profile
 set -e
 D=$(cd "$(dirname "$0")" && pwd); R=$D/../..
 mkdir -p $D/bin
-g++ -std=c++17 -O2 -g ${PG:+-pg} -I$R/include $R/tests/native/pull_bench.cc $D/null_glue.cc -o $D/bin/pull_bench_null
-cd $D/bin && ./pull_bench_null ${1:-1}
-if [ -n "$PG" ]; then gprof -b -p ./pull_bench_null gmon.out | head -40; fi
+case "$1" in
+gprof_build)
+    g++ -std=c++17 -O2 -g -I$R/include $R/tests/native/pull_bench.cc -L$R/click_amd -lclick_amd_cksum \
+        -L/opt/rocm/lib -Wl,-rpath-link,/opt/rocm/lib -Wl,-rpath,'$ORIGIN/../../../click_amd' \
+        -Wl,-rpath,/opt/rocm/lib -pg -o $D/bin/pull_bench_pg
+    ;;
+gprof_run)
+    cd $D/bin
+    ./pull_bench_pg 1 chain ${REPS:-100} | tail -2
+    gprof -b -p ./pull_bench_pg gmon.out 2>/dev/null | head -${TOP:-40}
+    ;;
+*)
+    g++ -std=c++17 -O2 -g ${PG:+-pg} -I$R/include $R/tests/native/pull_bench.cc $D/null_glue.cc -o $D/bin/pull_bench_null
+    cd $D/bin && ./pull_bench_null ${1:-1}
+    if [ -n "$PG" ]; then gprof -b -p ./pull_bench_null gmon.out | head -40; fi
+    ;;
+esac
