@@ -521,6 +521,8 @@ template <class P, class Host, class L> class Core {
                     r.made = h.make_packet(r.member, t.chain ? t.mem[(size_t) r.member] : t.e, aux[i]);
                     r.parent = t.last_primary;
                 }
+                if (r.p)                 // finish() reads it soon: the packet staged long ago is
+                    __builtin_prefetch(r.p);     // out of the cache by now
                 t.outbox.push_back(r);
             }
             while (!t.held.empty() && !t.held.front().p && !t.held.front().extra) {
@@ -576,6 +578,8 @@ template <class P, class Host, class L> class Core {
             t.lock.release();
             for (size_t i = 0; i < work.size(); i++) {
                 R &r = work[i];
+                if (i + 8 < work.size() && work[i + 8].p)   // its bytes, 8 results ahead
+                    __builtin_prefetch(h.data(work[i + 8].p));
                 if (r.end) {
                     const size_t nm = t.chain ? t.mem.size() : 1;
                     for (size_t m = 0; m < nm; m++)
