@@ -341,9 +341,12 @@ template <class P, class Host, class L> class Core {
                 g++;
             dry = g < want;
             t.lock.acquire();
-            for (uint32_t j = 0; j < g; j++)
+            for (uint32_t j = 0; j < g; j++) {
+                if (j + 4 < g)           // the bytes staging reads, 4 packets ahead
+                    __builtin_prefetch(h.data(grp[j + 4]));
                 if (stage(h, t, grp[j], false))
                     k++;
+            }
             t.lock.release();
         }
         t.lock.acquire();
@@ -487,8 +490,8 @@ template <class P, class Host, class L> class Core {
             if (n)
                 t.routed_any = true;
             for (uint64_t i = 0; i < n; i++) {
-                R r;
-                memset(&r, 0, sizeof(r));
+                t.outbox.emplace_back(); // built in place, zeroed (value-initialized)
+                R &r = t.outbox.back();
                 r.member = mem[i];
                 r.port = port[i];
                 r.len = len[i];
@@ -523,7 +526,6 @@ template <class P, class Host, class L> class Core {
                 }
                 if (r.p)                 // finish() reads it soon: the packet staged long ago is
                     __builtin_prefetch(r.p);     // out of the cache by now
-                t.outbox.push_back(r);
             }
             while (!t.held.empty() && !t.held.front().p && !t.held.front().extra) {
                 t.held.pop_front();

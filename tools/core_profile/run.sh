@@ -4,17 +4,20 @@
 #                       (tests/native/pull_bench.cc) over the null glue,
 #                       with gprof when PG=1
 #   run.sh gprof_build  here: pull_bench over the real glue library, linked
-#                       with -pg (gprof's PC sampling of the core's code; the
-#                       library's own time is not sampled)
+#                       (not compiled) with -pg: gprof's PC sampling of the
+#                       core's code, no mcount calls; the library's own time
+#                       is not sampled
 #   run.sh gprof_run    on the GPU box: its chain leg REPS times, flat profile
 set -e
 D=$(cd "$(dirname "$0")" && pwd); R=$D/../..
 mkdir -p $D/bin
 case "$1" in
 gprof_build)
-    g++ -std=c++17 -O2 -g -I$R/include $R/tests/native/pull_bench.cc -L$R/click_amd -lclick_amd_cksum \
+    g++ -std=c++17 -O2 -g -I$R/include -c $R/tests/native/pull_bench.cc -o $D/bin/pull_bench.o
+    g++ -pg $D/bin/pull_bench.o -L$R/click_amd -lclick_amd_cksum \
         -L/opt/rocm/lib -Wl,-rpath-link,/opt/rocm/lib -Wl,-rpath,'$ORIGIN/../../../click_amd' \
-        -Wl,-rpath,/opt/rocm/lib -pg -o $D/bin/pull_bench_pg
+        -Wl,-rpath,/opt/rocm/lib -o $D/bin/pull_bench_pg
+    rm -f $D/bin/pull_bench.o
     ;;
 gprof_run)
     cd $D/bin
