@@ -5,7 +5,7 @@
   python tools/tune.py --workload c3 ...       # on the GPU box (via gpurun)
 
 Variants are compile-time flags (-DCLK_K, -DCLK_NT_LOADS, ...) built into
-their own library under build/variants/, and/or the speed-only context knobs
+their own library under tools/variants/, and/or the speed-only context knobs
 of clk_ctx_tune (Context.tune: max_blocks, scatter_blocks, set_mode,
 stream_min, group).  Nothing is read from the environment by the library.
 Every variant runs the same element over the same device-resident batch;
@@ -22,7 +22,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-VDIR = os.path.join(ROOT, "build", "variants")
+VDIR = os.path.join(ROOT, "tools", "variants")          # git-ignored; travels to the GPU box
 
 # name -> (compile flags, Context.tune knobs)
 VARIANTS = {
