@@ -50,7 +50,7 @@ struct ClickPacketOps {
  * HIPBatchElement -- what every GPU-backed checksum element of this group
  * shares (not an element itself): Click's side of the core in hipcore.hh,
  * which holds the packets while their batch is on the GPU, routes the
- * results, keeps the runcount and the latency timer, retries a failed
+ * results, keeps the runcount and the latency deadline, retries a failed
  * flush and batches in pull context.  The subclasses (one per reference
  * class) do what the reference element's simple_action() does around its
  * checksum: prepare() before staging (uniqueify, PaintTee clone) and

@@ -22,14 +22,17 @@
  * default of element.cc:1127) or push (IPOutputCombo, IPFragmenter), so:
  *   push context: push() stages the packet and holds it; a full batch is
  *     launched double-buffered (the previous one is routed), a partial one
- *     by the latency timer (timer()).  While a thread state holds packets it
+ *     once its latency deadline passes (poll(), run by the state's Task on
+ *     its own thread; timer() flushes at once).  While a thread state holds packets it
  *     holds one runcount reference (Router::adjust_runcount,
  *     router.cc:832-846), so the router cannot stop before they are routed.
  *   pull context: pull() on output 0 hands out one packet per call from a
- *     ready queue; when it is empty, it pulls up to BATCH packets from input
- *     0 (until the input returns null), runs them as one synchronous batch
- *     and queues the output-0 packets; other results leave on their push
- *     outputs as checked_output_push does (output 1 of a/ah).
+ *     ready queue; when it is empty, a refill pulls up to BATCH packets from
+ *     input 0 (until the input returns null), launches them and routes the
+ *     batch the previous refill launched, queueing its output-0 packets
+ *     (it waits for the GPU only when nothing is ready); other results
+ *     leave on their push outputs as checked_output_push does (output 1 of
+ *     a/ah).
  * Results are taken from the glue under the thread state's lock but
  * DELIVERED (annotations, output pushes) after it is released, in push
  * order: a downstream element that re-enters this element on the same
