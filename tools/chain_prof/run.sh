@@ -10,7 +10,7 @@ D=$(cd "$(dirname "$0")" && pwd); R=$D/../..
 B=$D/bin
 if [ "$1" = build ]; then
     mkdir -p $B
-    F="-O3 -std=c++17 -gdwarf-4 -I$R/include"
+    F="-O3 -std=c++17 -I$R/include"
     /opt/rocm/bin/hipcc --offload-arch=gfx950 $F -c $R/click_amd/csrc/cksum_api.hip -o $B/api.o
     for f in elements chain ingest; do /opt/rocm/bin/hipcc $F -g -c $R/click_amd/host/$f.cc -o $B/$f.o; done
     /opt/rocm/bin/hipcc $F -g -c $D/chain_prof.cc -o $B/main.o
@@ -21,5 +21,5 @@ else
     cd $B
     ./chain_prof $(cat frame.hex) ${RUNS:-5} ${BATCH:-65536}
     gprof -b -p ./chain_prof gmon.out 2>/dev/null | head -${TOP:-30}
-    gprof -b -p -l ./chain_prof gmon.out 2>/dev/null | head -${LTOP:-60}
+    gprof -b -p -l ./chain_prof gmon.out 2>/dev/null | head -${TOP:-30}
 fi
