@@ -880,31 +880,3 @@ int clk_read_stream(clk_ctx *ctx, const void *base, uint64_t bytes, uint64_t *ou
 }
 
 } // extern "C"
-
-#if CLK_ADDR_CHECK
-// Tools-only entry points of the address-check build (tools/addr_check);
-// the product library does not export them.
-extern "C" {
-int clk_dbg_window(uint64_t lo, uint64_t hi)
-{
-    unsigned long long z[clk::CHK_SITES] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(clk::dbg_lo), &lo, sizeof lo) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(clk::dbg_hi), &hi, sizeof hi) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(clk::dbg_count), z, sizeof z) != hipSuccess ||
-        hipMemcpyToSymbol(HIP_SYMBOL(clk::dbg_first), z, sizeof z) != hipSuccess)
-        return CLK_EHIP;
-    return hipDeviceSynchronize() == hipSuccess ? CLK_SUCCESS : CLK_EHIP;
-}
-
-int clk_dbg_counts(unsigned long long *count, unsigned long long *first)
-{
-    if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpyFromSymbol(count, HIP_SYMBOL(clk::dbg_count), sizeof(unsigned long long) * clk::CHK_SITES) !=
-            hipSuccess ||
-        hipMemcpyFromSymbol(first, HIP_SYMBOL(clk::dbg_first), sizeof(unsigned long long) * clk::CHK_SITES) !=
-            hipSuccess)
-        return CLK_EHIP;
-    return clk::CHK_SITES;
-}
-}   // extern "C"
-#endif

@@ -49,45 +49,13 @@
 #define CLK_L4_RUNS_SET_G 16   // Set kernels use runs from this G up (C5 -6 %; C3 -5 % with nontemporal scatter stores: DESIGN.md §6)
 #endif
 
-// Tools-only load-address check (tools/addr_check, built with
-// -DCLK_ADDR_CHECK=1; never in the product library).  Each load site of the
-// packet-stream kernel passes its address through chk_addr: an address whose
-// bytes leave the window registered by clk_dbg_window() is counted per site,
-// the first such address kept, and the load redirected to the window's start,
-// so a bad address is reported instead of faulting the GPU.
-#ifndef CLK_ADDR_CHECK
-#define CLK_ADDR_CHECK 0
-#endif
-#ifndef CLK_PHASEA_SGPR
-#define CLK_PHASEA_SGPR 0  // tools-only: 1 = round 3's readfirstlane phase A (int result widened: sign-extends), 2 = widened as unsigned
-#endif
-
-namespace clk {
-
-#if CLK_ADDR_CHECK
-enum { CHK_GENERIC = 0, CHK_DENSE = 1, CHK_HDR = 2, CHK_LAST = 3, CHK_RANGE = 4, CHK_UNDERFLOW = 5, CHK_SITES = 8 };
-__device__ uint64_t dbg_lo, dbg_hi;
-__device__ unsigned long long dbg_count[CHK_SITES], dbg_first[CHK_SITES];
-__device__ __forceinline__ void chk_note(int site, uint64_t a)
-{
-    atomicAdd(&dbg_count[site], 1ull);
-    atomicCAS(&dbg_first[site], 0ull, (unsigned long long)a);
-}
-__device__ __forceinline__ uint64_t chk_addr(uint64_t a, uint32_t bytes, int site)
-{
-    const uint64_t lo = dbg_lo, hi = dbg_hi;
-    if (hi && (a < lo || a > hi - bytes)) {     // (a + bytes would wrap for a sign-extended base)
-        chk_note(site, a);
-        return lo;
-    }
-    return a;
-}
-#define CLK_CHK(a, n, site) ::clk::chk_addr((a), (n), ::clk::site)
-#define CLK_CHK_IF(cond, site, a) do { if (cond) ::clk::chk_note(::clk::site, (a)); } while (0)
-#else
+// Load-site hooks: the identity in the library.  tools/addr_check builds a
+// copy of these sources in which each hook checks its address against a
+// registered window; nothing of that check is compiled here.
 #define CLK_CHK(a, n, site) (a)
 #define CLK_CHK_IF(cond, site, a) do { } while (0)
-#endif
+
+namespace clk {
 
 // The workgroup's place in the run order.  XCD-contiguous (XCD): workgroup b
 // (dispatched to XCD b % 8) takes position (b % 8) * q + min(b % 8, r) + b / 8
@@ -1146,20 +1114,6 @@ l4_stream_kernel(BatchArgs b, int fixoff, uint8_t *out_code,
                 R.start = live ? (uint32_t)((c0 - sb) >> 4) : (uint32_t)sp;
             }
         }
-#if CLK_PHASEA_SGPR == 1   // tools-only: round 3's faulting variant (the builtin returns int: sign-extended)
-        R.total = __builtin_amdgcn_readfirstlane(R.total);
-        R.sbase = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)R.sbase) |
-                  ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(R.sbase >> 32)) << 32);
-#elif CLK_PHASEA_SGPR == 2 // tools-only: the same, each half widened as unsigned
-        R.total = (uint32_t)__builtin_amdgcn_readfirstlane(R.total);
-        R.sbase = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)R.sbase) |
-                  ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(R.sbase >> 32)) << 32);
-#elif CLK_PHASEA_SGPR == 3 // tools-only: the chunk total alone
-        R.total = __builtin_amdgcn_readfirstlane(R.total);
-#elif CLK_PHASEA_SGPR == 4 // tools-only: the span base alone, as variant 1
-        R.sbase = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)R.sbase) |
-                  ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(R.sbase >> 32)) << 32);
-#endif
         return R;
     };
     uint64_t na;
