@@ -132,6 +132,7 @@ HIPBatchElement::ensure(PerThread &t, ErrorHandler *errh)
 	t.ctx = 0;
 	return r;
     }
+    t.xmask = cls_extra_results() ? 1 : 0;	// primary() asked only for such a class
     // this thread's element speaks its once-only chatter (first drop...)
     // together with the home thread's, as the one reference element does
     if (_gate && _gate != t.e)
@@ -217,6 +218,10 @@ HIPBatchElement::ensure_chain(PerThread &t)
 	&& clk_chain_create(t.mem.data(), (int) t.mem.size(), &t.chain) == CLK_SUCCESS) {
 	HIPChainGraph g;
 	clk_chain_report_passes(t.chain, hipcore::chain_report(g, _chain));
+	t.xmask = 0;
+	for (int m = 0; m < _chain.size(); m++)
+	    if (_chain[m]->cls_extra_results())
+		t.xmask |= uint64_t(1) << m;
 	for (int m = 1; m < _chain.size(); m++) {
 	    _chain[m]->_borrow_lock.acquire();
 	    _chain[m]->_borrowed.push_back(t.mem[m]);

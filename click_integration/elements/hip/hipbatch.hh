@@ -105,6 +105,15 @@ struct ClickPacketOps {
  * on some members only) is left as separate elements, with one message.
  * The rules are hipchain.hh's (HIPChainGraph answers its graph questions).
  */
+class HIPBatchElement;
+
+// deliver_run's output: member m's checked_output_push (element.hh)
+struct ClickPush {
+    Element *e;
+    explicit ClickPush(Element *e_) : e(e_) { }
+    void operator()(int port, Packet *p) const	{ e->checked_output_push(port, p); }
+};
+
 class HIPBatchElement : public Element { public:
 
     enum { ADAPTER_BATCH = 8192 };
@@ -132,8 +141,13 @@ class HIPBatchElement : public Element { public:
     virtual int32_t cls_nh_offset(Packet *p)	{ return _plain.nh_offset(p); }
     virtual bool cls_primary(int32_t port, uint32_t aux) const	{ return _plain.primary(port, aux); }
     virtual Packet *cls_make_packet(clk_element *e, uint32_t key)	{ return _plain.make_packet(e, key); }
-    virtual int cls_finish(PerThread &t, Routed &r, Packet **out)	{ return _plain.finish(t, r, out); }
+    typedef hipcore::Chunk<Packet> Chunk;
+    virtual void cls_deliver(PerThread &t, const Chunk &c, uint32_t i, uint32_t j, std::vector<Packet *> *ready) {
+	hipcore::deliver_run<Packet, hipcore::Plain<Packet, ClickPacketOps>, PerThread, ClickPacketOps>(
+	    _plain, t, c, i, j, ready, ClickPush(this));
+    }
     virtual void cls_end_of_batch(PerThread &t)	{ _plain.end_of_batch(t); }
+    virtual bool cls_extra_results() const	{ return false; }
     virtual bool cls_may_write() const		{ return false; }
     virtual bool cls_chain_last() const		{ return false; }
     virtual bool cls_chain_head_only() const	{ return false; }
@@ -144,11 +158,13 @@ class HIPBatchElement : public Element { public:
     int32_t nh_offset(Packet *p)		{ return cls_nh_offset(p); }
     bool primary(int m, int32_t port, uint32_t aux) const	{ return _chain[m]->cls_primary(port, aux); }
     Packet *make_packet(int m, clk_element *e, uint32_t key)	{ return _chain[m]->cls_make_packet(e, key); }
-    int finish(int m, PerThread &t, Routed &r, Packet **out)	{ return _chain[m]->cls_finish(t, r, out); }
+    bool extra_results(int m) const	{ return _chain[m]->cls_extra_results(); }
+    void deliver(int m, PerThread &t, const Chunk &c, uint32_t i, uint32_t j, std::vector<Packet *> *ready) {
+	_chain[m]->cls_deliver(t, c, i, j, ready);	// one call per run of member m's results
+    }
     void end_of_batch(int m, PerThread &t)	{ _chain[m]->cls_end_of_batch(t); }
     uint8_t *data(Packet *p)		{ return ClickPacketOps::data(p); }
     uint32_t length(Packet *p)		{ return p->length(); }
-    void output_push(int m, int port, Packet *p)	{ _chain[m]->checked_output_push(port, p); }
     Packet *input_pull()			{ return input(0).pull(); }
     void kill(Packet *p)			{ p->kill(); }
     void adjust_runcount(int delta);
@@ -207,8 +223,11 @@ class HIPClassElement : public HIPBatchElement { public:
     int32_t cls_nh_offset(Packet *p)	{ return _cls.nh_offset(p); }
     bool cls_primary(int32_t port, uint32_t aux) const	{ return _cls.primary(port, aux); }
     Packet *cls_make_packet(clk_element *e, uint32_t key)	{ return _cls.make_packet(e, key); }
-    int cls_finish(PerThread &t, Routed &r, Packet **out)	{ return _cls.finish(t, r, out); }
+    void cls_deliver(PerThread &t, const Chunk &c, uint32_t i, uint32_t j, std::vector<Packet *> *ready) {
+	hipcore::deliver_run<Packet, C, PerThread, ClickPacketOps>(_cls, t, c, i, j, ready, ClickPush(this));
+    }
     void cls_end_of_batch(PerThread &t)	{ _cls.end_of_batch(t); }
+    bool cls_extra_results() const	{ return C::extra_results != 0; }
     bool cls_may_write() const		{ return C::may_write != 0; }
     bool cls_chain_last() const		{ return C::chain_last != 0; }
     bool cls_chain_head_only() const	{ return C::chain_head_only != 0; }

@@ -52,6 +52,8 @@
  *   pass_effects     its finish() changes a packet it passes on (network
  *                    header, trim, Strip, annotations): the chain reports
  *                    those passes (clk_chain_report_passes)
+ * and extra_results  results besides its packets' own (a clone, fragments):
+ *                    the core asks primary() only for such a class
  */
 #include <stdint.h>
 #include <string.h>
@@ -63,7 +65,7 @@ namespace hipcore {
 // The glue's drop(): output 1 if it exists, killed otherwise (the port comes
 // routed; checkipheader.cc:143-159, checked_output_push).
 template <class P, class O> struct Plain {
-    enum { may_write = 0, chain_last = 0, chain_head_only = 0, pass_effects = 0 };
+    enum { may_write = 0, chain_last = 0, chain_head_only = 0, pass_effects = 0, extra_results = 0 };
     P *prepare(P *p, uint32_t *anno, P **extra) { (void) anno, (void) extra; return p; }
     int32_t nh_offset(P *p) const { return O::has_network_header(p) ? O::network_header_offset(p) : -1; }
     bool primary(int32_t port, uint32_t aux) const { (void) port, (void) aux; return true; }
@@ -218,7 +220,7 @@ template <class P, class O> struct FixIPSrcClass : Plain<P, O> {
 
 // IPOutputCombo (ipoutputcombo.cc:44-205), ports 0-4.
 template <class P, class O> struct IPOutputComboClass : Plain<P, O> {
-    enum { may_write = 1, chain_last = 0, chain_head_only = 1, pass_effects = 1 };
+    enum { may_write = 1, chain_last = 0, chain_head_only = 1, pass_effects = 1, extra_results = 1 };
     uint32_t color = 0;             // COLOR
     P *prepare(P *p, uint32_t *anno, P **extra)
     {
@@ -269,7 +271,7 @@ template <class P, class O> struct IPOutputComboClass : Plain<P, O> {
 
 // IPFragmenter (ipfragmenter.cc:88-171).
 template <class P, class O> struct IPFragmenterClass : Plain<P, O> {
-    enum { may_write = 1, chain_last = 1, chain_head_only = 0, pass_effects = 0 };
+    enum { may_write = 1, chain_last = 1, chain_head_only = 0, pass_effects = 0, extra_results = 1 };
     uint32_t mtu = 0, headroom = 0; // MTU / HEADROOM
     P *prepare(P *p, uint32_t *anno, P **extra)
     {

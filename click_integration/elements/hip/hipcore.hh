@@ -56,14 +56,27 @@
  * host's prepare() readies a packet for the whole chain (writable if any
  * member writes, the annotations every member reads).
  *
+ * Results are taken from the glue a chunk at a time into per-state arrays
+ * (Chunk: the held packets they belong to, ports, lengths, aux words) and
+ * delivered in runs of one member: the host's deliver(m, ..) finishes a
+ * whole run through member m's class logic -- one call per run, the class's
+ * finish() inlined in its loop (deliver_run) -- and pushes each packet on
+ * member m's output.  A packet's results stay in push order per member.
+ *
  * Host interface (all called on the thread that drives the core; m is the
  * chain member, 0 without a chain):
  *   the class hooks of hipclasses.hh -- prepare(), nh_offset(), primary(m,..),
- *        make_packet(m,..), finish(m,..), end_of_batch(m,..) -- which the
- *        host forwards to the element class's shipped logic (the Click
- *        adapter and the native test instantiate the same classes)
+ *        make_packet(m,..), end_of_batch(m,..) -- which the host forwards to
+ *        the element class's shipped logic (the Click adapter and the native
+ *        test instantiate the same classes)
+ *   bool extra_results(m)       member m's class has results besides its
+ *        packets' own (clones, fragments): primary() is asked only then
+ *   void deliver(int m, S &t, const Chunk<P> &c, uint32_t i, uint32_t j,
+ *        std::vector<P *> *ready)   results [i, j) of c, all member m's:
+ *        deliver_run() over member m's class, pushing on member m's outputs
+ *        (checked_output_push); with `ready` (pull context, last member) the
+ *        output-0 packets go there instead
  *   uint8_t *data(P *p); uint32_t length(P *p)
- *   void output_push(int m, int port, P *p)      member m's checked_output_push
  *   P *input_pull()                              input(0).pull(0)
  *   void kill(P *p)
  *   void adjust_runcount(int delta)
@@ -138,7 +151,8 @@ template <class T> class HeldRing {
     size_t h_ = 0, n_ = 0;
 };
 
-// One result, handed to the host's finish() after the lock is released.
+// One result as a class's finish() sees it (built in registers from a Chunk
+// entry by deliver_run, or for the rare result a stage leaves behind).
 template <class P> struct Routed {
     P *p;           // the held packet (its primary result), 0 otherwise
     P *extra;       // the held second packet (IPOutputCombo's clone result)
@@ -149,8 +163,54 @@ template <class P> struct Routed {
     uint32_t len, aux;
     int member;     // chains: the member whose result it is (0: the state's own element)
     bool pass;      // chains: p went on to the next member (its finish() applies, no push)
-    bool end;       // not a result: the end of a batch (host end_of_batch)
 };
+
+// A chunk of results taken from the glue, struct of arrays, in the glue's
+// order.  `end`: the glue had no more (the end of a batch follows them).
+template <class P> struct Chunk {
+    enum { CAP = 256 };
+    uint32_t n = 0;
+    bool end = false;
+    P *p[CAP];
+    P *extra[CAP];
+    P *made[CAP];
+    P *parent[CAP];
+    uint32_t anno[CAP], len[CAP], aux[CAP];
+    int32_t port[CAP], mem[CAP];
+    uint8_t pass[CAP];
+    void put(uint32_t k, const Routed<P> &r)
+    {
+        p[k] = r.p, extra[k] = r.extra, made[k] = r.made, parent[k] = r.parent;
+        anno[k] = r.anno, port[k] = r.port, len[k] = r.len, aux[k] = r.aux, mem[k] = r.member;
+        pass[k] = r.pass;
+    }
+    Routed<P> at(uint32_t k) const
+    {
+        Routed<P> r = {p[k], extra[k], made[k], parent[k], anno[k], port[k], len[k], aux[k], mem[k], pass[k] != 0};
+        return r;
+    }
+};
+
+// Deliver results [i, j) of chunk c -- all of one member -- through class
+// `cls` (its finish() inlined here), pushing each result's packet with
+// push(port, p); with `ready` (pull context) output-0 packets go there.
+template <class P, class C, class S, class O, class Push>
+inline void deliver_run(C &cls, S &t, const Chunk<P> &c, uint32_t i, uint32_t j, std::vector<P *> *ready, Push &&push)
+{
+    for (uint32_t k = i; k < j; k++) {
+        if (k + 4 < j && c.p[k + 4])              // its bytes, 4 results ahead (route()
+            __builtin_prefetch(O::data(c.p[k + 4]));  // prefetched the packet itself)
+        Routed<P> r = c.at(k);
+        P *out = 0;
+        const int port = cls.finish(t, r, &out);
+        if (r.pass || port < 0 || !out)           // a pass: the member's side effects only
+            continue;
+        if (ready && port == 0)
+            ready->push_back(out);
+        else
+            push(port, out);
+    }
+}
 
 template <class P, class L> struct State {
     clk_ctx *ctx;
@@ -168,15 +228,20 @@ template <class P, class L> struct State {
     bool armed;                   // the latency deadline is set
     uint64_t deadline;            // now_ns() at which poll() flushes
     uint64_t push_errors;         // packets push() could not stage (chatter is rate-limited)
-    std::vector<Routed<P> > outbox;
-    std::vector<Routed<P> > spare;    // delivery storage kept between batches
+    Chunk<P> *chunk;              // the results being delivered (route() fills it)
+    Chunk<P> *side_chunk;         // the same for `side`
+    std::vector<Routed<P> > side; // results a stage leaves behind (IPOutputCombo's clone when the copy fails)
+    uint64_t xmask;               // bit m: member m's class has extra results (host extra_results)
     std::deque<P *> ready;        // pull context: output-0 packets ready to hand out
     P *last_primary;              // route(): the packet of the last primary result
     P *frag_parent;               // host use (IPFragmenter's first-fragment parent)
     L lock;
     State() : ctx(0), e(0), chain(0), id(0), base(0), next(0), counted(false), fails(0), draining(false),
               unrouted(false), routed_any(false), armed(false),
-              deadline(0), push_errors(0), last_primary(0), frag_parent(0) { }
+              deadline(0), push_errors(0), chunk(0), side_chunk(0), xmask(~uint64_t(0)), last_primary(0), frag_parent(0) { }
+    ~State() { delete chunk; delete side_chunk; }
+    State(const State &) = delete;
+    State &operator=(const State &) = delete;
 };
 
 template <class P, class Host, class L> class Core {
@@ -197,7 +262,7 @@ template <class P, class Host, class L> class Core {
         t.lock.acquire();
         stage(h, t, p, true);
         // most pushes only stage: deliver when there is something to
-        const bool deliver = (!t.outbox.empty() || t.unrouted) && !t.draining;
+        const bool deliver = (!t.side.empty() || t.unrouted) && !t.draining;
         t.lock.release();
         if (deliver)
             drain(h, t, false);
@@ -285,15 +350,10 @@ template <class P, class Host, class L> class Core {
                 h.kill(t.held[i].extra);
         }
         t.held.clear();
-        for (size_t i = 0; i < t.outbox.size(); i++) {
-            R &r = t.outbox[i];
-            if (r.pass)                  // the packet is still held (killed above)
-                continue;
-            if (r.p) h.kill(r.p);
-            if (r.extra) h.kill(r.extra);
-            if (r.made) h.kill(r.made);
-        }
-        t.outbox.clear();
+        for (size_t i = 0; i < t.side.size(); i++)
+            if (t.side[i].extra)
+                h.kill(t.side[i].extra);
+        t.side.clear();
         while (!t.ready.empty()) {
             h.kill(t.ready.front());
             t.ready.pop_front();
@@ -374,7 +434,7 @@ template <class P, class Host, class L> class Core {
                 memset(&r, 0, sizeof(r));
                 r.extra = extra;
                 r.port = CLK_PORT_OUT1;
-                t.outbox.push_back(r);
+                t.side.push_back(r);
             }
             return false;
         }
@@ -473,78 +533,78 @@ template <class P, class Host, class L> class Core {
         return t.chain ? clk_chain_last_error(t.chain) : clk_element_last_error(t.e);
     }
 
-    // Move up to one chunk of the glue's results into the outbox (locked):
-    // drain() delivers them before it takes the next, so the results stay in
-    // cache between here and their delivery.  Once the glue has none left:
-    // the end of the batch, the elements' chatter, and the runcount released
-    // if nothing is held.
+    // Take up to one chunk of the glue's results into t.chunk (locked): each
+    // result with the held packet it belongs to (moved out of the held ring
+    // unless it is a pass record: the packet goes on in the chain).  drain()
+    // delivers them before it takes the next, so the results stay in cache
+    // between here and their delivery.  Once the glue has none left: the end
+    // of the batch, the elements' chatter, and the runcount released if
+    // nothing is held.
     void route(Host &h, S &t)
     {
-        enum { CAP = 256 };
+        enum { CAP = Chunk<P>::CAP };
+        if (!t.chunk)
+            t.chunk = new Chunk<P>;
+        Chunk<P> &c = *t.chunk;
         uint64_t tok[CAP];
-        int32_t mem[CAP], port[CAP];
-        uint32_t len[CAP], aux[CAP];
         uint64_t n;
-        {
-            if (t.chain)
-                n = clk_chain_results(t.chain, tok, mem, port, len, aux, CAP);
-            else if ((n = clk_element_results_aux(t.e, tok, port, len, aux, CAP)) > 0)
-                memset(mem, 0, sizeof(int32_t) * (size_t) n);
-            if (n)
-                t.routed_any = true;
-            for (uint64_t i = 0; i < n; i++) {
-                t.outbox.emplace_back(); // built in place, zeroed (value-initialized)
-                R &r = t.outbox.back();
-                r.member = mem[i];
-                r.port = port[i];
-                r.len = len[i];
-                r.aux = aux[i];
-                const bool have = tok[i] >= t.base && tok[i] - t.base < t.held.size();
-                Held<P> *e = have ? &t.held[(size_t) (tok[i] - t.base)] : 0;
-                if (e)
-                    r.anno = e->anno;
-                if (port[i] == CLK_PORT_NEXT) {  // chains: on to the next member, still held
-                    r.pass = true;
-                    r.port = CLK_PORT_OUT0;
-                    r.p = e ? e->p : 0;
-                    t.last_primary = r.p;
-                } else if (h.primary(r.member, port[i], aux[i])) {
-                    if (e) {
-                        r.p = e->p;
-                        e->p = 0;
-                        if (port[i] == CLK_PORT_KILL && e->extra) {   // e.g. a broadcast: no clone either
-                            r.extra = e->extra;
-                            e->extra = 0;
-                        }
-                    }
-                    t.last_primary = r.p;
-                } else if (aux[i] == CLK_AUX_CLONE) {
-                    if (e) {
-                        r.extra = e->extra;
+        if (t.chain)
+            n = clk_chain_results(t.chain, tok, c.mem, c.port, c.len, c.aux, CAP);
+        else if ((n = clk_element_results_aux(t.e, tok, c.port, c.len, c.aux, CAP)) > 0)
+            memset(c.mem, 0, sizeof(int32_t) * (size_t) n);
+        c.n = (uint32_t) n;
+        c.end = false;
+        if (n)
+            t.routed_any = true;
+        const uint64_t base = t.base, nheld = t.held.size();
+        for (uint64_t i = 0; i < n; i++) {
+            const uint64_t k = tok[i] - base;
+            Held<P> *e = tok[i] >= base && k < nheld ? &t.held[(size_t) k] : 0;
+            const int32_t port = c.port[i], m = c.mem[i];
+            P *p = 0, *extra = 0, *made = 0, *parent = 0;
+            uint8_t pass = 0;
+            if (port == CLK_PORT_NEXT) {         // chains: on to the next member, still held
+                pass = 1;
+                c.port[i] = CLK_PORT_OUT0;
+                p = e ? e->p : 0;
+                t.last_primary = p;
+            } else if (!(t.xmask >> (m & 63) & 1) || h.primary(m, port, c.aux[i])) {
+                if (e) {
+                    p = e->p;
+                    e->p = 0;
+                    if (port == CLK_PORT_KILL && e->extra) {   // e.g. a broadcast: no clone either
+                        extra = e->extra;
                         e->extra = 0;
                     }
-                } else {                 // a new packet made by the element
-                    r.made = h.make_packet(r.member, t.chain ? t.mem[(size_t) r.member] : t.e, aux[i]);
-                    r.parent = t.last_primary;
                 }
-                if (r.p)                 // finish() reads it soon: the packet staged long ago is
-                    __builtin_prefetch(r.p);     // out of the cache by now
+                t.last_primary = p;
+            } else if (c.aux[i] == CLK_AUX_CLONE) {
+                if (e) {
+                    extra = e->extra;
+                    e->extra = 0;
+                }
+            } else {                             // a new packet made by the element
+                made = h.make_packet(m, t.chain ? t.mem[(size_t) m] : t.e, c.aux[i]);
+                parent = t.last_primary;
             }
-            while (!t.held.empty() && !t.held.front().p && !t.held.front().extra) {
-                t.held.pop_front();
-                t.base++;
-            }
+            c.p[i] = p;
+            c.extra[i] = extra;
+            c.made[i] = made;
+            c.parent[i] = parent;
+            c.anno[i] = e ? e->anno : 0;
+            c.pass[i] = pass;
+            if (p)                               // finish() reads it soon: the packet staged long ago is
+                __builtin_prefetch(p);           // out of the cache by now
+        }
+        while (!t.held.empty() && !t.held.front().p && !t.held.front().extra) {
+            t.held.pop_front();
+            t.base++;
         }
         if (n == CAP)
-            return;                      // more to come
+            return;                              // more to come
         t.unrouted = false;
-        if (t.routed_any) {
-            t.routed_any = false;
-            R end;
-            memset(&end, 0, sizeof(end));
-            end.end = true;
-            t.outbox.push_back(end);
-        }
+        c.end = t.routed_any;
+        t.routed_any = false;
         release_if_idle(h, t);
         // the elements' click_chatter lines (e.g. the first drop's reason)
         char buf[8192];
@@ -560,9 +620,10 @@ template <class P, class Host, class L> class Core {
                 }
     }
 
-    // Deliver the outbox in order, without the lock.  Re-entrant calls on
-    // the same state (a downstream element pushing back into this one) only
-    // append: the running loop delivers their results after these.
+    // Deliver the results in order, without the lock: each chunk in runs of
+    // one member (one host call per run).  Re-entrant calls on the same state
+    // (a downstream element pushing back into this one) only stage: the
+    // running loop delivers their results after these.
     void drain(Host &h, S &t, bool pull_ctx)
     {
         std::vector<P *> ready;                 // pull context: output-0 packets, queued under one lock
@@ -572,44 +633,51 @@ template <class P, class Host, class L> class Core {
             return;
         }
         t.draining = true;
-        std::vector<R> work;
-        work.swap(t.spare);                     // a delivered outbox's storage, reused
+        const int last = (int) (t.chain ? t.mem.size() : 1) - 1;
         for (;;) {
-            if (t.outbox.empty() && t.unrouted && t.e)
-                route(h, t);
-            if (t.outbox.empty())
-                break;
-            work.swap(t.outbox);
-            t.lock.release();
-            for (size_t i = 0; i < work.size(); i++) {
-                R &r = work[i];
-                if (i + 8 < work.size() && work[i + 8].p)   // its bytes, 8 results ahead
-                    __builtin_prefetch(h.data(work[i + 8].p));
-                if (r.end) {
-                    const size_t nm = t.chain ? t.mem.size() : 1;
-                    for (size_t m = 0; m < nm; m++)
-                        h.end_of_batch((int) m, t);
-                    continue;
-                }
-                P *out = 0;
-                int port = h.finish(r.member, t, r, &out);
-                if (r.pass || port < 0 || !out)  // a pass: the member's side effects only
-                    continue;
-                if (pull_ctx && port == 0 && r.member + 1 == (int) (t.chain ? t.mem.size() : 1))
-                    ready.push_back(out);
-                else
-                    h.output_push(r.member, port, out);
+            if (!t.side.empty()) {               // results a stage left behind, as they stand
+                if (!t.side_chunk)
+                    t.side_chunk = new Chunk<P>;
+                Chunk<P> &c = *t.side_chunk;
+                c.n = 0;
+                for (size_t i = 0; i < t.side.size() && c.n < (uint32_t) Chunk<P>::CAP; i++)
+                    c.put(c.n++, t.side[i]);
+                t.side.erase(t.side.begin(), t.side.begin() + c.n);
+                t.lock.release();
+                deliver_chunk(h, t, c, 0, pull_ctx, last, ready);
+                t.lock.acquire();
+                continue;
             }
-            work.clear();
+            if (!t.unrouted || !t.e)
+                break;
+            route(h, t);
+            Chunk<P> &c = *t.chunk;
+            t.lock.release();
+            deliver_chunk(h, t, c, c.end, pull_ctx, last, ready);
             t.lock.acquire();
-            if (t.outbox.empty())
-                t.outbox.swap(work);             // the next chunk goes into this storage
-            t.ready.insert(t.ready.end(), ready.begin(), ready.end());
-            ready.clear();
+            if (!ready.empty()) {
+                t.ready.insert(t.ready.end(), ready.begin(), ready.end());
+                ready.clear();
+            }
         }
-        t.spare.swap(work);
         t.draining = false;
         t.lock.release();
+    }
+
+    // (unlocked) chunk c in runs of one member, then the end of the batch
+    void deliver_chunk(Host &h, S &t, Chunk<P> &c, bool end, bool pull_ctx, int last, std::vector<P *> &ready)
+    {
+        for (uint32_t i = 0, j; i < c.n; i = j) {
+            const int32_t m = c.mem[i];
+            for (j = i + 1; j < c.n && c.mem[j] == m; j++)
+                ;
+            h.deliver(m, t, c, i, j, pull_ctx && m == last ? &ready : 0);
+        }
+        c.n = 0;
+        c.end = false;
+        if (end)
+            for (int m = 0; m <= last; m++)
+                h.end_of_batch(m, t);
     }
 
     uint32_t _batch;

@@ -16,6 +16,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <deque>
 #include <functional>
@@ -45,6 +46,8 @@ struct TPacket {
     long nh = -1;                    // absolute offset of the network header in buf
     bool cloned = false;             // a clone of it was made, or it is one: uniqueify() asks the
                                      // buffer's count (Click keeps that count in the Packet itself)
+    bool ring = false;               // owned by a measurement's receive ring (raw points into it;
+                                     // kill() hands it back, the ring reuses it)
     TAnno a;
 };
 
@@ -52,17 +55,39 @@ std::atomic<long> g_live{0};
 std::atomic<long> g_kills{0};        // packets killed (by the core or a class)
 std::atomic<int> g_uniq_fail{0};     // the n-th uniqueify() that must copy fails
 
+// A recycling packet pool, as Click's (packet.cc: a killed packet whose
+// buffer is not shared goes back to the thread's pool and Packet::make
+// takes it from there).  Off unless a measurement turns it on (one thread).
+struct TPool {
+    bool on = false;                 // (one thread only: no atomic counts then)
+    std::vector<TPacket *> free;
+    long made = 0, killed = 0;
+};
+TPool g_pool;
+
 TPacket *make(const uint8_t *bytes, size_t len, long id, size_t headroom = 0)
 {
-    TPacket *p = new TPacket;
-    p->buf = std::make_shared<std::vector<uint8_t> >(headroom + len);
+    TPacket *p;
+    if (g_pool.on && !g_pool.free.empty() && g_pool.free.back()->buf->size() >= headroom + len) {
+        p = g_pool.free.back();
+        g_pool.free.pop_back();
+        p->a = TAnno();
+        p->nh = -1;
+        p->cloned = false;
+    } else {
+        p = new TPacket;
+        p->buf = std::make_shared<std::vector<uint8_t> >(std::max<size_t>(headroom + len, g_pool.on ? 2048 : 0));
+    }
     p->raw = p->buf->data();
     if (len && bytes)
         std::memcpy(p->raw + headroom, bytes, len);
     p->off = headroom;
     p->len = len;
     p->a.id = id;
-    g_live++;
+    if (g_pool.on)
+        g_pool.made++;
+    else
+        g_live++;
     return p;
 }
 
@@ -87,13 +112,28 @@ struct TOps {
     {
         p->cloned = true;
         TPacket *q = new TPacket(*p);
-        g_live++;
+        if (g_pool.on)
+            g_pool.made++;
+        else
+            g_live++;
         return q;
     }
     static void kill(TPacket *p)
     {
-        g_kills++;
-        g_live--;
+        if (p->ring) {
+            g_pool.killed++;
+            return;
+        }
+        if (g_pool.on) {
+            g_pool.killed++;
+            if (p->buf.use_count() == 1) {
+                g_pool.free.push_back(p);
+                return;
+            }
+        } else {
+            g_kills++;
+            g_live--;
+        }
         delete p;
     }
     static uint8_t *data(TPacket *p) { return p->raw + p->off; }
@@ -159,6 +199,7 @@ class Host {
     {
         for (int k = 0; k < nstates; k++) {
             st[k].id = k;
+            st[k].xmask = C::extra_results ? 1 : 0;
             if (clk_ctx_create(0, &st[k].ctx) != CLK_SUCCESS ||
                 clk_element_create(st[k].ctx, glue_class, conf.c_str(), glue_class, noutputs, &st[k].e) !=
                     CLK_SUCCESS) {
@@ -184,11 +225,16 @@ class Host {
     int32_t nh_offset(TPacket *p) { return cls.nh_offset(p); }
     bool primary(int, int32_t port, uint32_t aux) { return cls.primary(port, aux); }
     TPacket *make_packet(int, clk_element *e, uint32_t key) { return cls.make_packet(e, key); }
-    int finish(int, St &t, hipcore::Routed<TPacket> &r, TPacket **o) { return cls.finish(t, r, o); }
+    bool extra_results(int) const { return C::extra_results != 0; }
+    void deliver(int, St &t, const hipcore::Chunk<TPacket> &c, uint32_t i, uint32_t j, std::vector<TPacket *> *ready)
+    {
+        hipcore::deliver_run<TPacket, C, St, TOps>(cls, t, c, i, j, ready,
+                                                   [this](int port, TPacket *p) { output_push(port, p); });
+    }
     void end_of_batch(int, St &t) { cls.end_of_batch(t); }
     uint8_t *data(TPacket *p) { return TOps::data(p); }
     uint32_t length(TPacket *p) { return TOps::length(p); }
-    void output_push(int, int port, TPacket *p)
+    void output_push(int port, TPacket *p)
     {
         if (port == 0 && downstream) {                  // output 0 connected to another element
             downstream(p);
@@ -268,9 +314,12 @@ struct MemberBase {
     virtual int32_t nh_offset(TPacket *p) = 0;
     virtual bool primary(int32_t port, uint32_t aux) = 0;
     virtual TPacket *make_packet(clk_element *e, uint32_t key) = 0;
-    virtual int finish(St &t, hipcore::Routed<TPacket> &r, TPacket **o) = 0;
+    virtual void deliver(St &t, const hipcore::Chunk<TPacket> &c, uint32_t i, uint32_t j,
+                         std::vector<TPacket *> *ready) = 0;
     virtual void end_of_batch(St &t) = 0;
     virtual bool may_write() const = 0;
+    virtual bool extra_results() const = 0;
+    std::function<void(int, TPacket *)> push;           // the member's outputs (ChainHost sets it)
     virtual bool pass_effects() const = 0;
 };
 
@@ -281,9 +330,14 @@ template <class C> struct Member : MemberBase {
     int32_t nh_offset(TPacket *p) override { return cls.nh_offset(p); }
     bool primary(int32_t port, uint32_t aux) override { return cls.primary(port, aux); }
     TPacket *make_packet(clk_element *e, uint32_t key) override { return cls.make_packet(e, key); }
-    int finish(St &t, hipcore::Routed<TPacket> &r, TPacket **o) override { return cls.finish(t, r, o); }
+    void deliver(St &t, const hipcore::Chunk<TPacket> &c, uint32_t i, uint32_t j,
+                 std::vector<TPacket *> *ready) override
+    {
+        hipcore::deliver_run<TPacket, C, St, TOps>(cls, t, c, i, j, ready, push);
+    }
     void end_of_batch(St &t) override { cls.end_of_batch(t); }
     bool may_write() const override { return C::may_write != 0; }
+    bool extra_results() const override { return C::extra_results != 0; }
     bool pass_effects() const override { return C::pass_effects != 0; }
 };
 
@@ -318,6 +372,12 @@ class ChainHost {
             st.mem.push_back(e);
         }
         st.e = st.mem[0];
+        st.xmask = 0;
+        for (size_t k = 0; k < m.size(); k++) {
+            if (m[k]->extra_results())
+                st.xmask |= uint64_t(1) << (k & 63);
+            m[k]->push = [this, k](int port, TPacket *p) { output_push((int)k, port, p); };
+        }
         if (clk_chain_create(st.mem.data(), (int)st.mem.size(), &st.chain) != CLK_SUCCESS) {
             std::fprintf(stderr, "chain: %s\n", clk_last_error(0));
             std::exit(3);
@@ -347,11 +407,21 @@ class ChainHost {
     int32_t nh_offset(TPacket *p) { return m[0]->nh_offset(p); }
     bool primary(int k, int32_t port, uint32_t aux) { return m[(size_t)k]->primary(port, aux); }
     TPacket *make_packet(int k, clk_element *e, uint32_t key) { return m[(size_t)k]->make_packet(e, key); }
-    int finish(int k, St &t, hipcore::Routed<TPacket> &r, TPacket **o) { return m[(size_t)k]->finish(t, r, o); }
+    void deliver(int k, St &t, const hipcore::Chunk<TPacket> &c, uint32_t i, uint32_t j, std::vector<TPacket *> *ready)
+    {
+        m[(size_t)k]->deliver(t, c, i, j, ready);
+    }
     void end_of_batch(int k, St &t) { m[(size_t)k]->end_of_batch(t); }
     uint8_t *data(TPacket *p) { return TOps::data(p); }
     uint32_t length(TPacket *p) { return TOps::length(p); }
-    void output_push(int k, int port, TPacket *p) { m[(size_t)k]->out[(size_t)port].push_back(p); }
+    std::function<void(int, int, TPacket *)> sink;      // set: every output goes there (a Discard)
+    void output_push(int k, int port, TPacket *p)
+    {
+        if (sink)
+            sink(k, port, p);
+        else
+            m[(size_t)k]->out[(size_t)port].push_back(p);
+    }
     TPacket *input_pull() { return nullptr; }
     void kill(TPacket *p) { TOps::kill(p); }
     void adjust_runcount(int d) { runcount += d; }

@@ -114,8 +114,12 @@ void leg(const char *name, const char *ga, const char *gb, uint32_t L, int n, ui
 // CheckIPHeader OFFSET 14 -> IPGWOptions -> FixIPSrc -> DecIPTTL ->
 // IPFragmenter), through the adapter core: five elements, each output 0
 // pushing into the next, or one chain (hipcore chains, as the Click adapter
-// forms it).  The frames are made before the clock starts; all are pushed,
-// then the latency timer's flush runs.
+// forms it).  Two sources: the frames all made before the clock starts (each
+// push then meets a packet out of the host caches), or -- as fake-iprouter's
+// InfiniteSource does, pushing a clone of its packet that the first writer
+// uniqueifies (infinitesource.cc:125-153) -- each frame made from a packet
+// pool (Click's, packet.cc) as it is pushed, Discard after the last element;
+// all are pushed, then the latency timer's flush runs.
 std::vector<uint8_t> c1_frame()
 {
     std::vector<uint8_t> f(14, 0);
@@ -125,8 +129,9 @@ std::vector<uint8_t> c1_frame()
     return f;
 }
 
-void push_c1(int n, bool chained, uint32_t batch)
+void push_c1(int n, bool chained, uint32_t batch, bool source = false)
 {
+    g_pool.on = source;
     const std::string B = "BATCH " + std::to_string(batch);
     const std::vector<uint8_t> f = c1_frame();
     std::vector<TPacket *> in((size_t)n);
@@ -145,14 +150,26 @@ void push_c1(int n, bool chained, uint32_t batch)
         Member<FragC> c4("IPFragmenter", "1500, " + B, 2);
         c4.cls.mtu = 1500;
         ChainHost ch({&c0, &c1, &c2, &c3, &c4});
+        size_t fwd = 0;
+        if (source)                                     // Discard after the chain
+            ch.sink = [&fwd](int k, int port, TPacket *p) {
+                fwd += k == 4 && port == 0;
+                TOps::kill(p);
+            };
         for (int run = 0; run < 2; run++) {            // the first run warms up
-            fill();
+            if (!source)
+                fill();
             const auto t0 = std::chrono::steady_clock::now();
-            for (TPacket *p : in)
-                ch.push(p);
+            if (source)                                 // packets made as they are pushed
+                for (int i = 0; i < n; i++)
+                    ch.push(make(f.data(), f.size(), i));
+            else
+                for (TPacket *p : in)
+                    ch.push(p);
             ch.timer();
             sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            out0 = c4.out[0].size();
+            out0 = source ? fwd : c4.out[0].size();
+            fwd = 0;
             for (auto *m : ch.m)
                 for (auto &v : m->out) {
                     for (TPacket *p : v)
@@ -172,18 +189,30 @@ void push_c1(int n, bool chained, uint32_t batch)
         h1.downstream = [&](TPacket *p) { h2.push(p); };
         h2.downstream = [&](TPacket *p) { h3.push(p); };
         h3.downstream = [&](TPacket *p) { h4.push(p); };
+        size_t fwd = 0;
+        if (source)                                     // Discard after the last element
+            h4.downstream = [&fwd](TPacket *p) {
+                fwd++;
+                TOps::kill(p);
+            };
         for (int run = 0; run < 2; run++) {
-            fill();
+            if (!source)
+                fill();
             const auto t0 = std::chrono::steady_clock::now();
-            for (TPacket *p : in)
-                h0.push(p);
+            if (source)                                 // packets made as they are pushed
+                for (int i = 0; i < n; i++)
+                    h0.push(make(f.data(), f.size(), i));
+            else
+                for (TPacket *p : in)
+                    h0.push(p);
             h0.timer();
             h1.timer();
             h2.timer();
             h3.timer();
             h4.timer();
             sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-            out0 = h4.out[0].size();
+            out0 = source ? fwd : h4.out[0].size();
+            fwd = 0;
             for (auto *h : std::initializer_list<std::vector<std::vector<TPacket *> > *>{&h0.out, &h1.out, &h2.out,
                                                                                          &h3.out, &h4.out})
                 for (auto &v : *h) {
@@ -193,11 +222,79 @@ void push_c1(int n, bool chained, uint32_t batch)
                 }
         }
     }
-    std::printf("{\"leg\": \"push_c1_%s\", \"graph\": \"CheckIPHeader(14) -> IPGWOptions -> FixIPSrc -> DecIPTTL -> "
+    g_pool.on = false;
+    std::printf("{\"leg\": \"push_c1_%s%s\", \"graph\": \"CheckIPHeader(14) -> IPGWOptions -> FixIPSrc -> DecIPTTL -> "
                 "IPFragmenter(1500), %s\", \"batch\": %u, \"bytes\": %zu, \"packets\": %d, \"forwarded\": %zu, "
                 "\"seconds\": %.4f, \"mpps\": %.2f}\n",
-                chained ? "chain" : "elements", chained ? "one chain" : "five elements", batch, f.size(), n, out0, sec,
+                chained ? "chain" : "elements", source ? "_source" : "", chained ? "one chain" : "five elements", batch, f.size(), n, out0, sec,
                 (double)n / sec / 1e6);
+    std::fflush(stdout);
+}
+
+// Push context, C3: CheckUDPHeader alone (1500 B packets), each packet
+// pushed through the core as Click pushes it (one push per packet from the
+// source, Discard after the element), staged (the glue gathers every packet
+// into pinned staging) or ZEROCOPY (the kernel reads the packet where it
+// lies, in host memory registered with clk_host_register).  The packets
+// come from a receive ring of RING 1536 B buffers (384 MiB: past the host's
+// last-level cache, so a packet is not cache-resident when it is pushed,
+// as NIC-written memory is not), the bytes written once; the source hands
+// out the next one with its metadata reset, as FromDPDKDevice wraps the
+// mbufs of its ring (fromdpdkdevice.cc:98-115).
+void push_c3(int n, bool zerocopy, uint32_t batch)
+{
+    enum { RING = 262144, SLOT = 1536, L = 1500 };
+    uint8_t *arena = (uint8_t *)std::aligned_alloc(4096, (size_t)RING * SLOT);
+    const std::vector<uint8_t> x = udp_packet(L);
+    for (size_t k = 0; k < RING; k++)
+        std::memcpy(arena + k * SLOT, x.data(), L);
+    std::vector<TPacket> ring(RING);
+    for (size_t k = 0; k < RING; k++) {
+        ring[k].raw = arena + k * SLOT;
+        ring[k].ring = true;
+    }
+    clk_ctx *rctx = nullptr;
+    void *dbase = nullptr;
+    if (zerocopy && (clk_ctx_create(0, &rctx) != CLK_SUCCESS ||
+                     clk_host_register(rctx, arena, (size_t)RING * SLOT, &dbase) != CLK_SUCCESS)) {
+        std::printf("{\"leg\": \"push_c3_zerocopy\", \"error\": \"clk_host_register failed\"}\n");
+        std::free(arena);
+        return;
+    }
+    const std::string conf = "BATCH " + std::to_string(batch) + (zerocopy ? ", ZEROCOPY true" : "");
+    double sec = 0;
+    size_t fwd = 0;
+    {
+        Host<PlainC> h("CheckUDPHeader", conf, 2);
+        h.downstream = [&fwd](TPacket *p) {           // Discard
+            fwd++;
+            TOps::kill(p);
+        };
+        size_t next = 0;
+        for (int run = 0; run < 2; run++) {            // the first run warms up
+            fwd = 0;
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < n; i++) {
+                TPacket *p = &ring[next];
+                next = next + 1 == RING ? 0 : next + 1;
+                p->off = 0, p->len = L, p->nh = 0;     // as received: the IP header at data()
+                p->a.id = i;
+                h.push(p);
+            }
+            h.timer();
+            sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        }
+    }
+    if (rctx) {
+        clk_host_unregister(rctx, arena);
+        clk_ctx_destroy(rctx);
+    }
+    std::free(arena);
+    std::printf("{\"leg\": \"push_c3_%s\", \"graph\": \"source -> CheckUDPHeader -> Discard\", \"batch\": %u, "
+                "\"bytes\": %d, \"packets\": %d, \"forwarded\": %zu, \"seconds\": %.4f, \"mpps\": %.2f, "
+                "\"gib_s\": %.2f}\n",
+                zerocopy ? "zerocopy" : "staged", batch, (int)L, n, fwd, sec, (double)n / sec / 1e6,
+                (double)n * L / sec / (1u << 30));
     std::fflush(stdout);
 }
 
@@ -210,17 +307,26 @@ int main(int argc, char **argv)
         return 0;
     }
     const int scale = argc > 1 ? std::max(1, std::atoi(argv[1])) : 1;
-    if (argc > 3 && std::string(argv[2]) == "chain") {   // profiling (tools/core_profile): the chain leg only
+    if (argc > 3 && (std::string(argv[2]) == "chain" || std::string(argv[2]) == "chain_source")) {
+        // profiling (tools/core_profile): the chain leg only
         for (int r = std::atoi(argv[3]); r > 0; r--)
-            push_c1(600000 / scale, true, ADAPTER_BATCH);
+            push_c1(600000 / scale, true, ADAPTER_BATCH, std::string(argv[2]) == "chain_source");
         return 0;
     }
+    if (argc > 2 && std::string(argv[2]) == "c3") {     // the C3 push legs only
+        for (bool zc : {false, true})
+            push_c3(2000000 / scale, zc, ADAPTER_BATCH);
+        return 0;
+    }
+    for (bool zc : {false, true})
+        push_c3(2000000 / scale, zc, ADAPTER_BATCH);
     // BATCH bounds the longest pull (one refill stages a batch and routes
     // the one before): the default and a small one
-    for (uint32_t batch : {65536u, 8192u}) {
-        push_c1(600000 / scale, false, batch);
-        push_c1(600000 / scale, true, batch);
-    }
+    for (uint32_t batch : {65536u, 8192u})
+        for (bool source : {false, true}) {
+            push_c1(600000 / scale, false, batch, source);
+            push_c1(600000 / scale, true, batch, source);
+        }
     for (uint32_t batch : {65536u, 4096u}) {
         leg<CheckIPC, SetC>("pull_c2", "CheckIPHeader", "SetIPChecksum", 64, 2000000 / scale, batch);
         leg<PlainC, SetC>("pull_c3", "CheckUDPHeader", "SetUDPChecksum", 1500, 1000000 / scale, batch);

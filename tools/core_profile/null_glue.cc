@@ -33,6 +33,8 @@ int clk_device_count(void) { return 1; }
 int clk_ctx_create(int device, clk_ctx **out) { *out = new clk_ctx{device}; return CLK_SUCCESS; }
 int clk_ctx_destroy(clk_ctx *c) { delete c; return CLK_SUCCESS; }
 const char *clk_last_error(clk_ctx *) { return "null glue"; }
+int clk_host_register(clk_ctx *, void *host, size_t, void **dev_base) { *dev_base = host; return CLK_SUCCESS; }
+int clk_host_unregister(clk_ctx *, void *) { return CLK_SUCCESS; }
 
 int clk_element_create(clk_ctx *, const char *, const char *config, const char *, int, clk_element **out)
 {
