@@ -436,24 +436,39 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
             "note": "kernel time (one plan + look-back + write launch, after a small memset); first-fragment headers restored between steps"}
 
 
-def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5):
-    """Measured HBM read-stream ceiling (16 B loads, grid-stride)."""
+READ_SHAPES = {0: "gs8_nt_8k", 1: "gs4_nt_8k", 2: "gs16_nt_2k", 3: "wave8_nt_4k"}
+
+
+def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5, launches=10, detail=None):
+    """Measured HBM read-stream ceiling: clk_read_stream in the four best
+    shapes of tools/probes/read_probe.hip (CLK_TUNE_READ_SHAPE: nontemporal
+    16 B loads, grid-stride with 4 / 8 / 16 in flight per lane on a capped
+    grid, or wave-contiguous runs), each `launches` back to back, best of
+    `reps`; the best shape's GB/s (`detail`: every shape's)."""
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     buf.fill_(1)
     out = torch.zeros(1, dtype=torch.int64, device="cuda")
-    ctx.read_stream(buf, out=out)
-    torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    best = 1e30
-    for _ in range(reps):
-        s.record()
+    rates = {}
+    for shape, name in READ_SHAPES.items():
+        ctx.tune(read_shape=shape)
         ctx.read_stream(buf, out=out)
-        e.record()
         torch.cuda.synchronize()
-        best = min(best, s.elapsed_time(e))
+        best = 1e30
+        for _ in range(reps):
+            s.record()
+            for _ in range(launches):
+                ctx.read_stream(buf, out=out)
+            e.record()
+            torch.cuda.synchronize()
+            best = min(best, s.elapsed_time(e) / launches)
+        rates[name] = round(nbytes / (best * 1e-3) / 1e9, 1)
+    ctx.tune(read_shape=0)
     del buf
     torch.cuda.empty_cache()
-    return nbytes / (best * 1e-3) / 1e9
+    if detail is not None:
+        detail.update(rates)
+    return max(rates.values())
 
 
 def host_topology():
@@ -517,7 +532,7 @@ CPU_LEGS = {"c2": ("CheckIPHeader", 20), "c3": ("CheckUDPHeader", 1500), "c4": (
             "c5": ("CheckTCPHeader", 9000)}
 
 
-def cpu_baseline(legs=("c2", "c3", "c4", "c5"), reps=5):
+def cpu_baseline(legs=("c2", "c3", "c4", "c5"), reps=5, single_only=False):
     """The oracle restatement of lib/in_cksum.c + the element (-O2 -g) on the
     host cores, per BASELINE.md §2: one thread, then one thread pinned per
     physical core (capped by the cgroup CPU quota; CLK_CPU_THREADS
@@ -553,7 +568,7 @@ def cpu_baseline(legs=("c2", "c3", "c4", "c5"), reps=5):
         element, ck = CPU_LEGS[wl]
         w = WORKLOADS[wl]
         res = {}
-        for label, t in (("single_thread", 1), ("all_cores", nthr)):
+        for label, t in (("single_thread", 1),) + ((("all_cores", nthr),) if not single_only else ()):
             cfg = Cfg()
             cfg.op, cfg.arg, cfg.proto, cfg.imix = ops[element], 1, w["proto"], 1 if wl == "c4" else 0
             cfg.fixed_len, cfg.stride = w["L"], w["stride"]
@@ -618,8 +633,7 @@ def summarize(r, steps, wname):
 
 
 def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24,
-        glue_pkts=int(os.environ.get("CLK_E2E_GLUE_PKTS", 1 << 21)),
-        glue_threads=int(os.environ.get("CLK_E2E_THREADS", 2))):
+        glue_pkts=int(os.environ.get("CLK_E2E_GLUE_PKTS", 1 << 21))):
     """End-to-end rates with the packets in HOST memory (DESIGN.md "E2E").
 
     (a) device C ABI over pinned SoA chunks: per chunk, hipMemcpyAsync H2D of
@@ -735,38 +749,6 @@ def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24,
         _, ports, _ = e.results()
         ok_d = int((ports == 0).sum())
         e.close()
-        # (e) as (d) from `glue_threads` host threads, one context (own
-        # stream) and one element per thread ("Threads"),
-        # each pushing a contiguous quarter of the packets
-        import threading
-        T = glue_threads
-        parts = np.array_split(np.arange(glue_pkts), T)
-        ctxs = [click_amd.Context(0, stream="own") for _ in range(T)]
-        els = [Element(c, element, ", ".join(x for x in (ELEMENT_CONF.get(element, ""),
-                                                          "BATCH 65536, ZEROCOPY true") if x), noutputs=2)
-               for c in ctxs]
-        ok_e = [0] * T
-
-        sl = [(zptrs[p_], lens[p_], nhs[p_], int(p_[0])) for p_ in parts]
-
-        def work(k):
-            els[k].push_burst(sl[k][0], sl[k][1], sl[k][2], first_token=sl[k][3])
-            els[k].flush()
-
-        for timed in (False, False, True):                # two warm-ups (both staging buffers of every element), then timed
-            ths = [threading.Thread(target=work, args=(k,)) for k in range(T)]
-            t0 = time.perf_counter()
-            for t in ths:
-                t.start()
-            for t in ths:
-                t.join()
-            dt_e = time.perf_counter() - t0
-            for k in range(T):                            # results are read outside the timed region, as in (d)
-                _, pts, _ = els[k].results()
-                ok_e[k] = int((pts == 0).sum())
-        for el, c in zip(els, ctxs):
-            el.close()
-            c.close()
     finally:
         ctx.host_unregister(hostnp)
     return {
@@ -782,10 +764,6 @@ def e2e(torch, ctx, wname, element, chunk_pkts=1 << 18, nchunks=24,
         "element_glue_zero_copy": {"value": round(glue_pkts * L / dt_d / GIB, 3), "unit": "GiB/s",
                                    "mpps": round(glue_pkts / dt_d / 1e6, 3), "packets": glue_pkts, "ok": ok_d,
                                    "note": "C++ push() per packet records the packet's offset in the registered region (no gather), 64K-packet batches double-buffered, 1 host thread"},
-        "element_glue_zero_copy_threads": {"value": round(glue_pkts * L / dt_e / GIB, 3), "unit": "GiB/s",
-                                           "mpps": round(glue_pkts / dt_e / 1e6, 3), "packets": glue_pkts,
-                                           "threads": glue_threads, "ok": sum(ok_e),
-                                           "note": "as element_glue_zero_copy from %d host threads, one context (own stream) and element per thread" % glue_threads},
         "element_glue": {"value": round(glue_pkts * L / dt_b / GIB, 3), "unit": "GiB/s",
                          "mpps": round(glue_pkts / dt_b / 1e6, 3), "packets": glue_pkts, "ok": ok_b,
                          "gpu_ms": round(gpu_ns / 1e6, 3), "wall_ms": round(dt_b * 1e3, 3),
@@ -806,6 +784,22 @@ C1_CHAINS = {
     "combos": [("IPInputCombo", "2, INTERFACES 18.26.4.1/24 18.26.7.1/24", 1),
                ("IPOutputCombo", "1, 18.26.4.24, 300", 5)],
 }
+
+
+def glue_thread_legs(timeout=300):
+    """The element glue from 1, 2 and 4 host threads on one GPU
+    (tests/native/mt_glue: click -j N's RouterThreads, each pinned to its own
+    physical core with its own glue element and context; C2 64 B packets,
+    ZEROCOPY, BATCH 65536).  A native program, as Click's threads are: from
+    Python threads the legs met the process's other (torch) threads in the
+    cgroup's CPU quota.  None if the program was not built."""
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "native", "bin", "mt_glue")
+    if not os.path.exists(exe):
+        return None
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=timeout)
+    if r.returncode:
+        return {"error": (r.stderr or r.stdout)[-400:]}
+    return [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
 
 
 def pull_legs(scale=1, timeout=300):
@@ -1171,8 +1165,20 @@ def main():
         w = WORKLOADS[args.workload]
         res = [e2e(torch, ctx, args.workload, el) for el in w["elements"]]
         pull = pull_legs() if rank == 0 else None
+        threads = glue_thread_legs() if rank == 0 else None
         if rank == 0:
-            print(json.dumps({"e2e": res, "pull": pull}), flush=True)
+            out = {"e2e": res, "pull": pull, "glue_threads": threads}
+            # the push legs through the adapter core beside the same run's
+            # one-thread CPU CheckUDPHeader (oracle, 1500 B, DRAM-resident)
+            try:
+                cpu1 = cpu_baseline(legs=("c3",), single_only=True)["legs"]["c3"]["single_thread"]
+                legs = {x["leg"]: x for x in pull if isinstance(x, dict) and "leg" in x} if isinstance(pull, list) else {}
+                out["core_vs_cpu_c3"] = {"cpu_one_thread_mpps": cpu1.get("mpps"),
+                                         **{k: {"mpps": legs[k]["mpps"], "x_cpu": round(legs[k]["mpps"] / cpu1["mpps"], 2)}
+                                            for k in ("push_c3_staged", "push_c3_zerocopy") if k in legs}}
+            except Exception as e:        # reported, not fatal
+                out["core_vs_cpu_c3"] = {"error": repr(e)}
+            print(json.dumps(out), flush=True)
         ctx.close()
         return
     pk = args.packets or None
@@ -1192,7 +1198,8 @@ def main():
     if args.workload == "c3" and not args.no_frag:
         frag = measure_fragmenter(torch, ctx, dist, rank, world, args.steps, args.warmup, packets=pk,
                                   coll_dev=coll_dev)
-    peak_meas = None if args.no_peak else read_stream_peak(torch, ctx)
+    peak_shapes = {}
+    peak_meas = None if args.no_peak else read_stream_peak(torch, ctx, detail=peak_shapes)
     c1 = None
     if rank == 0 and world == 1 and not args.no_c1:
         c1 = config1(ctx)
@@ -1219,6 +1226,10 @@ def main():
         head = main_res[w["elements"][0]]
         hs = summarize(head, args.steps, args.workload)
         hs["roofline"]["read_stream_measured_GBs"] = round(peak_meas, 1) if peak_meas else None
+        hs["roofline"]["read_stream_shapes_GBs"] = peak_shapes or None
+        # frac is against the 8 TB/s spec; this one against the read ceiling
+        # measured in the same run (read_stream_kernel: the best probe shape)
+        hs["roofline"]["frac_of_measured_read"] = round(hs["roofline"]["achieved"] / peak_meas, 4) if peak_meas else None
         line = {
             "metric": METRIC, "value": hs["value"], "unit": "GiB/s", "mpps": hs["mpps"],
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,

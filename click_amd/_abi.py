@@ -35,7 +35,8 @@ CLK_TTL_UNCHANGED = 2
 CLK_GWOPT_OK = 0
 CLK_GWOPT_ERROR = 1
 # clk_tune_knob
-TUNE = {"max_blocks": 1, "scatter_blocks": 2, "set_mode": 3, "stream_min": 4, "group": 5, "set_chunks": 6}
+TUNE = {"max_blocks": 1, "scatter_blocks": 2, "set_mode": 3, "stream_min": 4, "group": 5, "set_chunks": 6,
+        "read_shape": 7}
 
 
 class clk_batch(ctypes.Structure):
@@ -175,6 +176,7 @@ SIGNATURES = {
     "clk_chain_create": (ctypes.c_int, [_P, ctypes.c_int, _P]),
     "clk_chain_destroy": (ctypes.c_int, [_P]),
     "clk_chain_last_error": (ctypes.c_char_p, [_P]),
+    "clk_chain_flush_async": (ctypes.c_int, [_P]),
     "clk_chain_push_anno": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64]),
     "clk_chain_push_burst": (ctypes.c_int, [_P, _P, _P, _P, ctypes.c_uint64, ctypes.c_uint32]),
     "clk_chain_flush": (ctypes.c_int, [_P]),

@@ -80,7 +80,7 @@ def build_examples(force=False):
     return out
 
 
-NATIVE_TESTS = ["hipcore_test", "pull_bench"]
+NATIVE_TESTS = ["hipcore_test", "pull_bench", "mt_glue"]
 NATIVE_ORACLE = {"hipcore_test"}          # the measurement programs never link the oracle
 
 

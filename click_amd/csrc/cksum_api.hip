@@ -28,6 +28,7 @@ struct clk_ctx {
                          // (C3 scatter 0.57 vs 0.67 ms at 16K vs 64K blocks)
     uint64_t stream_min; // len[] batches of >= stream_min packets run by the packet-stream kernel
     int set_chunks;      // two-phase Set: packet ranges whose scatter overlaps the next range's compute
+    int read_shape;      // clk_read_stream's load shape (CLK_TUNE_READ_SHAPE)
     hipStream_t side;    // the scatters' stream (created on first use)
     hipEvent_t ev_pass, ev_side;
     void *scratch;       // two-phase work array (grown on demand)
@@ -378,6 +379,7 @@ int clk_ctx_create(int device, clk_ctx **out)
     c->scratch_bytes = 0;
     c->set_mode = -1;
     c->set_chunks = 1;
+    c->read_shape = 0;
     c->side = nullptr;
     c->ev_pass = c->ev_side = nullptr;
     c->scatter_blocks = 16384;
@@ -465,6 +467,10 @@ int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value)
     case CLK_TUNE_SET_CHUNKS:
         if (value < 1 || value > 64) break;
         ctx->set_chunks = (int)value;
+        return CLK_SUCCESS;
+    case CLK_TUNE_READ_SHAPE:
+        if (value < 0 || value > 3) break;
+        ctx->read_shape = (int)value;
         return CLK_SUCCESS;
     case CLK_TUNE_GROUP:
         if (!(value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16 || value == 32 ||
@@ -874,8 +880,23 @@ int clk_read_stream(clk_ctx *ctx, const void *base, uint64_t bytes, uint64_t *ou
         return fail(ctx, CLK_EINVAL, "clk_read_stream: bad arguments");
     const uint64_t n16 = bytes / 16;
     if (n16 == 0) return CLK_SUCCESS;
-    hipLaunchKernelGGL(clk::read_stream_kernel, dim3(grid_for(ctx, n16 / 4 + 1)), dim3(BLOCK), 0, ctx->cur,
-                       (const clk::u32x4 *)base, n16, (unsigned long long *)out_sum);
+    // tools/probes/read_probe.hip's best shapes (CLK_TUNE_READ_SHAPE)
+    const clk::u32x4 *p = (const clk::u32x4 *)base;
+    unsigned long long *o = (unsigned long long *)out_sum;
+    auto grid = [&](uint64_t cap, uint64_t per) { return (unsigned)std::min<uint64_t>(cap, std::max<uint64_t>(1, n16 / per)); };
+    switch (ctx->read_shape) {
+    case 1:
+        hipLaunchKernelGGL(clk::read_stream_kernel<4>, dim3(grid(8192, 4 * BLOCK)), dim3(BLOCK), 0, ctx->cur, p, n16, o);
+        break;
+    case 2:
+        hipLaunchKernelGGL(clk::read_stream_kernel<16>, dim3(grid(2048, 16 * BLOCK)), dim3(BLOCK), 0, ctx->cur, p, n16, o);
+        break;
+    case 3:
+        hipLaunchKernelGGL(clk::read_wave_kernel<8>, dim3(grid(4096, 8 * BLOCK)), dim3(BLOCK), 0, ctx->cur, p, n16, o);
+        break;
+    default:
+        hipLaunchKernelGGL(clk::read_stream_kernel<8>, dim3(grid(8192, 8 * BLOCK)), dim3(BLOCK), 0, ctx->cur, p, n16, o);
+    }
     return check_launch(ctx, "clk_read_stream");
 }
 

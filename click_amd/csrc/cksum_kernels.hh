@@ -1868,19 +1868,57 @@ __global__ void __launch_bounds__(256) corrupt_kernel(BatchArgs b, uint64_t seed
     }
 }
 
+// The measured read ceiling (bench only): grid-stride, U nontemporal 16 B
+// loads per lane in flight, launched on a capped grid -- the best of the
+// twelve shapes of tools/probes/read_probe.hip (gs8_nt at 8K workgroups,
+// 7.01-7.07 TB/s; the uncapped gs4 grid read 6.5).
+template <int U>
 __global__ void __launch_bounds__(256) read_stream_kernel(const u32x4 *p, uint64_t n16, unsigned long long *out)
 {
     const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
     uint32_t acc = 0;
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * nthreads < n16; i += 4 * nthreads) {     // nontemporal, as the Check kernels' stream
-        const u32x4 a0 = __builtin_nontemporal_load(p + i), a1 = __builtin_nontemporal_load(p + i + nthreads),
-                    a2 = __builtin_nontemporal_load(p + i + 2 * nthreads),
-                    a3 = __builtin_nontemporal_load(p + i + 3 * nthreads);
-        acc += (a0[0] ^ a0[1] ^ a0[2] ^ a0[3]) + (a1[0] ^ a1[1] ^ a1[2] ^ a1[3])
-             + (a2[0] ^ a2[1] ^ a2[2] ^ a2[3]) + (a3[0] ^ a3[1] ^ a3[2] ^ a3[3]);
+    for (; i + (U - 1) * nthreads < n16; i += U * nthreads) {
+        u32x4 a[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            a[u] = __builtin_nontemporal_load(p + i + u * nthreads);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            acc += a[u][0] ^ a[u][1] ^ a[u][2] ^ a[u][3];
     }
     for (; i < n16; i += nthreads) {
+        const u32x4 a0 = p[i];
+        acc += a0[0] ^ a0[1] ^ a0[2] ^ a0[3];
+    }
+    for (int m = 32; m >= 1; m >>= 1)
+        acc += __shfl_xor(acc, m, 64);
+    if ((threadIdx.x & 63) == 0 && acc)
+        atomicAdd(out, (unsigned long long)acc);
+}
+
+// ... each wave reading U KiB contiguous per step (lane l: 16 B at l*16 +
+// u*1 KiB), the steps dealt round-robin to the waves; the tail grid-strided
+template <int U>
+__global__ void __launch_bounds__(256) read_wave_kernel(const u32x4 *p, uint64_t n16, unsigned long long *out)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    const uint64_t w0 = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const uint64_t nsteps = n16 / (64 * U);
+    uint32_t acc = 0;
+    for (uint64_t s = w0; s < nsteps; s += nwaves) {
+        const u32x4 *q = p + s * 64 * U + lane;
+        u32x4 a[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            a[u] = __builtin_nontemporal_load(q + 64 * u);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            acc += a[u][0] ^ a[u][1] ^ a[u][2] ^ a[u][3];
+    }
+    for (uint64_t i = nsteps * 64 * U + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+         i += (uint64_t)gridDim.x * blockDim.x) {
         const u32x4 a0 = p[i];
         acc += a0[0] ^ a0[1] ^ a0[2] ^ a0[3];
     }

@@ -232,6 +232,14 @@ class Chain:
             err.rc = rc
             raise err
 
+    def flush_async(self):
+        """Double-buffered flush (clk_chain_flush_async)."""
+        rc = self.lib.clk_chain_flush_async(self.h)
+        if rc != 0:
+            err = ClickAmdError("flush_async failed: %d (%s)" % (rc, self.last_error()))
+            err.rc = rc
+            raise err
+
     def abandon(self):
         """Kill every packet still in the chain (clk_chain_abandon); returns the count."""
         return int(self.lib.clk_chain_abandon(self.h))

@@ -5,15 +5,24 @@
 // combo elements so the per-element cost is paid once (ipinputcombo.cc:66-140,
 // ipoutputcombo.cc:44-205).  Here a chain of glue elements in one thread --
 // member k+1 connected to member k's output 0 -- shares one staged batch:
-//   push     each packet's bytes are gathered once (the most any member reads);
-//   flush    one H2D of the batch; every packet enters member 0 and goes on
-//            at once through the members that decide it on the host (span()
-//            false); member k's kernel then runs over the packets that reached
-//            it and wait for the GPU, and routing its verdicts sends each one
-//            on to member k+1 (the next kernel's descriptors) or out of the
-//            chain at member k -- each member's own route() (counters,
-//            handlers, chatter as if it had run alone), in push order per
-//            member; one D2H of the rewritten bytes at the end.
+//   push     each packet's bytes are gathered once (the most any member reads)
+//            and the packet reaches member 0;
+//   flush    one H2D of the batch; then member by member: the packets that
+//            reached it (in push order) get their descriptors (chain_prep:
+//            one loop with the class's span() inlined), its kernel runs over
+//            those that need the GPU, and one loop routes them all with the
+//            class's route() inlined (counters, handlers, chatter as if it
+//            had run alone) -- each one passed on reaches member k+1's list,
+//            the others leave the chain at member k; a pass rule lets a
+//            packet through a member that would change nothing without
+//            asking it; one D2H of the rewritten bytes at the end.
+// Two batches are in flight, as an element's stages are (double buffering):
+// flush_async() launches the staged batch's first GPU step, finishes the
+// batch before it (whose last GPU step ran while this one was pushed), then
+// routes this one's first step and launches its second -- so for chains of
+// up to two GPU steps (config 1: CheckIPHeader + DecIPTTL; the combos) every
+// kernel and copy runs while the host routes or stages the other batch.
+// Results are handed out batch by batch, once their bytes are back.
 // A member's GPU step that fails leaves the packets it had not routed in the
 // chain; the next flush builds its batch again and resumes there.
 #include "elements.hh"
@@ -60,6 +69,11 @@ void Chain::attach()
         e->chains_.push_back(this);
 }
 
+hipStream_t Chain::stream() const
+{
+    return (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
+}
+
 // A member element is destroyed while the chain lives (the caller's order,
 // or a garbage collector's): the chain lets go of every member and refuses
 // all further work; its own destructor then touches no member.
@@ -77,23 +91,14 @@ void Chain::member_gone(BatchElement *gone)
     err_ = "a member element was destroyed";
 }
 
-Chain::~Chain()
+void Chain::free_batch(Batch &B)
 {
-    if (!dead_) {
-        if (init_)
-            (void)clk_ctx_sync(m_[0]->ctx_);
-        for (BatchElement *e : m_) {
-            e->in_place_ = false, e->chain_ = false;
-            auto &v = e->chains_;
-            v.erase(std::remove(v.begin(), v.end(), this), v.end());
-        }
-    }
-    for (void *q : {(void *)h_arena_, (void *)h_back_})
+    for (void *q : {(void *)B.h_arena, (void *)B.h_back, (void *)B.h_snap})
         if (q)
             (void)hipHostFree(q);
-    if (d_arena_)
-        (void)hipFree(d_arena_);
-    for (Member &M : mm_) {
+    if (B.d_arena)
+        (void)hipFree(B.d_arena);
+    for (Member &M : B.mm) {
         for (void *q : {(void *)M.h_off, (void *)M.h_len, (void *)M.h_codes, (void *)M.h_anno, (void *)M.h_aux8,
                         (void *)M.h_sums})
             if (q)
@@ -106,6 +111,21 @@ Chain::~Chain()
             if (e)
                 (void)hipEventDestroy((hipEvent_t)e);
     }
+}
+
+Chain::~Chain()
+{
+    if (!dead_) {
+        if (init_)
+            (void)clk_ctx_sync(m_[0]->ctx_);
+        for (BatchElement *e : m_) {
+            e->in_place_ = false, e->chain_ = false;
+            auto &v = e->chains_;
+            v.erase(std::remove(v.begin(), v.end(), this), v.end());
+        }
+    }
+    for (Batch &B : b_)
+        free_batch(B);
 }
 
 int Chain::check(std::string *err) const
@@ -156,30 +176,23 @@ uint32_t Chain::extent(int32_t nh, uint32_t length)
     return ext_;
 }
 
-// A new batch: every member's work state reset, the per-packet arrays
-// reserved for BATCH packets (member 0's).
-int Chain::begin_batch()
+// Batch B starts taking packets: every member's work state reset, the
+// per-packet arrays sized for BATCH packets (member 0's).
+int Chain::begin_batch(Batch &B)
 {
     if (!init_) {
         init_ = true;
-        mm_.resize(m_.size());
+        for (Batch &X : b_)
+            X.mm.resize(m_.size());
     }
     const size_t cap = std::max<size_t>(m_[0]->batch_cap_, 1);
-    if (grow_members(cap, 0))
+    if (grow_members(B, cap, 0))
         return -1;
-    views_.clear();
-    done_.clear();
-    copied_.clear();
-    for (auto *v : {&views0_, &views_})
-        v->reserve(mcap_);
-    for (auto *v : {&staged_, &back_})
-        v->reserve(mcap_);
-    done_.reserve(mcap_);
-    copied_.reserve(mcap_);
+    size_packets(B, B.mcap);
     for (size_t k = 0; k < m_.size(); k++) {
-        setup(k);
-        mm_[k].w.reset();
-        mm_[k].rebuild = false;
+        setup(B, k);
+        B.mm[k].w.reset();
+        B.mm[k].rebuild = false;
         // the chain copies the members' rewritten bytes back, except a staged
         // member whose verdict carries its whole rewrite (DecIPTTL, the Set
         // elements: the new checksum): its route() writes those few bytes
@@ -187,59 +200,75 @@ int Chain::begin_batch()
         m_[k]->in_place_ = !host_writes(m_[k]);
         m_[k]->chain_ = true;
     }
-    h2d_done_ = false;
-    sent_ = 0;
-    sent_ok_ = true;
+    B.h2d_done = false;
+    B.sent = 0;
+    B.sent_ok = true;
+    B.at = 0;
+    B.waiting = false;
+    B.launched = false;
+    B.kill_rc = CLK_SUCCESS;
+    B.kill_why.clear();
+    B.out.clear();
+    B.pub = 0;
+    B.seq = ++seq_;
     return 0;
 }
 
 // Staged bytes go to the device while the batch fills (one async copy per
 // H2D_CHUNK), so the flush waits only for the tail.  A copy that fails is
 // sent again, whole, by the flush.
-int Chain::device_arena(size_t bytes)
+int Chain::device_arena(Batch &B, size_t bytes)
 {
-    if (d_cap_ >= bytes)
+    if (B.d_cap >= bytes)
         return 0;
-    hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
-    (void)hipStreamSynchronize(s);
-    if (d_arena_)
-        (void)hipFree(d_arena_);
-    d_arena_ = nullptr;
-    d_cap_ = 0;
-    sent_ = 0;                                       // what was sent is gone with the old arena
-    const size_t c = std::max(bytes, h_cap_);
-    if (hipMalloc(&d_arena_, c) != hipSuccess)
+    (void)hipStreamSynchronize(stream());
+    if (B.d_arena)
+        (void)hipFree(B.d_arena);
+    B.d_arena = nullptr;
+    B.d_cap = 0;
+    B.sent = 0;                                      // what was sent is gone with the old arena
+    const size_t c = std::max(bytes, B.h_cap);
+    if (hipMalloc(&B.d_arena, c) != hipSuccess)
         return -1;
-    d_cap_ = c;
+    B.d_cap = c;
     return 0;
 }
 
-void Chain::send_chunk()
+void Chain::send_chunk(Batch &B)
 {
-    if (!sent_ok_ || device_arena(used_ + 64))
+    if (!B.sent_ok || device_arena(B, B.used + 64))
         return;
-    hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
-    if (glue_checked(hipMemcpyAsync(d_arena_ + sent_, h_arena_ + sent_, used_ - sent_, hipMemcpyHostToDevice, s)) !=
-        hipSuccess)
-        sent_ok_ = false;
+    if (glue_checked(hipMemcpyAsync(B.d_arena + B.sent, B.h_arena + B.sent, B.used - B.sent, hipMemcpyHostToDevice,
+                                    stream())) != hipSuccess)
+        B.sent_ok = false;
     else
-        sent_ = used_;
+        B.sent = B.used;
+}
+
+// The per-packet arrays sized for c packets (kept between batches; a
+// packet's entries are written at push)
+void Chain::size_packets(Batch &B, size_t c)
+{
+    for (auto *v : {&B.views0, &B.views})
+        if (v->size() < c)
+            v->resize(c);
+    for (auto *v : {&B.staged, &B.back, &B.clone_key})
+        if (v->size() < c)
+            v->resize(c);
+    for (auto *v : {&B.done, &B.copied})
+        if (v->size() < c)
+            v->resize(c);
 }
 
 // The batch outgrew its arrays (a caller that pushes past a full batch)
-int Chain::grow_batch()
+int Chain::grow_batch(Batch &B)
 {
-    const size_t c = mcap_ * 2;
-    if (grow_members(c, 1))
+    const size_t c = B.mcap * 2;
+    if (grow_members(B, c, 1))
         return -1;
-    for (auto *v : {&views0_, &views_})
-        v->reserve(c);
-    for (auto *v : {&staged_, &back_})
-        v->reserve(c);
-    done_.reserve(c);
-    copied_.reserve(c);
+    size_packets(B, c);
     for (size_t k = 0; k < m_.size(); k++)
-        setup(k);                                    // the arrays moved
+        setup(B, k);                                 // the arrays moved
     return 0;
 }
 
@@ -248,9 +277,14 @@ int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t toke
     if (dead_)
         return CLK_EINVAL;
     if (failed_) {
-        err_ = "the chain's failed flush must be retried (or the packets abandoned) first";
-        return CLK_EINVAL;
+        // the failed flush is retried first (a transient failure then loses
+        // no packet); still failing: the packet is refused, CLK_EHIP (the
+        // adapter counts it as a failed flush of the staged batch)
+        const int r = flush();
+        if (failed_)
+            return r == CLK_SUCCESS ? CLK_EHIP : (r == CLK_EINVAL ? CLK_EHIP : r);
     }
+    Batch *B = &b_[cur_];
     uint64_t slot = 0;
     uint32_t need = 0;
     if (m_[0]->zerocopy_) {
@@ -270,52 +304,58 @@ int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t toke
             zc_last_dev_ = (uint8_t *)db;
             zc_gen_ = gen;
         }
-        if (!views0_.empty() && zc_host_ != zc_last_) {         // the batch's region ends here
-            int r = flush();
-            if (r)
-                return r;
+        if (B->np && B->zc_host != zc_last_) {       // the batch's region ends here
+            // (a flush that ended its batch with packets killed has routed
+            // them: this packet starts the next batch; one that left the
+            // batch staged refuses it, as a failed flush)
+            const int r = flush_async();
+            if (failed_)
+                return r == CLK_EINVAL ? CLK_EHIP : r;
+            B = &b_[cur_];
         }
-        if (views0_.empty() && begin_batch()) {
+        if (!B->np && begin_batch(*B)) {
             err_ = "out of device / pinned memory";
             return CLK_EINVAL;
         }
-        zc_host_ = zc_last_;
-        zc_dev_ = zc_last_dev_;
-        slot = (uint64_t)(a - zc_host_);
+        B->zc_host = zc_last_;
+        B->zc_dev = zc_last_dev_;
+        slot = (uint64_t)(a - B->zc_host);
     } else {
-        if (views0_.empty() && begin_batch()) {
+        if (!B->np && begin_batch(*B)) {
             err_ = "out of device / pinned memory";
             return CLK_EINVAL;
         }
         need = std::min(length, extent(nh_offset, length));
-        slot = (used_ + 15) & ~size_t(15);
-        if (slot + need + 64 > h_cap_) {
-            if (sent_)                               // copies from the old arena may be in flight
-                (void)hipStreamSynchronize((hipStream_t)clk_ctx_stream(m_[0]->ctx_));
-            if (pinned_grow(&h_arena_, &h_cap_, std::max<size_t>(slot + need + 64, size_t(1) << 20), used_)) {
+        slot = (B->used + 15) & ~size_t(15);
+        if (slot + need + 64 > B->h_cap) {
+            if (B->sent)                             // copies from the old arena may be in flight
+                (void)hipStreamSynchronize(stream());
+            if (pinned_grow(&B->h_arena, &B->h_cap, std::max<size_t>(slot + need + 64, size_t(1) << 20), B->used)) {
                 err_ = "out of pinned host memory";
                 return CLK_EINVAL;
             }
         }
-        stage_copy(h_arena_ + slot, data, need, length);
-        used_ = slot + need;
-        if (used_ - sent_ >= H2D_CHUNK)
-            send_chunk();
+        stage_copy(B->h_arena + slot, data, need, length);
+        B->used = slot + need;
+        if (B->used - B->sent >= H2D_CHUNK)
+            send_chunk(*B);
     }
-    if (views0_.size() == mcap_ && grow_batch()) {
+    if (B->np == B->mcap && grow_batch(*B)) {
         err_ = "out of device / pinned memory";
         return CLK_EINVAL;
     }
     const ChainView v{data, token, slot, length, nh_offset, (uint16_t)anno};
-    const uint32_t i = (uint32_t)views0_.size();
-    views0_.push_back(v);
-    views_.push_back(v);
-    staged_.push_back(need);
-    back_.push_back(0);                              // grown by each member whose kernel may rewrite it
-    done_.push_back(0);
-    copied_.push_back(0);
-    advance(i, 0);                                   // into member 0, and on through host decisions
-    return views0_.size() >= m_[0]->batch_cap_ ? 1 : 0;
+    const uint32_t i = (uint32_t)B->np++;
+    B->views0[i] = v;
+    B->views[i] = v;
+    B->staged[i] = need;
+    B->clone_key[i] = 0;
+    B->back[i] = 0;                                  // grown by each member whose kernel may rewrite it
+    B->done[i] = 0;
+    B->copied[i] = 0;
+    ChainWork &w0 = B->mm[0].w;                      // it reaches member 0 (its descriptors at the flush)
+    w0.reached[w0.nreached++] = i;
+    return B->np >= m_[0]->batch_cap_ ? 1 : 0;
 }
 
 int Chain::push_burst(uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets, uint64_t first_token,
@@ -330,7 +370,7 @@ int Chain::push_burst(uint8_t *const *datas, const uint32_t *lengths, const int3
             return r;
         if (r == 1) {
             stats_[0] += now_s() - t0;
-            if ((r = flush()) != 0)
+            if ((r = flush_async()) != 0)           // the next batch is staged while this one runs
                 return r;
             t0 = now_s();
         }
@@ -341,9 +381,9 @@ int Chain::push_burst(uint8_t *const *datas, const uint32_t *lengths, const int3
 
 // Member buffers for c packets (pinned descriptors / verdicts, device
 // copies, events, work arrays); keep: the descriptors filled so far survive.
-int Chain::grow_members(size_t c, int keep)
+int Chain::grow_members(Batch &B, size_t c, int keep)
 {
-    for (Member &M : mm_) {
+    for (Member &M : B.mm) {
         for (void *&e : M.ev)
             if (!e) {
                 hipEvent_t h = nullptr;
@@ -377,7 +417,7 @@ int Chain::grow_members(size_t c, int keep)
             M.span_len.resize(c);
         }
     }
-    mcap_ = std::max(mcap_, c);
+    B.mcap = std::max(B.mcap, c);
     return 0;
 }
 
@@ -387,20 +427,22 @@ bool Chain::host_writes(const BatchElement *e)
     return !e->zerocopy_ && e->chain_host_rewrite() != CHAIN_HOST_NONE;
 }
 
-// Member k's work state: where its arrays are, what it is.
-void Chain::setup(size_t k)
+// Member k's work state in batch B: where its arrays are, what it is.
+void Chain::setup(Batch &B, size_t k)
 {
     BatchElement *e = m_[k];
-    Member &M = mm_[k];
+    Member &M = B.mm[k];
     ChainWork &w = M.w;
     w.reached = M.reached.data(), w.code = M.code.data(), w.span_off = M.span_off.data();
     w.span_len = M.span_len.data();
-    w.views = &views_;
-    w.done = &done_;
-    w.out = &out_;
-    w.back = e->zerocopy_ ? nullptr : back_.data();
-    w.staged = staged_.data();
-    w.views0 = views0_.data();
+    w.views = B.views.data();                        // (sized for mcap packets: they stay put)
+    w.done = B.done.data();
+    w.next = k + 1 < B.mm.size() ? &B.mm[k + 1].w : nullptr;
+    w.elem = e;
+    w.out = &B.out;
+    w.back = e->zerocopy_ ? nullptr : B.back.data();
+    w.staged = B.staged.data();
+    w.views0 = B.views0.data();
     const uint8_t hr = e->zerocopy_ ? (uint8_t)CHAIN_HOST_NONE : e->chain_host_rewrite();
     w.wext = hr == CHAIN_HOST_ALL ? 0u : e->chain_write_past_nh();
     w.wext_unless_simple = hr == CHAIN_HOST_SIMPLE;
@@ -412,250 +454,426 @@ void Chain::setup(size_t k)
     w.strip = e->strip();
     w.nh_after = e->nh_after();
     w.last = k + 1 == m_.size();
-    w.inline_ok = !e->has_pre_route_ && !e->has_post_route_;
+    w.clone_key = k > 0 && e->has_pre_route_ ? B.clone_key.data() : nullptr;
     w.report_passes = k < 64 && (report_passes_ >> k & 1);
-    e->h_aux8_ = M.h_aux8;
 }
 
-// Packet i reaches member k: its descriptor there, or its host decision.  A
-// host decision is routed at once while the member has routed every packet
-// before it (none of them waits for the GPU), so results stay in push order
-// at every member; a packet passed on goes straight to the next member.  A
-// member that decides every packet on the host (IPGWOptions without options,
-// FixIPSrc without the annotation, IPFragmenter within the MTU) so costs no
-// pass of its own; the ones that pass such a member unchanged are not even
-// asked (ChainWork::passes).
-void Chain::advance(uint32_t i, size_t k)
-{
-    const ChainView &v = views_[i];
-    for (;;) {
-        ChainWork &w = mm_[k].w;
-        if (w.routed == w.nreached && w.passes(v)) {
-            m_[k]->packets_++;
-            if (w.last) {
-                out_.push_back(ChainExit{v.token, (int32_t)k, 0, v.length, 0, i});
-                done_[i] = 1;
-                return;
-            }
-            k++;
-            continue;
-        }
-        if (m_[k]->chain_step(w, i) != 1)
-            return;
-        k++;
-    }
-}
-
-// Member k's GPU step over the packets that reached it and are not routed
-// yet -- descriptors up, its kernel, its verdicts back -- then their routing
-// (the class's route(), chain_route_all): output 0 goes on to member k+1,
-// anything else leaves the chain at member k.  *launched: the member's
-// kernels were queued (a failure after that leaves the device bytes
-// rewritten by them).
-int Chain::run_member(size_t k, bool *launched)
+// Batch B's GPU step at member k over the packets that reached it and are
+// not routed yet: descriptors up, its kernel, its verdicts (and rewritten
+// aux bytes) back and a completion event -- queued, nothing waits.
+// B.launched: the member's kernels were queued (a failure after that leaves
+// the device bytes rewritten by them).
+int Chain::launch_member(Batch &B, size_t k)
 {
     BatchElement *e = m_[k];
-    Member &M = mm_[k];
+    Member &M = B.mm[k];
     ChainWork &w = M.w;
-    hipStream_t s = (hipStream_t)clk_ctx_stream(e->ctx_);
-    double t0 = now_s();
-    if (M.rebuild) {                                 // after a failure: a new batch of the packets left
-        M.rebuild = false;
-        std::vector<uint32_t> left(w.reached + w.routed, w.reached + w.nreached);
-        w.reset();
-        for (uint32_t i : left)
-            advance(i, k);
-    }
-    stats_[1] += now_s() - t0;
-    t0 = now_s();
-    M.ms = 0;
-    if (w.n) {
-        const size_t n = w.n;
-        hipError_t er;
-        if ((er = glue_checked(hipMemcpyAsync(M.d_off, M.h_off, n * 8, hipMemcpyHostToDevice, s))) != hipSuccess ||
-            (er = glue_checked(hipMemcpyAsync(M.d_len, M.h_len, n * 4, hipMemcpyHostToDevice, s))) != hipSuccess ||
-            (e->wants_anno() &&
-             (er = glue_checked(hipMemcpyAsync(M.d_anno, M.h_anno, n, hipMemcpyHostToDevice, s))) != hipSuccess)) {
-            err_ = e->name() + ": hipMemcpyAsync(descriptors): " + hipGetErrorString(er);
-            return CLK_EHIP;
-        }
-        (void)hipEventRecord((hipEvent_t)M.ev[0], s);
-        clk_batch b;
-        b.base = m_[0]->zerocopy_ ? zc_dev_ : d_arena_;
-        b.off = M.d_off;
-        b.stride = 0;
-        b.len = M.d_len;
-        b.fixed_len = 0;
-        b.max_len = w.maxlen;
-        b.n = n;
-        e->d_anno_ = M.d_anno;
-        e->d_aux8_ = M.d_aux8;
-        e->err_.clear();
-        *launched = true;
-        int r = e->run(&b, M.d_codes, M.d_sums);
-        er = hipSuccess;
-        if (r == 0) {
-            (void)hipEventRecord((hipEvent_t)M.ev[1], s);
-            if ((er = glue_checked(hipMemcpyAsync(M.h_codes, M.d_codes, n, hipMemcpyDeviceToHost, s))) != hipSuccess ||
-                (e->wants_sums() &&
-                 (er = glue_checked(hipMemcpyAsync(M.h_sums, M.d_sums, n * 2, hipMemcpyDeviceToHost, s))) != hipSuccess) ||
-                (e->wants_arena_back() &&
-                 (er = glue_checked(hipMemcpyAsync(M.h_aux8, M.d_aux8, n, hipMemcpyDeviceToHost, s))) != hipSuccess) ||
-                (er = glue_checked(hipStreamSynchronize(s))) != hipSuccess)
-                r = CLK_EHIP;
-        }
-        if (r) {
-            (void)hipStreamSynchronize(s);
-            err_ = e->name() + ": " + (!e->err_.empty() ? e->err_
-                                        : er != hipSuccess ? std::string(hipGetErrorString(er))
-                                                           : std::string(clk_last_error(e->ctx_)));
-            return r;
-        }
-        (void)hipEventElapsedTime(&M.ms, (hipEvent_t)M.ev[0], (hipEvent_t)M.ev[1]);
-        if ((r = e->verify(M.h_codes, n)) != 0) {
-            err_ = e->name() + ": " + e->err_;
-            return r;
-        }
-        e->batches_++;
-        e->gpu_ns_ += (uint64_t)(M.ms * 1e6);
-    }
-    stats_[2] += now_s() - t0;
-    t0 = now_s();
-    e->h_aux8_ = M.h_aux8;
-    e->chain_route_all(w, *this, k);
-    stats_[6] += now_s() - t0;
-    return CLK_SUCCESS;
-}
-
-// The rewritten bytes into the packets that have left the chain (all: every
-// packet of the batch), from one D2H of the device batch.
-int Chain::copy_back(bool all)
-{
-    bool any = false;
-    for (size_t i = 0; i < views0_.size() && !any; i++)
-        any = back_[i] && !copied_[i] && (all || done_[i]);
-    if (!any) {
-        pub_ = out_.size();
-        return CLK_SUCCESS;
-    }
-    hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
-    double t0 = now_s();
+    hipStream_t s = stream();
+    const double t0 = now_s();
+    const size_t n = w.n;
     hipError_t er;
-    if (pinned_grow(&h_back_, &back_cap_, used_ + 64, 0) ||
-        (er = glue_checked(hipMemcpyAsync(h_back_, d_arena_, used_, hipMemcpyDeviceToHost, s))) != hipSuccess ||
-        (er = glue_checked(hipStreamSynchronize(s))) != hipSuccess) {
+    M.ms = 0;
+    if ((er = glue_checked(hipMemcpyAsync(M.d_off, M.h_off, n * 8, hipMemcpyHostToDevice, s))) != hipSuccess ||
+        (er = glue_checked(hipMemcpyAsync(M.d_len, M.h_len, n * 4, hipMemcpyHostToDevice, s))) != hipSuccess ||
+        (e->wants_anno() &&
+         (er = glue_checked(hipMemcpyAsync(M.d_anno, M.h_anno, n, hipMemcpyHostToDevice, s))) != hipSuccess)) {
         (void)hipStreamSynchronize(s);
-        err_ = "hipMemcpyAsync(packets back) failed";
+        err_ = e->name() + ": hipMemcpyAsync(descriptors): " + hipGetErrorString(er);
+        stats_[2] += now_s() - t0;
         return CLK_EHIP;
     }
-    stats_[5] += now_s() - t0;
-    t0 = now_s();
-    for (size_t i = 0; i < views0_.size(); i++)
-        if (back_[i] && !copied_[i] && (all || done_[i])) {
-            std::memcpy(views0_[i].data, h_back_ + views0_[i].slot, back_[i]);
-            copied_[i] = 1;
-        }
-    stats_[7] += now_s() - t0;
-    pub_ = out_.size();                              // every result so far has its bytes
+    (void)hipEventRecord((hipEvent_t)M.ev[0], s);
+    clk_batch b;
+    b.base = m_[0]->zerocopy_ ? B.zc_dev : B.d_arena;
+    b.off = M.d_off;
+    b.stride = 0;
+    b.len = M.d_len;
+    b.fixed_len = 0;
+    b.max_len = w.maxlen;
+    b.n = n;
+    e->d_anno_ = M.d_anno;
+    e->d_aux8_ = M.d_aux8;
+    e->err_.clear();
+    B.launched = true;
+    int r = e->run(&b, M.d_codes, M.d_sums);
+    er = hipSuccess;
+    if (r == 0) {
+        (void)hipEventRecord((hipEvent_t)M.ev[1], s);
+        if ((er = glue_checked(hipMemcpyAsync(M.h_codes, M.d_codes, n, hipMemcpyDeviceToHost, s))) != hipSuccess ||
+            (e->wants_sums() &&
+             (er = glue_checked(hipMemcpyAsync(M.h_sums, M.d_sums, n * 2, hipMemcpyDeviceToHost, s))) != hipSuccess) ||
+            (e->wants_arena_back() &&
+             (er = glue_checked(hipMemcpyAsync(M.h_aux8, M.d_aux8, n, hipMemcpyDeviceToHost, s))) != hipSuccess))
+            r = CLK_EHIP;
+        else
+            (void)hipEventRecord((hipEvent_t)M.ev[2], s);
+    }
+    stats_[2] += now_s() - t0;
+    if (r) {
+        (void)hipStreamSynchronize(s);
+        err_ = e->name() + ": " + (!e->err_.empty() ? e->err_
+                                    : er != hipSuccess ? std::string(hipGetErrorString(er))
+                                                       : std::string(clk_last_error(e->ctx_)));
+        return r;
+    }
+    B.waiting = true;
     return CLK_SUCCESS;
 }
 
-// Run the staged batch through the members and route it.  A member whose
-// step fails stops the flush there: the packets that left the chain before it
-// stay routed (their bytes copied back); the rest stay in the chain, and the
-// next flush resumes at that member (push() refuses packets until then).
-int Chain::flush()
+// Wait for batch B's GPU step at member B.at (launch_member), then check it.
+int Chain::await_member(Batch &B)
 {
-    if (dead_)
-        return views0_.empty() ? CLK_SUCCESS : CLK_EINVAL;
-    if (views0_.empty())
-        return CLK_SUCCESS;
-    err_.clear();
-    hipStream_t s = (hipStream_t)clk_ctx_stream(m_[0]->ctx_);
-    if (!h2d_done_ && !m_[0]->zerocopy_) {
-        if (device_arena(used_ + 64)) {
+    const size_t k = B.at;
+    BatchElement *e = m_[k];
+    Member &M = B.mm[k];
+    const double t0 = now_s();
+    hipError_t er = glue_checked(hipEventSynchronize((hipEvent_t)M.ev[2]));
+    stats_[2] += now_s() - t0;
+    B.waiting = false;
+    if (er != hipSuccess) {
+        (void)hipStreamSynchronize(stream());
+        err_ = e->name() + ": " + hipGetErrorString(er);
+        return CLK_EHIP;
+    }
+    (void)hipEventElapsedTime(&M.ms, (hipEvent_t)M.ev[0], (hipEvent_t)M.ev[1]);
+    int r = e->verify(M.h_codes, M.w.n);
+    if (r) {
+        err_ = e->name() + ": " + e->err_;
+        return r;
+    }
+    e->batches_++;
+    e->gpu_ns_ += (uint64_t)(M.ms * 1e6);
+    return CLK_SUCCESS;
+}
+
+// Member k's step failed after its kernel was queued: the device bytes may
+// be rewritten by it, and a member that is not idempotent must not run twice
+// on them (a second TTL decrement) -- its packets not routed are killed, as
+// a ZEROCOPY batch of such an element is; the ones it passed before go on.
+// Returns whether it did (else the packets stay at k for a retry).
+bool Chain::kill_member(Batch &B, size_t k, int r)
+{
+    if (!B.launched || m_[k]->idempotent())
+        return false;
+    BatchElement *e = m_[k];
+    ChainWork &w = B.mm[k].w;
+    drop_clones(B, k, w.routed, w.nreached);
+    for (size_t q = w.routed; q < w.nreached; q++) {
+        const uint32_t i = w.reached[q];
+        B.out.push_back(ChainExit{B.views[i].token, (int32_t)k, CLK_PORT_KILL, B.views[i].length, 0, i});
+        B.done[i] = 1;
+        e->lost_++;
+    }
+    w.routed = w.nreached;
+    B.kill_rc = r;
+    B.kill_why = err_ + " (its packets were killed, not retried)";
+    return true;
+}
+
+// Move batch B on by one GPU step: wait for the step in flight (if any) and
+// route its member; then the members after it -- each one's prep loop, its
+// route loop when it needs no GPU -- up to the next member with packets for
+// the GPU, whose step is launched; after the last member the rewritten bytes
+// come back and the batch's results are handed out (publish).  A failure
+// leaves B where it stopped (failed_, resumed by the next flush).
+int Chain::step(Batch &B)
+{
+    if (B.waiting) {
+        const size_t k = B.at;
+        int r = await_member(B);
+        if (r) {
+            if (!kill_member(B, k, r)) {
+                B.mm[k].rebuild = true;
+                return fail(B, r);
+            }
+        } else {
+            const double t0 = now_s();
+            m_[k]->h_aux8_ = B.mm[k].h_aux8;
+            m_[k]->chain_route_all(B.mm[k].w);
+            stats_[6] += now_s() - t0;
+        }
+        B.at = k + 1;
+    }
+    while (B.at < m_.size()) {
+        const size_t k = B.at;
+        BatchElement *e = m_[k];
+        Member &M = B.mm[k];
+        ChainWork &w = M.w;
+        if (w.routed == w.nreached && w.nprep == w.nreached) {
+            B.at++;
+            continue;
+        }
+        const double t0 = now_s();
+        if (M.rebuild) {                             // after a failure: a new batch of the packets left
+            M.rebuild = false;
+            w.n = 0;
+            w.maxlen = 0;
+            w.nprep = w.routed;
+        }
+        e->chain_prep(w);                            // the packets members before it passed on
+        stats_[6] += now_s() - t0;
+        if (w.clone_key) {                           // clones of the packets as they reach member k
+            const int r = keep_clones(B, k);
+            if (r)
+                return fail(B, r);
+        }
+        if (w.n) {
+            B.launched = false;
+            const int r = launch_member(B, k);
+            if (r) {
+                if (!kill_member(B, k, r)) {
+                    M.rebuild = true;
+                    return fail(B, r);
+                }
+                B.at++;
+                continue;
+            }
+            return CLK_SUCCESS;                      // waiting for the GPU
+        }
+        const double t1 = now_s();
+        e->h_aux8_ = M.h_aux8;
+        e->chain_route_all(w);                       // every packet decided on the host
+        stats_[6] += now_s() - t1;
+        B.at++;
+    }
+    int r = copy_back(B, true);
+    if (r) {                                         // only the copy back is left; nothing handed out
+        failed_ = true;
+        return r;
+    }
+    const int rc = B.kill_rc;
+    const std::string why = B.kill_why;
+    end_batch(B);
+    if (rc) {
+        err_ = why;
+        return rc;
+    }
+    return CLK_SUCCESS;
+}
+
+// A step of B failed at B.at: the results of the packets that left before it
+// are handed out (their bytes copied back), the rest stay in the chain, and
+// push() retries the flush first (failed_).
+int Chain::fail(Batch &B, int r)
+{
+    failed_ = true;
+    const std::string why = B.kill_rc ? B.kill_why + "; " + err_ : err_;
+    (void)copy_back(B, false);
+    err_ = why;
+    return r;
+}
+
+// Batch B from the H2D of its staged bytes (the tail the pushes have not
+// sent yet) to its first GPU step launched.
+int Chain::start(Batch &B)
+{
+    if (!B.h2d_done && !m_[0]->zerocopy_) {
+        if (device_arena(B, B.used + 64)) {
             failed_ = true;
             err_ = "out of device memory";
             return CLK_EHIP;
         }
-        if (!sent_ok_)
-            sent_ = 0, sent_ok_ = true;
-        double t0 = now_s();
-        hipError_t er = glue_checked(hipMemcpyAsync(d_arena_ + sent_, h_arena_ + sent_, used_ - sent_,
-                                                    hipMemcpyHostToDevice, s));
+        if (!B.sent_ok)
+            B.sent = 0, B.sent_ok = true;
+        const double t0 = now_s();
+        hipError_t er = glue_checked(hipMemcpyAsync(B.d_arena + B.sent, B.h_arena + B.sent, B.used - B.sent,
+                                                    hipMemcpyHostToDevice, stream()));
         if (er != hipSuccess) {
-            (void)hipStreamSynchronize(s);
+            (void)hipStreamSynchronize(stream());
             failed_ = true;
-            sent_ = 0;
+            B.sent = 0;
             err_ = std::string("hipMemcpyAsync(packets): ") + hipGetErrorString(er);
             return CLK_EHIP;
         }
-        sent_ = used_;
+        B.sent = B.used;
         stats_[4] += now_s() - t0;
     }
-    h2d_done_ = true;
-    int failed = CLK_SUCCESS;
-    std::string failed_why;
-    for (size_t k = 0; k < m_.size(); k++) {
-        ChainWork &w = mm_[k].w;
-        if (w.routed == w.nreached)
-            continue;
-        bool launched = false;
-        int r = run_member(k, &launched);
-        if (r == CLK_SUCCESS)
-            continue;
-        if (launched && !m_[k]->idempotent()) {
-            // the member's kernel may have rewritten the device bytes: running
-            // it again would apply it twice (a second TTL decrement), so the
-            // packets it had not routed are killed, as a ZEROCOPY batch of such
-            // an element is; the ones it passed before that go on
-            BatchElement *e = m_[k];
-            for (size_t q = w.routed; q < w.nreached; q++) {
-                const uint32_t i = w.reached[q];
-                out_.push_back(ChainExit{views_[i].token, (int32_t)k, CLK_PORT_KILL, views_[i].length, 0, i});
-                done_[i] = 1;
-                e->lost_++;
-            }
-            w.routed = w.nreached;
-            failed = r;
-            failed_why = err_ + " (its packets were killed, not retried)";
-            continue;
-        }
-        // the packets at member k that it had not routed stay in the chain
-        // (the ones it routed before the failure -- host decisions -- are
-        // routed, and the ones those passed are at the next members already);
-        // the next flush builds member k's batch of them again
-        mm_[k].rebuild = true;
-        failed_ = true;
-        const std::string why = failed ? failed_why + "; " + err_ : err_;
-        (void)copy_back(false);
-        err_ = why;
-        return r;
-    }
-    int r = copy_back(true);
-    if (r) {
-        failed_ = true;                              // only the copy back is left
-        return r;
-    }
-    end_batch();
-    if (failed)
-        err_ = failed_why;
-    return failed;
+    B.h2d_done = true;
+    B.started = true;
+    return step(B);
 }
 
-void Chain::end_batch()
+// Every step of batch B, waiting for each
+int Chain::finish(Batch &B)
 {
+    while (B.started) {
+        const int r = step(B);
+        if (r)
+            return r;
+    }
+    return CLK_SUCCESS;
+}
+
+// Double-buffered flush: the staged batch's first GPU step is launched, the
+// batch in flight before it is finished (its last GPU step ran while this
+// one was pushed, its first one while the other was routed), and this one
+// is moved on by one step (routed to its next GPU step), then pushes go to
+// the other batch.  Results are handed out a whole batch at a time, in push
+// order of the batches.
+int Chain::flush_async()
+{
+    if (dead_) {
+        const bool any = b_[0].np || b_[1].np;
+        return any ? CLK_EINVAL : CLK_SUCCESS;
+    }
+    err_.clear();
+    Batch &B = b_[cur_], &O = b_[cur_ ^ 1];
+    int r;
+    if (B.np && !B.started && (r = start(B)) != CLK_SUCCESS)
+        return r;
+    if (O.started && (r = finish(O)) != CLK_SUCCESS)
+        return r;
+    if (B.started) {
+        cur_ ^= 1;                                   // pushes go to the other batch (O is free now)
+        if ((r = step(B)) != CLK_SUCCESS)
+            return r;
+    }
+    if (!b_[0].started && !b_[1].started)
+        failed_ = false;
+    return CLK_SUCCESS;
+}
+
+// Run the staged batch through the members and route it, and the one before
+// it: everything pushed is routed when it returns.  A member whose step fails
+// stops there: the packets that left the chain before it stay routed (their
+// bytes copied back); the rest stay in the chain, and the next flush resumes
+// at that member (push() retries it first).
+int Chain::flush()
+{
+    int r = flush_async();
+    if (r)
+        return r;
+    Batch &O = b_[cur_ ^ 1];
+    if (O.started && (r = finish(O)) != CLK_SUCCESS)
+        return r;
     failed_ = false;
-    views0_.clear();
-    views_.clear();
-    staged_.clear();
-    back_.clear();
-    done_.clear();
-    copied_.clear();
-    used_ = 0;
-    zc_host_ = nullptr;
-    for (BatchElement *e : m_)
-        e->in_place_ = false, e->chain_ = false;
+    return CLK_SUCCESS;
+}
+
+// A member after the head that clones packets as they reach it (IPOutputCombo's
+// PaintTee, ipoutputcombo.cc:56-57): before its kernel runs, the bytes of
+// each packet it will clone are kept (BatchElement::keep_packet) as the
+// members before it left them -- staged: the device batch (one D2H, only
+// when some packet is cloned) for the staged bytes, the packet for the rest;
+// ZEROCOPY: the packet itself, where the kernels before it wrote.  Its
+// clone result then names the kept packet (aux CLK_AUX_CLONE | key).
+int Chain::keep_clones(Batch &B, size_t k)
+{
+    BatchElement *e = m_[k];
+    ChainWork &w = B.mm[k].w;
+    bool any = false;
+    for (size_t q = w.routed; q < w.nreached && !any; q++) {
+        const uint32_t i = w.reached[q];
+        any = !B.clone_key[i] && e->pre_clone(B.views[i]);
+    }
+    if (!any)
+        return CLK_SUCCESS;
+    const uint8_t *dev = nullptr;
+    hipStream_t s = stream();
+    if (!m_[0]->zerocopy_) {
+        hipError_t er = hipSuccess;
+        if (pinned_grow(&B.h_snap, &B.snap_cap, B.used + 64, 0) ||
+            (er = glue_checked(hipMemcpyAsync(B.h_snap, B.d_arena, B.used, hipMemcpyDeviceToHost, s))) != hipSuccess ||
+            (er = glue_checked(hipStreamSynchronize(s))) != hipSuccess) {
+            (void)hipStreamSynchronize(s);
+            err_ = e->name() + ": hipMemcpyAsync(clones): " + hipGetErrorString(er);
+            return CLK_EHIP;
+        }
+        dev = B.h_snap;
+    } else if (glue_checked(hipStreamSynchronize(s)) != hipSuccess) {   // the kernels before it done
+        err_ = e->name() + ": hipStreamSynchronize(clones)";
+        return CLK_EHIP;
+    }
+    std::vector<uint8_t> b;
+    for (size_t q = w.routed; q < w.nreached; q++) {
+        const uint32_t i = w.reached[q];
+        const ChainView &v = B.views[i];
+        if (B.clone_key[i] || !e->pre_clone(v))
+            continue;
+        b.resize(v.length);
+        size_t from_dev = 0;
+        if (dev) {                                   // the staged bytes from where this view's start
+            const uint64_t shift = v.slot - B.views0[i].slot;
+            from_dev = shift < B.staged[i] ? std::min<size_t>(v.length, B.staged[i] - shift) : 0;
+            std::memcpy(b.data(), dev + v.slot, from_dev);
+        }
+        std::memcpy(b.data() + from_dev, v.data + from_dev, v.length - from_dev);
+        B.clone_key[i] = e->keep_packet(b.data(), v.length);
+    }
+    return CLK_SUCCESS;
+}
+
+// Packets [q0, q1) of member k leave without their clone results (killed):
+// the bytes kept for them go
+void Chain::drop_clones(Batch &B, size_t k, size_t q0, size_t q1)
+{
+    for (size_t q = q0; q < q1; q++) {
+        const uint32_t i = B.mm[k].w.reached[q];
+        if (B.clone_key[i]) {
+            m_[k]->drop_packet(B.clone_key[i]);
+            B.clone_key[i] = 0;
+        }
+    }
+}
+
+// The rewritten bytes into the packets that have left the chain (all: every
+// packet of the batch), from one D2H of the device batch; then the results
+// routed so far are handed out.
+int Chain::copy_back(Batch &B, bool all)
+{
+    bool any = false;
+    for (size_t i = 0; i < B.np && !any; i++)
+        any = B.back[i] && !B.copied[i] && (all || B.done[i]);
+    if (any) {
+        hipStream_t s = stream();
+        double t0 = now_s();
+        hipError_t er;
+        if (pinned_grow(&B.h_back, &B.back_cap, B.used + 64, 0) ||
+            (er = glue_checked(hipMemcpyAsync(B.h_back, B.d_arena, B.used, hipMemcpyDeviceToHost, s))) != hipSuccess ||
+            (er = glue_checked(hipStreamSynchronize(s))) != hipSuccess) {
+            (void)hipStreamSynchronize(s);
+            err_ = "hipMemcpyAsync(packets back) failed";
+            return CLK_EHIP;
+        }
+        stats_[5] += now_s() - t0;
+        t0 = now_s();
+        for (size_t i = 0; i < B.np; i++)
+            if (B.back[i] && !B.copied[i] && (all || B.done[i])) {
+                std::memcpy(B.views0[i].data, B.h_back + B.views0[i].slot, B.back[i]);
+                B.copied[i] = 1;
+            }
+        stats_[7] += now_s() - t0;
+    }
+    publish(B);                                      // every result so far has its bytes
+    return CLK_SUCCESS;
+}
+
+// B's routed results so far join the ones handed out (the batch before B
+// was finished first: batches come out in order)
+void Chain::publish(Batch &B)
+{
+    const Batch &X = &B == &b_[0] ? b_[1] : b_[0];
+    if (X.started && X.seq < B.seq)                  // the batch before it has results to come first
+        return;
+    if (B.pub < B.out.size()) {
+        out_.insert(out_.end(), B.out.begin() + (ptrdiff_t)B.pub, B.out.end());
+        B.pub = B.out.size();
+    }
+}
+
+void Chain::end_batch(Batch &B)
+{
+    B.np = 0;
+    B.used = 0;
+    B.zc_host = nullptr;
+    B.started = false;
+    B.waiting = false;
+    B.at = 0;
+    B.out.clear();
+    B.pub = 0;
+    if (!b_[0].np && !b_[1].np)
+        for (BatchElement *e : m_)
+            e->in_place_ = false, e->chain_ = false;
 }
 
 // A GPU that keeps failing: every packet still in the chain -- staged, or
@@ -666,40 +884,52 @@ void Chain::end_batch()
 uint64_t Chain::abandon()
 {
     uint64_t k = 0;
-    if (views0_.empty() || dead_)
+    if (dead_)
         return 0;
-    if (h2d_done_)
-        (void)copy_back(false);                      // one more try for the bytes of the routed ones
-    for (size_t j = 0; j < mm_.size(); j++) {
-        ChainWork &w = mm_[j].w;
-        for (size_t q = w.routed; q < w.nreached; q++) {
-            const uint32_t i = w.reached[q];
-            if (done_[i])
-                continue;
-            out_.push_back(ChainExit{views_[i].token, (int32_t)j, CLK_PORT_KILL, views_[i].length, 0, i});
-            done_[i] = 1;
-            m_[j]->lost_++;
-            k++;
+    for (int x = 0; x < 2; x++) {
+        Batch &B = b_[cur_ ^ 1 ^ x];                 // the older batch first
+        if (!B.np)
+            continue;
+        if (B.waiting) {                             // its queued step: quiet, its outcome ignored
+            (void)hipEventSynchronize((hipEvent_t)B.mm[B.at].ev[2]);
+            B.waiting = false;
         }
-        w.routed = w.nreached;
-        mm_[j].rebuild = false;
-    }
-    for (size_t r = pub_; r < out_.size(); r++) {
-        ChainExit &x = out_[r];
-        if (x.idx != ~0u && x.port != CLK_PORT_KILL && x.port != CLK_PORT_NEXT && back_[x.idx] && !copied_[x.idx]) {
-            x.port = CLK_PORT_KILL;
-            m_[(size_t)x.member]->lost_++;
-            k++;
+        if (B.h2d_done)
+            (void)copy_back(B, false);               // one more try for the bytes of the routed ones
+        for (size_t j = 0; j < B.mm.size(); j++) {
+            ChainWork &w = B.mm[j].w;
+            drop_clones(B, j, w.routed, w.nreached);
+            for (size_t q = w.routed; q < w.nreached; q++) {
+                const uint32_t i = w.reached[q];
+                if (B.done[i])
+                    continue;
+                B.out.push_back(ChainExit{B.views[i].token, (int32_t)j, CLK_PORT_KILL, B.views[i].length, 0, i});
+                B.done[i] = 1;
+                m_[j]->lost_++;
+                k++;
+            }
+            w.routed = w.nreached;
+            B.mm[j].rebuild = false;
         }
+        for (size_t r = B.pub; r < B.out.size(); r++) {
+            ChainExit &x = B.out[r];
+            if (x.idx != ~0u && x.port != CLK_PORT_KILL && x.port != CLK_PORT_NEXT && B.back[x.idx] &&
+                !B.copied[x.idx]) {
+                x.port = CLK_PORT_KILL;
+                m_[(size_t)x.member]->lost_++;
+                k++;
+            }
+        }
+        publish(B);
+        end_batch(B);
     }
-    pub_ = out_.size();
-    end_batch();
+    failed_ = false;
     return k;
 }
 
 uint64_t Chain::pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap)
 {
-    const size_t k = (size_t)std::min<uint64_t>(cap, pub_ - head_);
+    const size_t k = (size_t)std::min<uint64_t>(cap, out_.size() - head_);
     for (size_t q = 0; q < k; q++) {
         const ChainExit &x = out_[head_ + q];
         if (tokens) tokens[q] = x.token;
@@ -710,7 +940,7 @@ uint64_t Chain::pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t
     }
     head_ += k;
     if (head_ == out_.size())
-        out_.clear(), head_ = 0, pub_ = 0;
+        out_.clear(), head_ = 0;
     return k;
 }
 
@@ -805,6 +1035,13 @@ int clk_chain_flush(clk_chain *w)
     if (!w)
         return CLK_EINVAL;
     return w->c->flush();
+}
+
+int clk_chain_flush_async(clk_chain *w)
+{
+    if (!w)
+        return CLK_EINVAL;
+    return w->c->flush_async();
 }
 
 int clk_chain_stats(clk_chain *w, double *sec, int n)

@@ -243,6 +243,13 @@ static int host_grow(T **p, size_t *cap_elems, size_t need, size_t keep)
 
 int BatchElement::grow_host(Stage &g, size_t bytes, size_t n)
 {
+    // the first growth takes a whole batch's worth (pinned allocations and
+    // frees cost 0.1-0.6 ms each: profiles/r05/mt_glue_hip_api_stats.csv), so
+    // a stage reallocates only for a caller that pushes past BATCH
+    if (bytes && !g.h_arena_cap && !zerocopy_)
+        bytes = std::max<size_t>(bytes, size_t(1) << 20);
+    if (n && !g.h_n_cap)
+        n = std::max<size_t>(n, std::min<size_t>(batch_cap_ + 1, size_t(1) << 20));
     if (host_grow(&g.h_arena, &g.h_arena_cap, bytes, g.h_used))
         return -1;
     if (g.h_n_cap < n) {
@@ -283,15 +290,14 @@ int BatchElement::grow_dev(Stage &g, size_t bytes, size_t n)
     return 0;
 }
 
-int BatchElement::chain_step(ChainWork &w, uint32_t i)
+void BatchElement::chain_prep(ChainWork &w)
 {
-    return chain_step_one(w, i, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); },
-                          [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
+    chain_prep_loop(w, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); });
 }
 
-void BatchElement::chain_route_all(ChainWork &w, Chain &c, size_t k)
+void BatchElement::chain_route_all(ChainWork &w)
 {
-    chain_route_loop(w, c, k, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
+    chain_route_loop(w, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
 }
 
 template <class SpanF>

@@ -147,6 +147,8 @@ inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t av
     }
 }
 
+class BatchElement;
+
 // One member's share of a chain flush (class Chain, chain.cc).
 struct ChainView {           // a packet as a chain member sees it
     uint8_t *data;
@@ -177,14 +179,19 @@ enum ChainPass {
     CHAIN_PASS_WITHIN,       // IPFragmenter: network length <= param (MTU), or no header
     CHAIN_PASS_TTL,          // DecIPTTL: param == 0 (ACTIVE false), or no header
 };
+// A reached packet's code at a member: its GPU index (>= 0), its host
+// decision (-1 - code), a pass rule's pass (CHAIN_CODE_PASS), or not looked
+// at yet (the member's prep loop has not run over it)
+enum : int32_t { CHAIN_CODE_PASS = INT32_MIN };
 struct ChainWork {
-    std::vector<ChainView> *views;            // per chain packet, updated as it passes members
-    std::vector<uint8_t> *done;               // per chain packet: has left the chain
+    ChainView *views = nullptr;               // per chain packet, updated as it passes members
+    uint8_t *done = nullptr;                  // per chain packet: has left the chain
     uint32_t *reached = nullptr;              // the packets that reached this member, in push order
-    int32_t *code = nullptr;                  // per reached packet: GPU index, or -1 - host code
+    int32_t *code = nullptr;                  // per reached packet (CHAIN_CODE_PASS, GPU index, -1 - host code)
     uint32_t *span_off = nullptr;             // per reached packet with a descriptor: its span
     uint32_t *span_len = nullptr;
     size_t nreached = 0;
+    size_t nprep = 0;                         // reached packets the prep loop has looked at
     size_t routed = 0;                        // reached packets routed so far
     uint64_t *h_off = nullptr;                // the member's batch (pinned)
     uint32_t *h_len = nullptr;
@@ -206,12 +213,17 @@ struct ChainWork {
     int32_t nh_after = -2;
     uint8_t pass = CHAIN_PASS_NONE;           // ChainPass, with pass_param
     uint32_t pass_param = 0;
+    uint32_t *clone_key = nullptr;            // a member after the head with pre results (IPOutputCombo's
+                                              // PaintTee clone): per chain packet, the key of the bytes
+                                              // as they reached the member (Chain::run_member), 0: none
     bool last = false;
-    bool inline_ok = false;                   // no pre/post results: a host decision may route at once
     bool report_passes = false;               // a CLK_PORT_NEXT record for each packet passed on
+    ChainWork *next = nullptr;                // member k+1's (0 for the last)
+    BatchElement *elem = nullptr;             // member k
     void reset()
     {
         nreached = 0;
+        nprep = 0;
         routed = 0;
         n = 0;
         maxlen = 0;
@@ -251,15 +263,15 @@ struct ChainWork {
     {                                                                                                           \
         route_loop(g_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
     }                                                                                                           \
-    int chain_step(ChainWork &w_, uint32_t i_) override                                                         \
+    void chain_prep(ChainWork &w_) override                                                                    \
     {                                                                                                           \
-        return chain_step_one(w_, i_, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {           \
+        chain_prep_loop(w_, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {                     \
             return this->C::span(p, o, l, c);                                                                   \
-        }, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); });         \
+        });                                                                                                     \
     }                                                                                                           \
-    void chain_route_all(ChainWork &w_, Chain &c_, size_t k_) override                                        \
+    void chain_route_all(ChainWork &w_) override                                                               \
     {                                                                                                           \
-        chain_route_loop(w_, c_, k_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
+        chain_route_loop(w_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
     }
 
 class Chain;
@@ -338,19 +350,22 @@ class BatchElement {
     virtual uint32_t chain_extent(int32_t nh, uint32_t length) const { (void)nh, (void)length; return 0xFFFFFFFFu; }
     // the element's kernel writes packet bytes (a chain copies them back)
     virtual bool writes() const { return wants_sums() || wants_arena_back() || !idempotent(); }
-    // a chain's per-packet steps (CLK_GLUE_LOOPS inlines the class's span /
-    // route into them).  chain_step(): packet i reaches the member -- its
-    // descriptor (0: it waits for the GPU), or its host decision, routed at
-    // once while no packet before it waits (1: passed on, 2: left the
-    // chain).  chain_route_all(): route the packets waiting at member k
-    // after its kernel, each one passed on going into member k+1
-    // (Chain::advance).
-    virtual int chain_step(ChainWork &w, uint32_t i);
-    virtual void chain_route_all(ChainWork &w, Chain &c, size_t k);
+    // a chain's loops over the packets that reached a member (CLK_GLUE_LOOPS
+    // inlines the class's span / route into them: one call per member and
+    // batch).  chain_prep(): each reached packet not looked at yet -- a pass
+    // rule's pass, its descriptor (it waits for the GPU) or its host decision.
+    // chain_route_all(): after the member's kernel, every reached packet not
+    // routed yet, in push order; each one passed on reaches member k+1.
+    virtual void chain_prep(ChainWork &w);
+    virtual void chain_route_all(ChainWork &w);
     // the decision the chain may take for the member (ChainPass)
     virtual void chain_pass(uint8_t *kind, uint32_t *param) const { *kind = CHAIN_PASS_NONE, *param = 0; }
     // the bytes past the network header the kernel may write (~0u: any)
     virtual uint32_t chain_write_past_nh() const { return writes() ? 0xFFFFFFFFu : 0u; }
+    // a chain member after the head: pre_route() will make a clone of this
+    // packet as it reaches the member (the chain keeps its bytes first)
+    virtual bool pre_clone(const ChainView &v) const { (void)v; return false; }
+    void drop_packet(uint32_t key) { packets_kept_.erase(key); }
     // in a staged chain, route() writes the member's rewrite into the packet
     // from its verdict (ChainHostRewrite) instead of the chain copying it back
     virtual uint8_t chain_host_rewrite() const
@@ -359,12 +374,46 @@ class BatchElement {
     }
     bool chain_ = false;             // a chain runs the element (it copies the rewritten bytes back)
     std::vector<Chain *> chains_;    // the chains the element is a member of (detached when it goes)
-    template <class SpanF, class RouteF>
-    int chain_step_one(ChainWork &w, uint32_t i, SpanF &&span_f, RouteF &&route_f);
+    template <class SpanF>
+    void chain_prep_loop(ChainWork &w, SpanF &&span_f);
+    // a pass rule's pass: counted, on to member k+1 (the last member: a
+    // result on output 0)
+    void chain_pass_on(ChainWork &w, uint32_t i)
+    {
+        packets_++;
+        if (w.last) {
+            const ChainView &v = w.views[i];
+            w.out->push_back(ChainExit{v.token, w.member, 0, v.length, 0, i});
+            w.done[i] = 1;
+        } else {
+            chain_forward(w, i);
+        }
+    }
+    // packet i, passed on by member k, reaches member k+1 -- and goes on at
+    // once through each member after it whose pass rule lets it through
+    // while no packet before it waits there (that member's list is empty),
+    // counted by each (the member would route it to output 0 unchanged); it
+    // joins the list of the first member that must look at it, or leaves
+    // the last on output 0
+    static void chain_forward(ChainWork &w, uint32_t i)
+    {
+        ChainWork *n = w.next;
+        const ChainView &v = w.views[i];
+        while (n->pass && n->routed == n->nreached && n->passes(v)) {
+            n->elem->packets_++;
+            if (n->last) {
+                n->out->push_back(ChainExit{v.token, n->member, 0, v.length, 0, i});
+                n->done[i] = 1;
+                return;
+            }
+            n = n->next;
+        }
+        n->reached[n->nreached++] = i;
+    }
     template <class RouteF>
     bool chain_route_at(ChainWork &w, size_t q, RouteF &&route_f);
     template <class RouteF>
-    void chain_route_loop(ChainWork &w, Chain &c, size_t k, RouteF &&route_f);
+    void chain_route_loop(ChainWork &w, RouteF &&route_f);
     template <class RouteF>
     bool chain_route_pending(ChainWork &w, uint32_t i, Pending &p, int code, uint16_t sum, RouteF &&route_f);
     ResultQueue chain_side_;          // a member's pre/post results while a chain routes
@@ -706,6 +755,10 @@ class IPOutputCombo : public BatchElement {
     bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const override;
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     bool pre_route(Pending &p, Result *r) override;
+    bool pre_clone(const ChainView &v) const override
+    {
+        return !(v.anno & CLK_ANNO_BCAST) && (long)((v.anno >> 8) & 0xFF) == color_ && noutputs_ >= 2;
+    }
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
     uint32_t chain_extent(int32_t nh, uint32_t) const override { return (nh > 0 ? (uint32_t)nh : 0u) + 64; }
     uint32_t chain_write_past_nh() const override { return 64; }
@@ -779,50 +832,66 @@ class IPFragmenter : public BatchElement {
     uint64_t nfrag_ = 0;
 };
 
-template <class SpanF, class RouteF>
-inline int BatchElement::chain_step_one(ChainWork &w, uint32_t i, SpanF &&span_f, RouteF &&route_f)
+// The packets that reached the member and were not looked at yet: a pass
+// rule's pass, or the class's span() -- a descriptor of the member's batch
+// (the bytes to copy back grown for a writing member) or a host decision.
+template <class SpanF>
+inline void BatchElement::chain_prep_loop(ChainWork &w, SpanF &&span_f)
 {
-    const ChainView &v = (*w.views)[i];
-    Pending p{v.data, v.token, v.slot, v.length, v.nh, 0, 0, 0, -1, v.anno};
-    uint32_t off = 0, len = 0;
-    int32_t hc = 0;
-    const size_t q = w.nreached++;
-    w.reached[q] = i;
-    if (!span_f(p, &off, &len, &hc)) {
-        w.code[q] = -1 - hc;
-        w.span_off[q] = 0;
-        w.span_len[q] = 0;
-        if (!w.inline_ok || w.routed != q)
-            return 0;
-        w.routed = q + 1;
-        p.host_code = (int16_t)hc;
-        return chain_route_pending(w, i, p, hc, 0, route_f) ? 1 : 2;
+    for (size_t q = w.nprep; q < w.nreached; q++) {
+        const uint32_t i = w.reached[q];
+        if (q + 8 < w.nreached)                  // the header a pass rule / span reads, 8 ahead
+            __builtin_prefetch(w.views[w.reached[q + 8]].data);
+        const ChainView &v = w.views[i];
+        if (w.pass && w.passes(v)) {
+            w.code[q] = CHAIN_CODE_PASS;
+            if (w.routed == q) {                 // nothing before it waits: it goes on now
+                w.routed = q + 1;
+                chain_pass_on(w, i);
+            }
+            continue;
+        }
+        Pending p{v.data, v.token, v.slot, v.length, v.nh, 0, 0, 0, -1, v.anno};
+        uint32_t off = 0, len = 0;
+        int32_t hc = 0;
+        if (!span_f(p, &off, &len, &hc)) {
+            w.code[q] = -1 - hc;
+            w.span_off[q] = 0;
+            w.span_len[q] = 0;
+            continue;
+        }
+        w.h_off[w.n] = v.slot + off;
+        w.h_len[w.n] = len;
+        w.h_anno[w.n] = (uint8_t)v.anno;
+        w.maxlen = std::max(w.maxlen, len);
+        w.span_off[q] = off;
+        w.span_len[q] = len;
+        w.code[q] = (int32_t)w.n++;
+        if (w.wext && w.back &&                  // the bytes this member's kernel may rewrite, to copy back
+            !(w.wext_unless_simple && IPOutputCombo::simple_rewrite(v.data + off, len, v.anno))) {
+            const uint64_t shift = v.slot - w.views0[i].slot;
+            const uint64_t e = w.wext == 0xFFFFFFFFu ? (uint64_t)0xFFFFFFFFu
+                                                     : shift + (v.nh > 0 ? (uint32_t)v.nh : 0u) + w.wext;
+            w.back[i] = (uint32_t)std::max<uint64_t>(w.back[i], std::min<uint64_t>(e, w.staged[i]));
+        }
     }
-    w.h_off[w.n] = v.slot + off;
-    w.h_len[w.n] = len;
-    w.h_anno[w.n] = (uint8_t)v.anno;
-    w.maxlen = std::max(w.maxlen, len);
-    w.span_off[q] = off;
-    w.span_len[q] = len;
-    w.code[q] = (int32_t)w.n++;
-    if (w.wext && w.back &&                  // the bytes this member's kernel may rewrite, to copy back
-        !(w.wext_unless_simple && IPOutputCombo::simple_rewrite(v.data + off, len, v.anno))) {
-        const uint64_t shift = v.slot - w.views0[i].slot;
-        const uint64_t e = w.wext == 0xFFFFFFFFu ? (uint64_t)0xFFFFFFFFu
-                                                 : shift + (v.nh > 0 ? (uint32_t)v.nh : 0u) + w.wext;
-        w.back[i] = (uint32_t)std::max<uint64_t>(w.back[i], std::min<uint64_t>(e, w.staged[i]));
-    }
-    return 0;
+    w.nprep = w.nreached;
 }
 
 template <class RouteF>
 inline bool BatchElement::chain_route_pending(ChainWork &w, uint32_t i, Pending &p, int code, uint16_t sum,
                                               RouteF &&route_f)
 {
-    ChainView &v = (*w.views)[i];
+    ChainView &v = w.views[i];
     Result pr;
-    if (has_pre_route_ && pre_route(p, &pr))
-        w.out->push_back(ChainExit{pr.token, w.member, pr.port, pr.length, pr.aux, ~0u});
+    if (has_pre_route_ && pre_route(p, &pr)) {
+        uint32_t aux = pr.aux;
+        if (w.clone_key && w.clone_key[i]) {  // the clone's bytes, kept as it reached this member
+            aux = CLK_AUX_CLONE | w.clone_key[i];
+            w.clone_key[i] = 0;
+        }
+        w.out->push_back(ChainExit{pr.token, w.member, pr.port, pr.length, aux, ~0u});
+    }
     Result r{p.token, 0, p.length, 0};
     packets_++;
     route_f(p, code, sum, &r);
@@ -838,7 +907,7 @@ inline bool BatchElement::chain_route_pending(ChainWork &w, uint32_t i, Pending 
             w.out->push_back(ChainExit{r.token, w.member, CLK_PORT_NEXT, r.length, r.aux, i});
     } else {
         w.out->push_back(ChainExit{r.token, w.member, r.port, r.length, r.aux, i});
-        (*w.done)[i] = 1;
+        w.done[i] = 1;
     }
     if (has_post_route_) {                    // results that follow the packet's own (fragments)
         post_route(p, code, chain_side_);
@@ -859,7 +928,7 @@ inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_
     const uint32_t i = w.reached[q];
     const int32_t c = w.code[q];
     const int code = c >= 0 ? w.h_codes[c] : -1 - c;
-    const ChainView &v = (*w.views)[i];
+    const ChainView &v = w.views[i];
     Pending p{v.data, v.token, v.slot, v.length, v.nh, w.span_off[q], w.span_len[q], c >= 0 ? (uint32_t)c : 0u,
               (int16_t)(c >= 0 ? -1 : code), v.anno};
     return chain_route_pending(w, i, p, code, c >= 0 && w.h_sums ? w.h_sums[c] : 0, route_f);
@@ -889,13 +958,12 @@ class Chain {
     int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno);
     int push_burst(uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets, uint64_t first_token,
                    uint32_t n);
-    int flush();
+    int flush();                              // everything pushed routed (both batches)
+    int flush_async();                        // double-buffered (the batch before finished, this one launched)
     uint64_t abandon();
-    // packet i reaches member k (and goes on through host decisions)
-    void advance(uint32_t i, size_t k);
     uint64_t pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap);
     const std::string &last_error() const { return err_; }
-    size_t pending() const { return views0_.size(); }
+    size_t pending() const { return b_[0].np + b_[1].np; }
     void report_passes(uint64_t members) { report_passes_ = members; }
     // host seconds spent so far, by phase (include/click_amd_elements.h,
     // clk_chain_stats)
@@ -907,54 +975,81 @@ class Chain {
     }
 
   private:
-    struct Member {          // one member's batch buffers
+    struct Member {          // one member's batch buffers (per chain batch)
         uint64_t *h_off = nullptr, *d_off = nullptr;
         uint32_t *h_len = nullptr, *d_len = nullptr;
         uint8_t *h_codes = nullptr, *d_codes = nullptr, *h_anno = nullptr, *d_anno = nullptr;
         uint8_t *h_aux8 = nullptr, *d_aux8 = nullptr;
         uint16_t *h_sums = nullptr, *d_sums = nullptr;
         size_t cap = 0;
-        void *ev[2] = {nullptr, nullptr};
+        void *ev[3] = {nullptr, nullptr, nullptr};   // kernel start, kernel end, step done
         float ms = 0;
         bool rebuild = false;                 // resumed: rebuild the batch of the packets not routed
         std::vector<uint32_t> reached, span_off, span_len;
         std::vector<int32_t> code;
         ChainWork w;
     };
-    int begin_batch();
-    int grow_batch();
+    // One batch of the chain: its packets, staging, device copy, members'
+    // work, and its routed results until they are handed out.  Two: one is
+    // pushed into while the other is in flight.
+    struct Batch {
+        std::vector<Member> mm;
+        std::vector<ChainView> views0, views;     // as pushed; as they move through the members
+        std::vector<uint32_t> staged, back, clone_key;   // bytes staged / to copy back, a kept clone's key
+        std::vector<uint8_t> done, copied;        // left the chain; bytes copied back
+        size_t np = 0, mcap = 0;                  // packets in the batch; the arrays' size
+        uint8_t *h_arena = nullptr, *h_back = nullptr, *h_snap = nullptr, *d_arena = nullptr;
+        size_t h_cap = 0, back_cap = 0, snap_cap = 0, d_cap = 0, used = 0;
+        size_t sent = 0;                          // staged bytes already copied to the device
+        bool sent_ok = true, h2d_done = false;
+        const uint8_t *zc_host = nullptr;         // ZEROCOPY: the batch's registered region
+        uint8_t *zc_dev = nullptr;
+        uint64_t seq = 0;                         // batches in push order
+        bool started = false;                     // flushed: in flight until its last member is routed
+        size_t at = 0;                            // the member its routing has reached
+        bool waiting = false;                     // member at's GPU step is queued, not awaited
+        bool launched = false;                    // ... and its kernels were queued
+        int kill_rc = CLK_SUCCESS;                // a rewriting member's packets were killed (kill_member)
+        std::string kill_why;
+        std::vector<ChainExit> out;               // routed results, out[pub..] not handed out yet
+        size_t pub = 0;
+    };
+    hipStream_t stream() const;
+    int begin_batch(Batch &B);
+    int grow_batch(Batch &B);
+    void size_packets(Batch &B, size_t c);
     static bool host_writes(const BatchElement *e);
-    int device_arena(size_t bytes);
-    void send_chunk();
+    int device_arena(Batch &B, size_t bytes);
+    void send_chunk(Batch &B);
     static constexpr size_t H2D_CHUNK = size_t(1) << 20;
-    int grow_members(size_t c, int keep);
-    void end_batch();
-    void setup(size_t k);
-    int run_member(size_t k, bool *launched);
-    int copy_back(bool all);
+    int grow_members(Batch &B, size_t c, int keep);
+    void setup(Batch &B, size_t k);
+    int start(Batch &B);
+    int step(Batch &B);
+    int finish(Batch &B);
+    int fail(Batch &B, int r);
+    int launch_member(Batch &B, size_t k);
+    int await_member(Batch &B);
+    bool kill_member(Batch &B, size_t k, int r);
+    int keep_clones(Batch &B, size_t k);
+    void drop_clones(Batch &B, size_t k, size_t q0, size_t q1);
+    int copy_back(Batch &B, bool all);
+    void publish(Batch &B);
+    void end_batch(Batch &B);
+    void free_batch(Batch &B);
     uint32_t extent(int32_t nh, uint32_t length);
     std::vector<BatchElement *> m_;
-    std::vector<Member> mm_;
-    std::vector<ChainView> views0_, views_;   // as pushed; as they move through the members
-    std::vector<uint32_t> staged_, back_;     // bytes staged / written back per packet
-    std::vector<uint8_t> done_, copied_;      // per packet: left the chain; bytes copied back
-    bool failed_ = false;                     // a flush failed: the batch must be flushed (or abandoned)
+    Batch b_[2];
+    int cur_ = 0;                             // the batch pushes go to
+    uint64_t seq_ = 0;
+    bool failed_ = false;                     // a flush failed: the chain must be flushed (or abandoned)
     bool dead_ = false;                       // a member was destroyed first: nothing runs any more
-    bool h2d_done_ = false;                   // the staged batch is on the device
-    size_t sent_ = 0;                         // staged bytes already copied to the device this batch
-    bool sent_ok_ = true;
-    size_t mcap_ = 0;                         // packets the per-packet arrays hold
-    const uint8_t *zc_host_ = nullptr;        // ZEROCOPY: the batch's registered region
-    uint8_t *zc_dev_ = nullptr;
     const uint8_t *zc_last_ = nullptr;        // last region found (lookup cache)
     size_t zc_last_bytes_ = 0;
     uint8_t *zc_last_dev_ = nullptr;
     uint64_t zc_gen_ = 0;
-    uint8_t *h_arena_ = nullptr, *h_back_ = nullptr, *d_arena_ = nullptr;
-    size_t h_cap_ = 0, back_cap_ = 0, d_cap_ = 0, used_ = 0;
-    std::vector<ChainExit> out_;
+    std::vector<ChainExit> out_;              // results handed out (pop), batch after batch
     size_t head_ = 0;
-    size_t pub_ = 0;                          // out_[head_, pub_): results whose bytes are back
     double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int32_t ext_nh_ = -3;                     // extent() cache: the nh and length it was computed for
     uint32_t ext_len_ = 0, ext_ = 0;
@@ -964,14 +1059,17 @@ class Chain {
 };
 
 template <class RouteF>
-void BatchElement::chain_route_loop(ChainWork &w, Chain &c, size_t k, RouteF &&route_f)
+void BatchElement::chain_route_loop(ChainWork &w, RouteF &&route_f)
 {
     for (size_t q = w.routed; q < w.nreached; q++) {
         w.routed = q + 1;
         if (q + 8 < w.nreached)              // the packet route() reads 8 ahead
-            __builtin_prefetch((*w.views)[w.reached[q + 8]].data);
-        if (chain_route_at(w, q, route_f) && !w.last)
-            c.advance(w.reached[q], k + 1);
+            __builtin_prefetch(w.views[w.reached[q + 8]].data);
+        const uint32_t i = w.reached[q];
+        if (w.code[q] == CHAIN_CODE_PASS)
+            chain_pass_on(w, i);
+        else if (chain_route_at(w, q, route_f) && !w.last)
+            chain_forward(w, i);
     }
 }
 

@@ -110,9 +110,15 @@ enum clk_tune_knob {
                                          packet-stream kernel (65536)                     */
     CLK_TUNE_GROUP = 5,               /* lanes per packet of the fixed-geometry kernels:
                                          0 (by max_len), 1, 2, 4, ..., 64                 */
-    CLK_TUNE_SET_CHUNKS = 6           /* two-phase Set in this many packet ranges, each
+    CLK_TUNE_SET_CHUNKS = 6,          /* two-phase Set in this many packet ranges, each
                                          range's scatter on a side stream overlapping the
                                          next range's compute pass (1: one of each)       */
+    CLK_TUNE_READ_SHAPE = 7           /* clk_read_stream's load shape: 0 grid-stride, 8
+                                         16 B loads per lane in flight, 8K workgroups;
+                                         1 the same with 4 loads; 2 with 16 loads, 2K
+                                         workgroups; 3 each wave 8 KiB contiguous per
+                                         step, 4K workgroups (bench: the best is the
+                                         measured read ceiling)                      */
 };
 int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value);
 /* Last error text for `ctx` (or for the calling thread when ctx == NULL). */

@@ -195,6 +195,13 @@ int clk_element_take_messages(clk_element *e, char *buf, size_t cap);
  * clk_port); a member's extra results (IPOutputCombo's clone before the
  * packet, IPFragmenter's fragments after it) come with their member; new
  * packets are taken with clk_element_take_packet(members[member], aux).
+ * IPOutputCombo as member k > 0: its PaintTee clone (ipoutputcombo.cc:56-57)
+ * must be the packet as it reaches the member, which the caller no longer
+ * has once the chain copied the members' rewrites back; the chain keeps
+ * those bytes before member k's kernel runs and the clone result names them:
+ * aux = CLK_AUX_CLONE | key, the bytes from clk_element_take_packet(
+ * members[k], key) (at member 0, aux = CLK_AUX_CLONE: the caller clones the
+ * packet as it pushes it, as for the element alone).
  * The GPU analogue of click-xform's combos (ipinputcombo.cc:66-140,
  * ipoutputcombo.cc:44-205): one gather, one H2D, one D2H and one routing
  * pass per packet instead of one per element.  Each member's results come
@@ -204,7 +211,8 @@ int clk_element_take_messages(clk_element *e, char *buf, size_t cap);
  * while that member has no packet before it waiting for the GPU).  A flush
  * that fails at member k has routed what left the chain before k (their
  * bytes written back); the packets at k stay in the chain and the next
- * flush resumes there (push refuses packets until it has) -- except after
+ * flush resumes there (a push retries that flush first; while it still
+ * fails the push is refused with CLK_EHIP) -- except after
  * the kernel of a member that is not idempotent (DecIPTTL, IPGWOptions,
  * IPOutputCombo, IPFragmenter) was launched: its packets are then killed
  * (results with CLK_PORT_KILL, counted by its "lost" handler), never run
@@ -218,6 +226,14 @@ int clk_chain_push_anno(clk_chain *c, uint8_t *data, uint32_t length, int32_t nh
 int clk_chain_push_burst(clk_chain *c, uint8_t *const *datas, const uint32_t *lengths,
                          const int32_t *nh_offsets, uint64_t first_token, uint32_t n);
 int clk_chain_flush(clk_chain *c);
+/* Double-buffered flush (as clk_element_flush_async): launch the staged
+ * batch's first GPU step, finish the batch flushed before it (its results
+ * are handed out), move the staged one on to its next GPU step, and return;
+ * pushes go to the other batch while it runs.  clk_chain_flush routes
+ * everything pushed.  Results come out batch by batch, in push order of the
+ * batches; a failure anywhere leaves the chain to be flushed again (or
+ * abandoned) before it takes packets.                                      */
+int clk_chain_flush_async(clk_chain *c);
 /* A GPU that keeps failing: every packet still in the chain (staged, or at
  * the member a failed flush stopped at) becomes a CLK_PORT_KILL result at
  * the member it has reached, counted by that member's "lost" handler; so

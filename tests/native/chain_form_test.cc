@@ -222,8 +222,9 @@ void five_then_set()
     expect_u64("five_report", hipcore::chain_report(t, c), 0x5);   // CheckIPHeader (0), FixIPSrc (2)
 }
 
-// the combos: IPOutputCombo never joins (its PaintTee clones the packet as
-// it arrives), it heads its own chain
+// the combos: IPOutputCombo joins the chain of IPInputCombo (its PaintTee
+// clone, as a member after the head, comes from the bytes the glue keeps as
+// the packet reaches it), and the chain writes
 void combos()
 {
     Graph g;
@@ -233,11 +234,28 @@ void combos()
     g.gpu<Check>("cu");
     g.gpu<Set>("su");
     g.line({"src", "in", "out", "cu", "su"});
-    expect("combos", chains(g), "in[in] out[out,cu,su] cu[cu]* su[su]*");
+    expect("combos", chains(g), "in[in,out,cu,su] out[out]* cu[cu]* su[su]*");
     G t{g};
     std::vector<Elt *> c;
     hipcore::form_chain(t, g.by["in"], c);
-    expect("combos_in_reads", hipcore::chain_writes(t, c) ? "writes" : "reads", "reads");
+    expect("combos_in_writes", hipcore::chain_writes(t, c) ? "writes" : "reads", "writes");
+    expect_u64("combos_report", hipcore::chain_report(t, c), 0x3);   // IPInputCombo (0), IPOutputCombo (1)
+}
+
+// a class that may only head a chain (chain_head_only: none of the shipped
+// classes, the rule stays) never joins one: it heads its own
+struct HeadOnly {
+    enum { may_write = 1, chain_last = 0, chain_head_only = 1, pass_effects = 0 };
+};
+void head_only()
+{
+    Graph g;
+    g.add("src");
+    g.gpu<InCombo>("in");
+    g.gpu<HeadOnly>("h");
+    g.gpu<Check>("cu");
+    g.line({"src", "in", "h", "cu"});
+    expect("head_only", chains(g), "in[in] h[h,cu] cu[cu]*");
 }
 
 // a member pushed into by two outputs cannot join: it heads its own chain
@@ -395,6 +413,7 @@ int main()
     fake_iprouter();
     five_then_set();
     combos();
+    head_only();
     two_upstreams();
     devices();
     chain_false();

@@ -13,7 +13,9 @@
 // IPFragmenter extras; IPOutputCombo when the copy fails; a failed flush
 // and its retry; the retry limit; a downstream element that pushes back into
 // the element while it delivers; four threads each polling its own state
-// (packets delivered on their own thread only); cleanup of a held batch.
+// (packets delivered on their own thread only); cleanup of a held batch;
+// chains of five elements and of the combos (IPOutputCombo a member after
+// the head: its clones from the bytes the glue kept) against the elements.
 // Prints one line per scenario and exits nonzero if any fails.
 #include <algorithm>
 #include <atomic>
@@ -937,6 +939,78 @@ void chain_vs_elements(uint32_t batch, uint32_t flush_every)
     report(label.c_str(), ok);
 }
 
+// 13. the combos as one chain: IPInputCombo(1) -> IPOutputCombo(1, ..., 600)
+//     run by the core, against the two classes as separate elements.
+//     IPOutputCombo is a member after the head, so its PaintTee clone (most
+//     packets: IPInputCombo paints COLOR 1) is the bytes the glue kept as the
+//     packet reached it, with the packet's annotations at that point; every
+//     output (the clones on output 1 included) byte for byte, with lengths,
+//     network header and annotations; the handlers agree.
+void combos_chain_vs_elements(uint32_t batch)
+{
+    bool ok = true;
+    const int n = 2000;
+    const std::string B = "BATCH " + std::to_string(batch);
+    const std::string OC = std::string("1, ") + MY_IP_TXT + ", 600, " + B;
+    Member<InputComboC> c0("IPInputCombo", "1, " + B, 1);
+    Member<OutComboC> c1("IPOutputCombo", OC, 5);
+    c0.cls.color = c1.cls.color = 1;
+    ChainHost ch({&c0, &c1});
+    Host<InputComboC> h0("IPInputCombo", "1, " + B, 1);
+    Host<OutComboC> h1("IPOutputCombo", OC, 5);
+    h0.cls.color = h1.cls.color = 1;
+    for (int i = 0; i < n; i++) {
+        std::vector<uint8_t> b = ip_bytes(40 + (uint32_t)(i * 37) % 1300, i);
+        if (i % 7 == 3)
+            b = with_options(b, 1 + i % 4);
+        if (i % 11 == 5) {                           // TTL 0-2: IPOutputCombo's output 3
+            b[8] = (uint8_t)(i % 3);
+            oracle_set_ip_checksum(b.data(), (uint32_t)b.size());
+        }
+        if (i % 13 == 6)
+            b[12] ^= 1;                              // a bad checksum: IPInputCombo kills it
+        std::vector<uint8_t> f(14, 0);
+        f[0] = (uint8_t)i, f[12] = 0x08;
+        f.insert(f.end(), b.begin(), b.end());
+        for (int run = 0; run < 2; run++) {
+            TPacket *p = make(f.data(), f.size(), i);
+            p->a.fix_src = i % 5 == 0;
+            p->a.bcast = i % 17 == 2;                // DropBroadcasts: killed, no clone
+            p->a.paint = (uint32_t)(i % 3);
+            if (run == 0)
+                ch.push(p);
+            else
+                h0.push(p);
+        }
+    }
+    ch.timer();
+    h0.timer();
+    for (TPacket *p : h0.out[0])
+        h1.push(p);
+    h0.out[0].clear();
+    h1.timer();
+    std::vector<std::vector<std::vector<TPacket *> > *> sep = {&h0.out, &h1.out};
+    for (size_t k = 0; k < 2; k++)
+        for (size_t q = 0; q < 5; q++) {
+            const std::vector<TPacket *> &x = ch.m[k]->out[q], &y = (*sep[k])[q];
+            CHECK(x.size() == y.size());
+            for (size_t j = 0; j < x.size() && j < y.size(); j++)
+                if (!same_packet(x[j], y[j])) {
+                    std::printf("  member %zu port %zu #%zu: id %ld / %ld\n", k, q, j, x[j]->a.id, y[j]->a.id);
+                    CHECK(same_packet(x[j], y[j]));
+                    break;
+                }
+        }
+    CHECK(ch.m[1]->out[1].size() > (size_t)n / 2);   // the clones
+    CHECK(!ch.m[1]->out[0].empty() && !ch.m[1]->out[3].empty());
+    for (const char *h : {"drops", "packets", "lost"}) {
+        CHECK(ch.handler(0, h) == h0.handler(h));
+        CHECK(ch.handler(1, h) == h1.handler(h));
+    }
+    CHECK(ch.runcount == 0 && h0.runcount == 0 && h1.runcount == 0);
+    report(("combos_chain_matches_separate_elements_batch_" + std::to_string(batch)).c_str(), ok);
+}
+
 }   // namespace
 
 int main()
@@ -967,6 +1041,8 @@ int main()
     chain_vs_elements(65536, 0);
     chain_vs_elements(300, 0);
     chain_vs_elements(1000, 777);
+    combos_chain_vs_elements(65536);
+    combos_chain_vs_elements(300);
     std::printf("live packets at exit: %ld\n", (long)g_live);
     return g_fail ? 1 : 0;
 }

@@ -4,7 +4,7 @@
 elements run as one clk_chain (hipbatch.cc applies it over Click's Router at
 initialize()).  `tests/native/chain_form_test.cc` instantiates the same
 templates over router graphs built in the test -- conf/fake-iprouter.click's
-interface path, the five elements back to back, the combos, two upstreams,
+interface path, the five elements back to back, the combos (IPOutputCombo a member), a head-only class, two upstreams,
 DEVICE and CHAIN differences, other ports, pull context, a ring, a line
 longer than the pass report's 64 members -- with the shipped class traits
 (hipclasses.hh), and checks each chain and the head's packet readying.
@@ -25,4 +25,4 @@ def test_chain_formation_rules(tmp_path):
     assert r.returncode == 0, r.stdout + r.stderr
     lines = r.stdout.splitlines()
     assert lines[-1] == "ALL OK"
-    assert sum(ln.startswith("PASS ") for ln in lines) == 17
+    assert sum(ln.startswith("PASS ") for ln in lines) == 19

@@ -59,7 +59,7 @@ def run_separate(ctx, spec, arena, foff, flen, nh0, anno):
     passed on output 0 (views as the Click adapters leave them: CheckIPHeader
     sets the network header at OFFSET, IPInputCombo strips 14 bytes).
     Returns the results in the chain's order and the elements."""
-    from click_amd.elements import AUX_CLONE
+    from click_amd.elements import AUX_CLONE, ANNO_BCAST
     els = make(ctx, spec)
     base = arena.ctypes.data
     n = len(foff)
@@ -69,7 +69,14 @@ def run_separate(ctx, spec, arena, foff, flen, nh0, anno):
     anno = [int(a) for a in anno]
     out = []                                    # member-major: each member's results in its own order
     alive = list(range(n))
+    clones = {}                                 # (member, token): the bytes as they reached the member
     for k, e in enumerate(els):
+        if spec[k][0] == "IPOutputCombo" and k > 0:
+            color = int(spec[k][1].split(",")[0])
+            for i in alive:
+                if not anno[i] & ANNO_BCAST and (anno[i] >> 8) & 0xFF == color and spec[k][2] >= 2:
+                    o = ptr[i] - base
+                    clones[(k, i)] = bytes(arena[o:o + ln[i]])
         for i in alive:
             rc = e.lib.clk_element_push_anno(e.h, ctypes.c_void_p(ptr[i]), ln[i], nh[i], anno[i], i)
             assert rc >= 0
@@ -101,10 +108,14 @@ def run_separate(ctx, spec, arena, foff, flen, nh0, anno):
                 continue
             out.append((t, k, p, l_, a))
         alive = nxt
+    run_separate.clones = clones
     return out, els
 
 
-def run_chain(ctx, spec, arena, foff, flen, nh0, anno, batch_flush=None):
+def run_chain(ctx, spec, arena, foff, flen, nh0, anno, batch_flush=None, async_flush=False):
+    """The chain over the frames; a full batch (or every batch_flush
+    packets) flushed with clk_chain_flush, or double-buffered with
+    clk_chain_flush_async (async_flush), then everything flushed."""
     from click_amd.elements import Chain
     els = make(ctx, spec)
     ch = Chain(els)
@@ -112,18 +123,19 @@ def run_chain(ctx, spec, arena, foff, flen, nh0, anno, batch_flush=None):
     for i in range(len(foff)):
         if ch.push_anno(base + int(foff[i]), int(flen[i]), nh0, int(anno[i]), i) or \
                 (batch_flush and (i + 1) % batch_flush == 0):
-            ch.flush()
+            ch.flush_async() if async_flush else ch.flush()
     ch.flush()
     tok, mem, port, length, aux = ch.results()
     return list(zip(tok.tolist(), mem.tolist(), port.tolist(), length.tolist(), aux.tolist())), els, ch
 
 
 def compare_chain(ctx, spec, arena, foff, flen, nh0=-1, anno=None, batch_flush=None,
-                  handlers=("drops", "fragments", "packets", "lost")):
+                  handlers=("drops", "fragments", "packets", "lost"), async_flush=False):
+    from click_amd.elements import AUX_CLONE
     anno = np.zeros(len(foff), np.uint32) if anno is None else anno
     a1, a2 = arena.copy(), arena.copy()
     r1, e1 = run_separate(ctx, spec, a1, foff, flen, nh0, anno)
-    r2, e2, ch = run_chain(ctx, spec, a2, foff, flen, nh0, anno, batch_flush)
+    r2, e2, ch = run_chain(ctx, spec, a2, foff, flen, nh0, anno, batch_flush, async_flush)
     assert len(r1) == len(r2)
     # each member's results in its own (push) order, as the elements one by
     # one give them (a chain flush interleaves members batch by batch)
@@ -135,10 +147,16 @@ def compare_chain(ctx, spec, arena, foff, flen, nh0=-1, anno=None, batch_flush=N
             if x[:4] != y[:4]:
                 raise AssertionError(("first difference", x, y))
     assert np.array_equal(a1, a2), np.nonzero(a1 != a2)[0][:10]
-    for k in range(len(spec)):                  # new packets (fragments), byte for byte
+    clones = run_separate.clones
+    for k in range(len(spec)):                  # new packets (fragments, clones), byte for byte
         for x, y in zip([x for x in r1 if x[1] == k], [y for y in r2 if y[1] == k]):
             if spec[k][0] == "IPFragmenter" and x[4] != 0:
                 assert e1[k].take_packet(x[4]) == e2[k].take_packet(y[4])
+            if spec[k][0] == "IPOutputCombo" and k > 0 and x[4] == AUX_CLONE and x[2] == 1:
+                # a member after the head: its PaintTee clone carries the
+                # bytes as they reached it (clk_element_take_packet)
+                assert y[4] & AUX_CLONE and y[4] != AUX_CLONE, y
+                assert e2[k].take_packet(y[4] & ~AUX_CLONE) == clones[(k, y[0])]
         for h in handlers:
             assert e1[k].read_handler(h) == e2[k].read_handler(h), (spec[k][0], h)
         assert e1[k].messages() == e2[k].messages(), spec[k][0]
@@ -226,6 +244,29 @@ def test_fuzzed_element_chain(ctx, batch_flush):
     assert {(0, 1), (1, 1), (3, 1), (4, 0)} <= seen, seen
 
 
+@pytest.mark.parametrize("which", ["elements", "combos"])
+def test_chain_double_buffered(ctx, which):
+    """clk_chain_flush_async: a full batch is launched while the one before
+    it is finished, two batches in flight (BATCH 1000 and 777 on the head,
+    so 6000 frames make 6-8 batches): every member's results in push
+    order, bytes, clones and handlers as the elements one by one."""
+    from click_amd.elements import ANNO_BCAST, anno_paint
+    if which == "elements":
+        rng, arena, foff, flen = fuzzed_frames(21, n=6000)
+        anno = (rng.random(len(foff)) < 0.3).astype(np.uint32)
+        spec = [("CheckIPHeader", "OFFSET 14, DETAILS true, BATCH 1000", 2), ("IPGWOptions", MY_IP_TXT, 2),
+                ("FixIPSrc", MY_IP_TXT, 1), ("DecIPTTL", "", 2), ("IPFragmenter", "576, HONOR_DF true", 2)]
+    else:
+        rng, arena, foff, flen = fuzzed_frames(23, n=6000)
+        n = len(foff)
+        anno = np.array([anno_paint(int(p)) for p in rng.integers(0, 3, n)], np.uint32) + \
+            (rng.random(n) < 0.05) * ANNO_BCAST + (rng.random(n) < 0.2).astype(np.uint32)
+        spec = [("IPInputCombo", "1, BATCH 777", 1), ("IPOutputCombo", "1, %s, 120" % MY_IP_TXT, 5)]
+    for async_flush in (False, True):
+        compare_chain(ctx, spec, arena, foff, flen, anno=anno, async_flush=async_flush,
+                      handlers=("drops", "packets", "lost"))
+
+
 def test_fuzzed_combos_chain(ctx):
     from click_amd.elements import ANNO_BCAST, anno_paint
     rng, arena, foff, flen = fuzzed_frames(9)
@@ -253,7 +294,9 @@ def test_chain_failed_flush(ctx, nth):
     6 DecIPTTL's descriptors, 8 its verdicts back).  Before any kernel of a
     member that is not idempotent ran (1-6): nothing is routed, nothing
     written, push() refuses packets, and the next flush resumes and routes
-    every packet exactly as a chain that never failed.  After DecIPTTL's
+    every packet exactly as a chain that never failed.  A push meanwhile
+    retries the failed flush first and is staged once that goes through
+    (no packet lost to a transient failure).  After DecIPTTL's
     kernel (8): its packets are killed, never decremented twice."""
     from click_amd import ClickAmdError
     from click_amd.elements import Chain
@@ -281,12 +324,12 @@ def test_chain_failed_flush(ctx, nth):
         assert len(ch.results()[0]) == 0
     else:
         assert len(tok) == 0 and np.array_equal(arena, before)
-        if nth > 1:                              # a member failed: the chain holds its packets
-            with pytest.raises(ClickAmdError):
-                ch.push_anno(base, int(flen[0]), -1, 0, 99999)
+        extra, _, _ = fake_frames(1)             # a packet pushed before the retry
+        ch.push_anno(extra.ctypes.data, len(extra), -1, 0, 99999)
         ch.flush()
         tok, mem, port, _, _ = ch.results()
-        assert len(tok) == 3000 and (mem == 4).all() and (port == 0).all()
+        assert len(tok) == 3001 and (mem == 4).all() and (port == 0).all()
+        assert tok.tolist() == list(range(3000)) + [99999]
         ref = before.copy()                     # the same frames through a chain that never failed
         run_chain(ctx, FAKE_IPROUTER, ref, foff, flen, -1, np.zeros(len(foff), np.uint32))
         assert np.array_equal(arena, ref)
@@ -298,7 +341,7 @@ def test_zerocopy_chain(ctx, which):
     """ZEROCOPY chains: the members' kernels read and rewrite the packets in
     registered host memory; routes, lengths, bytes and handlers equal the
     staged elements one by one."""
-    from click_amd.elements import ANNO_BCAST, anno_paint
+    from click_amd.elements import ANNO_BCAST, AUX_CLONE, anno_paint
     if which == "fuzzed":
         rng, arena0, foff, flen = fuzzed_frames(77)
         n = len(foff)
@@ -318,10 +361,14 @@ def test_zerocopy_chain(ctx, which):
     try:
         zspec = [(c, ", ".join(x for x in (conf, "ZEROCOPY true") if x), k) for c, conf, k in spec]
         r2, e2, ch = run_chain(ctx, zspec, a2, foff, flen, -1, anno)
+        clones = run_separate.clones
         for k in range(len(spec)):
             x1 = [x[:4] for x in r1 if x[1] == k]
             x2 = [y[:4] for y in r2 if y[1] == k]
             assert x1 == x2, spec[k][0]
+            for y in r2:                        # clones of a member after the head: the bytes it saw
+                if y[1] == k and k > 0 and spec[k][0] == "IPOutputCombo" and y[4] & AUX_CLONE:
+                    assert e2[k].take_packet(y[4] & ~AUX_CLONE) == clones[(k, y[0])]
             for h in ("drops", "packets", "lost"):
                 assert e1[k].read_handler(h) == e2[k].read_handler(h), (spec[k][0], h)
         assert np.array_equal(a1, a2), np.nonzero(a1 != a2)[0][:10]
@@ -409,11 +456,12 @@ def test_chain_copy_back_failure(ctx):
         hook(0)
     tok, mem, port, _, _ = ch.results()
     assert len(tok) == 0
-    with pytest.raises(ClickAmdError):
-        ch.push_anno(base, int(flen[0]), -1, 1, 99999)
-    ch.flush()
+    extra, _, _ = fake_frames(1)                 # a push retries the copy back first, then is staged
+    ch.push_anno(extra.ctypes.data, len(extra), -1, 1, 99999)
     tok, mem, port, _, _ = ch.results()
     assert len(tok) == 3000 and (mem == 4).all() and (port == 0).all()
+    ch.flush()
+    assert ch.results()[0].tolist() == [99999]
     ref = before.copy()
     run_chain(ctx, FAKE_IPROUTER, ref, foff, flen, -1, np.ones(len(foff), np.uint32))
     assert np.array_equal(arena, ref) and not np.array_equal(arena, before)

@@ -122,6 +122,7 @@ int clk_chain_flush(clk_chain *c)
     c->staged.clear();
     return CLK_SUCCESS;
 }
+int clk_chain_flush_async(clk_chain *c) { return clk_chain_flush(c); }
 uint64_t clk_chain_abandon(clk_chain *) { return 0; }
 uint64_t clk_chain_results(clk_chain *c, uint64_t *tok, int32_t *mem, int32_t *port, uint32_t *len, uint32_t *aux,
                            uint64_t cap)
