@@ -612,10 +612,13 @@ int Chain::step(Batch &B)
         }
         e->chain_prep(w);                            // the packets members before it passed on
         stats_[6] += now_s() - t0;
-        if (w.clone_key) {                           // clones of the packets as they reach member k
+        if (w.clones) {                              // clones of the packets as they reach member k
+            w.clones = false;
             const int r = keep_clones(B, k);
-            if (r)
+            if (r) {
+                M.rebuild = true;                    // (the prep loop finds them again)
                 return fail(B, r);
+            }
         }
         if (w.n) {
             B.launched = false;

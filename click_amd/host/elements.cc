@@ -292,12 +292,14 @@ int BatchElement::grow_dev(Stage &g, size_t bytes, size_t n)
 
 void BatchElement::chain_prep(ChainWork &w)
 {
-    chain_prep_loop(w, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); });
+    chain_prep_loop(w, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); },
+                    [this](const ChainView &v) { return pre_clone(v); });
 }
 
 void BatchElement::chain_route_all(ChainWork &w)
 {
-    chain_route_loop(w, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
+    chain_route_loop(w, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); },
+                     [this](Pending &p, Result *r) { return pre_route(p, r); });
 }
 
 template <class SpanF>

@@ -213,6 +213,7 @@ struct ChainWork {
     int32_t nh_after = -2;
     uint8_t pass = CHAIN_PASS_NONE;           // ChainPass, with pass_param
     uint32_t pass_param = 0;
+    bool clones = false;                      // the prep loop met a packet to clone (clone_key)
     uint32_t *clone_key = nullptr;            // a member after the head with pre results (IPOutputCombo's
                                               // PaintTee clone): per chain packet, the key of the bytes
                                               // as they reached the member (Chain::run_member), 0: none
@@ -224,6 +225,7 @@ struct ChainWork {
     {
         nreached = 0;
         nprep = 0;
+        clones = false;
         routed = 0;
         n = 0;
         maxlen = 0;
@@ -267,11 +269,12 @@ struct ChainWork {
     {                                                                                                           \
         chain_prep_loop(w_, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {                     \
             return this->C::span(p, o, l, c);                                                                   \
-        });                                                                                                     \
+        }, [this](const ChainView &v) { return this->C::pre_clone(v); });                                        \
     }                                                                                                           \
     void chain_route_all(ChainWork &w_) override                                                               \
     {                                                                                                           \
-        chain_route_loop(w_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
+        chain_route_loop(w_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }, \
+                         [this](Pending &p, Result *r) { return this->C::pre_route(p, r); });                   \
     }
 
 class Chain;
@@ -374,8 +377,8 @@ class BatchElement {
     }
     bool chain_ = false;             // a chain runs the element (it copies the rewritten bytes back)
     std::vector<Chain *> chains_;    // the chains the element is a member of (detached when it goes)
-    template <class SpanF>
-    void chain_prep_loop(ChainWork &w, SpanF &&span_f);
+    template <class SpanF, class CloneF>
+    void chain_prep_loop(ChainWork &w, SpanF &&span_f, CloneF &&clone_f);
     // a pass rule's pass: counted, on to member k+1 (the last member: a
     // result on output 0)
     void chain_pass_on(ChainWork &w, uint32_t i)
@@ -410,12 +413,13 @@ class BatchElement {
         }
         n->reached[n->nreached++] = i;
     }
-    template <class RouteF>
-    bool chain_route_at(ChainWork &w, size_t q, RouteF &&route_f);
-    template <class RouteF>
-    void chain_route_loop(ChainWork &w, RouteF &&route_f);
-    template <class RouteF>
-    bool chain_route_pending(ChainWork &w, uint32_t i, Pending &p, int code, uint16_t sum, RouteF &&route_f);
+    template <class RouteF, class PreF>
+    bool chain_route_at(ChainWork &w, size_t q, RouteF &&route_f, PreF &&pre_f);
+    template <class RouteF, class PreF>
+    void chain_route_loop(ChainWork &w, RouteF &&route_f, PreF &&pre_f);
+    template <class RouteF, class PreF>
+    bool chain_route_pending(ChainWork &w, uint32_t i, Pending &p, int code, uint16_t sum, RouteF &&route_f,
+                             PreF &&pre_f);
     ResultQueue chain_side_;          // a member's pre/post results while a chain routes
     friend class Chain;
     // after the batch completed, before any packet is routed: nonzero fails
@@ -835,8 +839,8 @@ class IPFragmenter : public BatchElement {
 // The packets that reached the member and were not looked at yet: a pass
 // rule's pass, or the class's span() -- a descriptor of the member's batch
 // (the bytes to copy back grown for a writing member) or a host decision.
-template <class SpanF>
-inline void BatchElement::chain_prep_loop(ChainWork &w, SpanF &&span_f)
+template <class SpanF, class CloneF>
+inline void BatchElement::chain_prep_loop(ChainWork &w, SpanF &&span_f, CloneF &&clone_f)
 {
     for (size_t q = w.nprep; q < w.nreached; q++) {
         const uint32_t i = w.reached[q];
@@ -851,6 +855,8 @@ inline void BatchElement::chain_prep_loop(ChainWork &w, SpanF &&span_f)
             }
             continue;
         }
+        if (w.clone_key && !w.clones && clone_f(v))   // a clone to keep before the kernel runs
+            w.clones = true;
         Pending p{v.data, v.token, v.slot, v.length, v.nh, 0, 0, 0, -1, v.anno};
         uint32_t off = 0, len = 0;
         int32_t hc = 0;
@@ -878,13 +884,13 @@ inline void BatchElement::chain_prep_loop(ChainWork &w, SpanF &&span_f)
     w.nprep = w.nreached;
 }
 
-template <class RouteF>
+template <class RouteF, class PreF>
 inline bool BatchElement::chain_route_pending(ChainWork &w, uint32_t i, Pending &p, int code, uint16_t sum,
-                                              RouteF &&route_f)
+                                              RouteF &&route_f, PreF &&pre_f)
 {
     ChainView &v = w.views[i];
     Result pr;
-    if (has_pre_route_ && pre_route(p, &pr)) {
+    if (has_pre_route_ && pre_f(p, &pr)) {
         uint32_t aux = pr.aux;
         if (w.clone_key && w.clone_key[i]) {  // the clone's bytes, kept as it reached this member
             aux = CLK_AUX_CLONE | w.clone_key[i];
@@ -922,8 +928,8 @@ inline bool BatchElement::chain_route_pending(ChainWork &w, uint32_t i, Pending 
     return pass;
 }
 
-template <class RouteF>
-inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_f)
+template <class RouteF, class PreF>
+inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_f, PreF &&pre_f)
 {
     const uint32_t i = w.reached[q];
     const int32_t c = w.code[q];
@@ -931,7 +937,7 @@ inline bool BatchElement::chain_route_at(ChainWork &w, size_t q, RouteF &&route_
     const ChainView &v = w.views[i];
     Pending p{v.data, v.token, v.slot, v.length, v.nh, w.span_off[q], w.span_len[q], c >= 0 ? (uint32_t)c : 0u,
               (int16_t)(c >= 0 ? -1 : code), v.anno};
-    return chain_route_pending(w, i, p, code, c >= 0 && w.h_sums ? w.h_sums[c] : 0, route_f);
+    return chain_route_pending(w, i, p, code, c >= 0 && w.h_sums ? w.h_sums[c] : 0, route_f, pre_f);
 }
 
 BatchElement *make_element(clk_ctx *ctx, const std::string &cls, const std::string &name, int noutputs);
@@ -1058,8 +1064,8 @@ class Chain {
     std::string err_;
 };
 
-template <class RouteF>
-void BatchElement::chain_route_loop(ChainWork &w, RouteF &&route_f)
+template <class RouteF, class PreF>
+void BatchElement::chain_route_loop(ChainWork &w, RouteF &&route_f, PreF &&pre_f)
 {
     for (size_t q = w.routed; q < w.nreached; q++) {
         w.routed = q + 1;
@@ -1068,7 +1074,7 @@ void BatchElement::chain_route_loop(ChainWork &w, RouteF &&route_f)
         const uint32_t i = w.reached[q];
         if (w.code[q] == CHAIN_CODE_PASS)
             chain_pass_on(w, i);
-        else if (chain_route_at(w, q, route_f) && !w.last)
+        else if (chain_route_at(w, q, route_f, pre_f) && !w.last)
             chain_forward(w, i);
     }
 }

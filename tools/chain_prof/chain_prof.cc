@@ -4,7 +4,7 @@
 // can be profiled with gprof (tools/chain_prof/run.sh builds the glue's host
 // files into this executable with -pg).  Prints the median Mpps of the timed
 // runs and clk_chain_stats.
-//   chain_prof FRAME_HEX [RUNS] [BATCH]
+//   chain_prof FRAME_HEX [RUNS] [BATCH] [combos]
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -30,9 +30,14 @@ int main(int argc, char **argv)
         return 0;
     }
     struct Spec { const char *cls, *conf; int nout; };
-    const Spec spec[] = {{"CheckIPHeader", "INTERFACES 18.26.4.1/24 18.26.7.1/24, OFFSET 14", 2},
-                         {"IPGWOptions", "18.26.4.24", 2}, {"FixIPSrc", "18.26.4.24", 1},
-                         {"DecIPTTL", "", 2}, {"IPFragmenter", "300", 2}};
+    const bool combos = argc > 4 && std::string(argv[4]) == "combos";
+    const std::vector<Spec> spec = combos
+        ? std::vector<Spec>{{"IPInputCombo", "2, INTERFACES 18.26.4.1/24 18.26.7.1/24", 1},
+                            {"IPOutputCombo", "1, 18.26.4.24, 300", 5}}
+        : std::vector<Spec>{{"CheckIPHeader", "INTERFACES 18.26.4.1/24 18.26.7.1/24, OFFSET 14", 2},
+                            {"IPGWOptions", "18.26.4.24", 2}, {"FixIPSrc", "18.26.4.24", 1},
+                            {"DecIPTTL", "", 2}, {"IPFragmenter", "300", 2}};
+    const int last = (int)spec.size() - 1;
     std::vector<clk_element *> els;
     for (const Spec &s : spec) {
         clk_element *e = nullptr;
@@ -68,7 +73,7 @@ int main(int argc, char **argv)
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         fwd = 0;
         for (uint64_t j = 0; j < k; j++)
-            fwd += mem[j] == 4 && port[j] == 0;
+            fwd += mem[j] == last && port[j] == 0;
         if (r)
             mpps.push_back(n / s / 1e6);
     }
@@ -76,8 +81,8 @@ int main(int argc, char **argv)
     std::sort(sorted.begin(), sorted.end());
     double st[8] = {0};
     clk_chain_stats(c, st, 8);
-    std::printf("{\"leg\": \"elements_chain\", \"forwarded\": %llu, \"mpps\": %.2f, \"runs_mpps\": [",
-                (unsigned long long)fwd, sorted[sorted.size() / 2]);
+    std::printf("{\"leg\": \"%s_chain\", \"forwarded\": %llu, \"mpps\": %.2f, \"runs_mpps\": [",
+                combos ? "combos" : "elements", (unsigned long long)fwd, sorted[sorted.size() / 2]);
     for (size_t k = 0; k < mpps.size(); k++)
         std::printf("%s%.2f", k ? ", " : "", mpps[k]);
     const double per = 1e9 / ((runs + 1) * (double)n);

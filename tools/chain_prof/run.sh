@@ -19,7 +19,7 @@ if [ "$1" = build ]; then
     python3 -c "import sys; sys.path.insert(0, '$R'); import bench; print(bench.c1_frame().hex())" > $B/frame.hex
 else
     cd $B
-    ./chain_prof $(cat frame.hex) ${RUNS:-5} ${BATCH:-65536}
+    ./chain_prof $(cat frame.hex) ${RUNS:-5} ${BATCH:-65536} ${CHAIN:-elements}
     gprof -b -p ./chain_prof gmon.out 2>/dev/null | head -${TOP:-30}
     gprof -b -p -l ./chain_prof gmon.out 2>/dev/null | head -${TOP:-30}
 fi
