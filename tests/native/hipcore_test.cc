@@ -1011,6 +1011,85 @@ void combos_chain_vs_elements(uint32_t batch)
     report(("combos_chain_matches_separate_elements_batch_" + std::to_string(batch)).c_str(), ok);
 }
 
+// 14. converging outputs (fake-iprouter.click: several members' error
+//     outputs reach one element, ICMPError -> rt): CheckIPHeader's output 1
+//     (bad checksums) and DecIPTTL's output 1 (expired TTLs) of one chain
+//     push into one recording sink.  The reference pushes depth first, so
+//     the sink would see the drops in push (token) order
+//     (element.cc:2891-2896).  A chain hands its results out a batch at a
+//     time, each member's in push order, member after member: the contract
+//     (INTEGRATION.md "Ordering") is that the sink sees, batch by batch,
+//     CheckIPHeader's drops of the batch in push order, then DecIPTTL's.
+//     Asserted exactly, for the batches the flushes formed; the same drops,
+//     each member's in push order, as the reference's.
+void converging_outputs(uint32_t batch)
+{
+    bool ok = true;
+    const int n = 3000;
+    const std::string B = "BATCH " + std::to_string(batch);
+    Member<CheckIPC> c0("CheckIPHeader", B, 2);
+    Member<GWOptC> c1("IPGWOptions", std::string(MY_IP_TXT) + ", " + B, 2);
+    Member<FixSrcC> c2("FixIPSrc", std::string(MY_IP_TXT) + ", " + B, 1);
+    Member<DecTTLC> c3("DecIPTTL", B, 2);
+    Member<FragC> c4("IPFragmenter", "1500, " + B, 2);
+    c4.cls.mtu = 1500;
+    ChainHost ch({&c0, &c1, &c2, &c3, &c4});
+    std::vector<std::pair<int, long> > sink;         // (member, packet id) as they arrive
+    size_t other = 0;
+    ch.sink = [&](int k, int port, TPacket *p) {
+        if (port == 1 && (k == 0 || k == 3))
+            sink.emplace_back(k, p->a.id);
+        else
+            other++;
+        TOps::kill(p);
+    };
+    std::vector<int> drop_at(n, -1);                 // the member that drops packet i (-1: none)
+    for (int i = 0; i < n; i++) {
+        std::vector<uint8_t> b = ip_bytes(60 + (uint32_t)(i * 29) % 900, i);
+        if (i % 11 == 5) {                           // TTL 0-1: DecIPTTL's output 1
+            b[8] = (uint8_t)(i % 2);
+            oracle_set_ip_checksum(b.data(), (uint32_t)b.size());
+            drop_at[i] = 3;
+        }
+        if (i % 13 == 6) {                           // a bad checksum: CheckIPHeader's output 1
+            b[12] ^= 1;
+            drop_at[i] = 0;
+        }
+        TPacket *p = make(b.data(), b.size(), i);
+        p->nh = 0;
+        ch.push(p);
+    }
+    ch.timer();
+    // the contract: batch by batch (the flushes' batches: BATCH packets in
+    // push order), member 0's drops in push order, then member 3's
+    std::vector<std::pair<int, long> > want, ref;
+    for (int b0 = 0; b0 < n; b0 += (int)batch)
+        for (int k : {0, 3})
+            for (int i = b0; i < n && i < b0 + (int)batch; i++)
+                if (drop_at[i] == k)
+                    want.emplace_back(k, i);
+    for (int i = 0; i < n; i++)                      // the reference's depth-first order
+        if (drop_at[i] >= 0)
+            ref.emplace_back(drop_at[i], i);
+    CHECK(sink == want);
+    std::vector<std::pair<int, long> > a = sink, r = ref;
+    std::sort(a.begin(), a.end());
+    std::sort(r.begin(), r.end());
+    CHECK(a == r);                                   // the same drops at the same members
+    for (int k : {0, 3}) {                           // each member's in push order
+        long last = -1;
+        for (auto &x : sink)
+            if (x.first == k) {
+                CHECK(x.second > last);
+                last = x.second;
+            }
+    }
+    CHECK(other + sink.size() == (size_t)n);
+    std::printf("  converging sink: %zu drops, %s the reference's order\n", sink.size(),
+                sink == ref ? "equal to" : "batch-major, not");
+    report(("converging_outputs_batch_order_" + std::to_string(batch)).c_str(), ok);
+}
+
 }   // namespace
 
 int main()
@@ -1043,6 +1122,8 @@ int main()
     chain_vs_elements(1000, 777);
     combos_chain_vs_elements(65536);
     combos_chain_vs_elements(300);
+    converging_outputs(300);
+    converging_outputs(65536);
     std::printf("live packets at exit: %ld\n", (long)g_live);
     return g_fail ? 1 : 0;
 }

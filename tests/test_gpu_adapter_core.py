@@ -32,7 +32,8 @@ SCENARIOS = ["class_" + c for c in CLASSES] + [
     "four_threads_each_delivered_on_its_own_thread", "cleanup_kills_held_packets_pushes_nothing",
     "chain_of_five_matches_separate_elements_batch_65536", "chain_of_five_matches_separate_elements_batch_300",
     "chain_of_five_matches_separate_elements_batch_1000_flush_777",
-    "combos_chain_matches_separate_elements_batch_65536", "combos_chain_matches_separate_elements_batch_300"]
+    "combos_chain_matches_separate_elements_batch_65536", "combos_chain_matches_separate_elements_batch_300",
+    "converging_outputs_batch_order_300", "converging_outputs_batch_order_65536"]
 
 
 def test_adapter_core_on_gpu():
