@@ -75,7 +75,7 @@ HIPBatchElement::~HIPBatchElement()
     delete[] _pt;
     delete[] _chain_tried;
     if (_tasks) {
-	for (int k = 0; k < _npt; k++)
+	for (int k = 0; k <= _npt; k++)
 	    _tasks[k].~Task();
 	operator delete[](static_cast<void *>(_tasks));
     }
@@ -143,16 +143,25 @@ HIPBatchElement::ensure(PerThread &t, ErrorHandler *errh)
 int
 HIPBatchElement::initialize(ErrorHandler *errh)
 {
+    // one state per RouterThread, driven by that thread alone (no lock:
+    // hipcore State::shared), plus a locked catch-all state for a push from
+    // a thread id past them
     _npt = click_max_cpu_ids();
-    _pt = new PerThread[_npt];
+    _pt = new PerThread[_npt + 1];
+    for (int k = 0; k < _npt; k++)
+	_pt[k].shared = false;
+    _pt[_npt].id = _npt;
+    _pt[_npt].shared = true;
     // one Task per state, moved to its RouterThread (task.hh:275), not
-    // scheduled until the state holds packets (hipcore: wake / poll)
-    _tasks = static_cast<Task *>(operator new[](sizeof(Task) * _npt));
-    for (int k = 0; k < _npt; k++) {
+    // scheduled until the state holds packets (hipcore: wake / poll); the
+    // catch-all state's stays on the element's home thread
+    _tasks = static_cast<Task *>(operator new[](sizeof(Task) * (_npt + 1)));
+    for (int k = 0; k <= _npt; k++) {
 	_pt[k].id = k;
 	new (&_tasks[k]) Task(this);
 	_tasks[k].initialize(this, false);
-	_tasks[k].move_thread(k);
+	if (k < _npt)
+	    _tasks[k].move_thread(k);
     }
     // the home thread's glue element now: configuration errors surface at
     // initialize time, as the reference element's configure() errors do
@@ -177,8 +186,8 @@ HIPBatchElement::initialize(ErrorHandler *errh)
     // a chain head collects the members down output 0 (the connections and
     // every element's configuration exist now; the states set their chains
     // up on first use, when every member is initialized)
-    _chain_tried = new bool[_npt];
-    for (int k = 0; k < _npt; k++)
+    _chain_tried = new bool[_npt + 1];
+    for (int k = 0; k <= _npt; k++)
 	_chain_tried[k] = false;
     HIPChainGraph g;
     hipcore::form_chain(g, this, _chain);
@@ -251,7 +260,7 @@ HIPBatchElement::PerThread &
 HIPBatchElement::state()
 {
     int thread = click_current_cpu_id();
-    PerThread &t = _pt[thread >= 0 && thread < _npt ? thread : 0];
+    PerThread &t = _pt[thread >= 0 && thread < _npt ? thread : _npt];
     if (!t.e) {
 	t.lock.acquire();
 	ensure(t, 0);			// no GPU for this thread: the core kills its packets
@@ -283,7 +292,7 @@ HIPBatchElement::run_task(Task *task)
 {
     // state k's latency deadline, on state k's RouterThread
     int k = task - _tasks;
-    if (k < 0 || k >= _npt)
+    if (k < 0 || k > _npt)
 	return false;
     if (_core.poll(*this, _pt[k]))
 	task->fast_reschedule();	// still holding packets: look again
@@ -314,7 +323,7 @@ HIPBatchElement::cleanup(CleanupStage)
     // nothing is pushed downstream: held, routed-but-undelivered and ready
     // packets are killed, the glue elements and contexts destroyed (the
     // members' copies taken out of their handler sums first)
-    for (int k = 0; k < _npt; k++) {
+    for (int k = 0; k <= _npt; k++) {
 	for (size_t m = 1; m < _pt[k].mem.size() && (int) m < _chain.size(); m++) {
 	    HIPBatchElement *y = _chain[m];
 	    y->_borrow_lock.acquire();
@@ -333,7 +342,7 @@ HIPBatchElement::cleanup(CleanupStage)
 String
 HIPBatchElement::glue_handler(const char *hname) const
 {
-    for (int k = 0; k < _npt; k++)
+    for (int k = 0; k <= _npt; k++)
 	if (_pt[k].e) {
 	    char buf[4096];
 	    clk_element_read_handler(_pt[k].e, hname, buf, sizeof(buf));
@@ -351,7 +360,7 @@ HIPBatchElement::read_handler(Element *e, void *thunk)
     const char *hname = static_cast<const char *>(thunk);
     // this element's glue elements: its states' and its copies in chains
     Vector<clk_element *> els;
-    for (int k = 0; k < he->_npt; k++)
+    for (int k = 0; k <= he->_npt; k++)
 	if (he->_pt[k].e)
 	    els.push_back(he->_pt[k].e);
     he->_borrow_lock.acquire();

@@ -78,8 +78,10 @@ struct ClickPacketOps {
  * where the glue's own default is 65536), ZEROCOPY, and the element's own.
  *
  * Threads (click -j N): one hipcore::State (context, glue element, held
- * packets, lock) per RouterThread, chosen by click_current_cpu_id()
- * (glue.hh:409-429), each created the first time its thread uses it.  Each
+ * packets) per RouterThread, chosen by click_current_cpu_id()
+ * (glue.hh:409-429), each created the first time its thread uses it and
+ * driven by that thread alone, so without a lock (State::shared false); a
+ * thread id past them shares one catch-all state, which is locked.  Each
  * state has a Task moved to its RouterThread (Task::move_thread,
  * task.hh:275): while the state holds packets the Task polls its latency
  * deadline (hipcore::Core::poll), so a partial batch is flushed, and its

@@ -13,9 +13,10 @@
  * GPU-backed element that nothing else pushes into, both with CHAIN true, on
  * the same DEVICE, makes the second a member of the first one's chain -- and
  * so on down output 0.  A chain_last class (IPFragmenter: its fragments are
- * extra results) ends a chain; a chain_head_only class (IPOutputCombo: its
- * PaintTee clones the packet as it arrives, ipoutputcombo.cc:50-60) never
- * joins one, it starts its own.  At most CHAIN_MAX members (the pass report
+ * extra results) ends a chain; a chain_head_only class never joins one, it
+ * starts its own (no shipped class is one now: IPOutputCombo's PaintTee
+ * clone, ipoutputcombo.cc:50-60, is taken by the glue from the bytes as the
+ * packet reaches it when it is a member after the head).  At most CHAIN_MAX members (the pass report
  * is a 64-bit member mask, clk_chain_report_passes).  The first element of a
  * run that is not itself a member heads it; every other element runs alone.
  *

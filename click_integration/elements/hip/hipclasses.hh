@@ -218,9 +218,12 @@ template <class P, class O> struct FixIPSrcClass : Plain<P, O> {
     }
 };
 
-// IPOutputCombo (ipoutputcombo.cc:44-205), ports 0-4.
+// IPOutputCombo (ipoutputcombo.cc:44-205), ports 0-4.  Alone or at the head
+// of a chain its prepare() takes the PaintTee clone as the packet arrives;
+// as a chain member after the head, the glue keeps the bytes as the packet
+// reaches it and the clone comes as a new packet (aux CLK_AUX_CLONE | key).
 template <class P, class O> struct IPOutputComboClass : Plain<P, O> {
-    enum { may_write = 1, chain_last = 0, chain_head_only = 1, pass_effects = 1, extra_results = 1 };
+    enum { may_write = 1, chain_last = 0, chain_head_only = 0, pass_effects = 1, extra_results = 1 };
     uint32_t color = 0;             // COLOR
     P *prepare(P *p, uint32_t *anno, P **extra)
     {
@@ -243,12 +246,26 @@ template <class P, class O> struct IPOutputComboClass : Plain<P, O> {
         *extra = clone;
         return q;
     }
-    bool primary(int32_t port, uint32_t aux) const { (void) port; return aux != CLK_AUX_CLONE; }
+    bool primary(int32_t port, uint32_t aux) const { (void) port; return !(aux & CLK_AUX_CLONE); }
+    // a chain member's clone: the bytes the glue kept, the IP header at data()
+    P *make_packet(clk_element *e, uint32_t aux) const
+    {
+        P *q = Plain<P, O>::take_glue_packet(e, aux & ~CLK_AUX_CLONE, 0);
+        if (q)
+            O::set_ip_header(q, O::data(q), (uint32_t) (O::data(q)[0] & 0xF) << 2);
+        return q;
+    }
     template <class S> int finish(S &t, Routed<P> &r, P **out)
     {
         (void) t;
         if (r.extra && !r.p) {                     // the PaintTee clone, before its packet
             *out = r.extra;
+            return 1;
+        }
+        if (r.made) {                              // the same, kept by a chain: the packet's
+            if (r.parent)                          // annotations as it reached this member
+                O::copy_annotations(r.made, r.parent);
+            *out = r.made;
             return 1;
         }
         P *p = r.p;

@@ -33,9 +33,9 @@
  *     (it waits for the GPU only when nothing is ready); other results
  *     leave on their push outputs as checked_output_push does (output 1 of
  *     a/ah).
- * Results are taken from the glue under the thread state's lock but
- * DELIVERED (annotations, output pushes) after it is released, in push
- * order: a downstream element that re-enters this element on the same
+ * Results are taken from the glue under the thread state's lock (a state
+ * one thread owns needs none: State::shared) but DELIVERED (annotations,
+ * output pushes) after it is released, in push order: a downstream element that re-enters this element on the same
  * thread stages its packet and returns (the running delivery loop delivers
  * the new results after the current ones), so there is no deadlock and no
  * reordering.  cleanup() kills whatever is held; it pushes nothing
@@ -236,9 +236,19 @@ template <class P, class L> struct State {
     P *last_primary;              // route(): the packet of the last primary result
     P *frag_parent;               // host use (IPFragmenter's first-fragment parent)
     L lock;
+    // several threads may drive the state (a host's catch-all state): its
+    // lock is taken.  A state one thread owns -- the Click adapter's state
+    // k is RouterThread k's, its Task moved there; teardown runs after the
+    // threads stopped -- is driven without it: the lock's atomic exchange
+    // was the largest single cost of a push (a full barrier per packet,
+    // profiles/r05/core_gprof_r05r.txt)
+    bool shared;
+    void enter() { if (shared) lock.acquire(); }
+    void leave() { if (shared) lock.release(); }
     State() : ctx(0), e(0), chain(0), id(0), base(0), next(0), counted(false), fails(0), draining(false),
               unrouted(false), routed_any(false), armed(false),
-              deadline(0), push_errors(0), chunk(0), side_chunk(0), xmask(~uint64_t(0)), last_primary(0), frag_parent(0) { }
+              deadline(0), push_errors(0), chunk(0), side_chunk(0), xmask(~uint64_t(0)), last_primary(0), frag_parent(0),
+              shared(true) { }
     ~State() { delete chunk; delete side_chunk; }
     State(const State &) = delete;
     State &operator=(const State &) = delete;
@@ -259,11 +269,11 @@ template <class P, class Host, class L> class Core {
     // ---- push context --------------------------------------------------------
     void push(Host &h, S &t, P *p)
     {
-        t.lock.acquire();
+        t.enter();
         stage(h, t, p, true);
         // most pushes only stage: deliver when there is something to
         const bool deliver = (!t.side.empty() || t.unrouted) && !t.draining;
-        t.lock.release();
+        t.leave();
         if (deliver)
             drain(h, t, false);
     }
@@ -272,9 +282,9 @@ template <class P, class Host, class L> class Core {
     // passed, or the router asks)
     void timer(Host &h, S &t)
     {
-        t.lock.acquire();
+        t.enter();
         flush(h, t, true);
-        t.lock.release();
+        t.leave();
         drain(h, t, false);
     }
 
@@ -282,40 +292,40 @@ template <class P, class Host, class L> class Core {
     // while the state still holds a deadline (the Task runs again).
     bool poll(Host &h, S &t)
     {
-        t.lock.acquire();
+        t.enter();
         if (!t.armed) {
-            t.lock.release();
+            t.leave();
             return false;
         }
         if (h.now_ns() < t.deadline) {
-            t.lock.release();
+            t.leave();
             return true;
         }
         flush(h, t, true);
-        t.lock.release();
+        t.leave();
         drain(h, t, false);
-        t.lock.acquire();
+        t.enter();
         const bool again = t.armed;
-        t.lock.release();
+        t.leave();
         return again;
     }
 
     bool armed(S &t)
     {
-        t.lock.acquire();
+        t.enter();
         const bool a = t.armed;
-        t.lock.release();
+        t.leave();
         return a;
     }
 
     // ---- pull context (output 0) --------------------------------------------
     P *pull(Host &h, S &t)
     {
-        t.lock.acquire();
+        t.enter();
         if (t.ready.empty()) {
-            t.lock.release();
+            t.leave();
             refill_and_launch(h, t);     // launches a batch, routes the one in flight
-            t.lock.acquire();
+            t.enter();
             // nothing ready (the first refill, or a batch that kept no packet
             // for output 0): wait for what is in flight -- retried at once,
             // abandoned after max_retries -- and launch the next batch before
@@ -323,11 +333,11 @@ template <class P, class Host, class L> class Core {
             while (t.ready.empty() && !t.held.empty() && t.e) {
                 flush(h, t, true);
                 const bool failed = t.fails != 0;
-                t.lock.release();
+                t.leave();
                 drain(h, t, true);
                 if (!failed)
                     refill_and_launch(h, t);
-                t.lock.acquire();
+                t.enter();
             }
         }
         P *p = 0;
@@ -335,14 +345,14 @@ template <class P, class Host, class L> class Core {
             p = t.ready.front();
             t.ready.pop_front();
         }
-        t.lock.release();
+        t.leave();
         return p;
     }
 
     // ---- teardown: kill everything held; no downstream pushes ----------------
     void cleanup(Host &h, S &t)
     {
-        t.lock.acquire();
+        t.enter();
         for (size_t i = 0; i < t.held.size(); i++) {
             if (t.held[i].p)
                 h.kill(t.held[i].p);
@@ -382,7 +392,7 @@ template <class P, class Host, class L> class Core {
             clk_ctx_destroy(t.ctx);
             t.ctx = 0;
         }
-        t.lock.release();
+        t.leave();
     }
 
   private:
@@ -403,19 +413,19 @@ template <class P, class Host, class L> class Core {
             while (g < want && (grp[g] = h.input_pull()) != 0)
                 g++;
             dry = g < want;
-            t.lock.acquire();
+            t.enter();
             for (uint32_t j = 0; j < g; j++) {
                 if (j + 4 < g)           // the bytes staging reads, 4 packets ahead
                     __builtin_prefetch(h.data(grp[j + 4]));
                 if (stage(h, t, grp[j], false))
                     k++;
             }
-            t.lock.release();
+            t.leave();
         }
-        t.lock.acquire();
+        t.enter();
         if (!t.held.empty())
             flush(h, t, false);
-        t.lock.release();
+        t.leave();
         drain(h, t, true);
     }
 
@@ -468,6 +478,10 @@ template <class P, class Host, class L> class Core {
             return false;
         }
         t.next++;
+        if (t.fails && t.chain) {        // the chain retried its failed flush first and it went through
+            t.fails = 0;                 // (clk_chain_push_anno): its results wait to be routed
+            t.unrouted = true;
+        }
         if (r == 1 && push_ctx)          // batch full: launch it, route the one before
             flush(h, t, false);
         return true;
@@ -506,8 +520,8 @@ template <class P, class Host, class L> class Core {
     {
         if (!t.e)
             return;
-        // a chain runs its members one after another on the batch: synchronous
-        int r = t.chain ? clk_chain_flush(t.chain) : wait ? clk_element_flush(t.e) : clk_element_flush_async(t.e);
+        int r = t.chain ? (wait ? clk_chain_flush(t.chain) : clk_chain_flush_async(t.chain))
+                        : wait ? clk_element_flush(t.e) : clk_element_flush_async(t.e);
         if (r != CLK_SUCCESS)            // nothing of the failed batch was routed; it stays staged
             failed_flush(h, t);
         else
@@ -585,7 +599,10 @@ template <class P, class Host, class L> class Core {
                 }
             } else {                             // a new packet made by the element
                 made = h.make_packet(m, t.chain ? t.mem[(size_t) m] : t.e, c.aux[i]);
-                parent = t.last_primary;
+                // a clone kept by a chain (CLK_AUX_CLONE | key: IPOutputCombo
+                // after the head) comes before its packet's own result: the
+                // packet is still held; a fragment follows its packet's
+                parent = (c.aux[i] & CLK_AUX_CLONE) && e ? e->p : t.last_primary;
             }
             c.p[i] = p;
             c.extra[i] = extra;
@@ -627,9 +644,9 @@ template <class P, class Host, class L> class Core {
     void drain(Host &h, S &t, bool pull_ctx)
     {
         std::vector<P *> ready;                 // pull context: output-0 packets, queued under one lock
-        t.lock.acquire();
+        t.enter();
         if (t.draining) {
-            t.lock.release();
+            t.leave();
             return;
         }
         t.draining = true;
@@ -643,25 +660,25 @@ template <class P, class Host, class L> class Core {
                 for (size_t i = 0; i < t.side.size() && c.n < (uint32_t) Chunk<P>::CAP; i++)
                     c.put(c.n++, t.side[i]);
                 t.side.erase(t.side.begin(), t.side.begin() + c.n);
-                t.lock.release();
+                t.leave();
                 deliver_chunk(h, t, c, 0, pull_ctx, last, ready);
-                t.lock.acquire();
+                t.enter();
                 continue;
             }
             if (!t.unrouted || !t.e)
                 break;
             route(h, t);
             Chunk<P> &c = *t.chunk;
-            t.lock.release();
+            t.leave();
             deliver_chunk(h, t, c, c.end, pull_ctx, last, ready);
-            t.lock.acquire();
+            t.enter();
             if (!ready.empty()) {
                 t.ready.insert(t.ready.end(), ready.begin(), ready.end());
                 ready.clear();
             }
         }
         t.draining = false;
-        t.lock.release();
+        t.leave();
     }
 
     // (unlocked) chunk c in runs of one member, then the end of the batch

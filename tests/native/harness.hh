@@ -199,6 +199,7 @@ class Host {
     {
         for (int k = 0; k < nstates; k++) {
             st[k].id = k;
+            st[k].shared = false;                       // state k is driven by one thread (the adapter's rule)
             st[k].xmask = C::extra_results ? 1 : 0;
             if (clk_ctx_create(0, &st[k].ctx) != CLK_SUCCESS ||
                 clk_element_create(st[k].ctx, glue_class, conf.c_str(), glue_class, noutputs, &st[k].e) !=
@@ -372,6 +373,7 @@ class ChainHost {
             st.mem.push_back(e);
         }
         st.e = st.mem[0];
+        st.shared = false;
         st.xmask = 0;
         for (size_t k = 0; k < m.size(); k++) {
             if (m[k]->extra_results())

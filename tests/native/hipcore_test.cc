@@ -819,6 +819,47 @@ void threads()
     report("four_threads_each_delivered_on_its_own_thread", ok);
 }
 
+// 10b. a catch-all state (State::shared: the Click adapter's state for a
+//      thread id past the RouterThreads) that two threads push into at once
+//      takes its lock: every packet is routed exactly once, each thread's in
+//      its push order
+void shared_state_two_threads()
+{
+    bool ok = true;
+    const int T = 2, n = 30000;
+    Host<CheckIPC> h("CheckIPHeader", "BATCH 2048", 2, 1);
+    h.st[0].shared = true;
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+        th.emplace_back([&h, t]() {
+            for (int i = 0; i < n; i++) {
+                std::vector<uint8_t> b = ip_bytes(64, (long)t * n + i);
+                if (i % 89 == 0) b[12] ^= 1;
+                h.push(make(b.data(), b.size(), (long)t * n + i), 0);
+            }
+        });
+    for (std::thread &x : th)
+        x.join();
+    h.timer();
+    CHECK(h.runcount == 0);
+    std::vector<long> last(T, -1);
+    size_t bad = 0;
+    std::vector<uint8_t> seen((size_t)T * n, 0);
+    for (int port = 0; port < 2; port++)
+        for (TPacket *p : h.out[(size_t)port]) {
+            const int t = (int)(p->a.id / n);
+            CHECK(!seen[(size_t)p->a.id]);
+            seen[(size_t)p->a.id] = 1;
+            if (port == 0) {
+                CHECK(p->a.id > last[(size_t)t] && (p->a.id % n) % 89 != 0);
+                last[(size_t)t] = p->a.id;
+            } else
+                bad += (p->a.id % n) % 89 == 0;
+        }
+    CHECK(h.out[0].size() + h.out[1].size() == (size_t)T * n && bad == h.out[1].size());
+    report("shared_state_two_threads_locked", ok);
+}
+
 // 11. cleanup of a held partial batch: everything killed, nothing pushed
 void cleanup_partial()
 {
@@ -1116,6 +1157,7 @@ int main()
     retry_limit();
     reentrant_push();
     threads();
+    shared_state_two_threads();
     cleanup_partial();
     chain_vs_elements(65536, 0);
     chain_vs_elements(300, 0);

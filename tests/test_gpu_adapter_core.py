@@ -29,7 +29,8 @@ SCENARIOS = ["class_" + c for c in CLASSES] + [
     "failed_flush_then_retry_SetUDPChecksum_fault4", "failed_flush_then_retry_SetUDPChecksum_completion",
     "failed_flush_then_retry_IPOutputCombo_fault11", "failed_flush_then_retry_IPOutputCombo_completion",
     "retry_limit_abandons_and_releases_runcount", "reentrant_push_from_downstream",
-    "four_threads_each_delivered_on_its_own_thread", "cleanup_kills_held_packets_pushes_nothing",
+    "four_threads_each_delivered_on_its_own_thread", "shared_state_two_threads_locked",
+    "cleanup_kills_held_packets_pushes_nothing",
     "chain_of_five_matches_separate_elements_batch_65536", "chain_of_five_matches_separate_elements_batch_300",
     "chain_of_five_matches_separate_elements_batch_1000_flush_777",
     "combos_chain_matches_separate_elements_batch_65536", "combos_chain_matches_separate_elements_batch_300",

@@ -7,7 +7,10 @@
 #                       (not compiled) with -pg: gprof's PC sampling of the
 #                       core's code, no mcount calls; the library's own time
 #                       is not sampled
-#   run.sh gprof_run    on the GPU box: its chain leg REPS times, flat profile
+#   run.sh gprof_run    on the GPU box: its chain leg REPS times (LEG=chain_source:
+#                       the frames made from a pool as they are pushed), flat profile
+#   run.sh null_build   here: the measurement program over the null glue, to
+#                       run on the GPU box's host cores (run.sh null_run)
 set -e
 D=$(cd "$(dirname "$0")" && pwd); R=$D/../..
 mkdir -p $D/bin
@@ -21,8 +24,14 @@ gprof_build)
     ;;
 gprof_run)
     cd $D/bin
-    ./pull_bench_pg 1 chain ${REPS:-100} | tail -2
+    ./pull_bench_pg 1 ${LEG:-chain} ${REPS:-100} | tail -2
     gprof -b -p ./pull_bench_pg gmon.out 2>/dev/null | head -${TOP:-40}
+    ;;
+null_build)
+    g++ -std=c++17 -O2 -g -I$R/include $R/tests/native/pull_bench.cc $D/null_glue.cc -o $D/bin/pull_bench_null
+    ;;
+null_run)
+    cd $D/bin && ./pull_bench_null ${1:-1}
     ;;
 *)
     g++ -std=c++17 -O2 -g ${PG:+-pg} -I$R/include $R/tests/native/pull_bench.cc $D/null_glue.cc -o $D/bin/pull_bench_null
