@@ -155,10 +155,8 @@ int Chain::check(std::string *err) const
 // The bytes from data() any member's kernel can read of a packet pushed with
 // network header nh: the largest chain_extent() over the members, following
 // the view (Strip, network header) from member to member.  ~0u: all.
-uint32_t Chain::extent(int32_t nh, uint32_t length)
+uint32_t Chain::extent_slow(int32_t nh, uint32_t length)
 {
-    if (nh == ext_nh_ && length == ext_len_)
-        return ext_;
     uint64_t need = 0, shift = 0;
     int32_t v = nh;
     for (const BatchElement *e : m_) {
@@ -186,6 +184,8 @@ int Chain::begin_batch(Batch &B)
             X.mm.resize(m_.size());
     }
     const size_t cap = std::max<size_t>(m_[0]->batch_cap_, 1);
+    cap0_ = m_[0]->batch_cap_;
+    zerocopy_ = m_[0]->zerocopy_;
     if (grow_members(B, cap, 0))
         return -1;
     size_packets(B, B.mcap);
@@ -249,9 +249,10 @@ void Chain::send_chunk(Batch &B)
 // packet's entries are written at push)
 void Chain::size_packets(Batch &B, size_t c)
 {
-    for (auto *v : {&B.views0, &B.views})
-        if (v->size() < c)
-            v->resize(c);
+    if (B.views.size() < c)
+        B.views.resize(c);
+    if (B.slot0.size() < c)
+        B.slot0.resize(c);
     for (auto *v : {&B.staged, &B.back, &B.clone_key})
         if (v->size() < c)
             v->resize(c);
@@ -272,7 +273,44 @@ int Chain::grow_batch(Batch &B)
     return 0;
 }
 
-int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
+// A packet's entries in the batch; it reaches member 0 (its descriptors at
+// the flush)
+inline void Chain::record(Batch &B, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno,
+                          uint64_t slot, uint32_t need)
+{
+    const uint32_t i = (uint32_t)B.np++;
+    B.views[i] = ChainView{data, token, slot, length, nh_offset, (uint16_t)anno};
+    B.slot0[i] = slot;
+    B.staged[i] = need;
+    B.clone_key[i] = 0;
+    B.back[i] = 0;                                   // grown by each member whose kernel may rewrite it
+    B.done[i] = 0;
+    B.copied[i] = 0;
+    ChainWork &w0 = B.mm[0].w;
+    w0.reached[w0.nreached++] = i;
+}
+
+// push(), the common case inlined: a staged batch under way, with room in
+// its arena and arrays; anything else is push_slow()'s
+inline int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
+{
+    Batch &B = b_[cur_];
+    if (B.np && B.np < B.mcap && !dead_ && !failed_ && !zerocopy_) {
+        const uint32_t need = std::min(length, extent(nh_offset, length));
+        const uint64_t slot = (B.used + 15) & ~size_t(15);
+        if (slot + need + 64 <= B.h_cap) {
+            stage_copy(B.h_arena + slot, data, need, length);
+            B.used = slot + need;
+            if (B.used - B.sent >= H2D_CHUNK)
+                send_chunk(B);
+            record(B, data, length, nh_offset, token, anno, slot, need);
+            return B.np >= cap0_ ? 1 : 0;
+        }
+    }
+    return push_slow(data, length, nh_offset, token, anno);
+}
+
+int Chain::push_slow(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
 {
     if (dead_)
         return CLK_EINVAL;
@@ -344,17 +382,7 @@ int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t toke
         err_ = "out of device / pinned memory";
         return CLK_EINVAL;
     }
-    const ChainView v{data, token, slot, length, nh_offset, (uint16_t)anno};
-    const uint32_t i = (uint32_t)B->np++;
-    B->views0[i] = v;
-    B->views[i] = v;
-    B->staged[i] = need;
-    B->clone_key[i] = 0;
-    B->back[i] = 0;                                  // grown by each member whose kernel may rewrite it
-    B->done[i] = 0;
-    B->copied[i] = 0;
-    ChainWork &w0 = B->mm[0].w;                      // it reaches member 0 (its descriptors at the flush)
-    w0.reached[w0.nreached++] = i;
+    record(*B, data, length, nh_offset, token, anno, slot, need);
     return B->np >= m_[0]->batch_cap_ ? 1 : 0;
 }
 
@@ -363,8 +391,10 @@ int Chain::push_burst(uint8_t *const *datas, const uint32_t *lengths, const int3
 {
     double t0 = now_s();
     for (uint32_t k = 0; k < n; k++) {
-        if (k + 8 < n)                               // the packet 8 ahead, while this one is staged
-            __builtin_prefetch(datas[k + 8]);
+        if (k + CLK_CHAIN_PF < n) {                  // the packet ahead, while this one is staged
+            __builtin_prefetch(datas[k + CLK_CHAIN_PF]);
+            __builtin_prefetch(datas[k + CLK_CHAIN_PF] + 64);
+        }
         int r = push(datas[k], lengths[k], nh_offsets ? nh_offsets[k] : -1, first_token + k, 0);
         if (r < 0)
             return r;
@@ -442,7 +472,7 @@ void Chain::setup(Batch &B, size_t k)
     w.out = &B.out;
     w.back = e->zerocopy_ ? nullptr : B.back.data();
     w.staged = B.staged.data();
-    w.views0 = B.views0.data();
+    w.slot0 = B.slot0.data();
     const uint8_t hr = e->zerocopy_ ? (uint8_t)CHAIN_HOST_NONE : e->chain_host_rewrite();
     w.wext = hr == CHAIN_HOST_ALL ? 0u : e->chain_write_past_nh();
     w.wext_unless_simple = hr == CHAIN_HOST_SIMPLE;
@@ -796,7 +826,7 @@ int Chain::keep_clones(Batch &B, size_t k)
         b.resize(v.length);
         size_t from_dev = 0;
         if (dev) {                                   // the staged bytes from where this view's start
-            const uint64_t shift = v.slot - B.views0[i].slot;
+            const uint64_t shift = v.slot - B.slot0[i];
             from_dev = shift < B.staged[i] ? std::min<size_t>(v.length, B.staged[i] - shift) : 0;
             std::memcpy(b.data(), dev + v.slot, from_dev);
         }
@@ -842,7 +872,7 @@ int Chain::copy_back(Batch &B, bool all)
         t0 = now_s();
         for (size_t i = 0; i < B.np; i++)
             if (B.back[i] && !B.copied[i] && (all || B.done[i])) {
-                std::memcpy(B.views0[i].data, B.h_back + B.views0[i].slot, B.back[i]);
+                std::memcpy(B.views[i].data - (B.views[i].slot - B.slot0[i]), B.h_back + B.slot0[i], B.back[i]);
                 B.copied[i] = 1;
             }
         stats_[7] += now_s() - t0;

@@ -134,6 +134,12 @@ bool parse_prefix(const std::string &s, uint32_t *saddr, uint32_t *mask);
 // instead of a variable-length memcpy call.  The bytes copied past n stay
 // inside the 64 B of slack every staging slot is grown with and are
 // overwritten by the next packet's slot.
+// how many packets ahead a chain loop prefetches the header it reads
+#ifndef CLK_CHAIN_PF
+#define CLK_CHAIN_PF 24
+#endif
+inline const uint8_t *chain_hdr(const uint8_t *data, int32_t nh) { return data + (nh > 0 ? nh : 0); }
+
 inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail)
 {
     if (n == 0)
@@ -205,7 +211,7 @@ struct ChainWork {
     // member that rewrites it: shift + its write extent), its first slot
     uint32_t *back = nullptr;
     const uint32_t *staged = nullptr;
-    const ChainView *views0 = nullptr;
+    const uint64_t *slot0 = nullptr;          // per chain packet: its staging offset as pushed
     uint32_t wext = 0;                        // the member's write extent past nh (~0u: all; 0: none)
     bool wext_unless_simple = false;          // CHAIN_HOST_SIMPLE: only packets that are not simple
     int member = 0;
@@ -254,27 +260,39 @@ struct ChainWork {
 // The final classes' fast loops: push_burst() and route_stage() over the
 // class's own span() / route(), called qualified so they inline (no
 // virtual call per packet).
+#define CLK_INL __attribute__((always_inline))
 #define CLK_GLUE_LOOPS(C)                                                                                       \
     int push_burst(uint8_t *const *d_, const uint32_t *l_, const int32_t *nh_, uint64_t t0_, uint32_t n_) override \
     {                                                                                                           \
-        return burst_loop([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {                       \
-            return this->C::span(p, o, l, c);                                                                   \
+        return burst_loop([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) CLK_INL {               \
+            bool r_; [[clang::always_inline]] r_ = this->C::span(p, o, l, c);                                   \
+            return r_;                                                                                          \
         }, d_, l_, nh_, t0_, n_);                                                                               \
     }                                                                                                           \
     void route_stage(Stage &g_) override                                                                        \
     {                                                                                                           \
-        route_loop(g_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }); \
+        route_loop(g_, [this](Pending &p, int code, uint16_t sum, Result *r) CLK_INL {                          \
+            [[clang::always_inline]] this->C::route(p, code, sum, r);                                           \
+        });                                                                                                     \
     }                                                                                                           \
     void chain_prep(ChainWork &w_) override                                                                    \
     {                                                                                                           \
-        chain_prep_loop(w_, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) {                     \
-            return this->C::span(p, o, l, c);                                                                   \
-        }, [this](const ChainView &v) { return this->C::pre_clone(v); });                                        \
+        chain_prep_loop(w_, [this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) CLK_INL {             \
+            bool r_; [[clang::always_inline]] r_ = this->C::span(p, o, l, c);                                   \
+            return r_;                                                                                          \
+        }, [this](const ChainView &v) CLK_INL {                                                                 \
+            bool r_; [[clang::always_inline]] r_ = this->C::pre_clone(v);                                       \
+            return r_;                                                                                          \
+        });                                                                                                     \
     }                                                                                                           \
     void chain_route_all(ChainWork &w_) override                                                               \
     {                                                                                                           \
-        chain_route_loop(w_, [this](Pending &p, int code, uint16_t sum, Result *r) { this->C::route(p, code, sum, r); }, \
-                         [this](Pending &p, Result *r) { return this->C::pre_route(p, r); });                   \
+        chain_route_loop(w_, [this](Pending &p, int code, uint16_t sum, Result *r) CLK_INL {                    \
+            [[clang::always_inline]] this->C::route(p, code, sum, r);                                           \
+        }, [this](Pending &p, Result *r) CLK_INL {                                                              \
+            bool r_; [[clang::always_inline]] r_ = this->C::pre_route(p, r);                                    \
+            return r_;                                                                                          \
+        });                                                                                                     \
     }
 
 class Chain;
@@ -381,7 +399,7 @@ class BatchElement {
     void chain_prep_loop(ChainWork &w, SpanF &&span_f, CloneF &&clone_f);
     // a pass rule's pass: counted, on to member k+1 (the last member: a
     // result on output 0)
-    void chain_pass_on(ChainWork &w, uint32_t i)
+    CLK_INL void chain_pass_on(ChainWork &w, uint32_t i)
     {
         packets_++;
         if (w.last) {
@@ -398,7 +416,7 @@ class BatchElement {
     // counted by each (the member would route it to output 0 unchanged); it
     // joins the list of the first member that must look at it, or leaves
     // the last on output 0
-    static void chain_forward(ChainWork &w, uint32_t i)
+    CLK_INL static void chain_forward(ChainWork &w, uint32_t i)
     {
         ChainWork *n = w.next;
         const ChainView &v = w.views[i];
@@ -414,12 +432,12 @@ class BatchElement {
         n->reached[n->nreached++] = i;
     }
     template <class RouteF, class PreF>
-    bool chain_route_at(ChainWork &w, size_t q, RouteF &&route_f, PreF &&pre_f);
+    CLK_INL bool chain_route_at(ChainWork &w, size_t q, RouteF &&route_f, PreF &&pre_f);
     template <class RouteF, class PreF>
     void chain_route_loop(ChainWork &w, RouteF &&route_f, PreF &&pre_f);
     template <class RouteF, class PreF>
-    bool chain_route_pending(ChainWork &w, uint32_t i, Pending &p, int code, uint16_t sum, RouteF &&route_f,
-                             PreF &&pre_f);
+    CLK_INL bool chain_route_pending(ChainWork &w, uint32_t i, Pending &p, int code, uint16_t sum, RouteF &&route_f,
+                                     PreF &&pre_f);
     ResultQueue chain_side_;          // a member's pre/post results while a chain routes
     friend class Chain;
     // after the batch completed, before any packet is routed: nonzero fails
@@ -844,8 +862,11 @@ inline void BatchElement::chain_prep_loop(ChainWork &w, SpanF &&span_f, CloneF &
 {
     for (size_t q = w.nprep; q < w.nreached; q++) {
         const uint32_t i = w.reached[q];
-        if (q + 8 < w.nreached)                  // the header a pass rule / span reads, 8 ahead
-            __builtin_prefetch(w.views[w.reached[q + 8]].data);
+        if (q + CLK_CHAIN_PF < w.nreached) {     // the header a pass rule / span reads
+            const ChainView &a = w.views[w.reached[q + CLK_CHAIN_PF]];
+            __builtin_prefetch(chain_hdr(a.data, a.nh));
+            __builtin_prefetch(chain_hdr(a.data, a.nh) + 16);
+        }
         const ChainView &v = w.views[i];
         if (w.pass && w.passes(v)) {
             w.code[q] = CHAIN_CODE_PASS;
@@ -875,7 +896,7 @@ inline void BatchElement::chain_prep_loop(ChainWork &w, SpanF &&span_f, CloneF &
         w.code[q] = (int32_t)w.n++;
         if (w.wext && w.back &&                  // the bytes this member's kernel may rewrite, to copy back
             !(w.wext_unless_simple && IPOutputCombo::simple_rewrite(v.data + off, len, v.anno))) {
-            const uint64_t shift = v.slot - w.views0[i].slot;
+            const uint64_t shift = v.slot - w.slot0[i];
             const uint64_t e = w.wext == 0xFFFFFFFFu ? (uint64_t)0xFFFFFFFFu
                                                      : shift + (v.nh > 0 ? (uint32_t)v.nh : 0u) + w.wext;
             w.back[i] = (uint32_t)std::max<uint64_t>(w.back[i], std::min<uint64_t>(e, w.staged[i]));
@@ -1000,7 +1021,8 @@ class Chain {
     // pushed into while the other is in flight.
     struct Batch {
         std::vector<Member> mm;
-        std::vector<ChainView> views0, views;     // as pushed; as they move through the members
+        std::vector<ChainView> views;             // as they move through the members
+        std::vector<uint64_t> slot0;              // staging offset as pushed (data moves with slot)
         std::vector<uint32_t> staged, back, clone_key;   // bytes staged / to copy back, a kept clone's key
         std::vector<uint8_t> done, copied;        // left the chain; bytes copied back
         size_t np = 0, mcap = 0;                  // packets in the batch; the arrays' size
@@ -1043,7 +1065,16 @@ class Chain {
     void publish(Batch &B);
     void end_batch(Batch &B);
     void free_batch(Batch &B);
-    uint32_t extent(int32_t nh, uint32_t length);
+    uint32_t extent(int32_t nh, uint32_t length)
+    {
+        return nh == ext_nh_ && length == ext_len_ ? ext_ : extent_slow(nh, length);
+    }
+    uint32_t extent_slow(int32_t nh, uint32_t length);
+    int push_slow(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno);
+    void record(Batch &B, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno,
+                uint64_t slot, uint32_t need);
+    size_t cap0_ = 0;                         // member 0's BATCH, ZEROCOPY (begin_batch)
+    bool zerocopy_ = false;
     std::vector<BatchElement *> m_;
     Batch b_[2];
     int cur_ = 0;                             // the batch pushes go to
@@ -1069,8 +1100,11 @@ void BatchElement::chain_route_loop(ChainWork &w, RouteF &&route_f, PreF &&pre_f
 {
     for (size_t q = w.routed; q < w.nreached; q++) {
         w.routed = q + 1;
-        if (q + 8 < w.nreached)              // the packet route() reads 8 ahead
-            __builtin_prefetch(w.views[w.reached[q + 8]].data);
+        if (q + CLK_CHAIN_PF < w.nreached) { // the header route() reads (and a member may write)
+            const ChainView &a = w.views[w.reached[q + CLK_CHAIN_PF]];
+            __builtin_prefetch(chain_hdr(a.data, a.nh), 1);
+            __builtin_prefetch(chain_hdr(a.data, a.nh) + 16, 1);
+        }
         const uint32_t i = w.reached[q];
         if (w.code[q] == CHAIN_CODE_PASS)
             chain_pass_on(w, i);

@@ -1,11 +1,21 @@
 // chain_prof.cc -- tools only (never shipped, not a test): config 1's
 // five-element chain (bench.py C1_CHAINS["elements"]) through the chain C
 // ABI from C++, as bench.py's elements_chain leg runs it, so the host glue
-// can be profiled with gprof (tools/chain_prof/run.sh builds the glue's host
-// files into this executable with -pg).  Prints the median Mpps of the timed
-// runs and clk_chain_stats.
+// can be profiled (tools/chain_prof/run.sh builds the glue's host files into
+// this executable).  Prints the median Mpps of the timed runs and
+// clk_chain_stats.  With SAMPLES=file it samples the program counter every
+// 50 us of CPU time inside the timed region (SIGPROF) and writes one line per
+// sample: the offset from the executable's start, or the shared object's
+// name; tools/chain_prof/resolve.py turns that into lines and functions.
 //   chain_prof FRAME_HEX [RUNS] [BATCH] [combos]
 #include <algorithm>
+#include <dlfcn.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <sys/time.h>
+#include <time.h>
+#include <unistd.h>
+#include <ucontext.h>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -14,8 +24,35 @@
 #include "click_amd_cksum.h"
 #include "click_amd_elements.h"
 
+extern "C" char __executable_start;
+static uintptr_t g_pc[1 << 22];
+static volatile size_t g_npc = 0;
+static volatile int g_on = 0;
+
+static void on_prof(int, siginfo_t *, void *uc)
+{
+    if (g_on && g_npc < (1u << 22))
+        g_pc[g_npc++] = (uintptr_t)((ucontext_t *)uc)->uc_mcontext.gregs[REG_RIP];
+}
+
+static void write_samples(const char *path)
+{
+    FILE *f = std::fopen(path, "w");
+    if (!f)
+        return;
+    for (size_t k = 0; k < g_npc; k++) {
+        Dl_info di;
+        if (dladdr((void *)g_pc[k], &di) && di.dli_fbase == (void *)&__executable_start)
+            std::fprintf(f, "0x%lx\n", (unsigned long)(g_pc[k] - (uintptr_t)&__executable_start));
+        else
+            std::fprintf(f, "@%s\n", dladdr((void *)g_pc[k], &di) && di.dli_fname ? di.dli_fname : "?");
+    }
+    std::fclose(f);
+}
+
 int main(int argc, char **argv)
 {
+    const char *samples = std::getenv("SAMPLES");
     if (argc < 2)
         return 2;
     std::vector<uint8_t> frame;
@@ -51,6 +88,21 @@ int main(int argc, char **argv)
     clk_chain *c = nullptr;
     if (clk_chain_create(els.data(), (int)els.size(), &c) != CLK_SUCCESS)
         return 3;
+    if (samples) {                                   // armed once the GPU is set up (a signal interrupts its ioctls)
+        struct sigaction sa = {};
+        sa.sa_sigaction = on_prof;
+        sa.sa_flags = SA_SIGINFO | SA_RESTART;
+        sigaction(SIGPROF, &sa, nullptr);
+        sigevent ev = {};                            // a high-resolution timer aimed at this thread
+        ev.sigev_notify = SIGEV_THREAD_ID;
+        ev.sigev_signo = SIGPROF;
+        ev._sigev_un._tid = (pid_t)syscall(SYS_gettid);
+        timer_t tm;
+        if (timer_create(CLOCK_MONOTONIC, &ev, &tm) == 0) {
+            itimerspec its = {{0, 20000}, {0, 20000}};
+            timer_settime(tm, 0, &its, nullptr);
+        }
+    }
     std::vector<uint64_t> tok(n + 1);
     std::vector<int32_t> mem(n + 1), port(n + 1);
     std::vector<uint32_t> len(n + 1), aux(n + 1), lens(n, L);
@@ -64,6 +116,7 @@ int main(int argc, char **argv)
             ptrs[i] = arena.data() + (size_t)i * L;
         }
         const auto t0 = std::chrono::steady_clock::now();
+        g_on = r > 0;
         if (clk_chain_push_burst(c, ptrs.data(), lens.data(), nullptr, 0, n) != CLK_SUCCESS ||
             clk_chain_flush(c) != CLK_SUCCESS) {
             std::fprintf(stderr, "chain: %s\n", clk_chain_last_error(c));
@@ -71,6 +124,7 @@ int main(int argc, char **argv)
         }
         const uint64_t k = clk_chain_results(c, tok.data(), mem.data(), port.data(), len.data(), aux.data(), n + 1);
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        g_on = 0;
         fwd = 0;
         for (uint64_t j = 0; j < k; j++)
             fwd += mem[j] == last && port[j] == 0;
@@ -88,6 +142,8 @@ int main(int argc, char **argv)
     const double per = 1e9 / ((runs + 1) * (double)n);
     std::printf("], \"ns_per_packet\": {\"push\": %.1f, \"gpu\": %.1f, \"h2d\": %.1f, \"route\": %.1f, \"copy_back\": %.1f}}\n",
                 st[0] * per, st[2] * per, st[4] * per, st[6] * per, st[7] * per);
+    if (samples)
+        write_samples(samples);
     clk_chain_destroy(c);
     for (clk_element *e : els)
         clk_element_destroy(e);
