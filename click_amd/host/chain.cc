@@ -295,7 +295,15 @@ inline void Chain::record(Batch &B, uint8_t *data, uint32_t length, int32_t nh_o
 inline int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
 {
     Batch &B = b_[cur_];
-    if (B.np && B.np < B.mcap && !dead_ && !failed_ && !zerocopy_) {
+    if (!B.np || B.np >= B.mcap || dead_ || failed_)
+        return push_slow(data, length, nh_offset, token, anno);
+    if (zerocopy_) {                                 // in the batch's registered region, as the packet before
+        if (data >= B.zc_host && data + (length ? length : 1) <= zc_last_ + zc_last_bytes_ &&
+            B.zc_host == zc_last_ && clk_host_generation_internal() == zc_gen_) {
+            record(B, data, length, nh_offset, token, anno, (uint64_t)(data - B.zc_host), 0);
+            return B.np >= cap0_ ? 1 : 0;
+        }
+    } else {
         const uint32_t need = std::min(length, extent(nh_offset, length));
         const uint64_t slot = (B.used + 15) & ~size_t(15);
         if (slot + need + 64 <= B.h_cap) {

@@ -227,6 +227,7 @@ struct ChainWork {
     bool report_passes = false;               // a CLK_PORT_NEXT record for each packet passed on
     ChainWork *next = nullptr;                // member k+1's (0 for the last)
     BatchElement *elem = nullptr;             // member k
+    uint64_t counted = 0;                     // packets member k took in a loop (its packets_, added at the end)
     void reset()
     {
         nreached = 0;
@@ -401,7 +402,7 @@ class BatchElement {
     // result on output 0)
     CLK_INL void chain_pass_on(ChainWork &w, uint32_t i)
     {
-        packets_++;
+        w.counted++;
         if (w.last) {
             const ChainView &v = w.views[i];
             w.out->push_back(ChainExit{v.token, w.member, 0, v.length, 0, i});
@@ -858,8 +859,12 @@ class IPFragmenter : public BatchElement {
 // rule's pass, or the class's span() -- a descriptor of the member's batch
 // (the bytes to copy back grown for a writing member) or a host decision.
 template <class SpanF, class CloneF>
-inline void BatchElement::chain_prep_loop(ChainWork &w, SpanF &&span_f, CloneF &&clone_f)
+inline void BatchElement::chain_prep_loop(ChainWork &w0, SpanF &&span_f, CloneF &&clone_f)
 {
+    // a private copy of the member's work: its fields stay in registers
+    // across the loop's byte stores (which may alias anything in memory)
+    ChainWork w = w0;
+    w.counted = 0;
     for (size_t q = w.nprep; q < w.nreached; q++) {
         const uint32_t i = w.reached[q];
         if (q + CLK_CHAIN_PF < w.nreached) {     // the header a pass rule / span reads
@@ -902,7 +907,12 @@ inline void BatchElement::chain_prep_loop(ChainWork &w, SpanF &&span_f, CloneF &
             w.back[i] = (uint32_t)std::max<uint64_t>(w.back[i], std::min<uint64_t>(e, w.staged[i]));
         }
     }
-    w.nprep = w.nreached;
+    w0.nprep = w.nreached;
+    w0.routed = w.routed;
+    w0.n = w.n;
+    w0.maxlen = w.maxlen;
+    w0.clones = w.clones;
+    packets_ += w.counted;
 }
 
 template <class RouteF, class PreF>
@@ -920,7 +930,7 @@ inline bool BatchElement::chain_route_pending(ChainWork &w, uint32_t i, Pending 
         w.out->push_back(ChainExit{pr.token, w.member, pr.port, pr.length, aux, ~0u});
     }
     Result r{p.token, 0, p.length, 0};
-    packets_++;
+    w.counted++;
     route_f(p, code, sum, &r);
     const bool pass = r.port == 0 && !w.last;
     if (pass) {
@@ -1096,8 +1106,10 @@ class Chain {
 };
 
 template <class RouteF, class PreF>
-void BatchElement::chain_route_loop(ChainWork &w, RouteF &&route_f, PreF &&pre_f)
+void BatchElement::chain_route_loop(ChainWork &w0, RouteF &&route_f, PreF &&pre_f)
 {
+    ChainWork w = w0;                         // a private copy, as in chain_prep_loop
+    w.counted = 0;
     for (size_t q = w.routed; q < w.nreached; q++) {
         w.routed = q + 1;
         if (q + CLK_CHAIN_PF < w.nreached) { // the header route() reads (and a member may write)
@@ -1111,6 +1123,8 @@ void BatchElement::chain_route_loop(ChainWork &w, RouteF &&route_f, PreF &&pre_f
         else if (chain_route_at(w, q, route_f, pre_f) && !w.last)
             chain_forward(w, i);
     }
+    w0.routed = w.routed;
+    packets_ += w.counted;
 }
 
 } // namespace host
