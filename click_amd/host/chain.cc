@@ -186,9 +186,15 @@ int Chain::begin_batch(Batch &B)
     const size_t cap = std::max<size_t>(m_[0]->batch_cap_, 1);
     cap0_ = m_[0]->batch_cap_;
     zerocopy_ = m_[0]->zerocopy_;
+    if (zerocopy_ && !B.zc_zeroed) {                 // ZEROCOPY batches never write these (record())
+        std::fill(B.staged.begin(), B.staged.end(), 0u);
+        std::fill(B.back.begin(), B.back.end(), 0u);
+        std::fill(B.copied.begin(), B.copied.end(), (uint8_t)0);
+    }
     if (grow_members(B, cap, 0))
         return -1;
     size_packets(B, B.mcap);
+    B.zc_zeroed = zerocopy_;
     for (size_t k = 0; k < m_.size(); k++) {
         setup(B, k);
         B.mm[k].w.reset();
@@ -275,17 +281,21 @@ int Chain::grow_batch(Batch &B)
 
 // A packet's entries in the batch; it reaches member 0 (its descriptors at
 // the flush)
+// (ZEROCOPY: nothing is staged or copied back -- staged / back / copied
+// stay 0 from begin_batch, slot0 is not read)
 inline void Chain::record(Batch &B, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno,
                           uint64_t slot, uint32_t need)
 {
     const uint32_t i = (uint32_t)B.np++;
     B.views[i] = ChainView{data, token, slot, length, nh_offset, (uint16_t)anno};
-    B.slot0[i] = slot;
-    B.staged[i] = need;
+    if (!zerocopy_) {
+        B.slot0[i] = slot;
+        B.staged[i] = need;
+        B.back[i] = 0;                               // grown by each member whose kernel may rewrite it
+        B.copied[i] = 0;
+    }
     B.clone_key[i] = 0;
-    B.back[i] = 0;                                   // grown by each member whose kernel may rewrite it
     B.done[i] = 0;
-    B.copied[i] = 0;
     ChainWork &w0 = B.mm[0].w;
     w0.reached[w0.nreached++] = i;
 }
@@ -897,8 +907,14 @@ void Chain::publish(Batch &B)
     if (X.started && X.seq < B.seq)                  // the batch before it has results to come first
         return;
     if (B.pub < B.out.size()) {
-        out_.insert(out_.end(), B.out.begin() + (ptrdiff_t)B.pub, B.out.end());
-        B.pub = B.out.size();
+        if (B.pub == 0 && head_ == out_.size()) {   // all handed out before: take the batch's vector whole
+            out_.swap(B.out);
+            B.out.clear();
+            head_ = 0;
+        } else {
+            out_.insert(out_.end(), B.out.begin() + (ptrdiff_t)B.pub, B.out.end());
+            B.pub = B.out.size();
+        }
     }
 }
 
@@ -971,7 +987,16 @@ uint64_t Chain::abandon()
 uint64_t Chain::pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap)
 {
     const size_t k = (size_t)std::min<uint64_t>(cap, out_.size() - head_);
-    for (size_t q = 0; q < k; q++) {
+    if (tokens && members && ports && lengths && aux) {
+        const ChainExit *x = out_.data() + head_;
+        for (size_t q = 0; q < k; q++) {
+            tokens[q] = x[q].token;
+            members[q] = x[q].member;
+            ports[q] = x[q].port;
+            lengths[q] = x[q].length;
+            aux[q] = x[q].aux;
+        }
+    } else for (size_t q = 0; q < k; q++) {
         const ChainExit &x = out_[head_ + q];
         if (tokens) tokens[q] = x.token;
         if (members) members[q] = x.member;

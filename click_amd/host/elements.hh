@@ -1043,6 +1043,7 @@ class Chain {
         const uint8_t *zc_host = nullptr;         // ZEROCOPY: the batch's registered region
         uint8_t *zc_dev = nullptr;
         uint64_t seq = 0;                         // batches in push order
+        bool zc_zeroed = false;                   // staged / back / copied all 0 (ZEROCOPY batches)
         bool started = false;                     // flushed: in flight until its last member is routed
         size_t at = 0;                            // the member its routing has reached
         bool waiting = false;                     // member at's GPU step is queued, not awaited
