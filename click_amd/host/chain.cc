@@ -283,7 +283,7 @@ int Chain::grow_batch(Batch &B)
 // the flush)
 // (ZEROCOPY: nothing is staged or copied back -- staged / back / copied
 // stay 0 from begin_batch, slot0 is not read)
-inline void Chain::record(Batch &B, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno,
+CLK_INL inline void Chain::record(Batch &B, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno,
                           uint64_t slot, uint32_t need)
 {
     const uint32_t i = (uint32_t)B.np++;

@@ -138,6 +138,10 @@ bool parse_prefix(const std::string &s, uint32_t *saddr, uint32_t *mask);
 #ifndef CLK_CHAIN_PF
 #define CLK_CHAIN_PF 24
 #endif
+// ... and the view (ChainView) it takes that header's address from
+#ifndef CLK_CHAIN_PFV
+#define CLK_CHAIN_PFV 0
+#endif
 inline const uint8_t *chain_hdr(const uint8_t *data, int32_t nh) { return data + (nh > 0 ? nh : 0); }
 
 inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail)
@@ -867,7 +871,9 @@ inline void BatchElement::chain_prep_loop(ChainWork &w0, SpanF &&span_f, CloneF 
     w.counted = 0;
     for (size_t q = w.nprep; q < w.nreached; q++) {
         const uint32_t i = w.reached[q];
-        if (q + CLK_CHAIN_PF < w.nreached) {     // the header a pass rule / span reads
+        if (CLK_CHAIN_PFV && q + CLK_CHAIN_PFV < w.nreached)
+            __builtin_prefetch(&w.views[w.reached[q + CLK_CHAIN_PFV]]);
+        if (CLK_CHAIN_PF && q + CLK_CHAIN_PF < w.nreached) {   // the header a pass rule / span reads
             const ChainView &a = w.views[w.reached[q + CLK_CHAIN_PF]];
             __builtin_prefetch(chain_hdr(a.data, a.nh));
             __builtin_prefetch(chain_hdr(a.data, a.nh) + 16);
@@ -1113,7 +1119,9 @@ void BatchElement::chain_route_loop(ChainWork &w0, RouteF &&route_f, PreF &&pre_
     w.counted = 0;
     for (size_t q = w.routed; q < w.nreached; q++) {
         w.routed = q + 1;
-        if (q + CLK_CHAIN_PF < w.nreached) { // the header route() reads (and a member may write)
+        if (CLK_CHAIN_PFV && q + CLK_CHAIN_PFV < w.nreached)
+            __builtin_prefetch(&w.views[w.reached[q + CLK_CHAIN_PFV]]);
+        if (CLK_CHAIN_PF && q + CLK_CHAIN_PF < w.nreached) {   // the header route() reads (and a member may write)
             const ChainView &a = w.views[w.reached[q + CLK_CHAIN_PF]];
             __builtin_prefetch(chain_hdr(a.data, a.nh), 1);
             __builtin_prefetch(chain_hdr(a.data, a.nh) + 16, 1);

@@ -11,9 +11,10 @@
 // after two warm-ups: the box's other tenants share its cores), Mpps, and
 // each thread's own rate in that run.
 // Built by click_amd.build.build_native_tests() into tests/native/bin/.
-//   mt_glue [PACKETS [ELEMENT [staged]]]   (staged: without ZEROCOPY, the
-//   packets gathered into pinned staging; the Set elements' checksums then
-//   written by the host, not by the kernel over PCIe)
+//   mt_glue [PACKETS [ELEMENT [staged|zerocopy [THREADS]]]]   (staged: without
+//   ZEROCOPY, the packets gathered into pinned staging; the Set elements'
+//   checksums then written by the host, not by the kernel over PCIe;
+//   THREADS: one thread count instead of 1, 2 and 4)
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -70,6 +71,7 @@ int main(int argc, char **argv)
     const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : (1u << 22);
     const char *only = argc > 2 && argv[2][0] ? argv[2] : nullptr;
     const bool staged = argc > 3 && std::strcmp(argv[3], "staged") == 0;
+    const int only_t = argc > 4 ? atoi(argv[4]) : 0;
     const uint32_t SLOT = 64, L = 46;
     const size_t bytes = (size_t)n * SLOT;
     uint8_t *arena = (uint8_t *)std::aligned_alloc(4096, bytes);
@@ -103,6 +105,8 @@ int main(int argc, char **argv)
         if (only && std::strcmp(only, el) != 0)
             continue;
         for (int T : {1, 2, 4}) {
+            if (only_t && T != only_t)
+                continue;
             std::vector<clk_ctx *> ctx(T);
             std::vector<clk_element *> e(T);
             const std::string conf = std::string(std::strcmp(el, "IPOutputCombo") == 0 ? "1, 10.0.0.1, 1500, " : "") +

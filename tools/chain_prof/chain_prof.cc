@@ -7,7 +7,9 @@
 // 50 us of CPU time inside the timed region (SIGPROF) and writes one line per
 // sample: the offset from the executable's start, or the shared object's
 // name; tools/chain_prof/resolve.py turns that into lines and functions.
-//   chain_prof FRAME_HEX [RUNS] [BATCH] [combos]
+//   chain_prof FRAME_HEX [RUNS] [BATCH] [combos|elements] [staged|zerocopy] [separate]
+// (separate: the members as separate elements, as bench.py's separate legs:
+// each takes all frames -- push_burst, flush, results -- then the next)
 #include <algorithm>
 #include <dlfcn.h>
 #include <signal.h>
@@ -59,7 +61,8 @@ int main(int argc, char **argv)
     for (const char *h = argv[1]; h[0] && h[1]; h += 2)
         frame.push_back((uint8_t)std::strtoul(std::string(h, 2).c_str(), nullptr, 16));
     const int runs = argc > 2 ? std::atoi(argv[2]) : 5;
-    const std::string B = ", BATCH " + std::string(argc > 3 ? argv[3] : "65536");
+    const bool zc = argc > 5 && std::string(argv[5]) == "zerocopy";
+    const std::string B = ", BATCH " + std::string(argc > 3 ? argv[3] : "65536") + (zc ? ", ZEROCOPY true" : "");
     const uint32_t n = 600000, L = (uint32_t)frame.size();
     clk_ctx *ctx = nullptr;
     if (clk_ctx_create(0, &ctx) != CLK_SUCCESS) {
@@ -85,9 +88,11 @@ int main(int argc, char **argv)
         }
         els.push_back(e);
     }
+    const bool sep = argc > 6 && std::string(argv[6]) == "separate";
     clk_chain *c = nullptr;
-    if (clk_chain_create(els.data(), (int)els.size(), &c) != CLK_SUCCESS)
+    if (!sep && clk_chain_create(els.data(), (int)els.size(), &c) != CLK_SUCCESS)
         return 3;
+    std::vector<int32_t> nhs(n, 14);
     if (samples) {                                   // armed once the GPU is set up (a signal interrupts its ioctls)
         struct sigaction sa = {};
         sa.sa_sigaction = on_prof;
@@ -115,16 +120,36 @@ int main(int argc, char **argv)
             std::copy(frame.begin(), frame.end(), arena.begin() + (size_t)i * L);
             ptrs[i] = arena.data() + (size_t)i * L;
         }
-        const auto t0 = std::chrono::steady_clock::now();
-        g_on = r > 0;
-        if (clk_chain_push_burst(c, ptrs.data(), lens.data(), nullptr, 0, n) != CLK_SUCCESS ||
-            clk_chain_flush(c) != CLK_SUCCESS) {
-            std::fprintf(stderr, "chain: %s\n", clk_chain_last_error(c));
+        void *dev = nullptr;
+        if (zc && clk_host_register(ctx, arena.data(), arena.size(), &dev) != CLK_SUCCESS) {
+            std::fprintf(stderr, "register: %s\n", clk_last_error(ctx));
             return 4;
         }
-        const uint64_t k = clk_chain_results(c, tok.data(), mem.data(), port.data(), len.data(), aux.data(), n + 1);
+        const auto t0 = std::chrono::steady_clock::now();
+        g_on = r > 0;
+        uint64_t k = 0;
+        if (sep) {
+            for (size_t m = 0; m < els.size(); m++) {
+                if (clk_element_push_burst(els[m], ptrs.data(), lens.data(), nhs.data(), 0, n) != CLK_SUCCESS ||
+                    clk_element_flush(els[m]) != CLK_SUCCESS) {
+                    std::fprintf(stderr, "element: %s\n", clk_element_last_error(els[m]));
+                    return 4;
+                }
+                k = clk_element_results(els[m], tok.data(), port.data(), len.data(), n + 1);
+                std::fill(mem.begin(), mem.begin() + (ptrdiff_t)k, (int32_t)m);
+            }
+        } else {
+            if (clk_chain_push_burst(c, ptrs.data(), lens.data(), nullptr, 0, n) != CLK_SUCCESS ||
+                clk_chain_flush(c) != CLK_SUCCESS) {
+                std::fprintf(stderr, "chain: %s\n", clk_chain_last_error(c));
+                return 4;
+            }
+            k = clk_chain_results(c, tok.data(), mem.data(), port.data(), len.data(), aux.data(), n + 1);
+        }
         const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         g_on = 0;
+        if (zc)
+            clk_host_unregister(ctx, arena.data());
         fwd = 0;
         for (uint64_t j = 0; j < k; j++)
             fwd += mem[j] == last && port[j] == 0;
@@ -134,9 +159,11 @@ int main(int argc, char **argv)
     std::vector<double> sorted = mpps;
     std::sort(sorted.begin(), sorted.end());
     double st[8] = {0};
-    clk_chain_stats(c, st, 8);
-    std::printf("{\"leg\": \"%s_chain\", \"forwarded\": %llu, \"mpps\": %.2f, \"runs_mpps\": [",
-                combos ? "combos" : "elements", (unsigned long long)fwd, sorted[sorted.size() / 2]);
+    if (c)
+        clk_chain_stats(c, st, 8);
+    std::printf("{\"leg\": \"%s%s_%s\", \"forwarded\": %llu, \"mpps\": %.2f, \"runs_mpps\": [",
+                combos ? "combos" : "elements", zc ? "_zerocopy" : "", sep ? "separate" : "chain",
+                (unsigned long long)fwd, sorted[sorted.size() / 2]);
     for (size_t k = 0; k < mpps.size(); k++)
         std::printf("%s%.2f", k ? ", " : "", mpps[k]);
     const double per = 1e9 / ((runs + 1) * (double)n);
@@ -144,7 +171,8 @@ int main(int argc, char **argv)
                 st[0] * per, st[2] * per, st[4] * per, st[6] * per, st[7] * per);
     if (samples)
         write_samples(samples);
-    clk_chain_destroy(c);
+    if (c)
+        clk_chain_destroy(c);
     for (clk_element *e : els)
         clk_element_destroy(e);
     clk_ctx_destroy(ctx);

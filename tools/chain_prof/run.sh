@@ -19,5 +19,5 @@ if [ "$1" = build ]; then
     python3 -c "import sys; sys.path.insert(0, '$R'); import bench; print(bench.c1_frame().hex())" > $B/frame.hex
 else
     cd $B
-    ./chain_prof $(cat frame.hex) ${RUNS:-5} ${BATCH:-65536} ${CHAIN:-elements}
+    ./chain_prof $(cat frame.hex) ${RUNS:-5} ${BATCH:-65536} ${CHAIN:-elements} ${MODE:-staged} ${SEP:-chain}
 fi
