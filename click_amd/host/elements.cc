@@ -547,7 +547,7 @@ int BatchElement::complete(Stage &g)
     if (!g.inflight)
         return 0;
     hipError_t e = checked(hipEventSynchronize((hipEvent_t)g.ev[2]));
-    if (g_fault_complete.exchange(0, std::memory_order_relaxed))
+    if (g_fault_complete.load(std::memory_order_relaxed) && g_fault_complete.exchange(0, std::memory_order_relaxed))
         e = hipErrorInvalidValue;
     g.inflight = false;
     int r = 0;

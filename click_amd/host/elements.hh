@@ -302,7 +302,9 @@ struct ChainWork {
 
 class Chain;
 
-class BatchElement {
+// Each element on cache lines of its own (alignas: no line shared with
+// another thread's element, whose per-packet fields would bounce it)
+class alignas(128) BatchElement {
   public:
     BatchElement(clk_ctx *ctx, const std::string &name, int noutputs);
     virtual ~BatchElement();
@@ -991,7 +993,7 @@ hipError_t glue_checked(hipError_t e);                        // the glue's test
 // rewritten bytes back once (a member whose verdict carries its rewrite
 // writes it from route() instead).  The GPU analogue of click-xform's combos
 // (ipinputcombo.cc:66-140, ipoutputcombo.cc:44-205).
-class Chain {
+class alignas(128) Chain {
   public:
     explicit Chain(const std::vector<BatchElement *> &members) : m_(members) {}
     ~Chain();
