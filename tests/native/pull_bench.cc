@@ -10,6 +10,7 @@
 //   pull_bench [SCALE]     packet counts divided by SCALE
 //   pull_bench SCALE chain REPS   the push_c1 chain leg only, REPS times
 //                                 (BATCH 8192, the Click adapter's default)
+//   pull_bench SCALE pull         the pull legs only
 #include <algorithm>
 #include "harness.hh"
 
@@ -53,17 +54,48 @@ std::vector<uint8_t> udp_packet(uint32_t L)
     return b;
 }
 
+// zerocopy: both elements ZEROCOPY true, the packets in a registered
+// receive ring (up to 384 MiB of 64 B-aligned slots, the bytes written once;
+// the kernels read them, and the Set element's kernel writes its checksum,
+// where they lie) instead of packets of their own
 template <class CA, class CB>
-void leg(const char *name, const char *ga, const char *gb, uint32_t L, int n, uint32_t batch)
+void leg(const char *name, const char *ga, const char *gb, uint32_t L, int n, uint32_t batch, bool zerocopy = false)
 {
-    const std::string conf = "BATCH " + std::to_string(batch);
+    const std::string conf = "BATCH " + std::to_string(batch) + (zerocopy ? ", ZEROCOPY true" : "");
+    const std::vector<uint8_t> x = udp_packet(L);
+    const size_t SLOT = (L + 63) & ~size_t(63);
+    const size_t RING = std::min<size_t>((size_t)n, (size_t(384) << 20) / SLOT);
+    uint8_t *arena = nullptr;
+    clk_ctx *rctx = nullptr;
+    std::vector<TPacket> pk;
+    if (zerocopy) {
+        arena = (uint8_t *)std::aligned_alloc(4096, RING * SLOT);
+        for (size_t k = 0; k < RING; k++)
+            std::memcpy(arena + k * SLOT, x.data(), L);
+        void *dbase = nullptr;
+        if (clk_ctx_create(0, &rctx) != CLK_SUCCESS || clk_host_register(rctx, arena, RING * SLOT, &dbase) != CLK_SUCCESS) {
+            std::printf("{\"leg\": \"%s_zerocopy\", \"error\": \"clk_host_register failed\"}\n", name);
+            std::free(arena);
+            return;
+        }
+        pk.resize((size_t)n);
+    }
     Host<CA> a(ga, conf, 2);
     Host<CB> b(gb, conf, 2);
     b.upstream = [&a]() { return a.pull(); };
-    const std::vector<uint8_t> x = udp_packet(L);
     auto fill = [&](int k) {
         for (int i = 0; i < k; i++) {
-            TPacket *p = make(x.data(), L, i);
+            TPacket *p;
+            if (zerocopy) {                            // the ring's slot, metadata reset
+                p = &pk[(size_t)i];
+                p->raw = arena + (size_t)i % RING * SLOT;
+                p->ring = true;
+                p->off = 0, p->len = L;
+                p->a = TAnno();
+                p->a.id = i;
+            } else {
+                p = make(x.data(), L, i);
+            }
             p->nh = 0;
             a.input.push_back(p);
         }
@@ -98,16 +130,21 @@ void leg(const char *name, const char *ga, const char *gb, uint32_t L, int n, ui
     size_t slow = 0;
     for (uint32_t t : v)
         slow += t > 10000;
-    std::printf("{\"leg\": \"%s\", \"graph\": \"Queue -> %s -> %s -> pull\", \"batch\": %u, \"bytes\": %u, \"packets\": %d, "
+    std::printf("{\"leg\": \"%s%s\", \"graph\": \"Queue -> %s -> %s -> pull\", \"batch\": %u, \"bytes\": %u, \"packets\": %d, "
                 "\"delivered\": %zu, \"dropped\": %zu, \"seconds\": %.4f, \"mpps\": %.2f, "
                 "\"pull_ns\": {\"p50\": %u, \"p99\": %u, \"p999\": %u, \"max\": %u}, \"pulls_over_10us\": %zu, "
                 "\"batches\": [%llu, %llu]}\n",
-                name, ga, gb, batch, L, n, got.size(), a.out[1].size() + b.out[1].size(), sec,
+                name, zerocopy ? "_zerocopy" : "", ga, gb, batch, L, n, got.size(), a.out[1].size() + b.out[1].size(), sec,
                 (double)got.size() / sec / 1e6, pct(0.5), pct(0.99), pct(0.999), v.empty() ? 0u : v.back(), slow,
                 std::stoull(a.handler("batches")) - std::stoull(b0), std::stoull(b.handler("batches")) - std::stoull(b1));
     std::fflush(stdout);
     for (TPacket *p : got)
         TOps::kill(p);
+    if (zerocopy) {
+        clk_host_unregister(rctx, arena);
+        clk_ctx_destroy(rctx);
+        std::free(arena);
+    }
 }
 
 // Push context, config 1 (fake-iprouter's forwarding path: 114 B frames,
@@ -313,6 +350,14 @@ int main(int argc, char **argv)
             push_c1(600000 / scale, true, ADAPTER_BATCH, std::string(argv[2]) == "chain_source");
         return 0;
     }
+    if (argc > 2 && std::string(argv[2]) == "pull") {   // the pull legs only
+        for (uint32_t batch : {65536u, 4096u})
+            for (bool zc : {false, true}) {
+                leg<CheckIPC, SetC>("pull_c2", "CheckIPHeader", "SetIPChecksum", 64, 2000000 / scale, batch, zc);
+                leg<PlainC, SetC>("pull_c3", "CheckUDPHeader", "SetUDPChecksum", 1500, 1000000 / scale, batch, zc);
+            }
+        return 0;
+    }
     if (argc > 2 && std::string(argv[2]) == "c3") {     // the C3 push legs only
         for (bool zc : {false, true})
             push_c3(2000000 / scale, zc, ADAPTER_BATCH);
@@ -327,9 +372,10 @@ int main(int argc, char **argv)
             push_c1(600000 / scale, false, batch, source);
             push_c1(600000 / scale, true, batch, source);
         }
-    for (uint32_t batch : {65536u, 4096u}) {
-        leg<CheckIPC, SetC>("pull_c2", "CheckIPHeader", "SetIPChecksum", 64, 2000000 / scale, batch);
-        leg<PlainC, SetC>("pull_c3", "CheckUDPHeader", "SetUDPChecksum", 1500, 1000000 / scale, batch);
-    }
+    for (uint32_t batch : {65536u, 4096u})
+        for (bool zc : {false, true}) {
+            leg<CheckIPC, SetC>("pull_c2", "CheckIPHeader", "SetIPChecksum", 64, 2000000 / scale, batch, zc);
+            leg<PlainC, SetC>("pull_c3", "CheckUDPHeader", "SetUDPChecksum", 1500, 1000000 / scale, batch, zc);
+        }
     return 0;
 }
