@@ -11,6 +11,9 @@
 #                       the frames made from a pool as they are pushed), flat profile
 #   run.sh null_build   here: the measurement program over the null glue, to
 #                       run on the GPU box's host cores (run.sh null_run)
+#   run.sh sampler_build  here: the same with sampler.hh in its main file
+#                       (bin/pull_bench_null_s; SAMPLES=file when run, then
+#                       tools/chain_prof/resolve.py bin/pull_bench_null_s file)
 set -e
 D=$(cd "$(dirname "$0")" && pwd); R=$D/../..
 mkdir -p $D/bin
@@ -29,6 +32,13 @@ gprof_run)
     ;;
 null_build)
     g++ -std=c++17 -O2 -g -I$R/include $R/tests/native/pull_bench.cc $D/null_glue.cc -o $D/bin/pull_bench_null
+    ;;
+sampler_build)
+    clang=/opt/rocm/llvm/bin/clang++
+    $clang -std=c++17 -O2 -gdwarf-4 -I$R/include -include $D/sampler.hh -c $R/tests/native/pull_bench.cc -o $D/bin/pb.o
+    $clang -std=c++17 -O2 -gdwarf-4 -I$R/include -c $D/null_glue.cc -o $D/bin/ng.o
+    $clang $D/bin/pb.o $D/bin/ng.o -o $D/bin/pull_bench_null_s -ldl
+    rm -f $D/bin/pb.o $D/bin/ng.o
     ;;
 null_run)
     cd $D/bin && ./pull_bench_null ${1:-1}
