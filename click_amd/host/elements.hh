@@ -138,10 +138,6 @@ bool parse_prefix(const std::string &s, uint32_t *saddr, uint32_t *mask);
 #ifndef CLK_CHAIN_PF
 #define CLK_CHAIN_PF 24
 #endif
-// ... and the view (ChainView) it takes that header's address from
-#ifndef CLK_CHAIN_PFV
-#define CLK_CHAIN_PFV 0
-#endif
 inline const uint8_t *chain_hdr(const uint8_t *data, int32_t nh) { return data + (nh > 0 ? nh : 0); }
 
 inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail)
@@ -167,11 +163,14 @@ struct ChainView {           // a packet as a chain member sees it
     int32_t nh;
     uint16_t anno;
 };
-struct ChainExit {           // a result leaving the chain at `member`
+struct ChainExit {           // a result leaving the chain at `member` (24 B)
     uint64_t token;
-    int32_t member, port;
     uint32_t length, aux;
     uint32_t idx;            // the packet's place in the batch (~0u: a clone / new packet)
+    int16_t member, port;    // (a chain has at most 64 members; ports are small, CLK_PORT_* negative)
+    ChainExit() = default;
+    ChainExit(uint64_t t, int32_t m, int32_t p, uint32_t l, uint32_t a, uint32_t i)
+        : token(t), length(l), aux(a), idx(i), member((int16_t)m), port((int16_t)p) { }
 };
 // A member's decision a chain can take without asking it: the packets its
 // span() decides on the host and its route() then passes on unchanged
@@ -873,8 +872,6 @@ inline void BatchElement::chain_prep_loop(ChainWork &w0, SpanF &&span_f, CloneF 
     w.counted = 0;
     for (size_t q = w.nprep; q < w.nreached; q++) {
         const uint32_t i = w.reached[q];
-        if (CLK_CHAIN_PFV && q + CLK_CHAIN_PFV < w.nreached)
-            __builtin_prefetch(&w.views[w.reached[q + CLK_CHAIN_PFV]]);
         if (CLK_CHAIN_PF && q + CLK_CHAIN_PF < w.nreached) {   // the header a pass rule / span reads
             const ChainView &a = w.views[w.reached[q + CLK_CHAIN_PF]];
             __builtin_prefetch(chain_hdr(a.data, a.nh));
@@ -1119,10 +1116,10 @@ void BatchElement::chain_route_loop(ChainWork &w0, RouteF &&route_f, PreF &&pre_
 {
     ChainWork w = w0;                         // a private copy, as in chain_prep_loop
     w.counted = 0;
+    if (w.out->capacity() < w.out->size() + 2 * (w.nreached - w.routed))   // a result and a clone per packet
+        w.out->reserve(std::max(w.out->size() + 2 * (w.nreached - w.routed), 2 * w.out->capacity()));
     for (size_t q = w.routed; q < w.nreached; q++) {
         w.routed = q + 1;
-        if (CLK_CHAIN_PFV && q + CLK_CHAIN_PFV < w.nreached)
-            __builtin_prefetch(&w.views[w.reached[q + CLK_CHAIN_PFV]]);
         if (CLK_CHAIN_PF && q + CLK_CHAIN_PF < w.nreached) {   // the header route() reads (and a member may write)
             const ChainView &a = w.views[w.reached[q + CLK_CHAIN_PF]];
             __builtin_prefetch(chain_hdr(a.data, a.nh), 1);
