@@ -122,18 +122,19 @@ template <class T> class HeldRing {
   public:
     size_t size() const { return n_; }
     bool empty() const { return n_ == 0; }
-    T &operator[](size_t k) { return v_[(h_ + k) & (v_.size() - 1)]; }
+    T &operator[](size_t k) { return v_[(h_ + k) & mask_]; }
     T &front() { return v_[h_]; }
     void push_back(const T &x)
     {
-        if (n_ == v_.size())
+        if (n_ == cap_)
             grow();
-        v_[(h_ + n_++) & (v_.size() - 1)] = x;
+        v_[(h_ + n_) & mask_] = x;
+        n_++;
     }
     void pop_back() { n_--; }
     void pop_front()
     {
-        h_ = (h_ + 1) & (v_.size() - 1);
+        h_ = (h_ + 1) & mask_;
         n_--;
     }
     void clear() { h_ = n_ = 0; }
@@ -146,9 +147,12 @@ template <class T> class HeldRing {
             w[k] = (*this)[k];
         v_.swap(w);
         h_ = 0;
+        cap_ = v_.size();
+        mask_ = cap_ - 1;
     }
     std::vector<T> v_;
     size_t h_ = 0, n_ = 0;
+    size_t cap_ = 0, mask_ = 0;     // v_.size() and v_.size() - 1, kept (no division per access)
 };
 
 // One result as a class's finish() sees it (built in registers from a Chunk

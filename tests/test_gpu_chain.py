@@ -379,6 +379,53 @@ def test_zerocopy_chain(ctx, which):
         ctx.host_unregister(a2)
 
 
+@pytest.mark.parametrize("which", ["elements", "combos"])
+def test_zerocopy_chain_two_regions(ctx, which):
+    """A ZEROCOPY chain fed from two registered regions in turns (runs of 500
+    frames from each, as packets from two mempools): a batch ends where the
+    region changes (push's fast path hands over to the slow one), and every
+    result and byte equals the staged elements one by one."""
+    arena0, foff, flen = fake_frames(6000)
+    n = len(foff)
+    anno = np.zeros(n, np.uint32)
+    spec = FAKE_IPROUTER if which == "elements" else COMBOS
+    a1 = arena0.copy()
+    r1, e1 = run_separate(ctx, spec, a1, foff, flen, -1, anno)
+    regions, raws = [], []
+    for _ in range(2):
+        raw = np.zeros(arena0.size + 8192, np.uint8)
+        a = raw[(-raw.ctypes.data) % 4096:][:arena0.size]
+        a[:] = arena0
+        ctx.host_register(a)
+        regions.append(a)
+        raws.append(raw)
+    try:
+        from click_amd.elements import Chain
+        zspec = [(c, ", ".join(x for x in (conf, "ZEROCOPY true") if x), k) for c, conf, k in spec]
+        els = make(ctx, zspec)
+        ch = Chain(els)
+        src = [(i // 500) % 2 for i in range(n)]
+        for i in range(n):
+            if ch.push_anno(regions[src[i]].ctypes.data + int(foff[i]), int(flen[i]), -1, 0, i):
+                ch.flush_async()
+        ch.flush()
+        tok, mem, port, length, aux = ch.results()
+        r2 = list(zip(tok.tolist(), mem.tolist(), port.tolist(), length.tolist(), aux.tolist()))
+        for k in range(len(spec)):
+            assert [x[:4] for x in r1 if x[1] == k] == [y[:4] for y in r2 if y[1] == k], spec[k][0]
+            for h in ("drops", "packets", "lost"):
+                assert e1[k].read_handler(h) == els[k].read_handler(h), (spec[k][0], h)
+        for i in range(n):                      # each frame's bytes in the region it was pushed from
+            o, ln = int(foff[i]), int(flen[i])
+            assert np.array_equal(regions[src[i]][o:o + ln], a1[o:o + ln]), i
+        ch.close()
+        for e in e1 + els:
+            e.close()
+    finally:
+        for a in regions:
+            ctx.host_unregister(a)
+
+
 def test_chain_refuses(ctx):
     import click_amd
     from click_amd import ClickAmdError
