@@ -770,8 +770,11 @@ struct HostRegion {
 };
 std::mutex g_regions_mu;
 std::vector<HostRegion> g_regions;
-std::atomic<uint64_t> g_regions_gen{1};
+std::atomic<uint64_t> &g_regions_gen = clk::host_regions_gen;
 }   // namespace
+namespace clk {
+alignas(64) std::atomic<uint64_t> host_regions_gen{1};   // its own line: read per packet by every thread
+}
 
 extern "C" {
 

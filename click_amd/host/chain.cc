@@ -309,7 +309,7 @@ inline int Chain::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
         return push_slow(data, length, nh_offset, token, anno);
     if (zerocopy_) {                                 // in the batch's registered region, as the packet before
         if (data >= B.zc_host && data + (length ? length : 1) <= zc_last_ + zc_last_bytes_ &&
-            B.zc_host == zc_last_ && clk_host_generation_internal() == zc_gen_) {
+            B.zc_host == zc_last_ && host_generation() == zc_gen_) {
             record(B, data, length, nh_offset, token, anno, (uint64_t)(data - B.zc_host), 0);
             return B.np >= cap0_ ? 1 : 0;
         }
@@ -347,7 +347,7 @@ int Chain::push_slow(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t
         // ZEROCOPY: the kernels read and write the packets where they lie,
         // in registered host memory (clk_host_register); one region per batch
         const uint8_t *a = data;
-        const uint64_t gen = clk_host_generation_internal();
+        const uint64_t gen = host_generation();
         if (gen != zc_gen_ || !(a >= zc_last_ && a + (length ? length : 1) <= zc_last_ + zc_last_bytes_)) {
             void *hs = nullptr, *db = nullptr;
             size_t nb = 0;

@@ -314,7 +314,7 @@ inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length
     } else if (zerocopy_) {
         // the kernel reads the span where it lies (clk_host_register)
         const uint8_t *a = data + off;
-        const uint64_t gen = clk_host_generation_internal();
+        const uint64_t gen = host_generation();
         if (gen != zc_gen_ || !(a >= zc_last_ && a + len <= zc_last_ + zc_last_bytes_)) {
             void *hs = nullptr, *db = nullptr;
             size_t nb = 0;
