@@ -266,6 +266,13 @@ struct ChainWork {
 // virtual call per packet).
 #define CLK_INL __attribute__((always_inline))
 #define CLK_GLUE_LOOPS(C)                                                                                       \
+    int push(uint8_t *d_, uint32_t l_, int32_t nh_, uint64_t t_, uint32_t a_ = 0) override                      \
+    {                                                                                                           \
+        return push_one([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) CLK_INL {                 \
+            bool r_; [[clang::always_inline]] r_ = this->C::span(p, o, l, c);                                   \
+            return r_;                                                                                          \
+        }, d_, l_, nh_, t_, a_);                                                                                \
+    }                                                                                                           \
     int push_burst(uint8_t *const *d_, const uint32_t *l_, const int32_t *nh_, uint64_t t0_, uint32_t n_) override \
     {                                                                                                           \
         return burst_loop([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) CLK_INL {               \
@@ -309,7 +316,8 @@ class alignas(128) BatchElement {
     virtual ~BatchElement();
     virtual const char *class_name() const = 0;
     virtual int configure(ConfArgs &args, std::string *err);
-    int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno = 0);
+    // one packet (the final classes run it with their span() inlined, CLK_GLUE_LOOPS)
+    virtual int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno = 0);
     // a burst of packets (tokens first_token + k), flushing double-buffered
     // whenever the batch fills; the final classes run it with their span()
     // inlined (CLK_GLUE_LOOPS)
