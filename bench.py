@@ -439,30 +439,32 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
 READ_SHAPES = {0: "gs8_nt_8k", 1: "gs4_nt_8k", 2: "gs16_nt_2k", 3: "wave8_nt_4k"}
 
 
-def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5, launches=10, detail=None):
+def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5, launches=10, rounds=3, detail=None):
     """Measured HBM read-stream ceiling: clk_read_stream in the four best
     shapes of tools/probes/read_probe.hip (CLK_TUNE_READ_SHAPE: nontemporal
     16 B loads, grid-stride with 4 / 8 / 16 in flight per lane on a capped
     grid, or wave-contiguous runs), each `launches` back to back, best of
-    `reps`; the best shape's GB/s (`detail`: every shape's)."""
+    `reps`, the shapes taken in turn for `rounds` rounds (one slow moment of
+    the box does not set a shape's figure); the best shape's GB/s (`detail`:
+    every shape's)."""
     buf = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     buf.fill_(1)
     out = torch.zeros(1, dtype=torch.int64, device="cuda")
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    rates = {}
-    for shape, name in READ_SHAPES.items():
-        ctx.tune(read_shape=shape)
-        ctx.read_stream(buf, out=out)
-        torch.cuda.synchronize()
-        best = 1e30
-        for _ in range(reps):
-            s.record()
-            for _ in range(launches):
-                ctx.read_stream(buf, out=out)
-            e.record()
+    best = {name: 1e30 for name in READ_SHAPES.values()}
+    for _ in range(rounds):
+        for shape, name in READ_SHAPES.items():
+            ctx.tune(read_shape=shape)
+            ctx.read_stream(buf, out=out)
             torch.cuda.synchronize()
-            best = min(best, s.elapsed_time(e) / launches)
-        rates[name] = round(nbytes / (best * 1e-3) / 1e9, 1)
+            for _ in range(reps):
+                s.record()
+                for _ in range(launches):
+                    ctx.read_stream(buf, out=out)
+                e.record()
+                torch.cuda.synchronize()
+                best[name] = min(best[name], s.elapsed_time(e) / launches)
+    rates = {name: round(nbytes / (ms * 1e-3) / 1e9, 1) for name, ms in best.items()}
     ctx.tune(read_shape=0)
     del buf
     torch.cuda.empty_cache()

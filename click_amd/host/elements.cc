@@ -590,29 +590,34 @@ int BatchElement::complete(Stage &g)
 // Route a completed stage's packets in push order: the kernel's code (or the
 // host's decision) through the class's route(), plus the results that
 // precede / follow a packet's own (IPOutputCombo's clone, fragments).
-template <class RouteF>
-void BatchElement::route_loop(Stage &g, RouteF &&route_f)
+template <class RouteF, class PreF>
+void BatchElement::route_loop(Stage &g, RouteF &&route_f, PreF &&pre_f)
 {
     size_t k = 0;
     const bool sums = wants_sums(), pre = has_pre_route_, post = has_post_route_;
     results_.reserve_more(g.pend.size());
+    // the stage's arrays in locals: route() stores packet bytes, which may
+    // alias anything in memory, and the loop would reload them per packet
+    Pending *const pend = g.pend.data();
+    const uint8_t *const codes = g.h_codes;
+    const uint16_t *const sumv = g.h_sums;
     const size_t np = g.pend.size();
     for (size_t q = 0; q < np; q++) {
-        Pending &p = g.pend[q];
+        Pending &p = pend[q];
         if (q + 8 < np)                      // the packet route() may read, 8 ahead
-            __builtin_prefetch(g.pend[q + 8].data + g.pend[q + 8].span_off);
+            __builtin_prefetch(pend[q + 8].data + pend[q + 8].span_off);
         int code;
         uint16_t sum = 0;
         if (p.host_code >= 0) {
             code = p.host_code;
         } else {
-            code = g.h_codes[k];
-            sum = sums ? g.h_sums[k] : 0;
+            code = codes[k];
+            sum = sums ? sumv[k] : 0;
             k++;
         }
         Result r{p.token, 0, p.length, 0};
         Result pr;
-        if (pre && pre_route(p, &pr))
+        if (pre && pre_f(p, &pr))
             results_.push_back(pr);
         route_f(p, code, sum, &r);
         if (pre || post)
@@ -626,7 +631,8 @@ void BatchElement::route_loop(Stage &g, RouteF &&route_f)
 
 void BatchElement::route_stage(Stage &g)
 {
-    route_loop(g, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); });
+    route_loop(g, [this](Pending &p, int code, uint16_t sum, Result *r) { route(p, code, sum, r); },
+               [this](Pending &p, Result *r) { return pre_route(p, r); });
 }
 
 // Route every packet of a stage as killed (CLK_PORT_KILL), in push order.

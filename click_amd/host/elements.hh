@@ -284,6 +284,9 @@ struct ChainWork {
     {                                                                                                           \
         route_loop(g_, [this](Pending &p, int code, uint16_t sum, Result *r) CLK_INL {                          \
             [[clang::always_inline]] this->C::route(p, code, sum, r);                                           \
+        }, [this](Pending &p, Result *r) CLK_INL {                                                              \
+            bool r_; [[clang::always_inline]] r_ = this->C::pre_route(p, r);                                    \
+            return r_;                                                                                          \
         });                                                                                                     \
     }                                                                                                           \
     void chain_prep(ChainWork &w_) override                                                                    \
@@ -496,8 +499,8 @@ class alignas(128) BatchElement {
     template <class SpanF>
     int burst_loop(SpanF &&span_f, uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets,
                    uint64_t first_token, uint32_t n);
-    template <class RouteF>
-    void route_loop(Stage &g, RouteF &&route_f);
+    template <class RouteF, class PreF>
+    void route_loop(Stage &g, RouteF &&route_f, PreF &&pre_f);
     // route every packet of a completed stage, in push order (results_)
     virtual void route_stage(Stage &g);
 
