@@ -262,9 +262,8 @@ void Chain::size_packets(Batch &B, size_t c)
     for (auto *v : {&B.staged, &B.back, &B.clone_key})
         if (v->size() < c)
             v->resize(c);
-    for (auto *v : {&B.done, &B.copied})
-        if (v->size() < c)
-            v->resize(c);
+    if (B.copied.size() < c)
+        B.copied.resize(c);
 }
 
 // The batch outgrew its arrays (a caller that pushes past a full batch)
@@ -287,7 +286,7 @@ CLK_INL inline void Chain::record(Batch &B, uint8_t *data, uint32_t length, int3
                           uint64_t slot, uint32_t need)
 {
     const uint32_t i = (uint32_t)B.np++;
-    B.views[i] = ChainView{data, token, slot, length, nh_offset, (uint16_t)anno};
+    B.views[i] = ChainView{data, token, slot, length, nh_offset, (uint16_t)anno, 0};
     if (!zerocopy_) {
         B.slot0[i] = slot;
         B.staged[i] = need;
@@ -295,7 +294,6 @@ CLK_INL inline void Chain::record(Batch &B, uint8_t *data, uint32_t length, int3
         B.copied[i] = 0;
     }
     B.clone_key[i] = 0;
-    B.done[i] = 0;
     ChainWork &w0 = B.mm[0].w;
     w0.reached[w0.nreached++] = i;
 }
@@ -484,7 +482,6 @@ void Chain::setup(Batch &B, size_t k)
     w.reached = M.reached.data(), w.code = M.code.data(), w.span_off = M.span_off.data();
     w.span_len = M.span_len.data();
     w.views = B.views.data();                        // (sized for mcap packets: they stay put)
-    w.done = B.done.data();
     w.next = k + 1 < B.mm.size() ? &B.mm[k + 1].w : nullptr;
     w.elem = e;
     w.out = &B.out;
@@ -609,7 +606,7 @@ bool Chain::kill_member(Batch &B, size_t k, int r)
     for (size_t q = w.routed; q < w.nreached; q++) {
         const uint32_t i = w.reached[q];
         B.out.push_back(ChainExit{B.views[i].token, (int32_t)k, CLK_PORT_KILL, B.views[i].length, 0, i});
-        B.done[i] = 1;
+        B.views[i].done = 1;
         e->lost_++;
     }
     w.routed = w.nreached;
@@ -874,7 +871,7 @@ int Chain::copy_back(Batch &B, bool all)
 {
     bool any = false;
     for (size_t i = 0; i < B.np && !any; i++)
-        any = B.back[i] && !B.copied[i] && (all || B.done[i]);
+        any = B.back[i] && !B.copied[i] && (all || B.views[i].done);
     if (any) {
         hipStream_t s = stream();
         double t0 = now_s();
@@ -889,7 +886,7 @@ int Chain::copy_back(Batch &B, bool all)
         stats_[5] += now_s() - t0;
         t0 = now_s();
         for (size_t i = 0; i < B.np; i++)
-            if (B.back[i] && !B.copied[i] && (all || B.done[i])) {
+            if (B.back[i] && !B.copied[i] && (all || B.views[i].done)) {
                 std::memcpy(B.views[i].data - (B.views[i].slot - B.slot0[i]), B.h_back + B.slot0[i], B.back[i]);
                 B.copied[i] = 1;
             }
@@ -958,10 +955,10 @@ uint64_t Chain::abandon()
             drop_clones(B, j, w.routed, w.nreached);
             for (size_t q = w.routed; q < w.nreached; q++) {
                 const uint32_t i = w.reached[q];
-                if (B.done[i])
+                if (B.views[i].done)
                     continue;
                 B.out.push_back(ChainExit{B.views[i].token, (int32_t)j, CLK_PORT_KILL, B.views[i].length, 0, i});
-                B.done[i] = 1;
+                B.views[i].done = 1;
                 m_[j]->lost_++;
                 k++;
             }

@@ -162,6 +162,8 @@ struct ChainView {           // a packet as a chain member sees it
     uint32_t length;
     int32_t nh;
     uint16_t anno;
+    uint16_t done;           // it has left the chain (a 16-bit store: a byte store would alias
+                             // every field the loops keep in registers)
 };
 struct ChainExit {           // a result leaving the chain at `member` (24 B)
     uint64_t token;
@@ -194,7 +196,6 @@ enum ChainPass {
 enum : int32_t { CHAIN_CODE_PASS = INT32_MIN };
 struct ChainWork {
     ChainView *views = nullptr;               // per chain packet, updated as it passes members
-    uint8_t *done = nullptr;                  // per chain packet: has left the chain
     uint32_t *reached = nullptr;              // the packets that reached this member, in push order
     int32_t *code = nullptr;                  // per reached packet (CHAIN_CODE_PASS, GPU index, -1 - host code)
     uint32_t *span_off = nullptr;             // per reached packet with a descriptor: its span
@@ -422,7 +423,7 @@ class alignas(128) BatchElement {
         if (w.last) {
             const ChainView &v = w.views[i];
             w.out->push_back(ChainExit{v.token, w.member, 0, v.length, 0, i});
-            w.done[i] = 1;
+            w.views[i].done = 1;
         } else {
             chain_forward(w, i);
         }
@@ -441,7 +442,7 @@ class alignas(128) BatchElement {
             n->elem->packets_++;
             if (n->last) {
                 n->out->push_back(ChainExit{v.token, n->member, 0, v.length, 0, i});
-                n->done[i] = 1;
+                n->views[i].done = 1;
                 return;
             }
             n = n->next;
@@ -960,7 +961,7 @@ inline bool BatchElement::chain_route_pending(ChainWork &w, uint32_t i, Pending 
             w.out->push_back(ChainExit{r.token, w.member, CLK_PORT_NEXT, r.length, r.aux, i});
     } else {
         w.out->push_back(ChainExit{r.token, w.member, r.port, r.length, r.aux, i});
-        w.done[i] = 1;
+        v.done = 1;
     }
     if (has_post_route_) {                    // results that follow the packet's own (fragments)
         post_route(p, code, chain_side_);
@@ -1050,7 +1051,7 @@ class alignas(128) Chain {
         std::vector<ChainView> views;             // as they move through the members
         std::vector<uint64_t> slot0;              // staging offset as pushed (data moves with slot)
         std::vector<uint32_t> staged, back, clone_key;   // bytes staged / to copy back, a kept clone's key
-        std::vector<uint8_t> done, copied;        // left the chain; bytes copied back
+        std::vector<uint8_t> copied;              // bytes copied back
         size_t np = 0, mcap = 0;                  // packets in the batch; the arrays' size
         uint8_t *h_arena = nullptr, *h_back = nullptr, *h_snap = nullptr, *d_arena = nullptr;
         size_t h_cap = 0, back_cap = 0, snap_cap = 0, d_cap = 0, used = 0;
