@@ -436,14 +436,17 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
             "note": "kernel time (one plan + look-back + write launch, after a small memset); first-fragment headers restored between steps"}
 
 
-READ_SHAPES = {0: "gs8_nt_8k", 1: "gs4_nt_8k", 2: "gs16_nt_2k", 3: "wave8_nt_4k"}
+READ_SHAPES = {0: "gs8_nt_8k", 1: "gs4_nt_8k", 2: "gs16_nt_2k", 3: "wave8_nt_4k", 4: "rows1536_nt",
+               5: "rows1536_nt_8k"}
 
 
 def read_stream_peak(torch, ctx, nbytes=8 << 30, reps=5, launches=10, rounds=3, detail=None):
     """Measured HBM read-stream ceiling: clk_read_stream in the four best
     shapes of tools/probes/read_probe.hip (CLK_TUNE_READ_SHAPE: nontemporal
     16 B loads, grid-stride with 4 / 8 / 16 in flight per lane on a capped
-    grid, or wave-contiguous runs), each `launches` back to back, best of
+    grid, or wave-contiguous runs) and the fixed-geometry Check kernels' own
+    pattern without their arithmetic (16-lane groups on 1536 B rows, 6 loads
+    per lane), each `launches` back to back, best of
     `reps`, the shapes taken in turn for `rounds` rounds (one slow moment of
     the box does not set a shape's figure); the best shape's GB/s (`detail`:
     every shape's)."""
@@ -964,8 +967,11 @@ def config1(ctx, n=C1_PACKETS, batch=65536):
         head.flush()
         tok, port, ln = head.results(bufs=rbufs)
         keep = port == 0
-        sel = tok[keep].astype(np.int64)
-        ch.push_burst(ptrs[sel], ln[keep].astype(np.uint32), nhs[sel], first_token=0)
+        if keep.all() and len(tok) == n:         # every frame on (in push order): no re-indexing
+            ch.push_burst(ptrs, ln if ln.dtype == np.uint32 else ln.astype(np.uint32), nhs, first_token=0)
+        else:
+            sel = tok[keep].astype(np.int64)
+            ch.push_burst(ptrs[sel], ln[keep].astype(np.uint32), nhs[sel], first_token=0)
         ch.flush()
         k = int(ch.lib.clk_chain_results(ch.h, *cptrs, n + 1))
         dt = time.perf_counter() - t0

@@ -469,7 +469,7 @@ int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value)
         ctx->set_chunks = (int)value;
         return CLK_SUCCESS;
     case CLK_TUNE_READ_SHAPE:
-        if (value < 0 || value > 3) break;
+        if (value < 0 || value > 5) break;
         ctx->read_shape = (int)value;
         return CLK_SUCCESS;
     case CLK_TUNE_GROUP:
@@ -896,6 +896,12 @@ int clk_read_stream(clk_ctx *ctx, const void *base, uint64_t bytes, uint64_t *ou
         break;
     case 3:
         hipLaunchKernelGGL(clk::read_wave_kernel<8>, dim3(grid(4096, 8 * BLOCK)), dim3(BLOCK), 0, ctx->cur, p, n16, o);
+        break;
+    case 4:     // rows of 1536 B, one step of 16 rows per workgroup (the C3 Check kernels' pattern)
+        hipLaunchKernelGGL(clk::read_rows_kernel<6>, dim3(grid(1u << 30, 16 * 96)), dim3(BLOCK), 0, ctx->cur, p, n16, o);
+        break;
+    case 5:     // ... on a grid capped at 8K workgroups
+        hipLaunchKernelGGL(clk::read_rows_kernel<6>, dim3(grid(8192, 16 * 96)), dim3(BLOCK), 0, ctx->cur, p, n16, o);
         break;
     default:
         hipLaunchKernelGGL(clk::read_stream_kernel<8>, dim3(grid(8192, 8 * BLOCK)), dim3(BLOCK), 0, ctx->cur, p, n16, o);

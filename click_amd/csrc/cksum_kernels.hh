@@ -1928,4 +1928,36 @@ __global__ void __launch_bounds__(256) read_wave_kernel(const u32x4 *p, uint64_t
         atomicAdd(out, (unsigned long long)acc);
 }
 
+// ... or as the fixed-geometry Check kernels read a C3 batch: 16-lane groups,
+// each reading one row of K x 256 B (K nontemporal 16 B loads per lane in
+// flight, lane l at l*16 + u*256), a workgroup's 16 groups on 16 consecutive
+// rows per step; the rows past the last whole step and the tail grid-strided
+template <int K>
+__global__ void __launch_bounds__(256) read_rows_kernel(const u32x4 *p, uint64_t n16, unsigned long long *out)
+{
+    const uint32_t gl = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const uint64_t row16 = 16 * K;                       // 16 B chunks per row
+    const uint64_t nsteps = n16 / (16 * row16);
+    uint32_t acc = 0;
+    for (uint64_t s = blockIdx.x; s < nsteps; s += gridDim.x) {
+        const u32x4 *q = p + (s * 16 + grp) * row16 + gl;
+        u32x4 a[K];
+#pragma unroll
+        for (int u = 0; u < K; u++)
+            a[u] = __builtin_nontemporal_load(q + 16 * u);
+#pragma unroll
+        for (int u = 0; u < K; u++)
+            acc += a[u][0] ^ a[u][1] ^ a[u][2] ^ a[u][3];
+    }
+    for (uint64_t i = nsteps * 16 * row16 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const u32x4 a0 = p[i];
+        acc += a0[0] ^ a0[1] ^ a0[2] ^ a0[3];
+    }
+    for (int m = 32; m >= 1; m >>= 1)
+        acc += __shfl_xor(acc, m, 64);
+    if ((threadIdx.x & 63) == 0 && acc)
+        atomicAdd(out, (unsigned long long)acc);
+}
+
 } // namespace clk

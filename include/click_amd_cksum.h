@@ -117,8 +117,12 @@ enum clk_tune_knob {
                                          16 B loads per lane in flight, 8K workgroups;
                                          1 the same with 4 loads; 2 with 16 loads, 2K
                                          workgroups; 3 each wave 8 KiB contiguous per
-                                         step, 4K workgroups (bench: the best is the
-                                         measured read ceiling)                      */
+                                         step, 4K workgroups; 4 16-lane groups each
+                                         reading a 1536 B row (6 loads per lane), 16
+                                         rows per workgroup step, one step per
+                                         workgroup; 5 the same on 8K workgroups
+                                         (bench: the best is the measured read
+                                         ceiling)                                    */
 };
 int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value);
 /* Last error text for `ctx` (or for the calling thread when ctx == NULL). */
