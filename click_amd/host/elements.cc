@@ -386,13 +386,26 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
                     length, nh_offset, token, anno);
 }
 
+#ifndef CLK_BURST_PF
+#define CLK_BURST_PF 3
+#endif
 template <class SpanF>
 int BatchElement::burst_loop(SpanF &&span_f, uint8_t *const *datas, const uint32_t *lengths,
                              const int32_t *nh_offsets, uint64_t first_token, uint32_t n)
 {
+    // the bytes a gather copies, CLK_BURST_PF packets ahead (staged long
+    // spans: a packet's lines are fetched while the ones before are copied)
+    const uint32_t ahead = zerocopy_ ? 0u : CLK_BURST_PF;
+    const uint32_t pf_bytes = std::min<uint32_t>(stage_cap_, 1u << 14);
     for (uint32_t k = 0; k < n; k++) {
         if (k + 8 < n)
             __builtin_prefetch(datas[k + 8]);                     // the header span() reads
+        if (ahead && k + ahead < n && pf_bytes > 256) {
+            const uint8_t *a = datas[k + ahead];
+            const uint32_t m = std::min(lengths[k + ahead], pf_bytes);
+            for (uint32_t o = 64; o < m; o += 64)
+                __builtin_prefetch(a + o);
+        }
         int r = push_one(span_f, datas[k], lengths[k], nh_offsets ? nh_offsets[k] : -1, first_token + k, 0);
         if (r < 0)
             return r;
