@@ -304,7 +304,7 @@ void BatchElement::chain_route_all(ChainWork &w)
 
 template <class SpanF>
 inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token,
-                                  uint32_t anno)
+                                  uint32_t anno, bool single)
 {
     Pending p{data, token, 0, length, nh_offset, 0, 0, 0, -1, (uint16_t)anno};
     uint32_t off = 0, len = 0;
@@ -359,7 +359,10 @@ inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length
             err_ = "out of pinned host memory";
             return CLK_EINVAL;
         }
-        stage_copy(g.h_arena + slot, data + off, copy, len);
+        if (single && CLK_STAGE_DEFER && copy >= CLK_STAGE_DEFER)   // copied by launch(), with the batch
+            g.gather.push_back(Stage::Gather{data + off, slot, copy, len});
+        else
+            stage_copy(g.h_arena + slot, data + off, copy, len);
         p.slot = slot;
         p.span_off = off;
         p.span_len = len;
@@ -383,12 +386,9 @@ inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length
 int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
 {
     return push_one([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); }, data,
-                    length, nh_offset, token, anno);
+                    length, nh_offset, token, anno, true);
 }
 
-#ifndef CLK_BURST_PF
-#define CLK_BURST_PF 3
-#endif
 template <class SpanF>
 int BatchElement::burst_loop(SpanF &&span_f, uint8_t *const *datas, const uint32_t *lengths,
                              const int32_t *nh_offsets, uint64_t first_token, uint32_t n)
@@ -406,7 +406,7 @@ int BatchElement::burst_loop(SpanF &&span_f, uint8_t *const *datas, const uint32
             for (uint32_t o = 64; o < m; o += 64)
                 __builtin_prefetch(a + o);
         }
-        int r = push_one(span_f, datas[k], lengths[k], nh_offsets ? nh_offsets[k] : -1, first_token + k, 0);
+        int r = push_one(span_f, datas[k], lengths[k], nh_offsets ? nh_offsets[k] : -1, first_token + k, 0, false);
         if (r < 0)
             return r;
         if (r == 1 && (r = flush_async()) != 0)                  // stage the next batch while this one runs
@@ -484,6 +484,16 @@ int BatchElement::launch(Stage &g)
             g.inflight = false;
             err_ = "out of device memory";
             return CLK_EHIP;
+        }
+        if (!g.zc && !g.gather.empty()) {        // the long spans, three packets' lines ahead
+            const size_t ng = g.gather.size();
+            const Stage::Gather *gv = g.gather.data();
+            for (size_t q = 0; q < ng; q++) {
+                if (q + 3 < ng)
+                    for (uint32_t o = 0; o < gv[q + 3].n; o += 64)
+                        __builtin_prefetch(gv[q + 3].src + o);
+                stage_copy(g.h_arena + gv[q].slot, gv[q].src, gv[q].n, gv[q].avail);
+            }
         }
         if (!g.zc && (e = checked(hipMemcpyAsync(g.d_arena, g.h_arena, g.h_used, hipMemcpyHostToDevice, s))) !=
                          hipSuccess)
@@ -592,6 +602,7 @@ int BatchElement::complete(Stage &g)
     packets_ += g.pend.size();
     gpu_ns_ += (uint64_t)(ms * 1e6);
     g.pend.clear();
+    g.gather.clear();
     g.h_used = 0;
     g.ngpu = 0;
     g.maxlen = 0;
@@ -661,6 +672,7 @@ int BatchElement::abandon_stage(Stage &g)
     const int k = (int)g.pend.size();
     lost_ += g.pend.size();
     g.pend.clear();
+    g.gather.clear();
     g.h_used = 0;
     g.ngpu = 0;
     g.maxlen = 0;

@@ -138,6 +138,16 @@ bool parse_prefix(const std::string &s, uint32_t *saddr, uint32_t *mask);
 #ifndef CLK_CHAIN_PF
 #define CLK_CHAIN_PF 24
 #endif
+// a push burst prefetches each staged packet's span this many packets ahead
+#ifndef CLK_BURST_PF
+#define CLK_BURST_PF 3
+#endif
+// a packet pushed alone (not in a burst) whose staged span is at least this
+// long is gathered at launch, in one loop over the batch with its next
+// packets' lines prefetched (0: at push)
+#ifndef CLK_STAGE_DEFER
+#define CLK_STAGE_DEFER 256
+#endif
 inline const uint8_t *chain_hdr(const uint8_t *data, int32_t nh) { return data + (nh > 0 ? nh : 0); }
 
 inline void stage_copy(uint8_t *dst, const uint8_t *src, uint32_t n, uint32_t avail)
@@ -272,7 +282,7 @@ struct ChainWork {
         return push_one([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) CLK_INL {                 \
             bool r_; [[clang::always_inline]] r_ = this->C::span(p, o, l, c);                                   \
             return r_;                                                                                          \
-        }, d_, l_, nh_, t_, a_);                                                                                \
+        }, d_, l_, nh_, t_, a_, true);                                                                          \
     }                                                                                                           \
     int push_burst(uint8_t *const *d_, const uint32_t *l_, const int32_t *nh_, uint64_t t0_, uint32_t n_) override \
     {                                                                                                           \
@@ -468,6 +478,14 @@ class alignas(128) BatchElement {
     // fragment buffers serves one batch at a time).
     struct Stage {
         std::vector<Pending> pend;
+        // long spans are gathered at launch, not at push: one loop over the
+        // batch that fetches the next packets' lines while it copies
+        struct Gather {
+            const uint8_t *src;
+            uint64_t slot;
+            uint32_t n, avail;
+        };
+        std::vector<Gather> gather;
         uint8_t *h_arena = nullptr;
         size_t h_arena_cap = 0, h_used = 0;
         uint8_t *h_back = nullptr;          // the rewritten arena (wants_arena_back): h_arena stays as
@@ -496,7 +514,10 @@ class alignas(128) BatchElement {
     // callables: the generic push() and route pass virtual calls; the final
     // classes pass qualified (inlined) ones through CLK_GLUE_LOOPS.
     template <class SpanF>
-    int push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno);
+    // one packet; `single`: pushed alone (its long span is gathered at
+    // launch), not from a burst (which prefetches the spans ahead itself)
+    int push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno,
+                 bool single);
     template <class SpanF>
     int burst_loop(SpanF &&span_f, uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets,
                    uint64_t first_token, uint32_t n);
