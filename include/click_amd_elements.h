@@ -101,9 +101,11 @@ const char *clk_element_last_error(clk_element *e);
 /* Stage one host packet.  data/length = Packet::data()/length();
  * nh_offset = network_header_offset() (-1 = no network header: the IP
  * elements then use data(), as SetIPChecksum does, setipchecksum.cc:78).
- * Set elements write their result into `data` at flush(), so the packet
- * memory must stay valid until then.  Returns 1 when the batch is full and
- * should be flushed, 0 otherwise, < 0 on error.                            */
+ * Set elements write their result into `data` at flush(), and a long span
+ * (>= 256 B) of a packet pushed alone is gathered at the flush (with the
+ * batch), so the packet memory must stay valid and unchanged until then.
+ * Returns 1 when the batch is full and should be flushed, 0 otherwise,
+ * < 0 on error.                                                            */
 int clk_element_push(clk_element *e, uint8_t *data, uint32_t length, int32_t nh_offset,
                      uint64_t token);
 
