@@ -12,6 +12,7 @@
 //                                 (BATCH 8192, the Click adapter's default)
 //   pull_bench SCALE pull         the pull legs only
 #include <algorithm>
+#include <x86intrin.h>
 #include "harness.hh"
 
 namespace {
@@ -111,19 +112,25 @@ void leg(const char *name, const char *ga, const char *gb, uint32_t L, int n, ui
     std::vector<uint32_t> lat;
     got.reserve((size_t)n);
     lat.reserve((size_t)n + 1);
+    // each pull timed with the TSC (a few ns, where a clock_gettime call per
+    // pull would add ~20 ns to every packet), scaled by the steady clock
     typedef std::chrono::steady_clock clock;
     const auto t0 = clock::now();
-    auto s = t0;
+    const uint64_t c0 = __rdtsc();
+    uint64_t s = c0;
     for (;;) {
         TPacket *p = b.pull();
-        const auto e = clock::now();
-        lat.push_back((uint32_t)std::chrono::duration_cast<std::chrono::nanoseconds>(e - s).count());
+        const uint64_t e = __rdtsc();
+        lat.push_back((uint32_t)std::min<uint64_t>(e - s, 0xFFFFFFFFu));
         s = e;
         if (!p)
             break;
         got.push_back(p);
     }
-    const double sec = std::chrono::duration<double>(s - t0).count();
+    const double sec = std::chrono::duration<double>(clock::now() - t0).count();
+    const double ns_per_tick = s > c0 ? sec * 1e9 / (double)(s - c0) : 1.0;
+    for (uint32_t &t : lat)
+        t = (uint32_t)std::min(4.0e9, t * ns_per_tick);
     std::vector<uint32_t> v(lat.begin(), lat.end() - 1);     // the pulls that returned a packet
     std::sort(v.begin(), v.end());
     auto pct = [&](double f) { return v.empty() ? 0u : v[(size_t)(f * (double)(v.size() - 1))]; };
