@@ -35,6 +35,7 @@
 #include <chrono>
 #include <climits>
 #include <cstring>
+#include <deque>
 #include <new>
 
 namespace clk {
@@ -215,7 +216,6 @@ int Chain::begin_batch(Batch &B)
     B.kill_rc = CLK_SUCCESS;
     B.kill_why.clear();
     B.out.clear();
-    B.pub = 0;
     B.seq = ++seq_;
     return 0;
 }
@@ -897,22 +897,23 @@ int Chain::copy_back(Batch &B, bool all)
 }
 
 // B's routed results so far join the ones handed out (the batch before B
-// was finished first: batches come out in order)
+// was finished first: batches come out in order).  The batch's vector itself
+// is queued -- no copy -- and B goes on with a drained one's storage.
 void Chain::publish(Batch &B)
 {
     const Batch &X = &B == &b_[0] ? b_[1] : b_[0];
     if (X.started && X.seq < B.seq)                  // the batch before it has results to come first
         return;
-    if (B.pub < B.out.size()) {
-        if (B.pub == 0 && head_ == out_.size()) {   // all handed out before: take the batch's vector whole
-            out_.swap(B.out);
-            B.out.clear();
-            head_ = 0;
-        } else {
-            out_.insert(out_.end(), B.out.begin() + (ptrdiff_t)B.pub, B.out.end());
-            B.pub = B.out.size();
-        }
+    if (B.out.empty())
+        return;
+    ready_.push_back(std::move(B.out));
+    if (!spare_.empty()) {
+        B.out = std::move(spare_.back());
+        spare_.pop_back();
+    } else {
+        B.out = std::vector<ChainExit>();
     }
+    B.out.clear();
 }
 
 void Chain::end_batch(Batch &B)
@@ -924,7 +925,6 @@ void Chain::end_batch(Batch &B)
     B.waiting = false;
     B.at = 0;
     B.out.clear();
-    B.pub = 0;
     if (!b_[0].np && !b_[1].np)
         for (BatchElement *e : m_)
             e->in_place_ = false, e->chain_ = false;
@@ -965,7 +965,7 @@ uint64_t Chain::abandon()
             w.routed = w.nreached;
             B.mm[j].rebuild = false;
         }
-        for (size_t r = B.pub; r < B.out.size(); r++) {
+        for (size_t r = 0; r < B.out.size(); r++) {
             ChainExit &x = B.out[r];
             if (x.idx != ~0u && x.port != CLK_PORT_KILL && x.port != CLK_PORT_NEXT && B.back[x.idx] &&
                 !B.copied[x.idx]) {
@@ -983,28 +983,38 @@ uint64_t Chain::abandon()
 
 uint64_t Chain::pop(uint64_t *tokens, int32_t *members, int32_t *ports, uint32_t *lengths, uint32_t *aux, uint64_t cap)
 {
-    const size_t k = (size_t)std::min<uint64_t>(cap, out_.size() - head_);
-    if (tokens && members && ports && lengths && aux) {
-        const ChainExit *x = out_.data() + head_;
-        for (size_t q = 0; q < k; q++) {
-            tokens[q] = x[q].token;
-            members[q] = x[q].member;
-            ports[q] = x[q].port;
-            lengths[q] = x[q].length;
-            aux[q] = x[q].aux;
+    uint64_t got = 0;
+    while (got < cap && !ready_.empty()) {
+        std::vector<ChainExit> &v = ready_.front();
+        const size_t k = (size_t)std::min<uint64_t>(cap - got, v.size() - head_);
+        const ChainExit *x = v.data() + head_;
+        if (tokens && members && ports && lengths && aux) {
+            for (size_t q = 0; q < k; q++) {
+                tokens[got + q] = x[q].token;
+                members[got + q] = x[q].member;
+                ports[got + q] = x[q].port;
+                lengths[got + q] = x[q].length;
+                aux[got + q] = x[q].aux;
+            }
+        } else for (size_t q = 0; q < k; q++) {
+            if (tokens) tokens[got + q] = x[q].token;
+            if (members) members[got + q] = x[q].member;
+            if (ports) ports[got + q] = x[q].port;
+            if (lengths) lengths[got + q] = x[q].length;
+            if (aux) aux[got + q] = x[q].aux;
         }
-    } else for (size_t q = 0; q < k; q++) {
-        const ChainExit &x = out_[head_ + q];
-        if (tokens) tokens[q] = x.token;
-        if (members) members[q] = x.member;
-        if (ports) ports[q] = x.port;
-        if (lengths) lengths[q] = x.length;
-        if (aux) aux[q] = x.aux;
+        head_ += k;
+        got += k;
+        if (head_ == v.size()) {                     // drained: its storage goes back to the batches
+            head_ = 0;
+            if (spare_.size() < 4) {
+                v.clear();
+                spare_.push_back(std::move(v));
+            }
+            ready_.pop_front();
+        }
     }
-    head_ += k;
-    if (head_ == out_.size())
-        out_.clear(), head_ = 0;
-    return k;
+    return got;
 }
 
 } // namespace host

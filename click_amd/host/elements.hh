@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <string>
 #include <memory>
@@ -1088,8 +1089,7 @@ class alignas(128) Chain {
         bool launched = false;                    // ... and its kernels were queued
         int kill_rc = CLK_SUCCESS;                // a rewriting member's packets were killed (kill_member)
         std::string kill_why;
-        std::vector<ChainExit> out;               // routed results, out[pub..] not handed out yet
-        size_t pub = 0;
+        std::vector<ChainExit> out;               // routed results not handed out yet (publish)
     };
     hipStream_t stream() const;
     int begin_batch(Batch &B);
@@ -1134,8 +1134,9 @@ class alignas(128) Chain {
     size_t zc_last_bytes_ = 0;
     uint8_t *zc_last_dev_ = nullptr;
     uint64_t zc_gen_ = 0;
-    std::vector<ChainExit> out_;              // results handed out (pop), batch after batch
-    size_t head_ = 0;
+    std::deque<std::vector<ChainExit>> ready_;   // results handed out (pop), one vector per publish
+    std::vector<std::vector<ChainExit>> spare_;  // drained vectors' storage, for the batches
+    size_t head_ = 0;                         // into ready_.front()
     double stats_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     int32_t ext_nh_ = -3;                     // extent() cache: the nh and length it was computed for
     uint32_t ext_len_ = 0, ext_ = 0;
