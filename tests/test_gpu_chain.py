@@ -553,3 +553,44 @@ def test_member_destroyed_before_chain(ctx):
     ch2.flush()
     assert len(ch2.results()[0]) == 1
     ch2.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cap", [1, 7, 64, 100])
+def test_chain_results_small_pops(ctx, cap):
+    """clk_chain_results in small pops: each published batch's results are
+    queued whole (chain.cc publish / pop); a pop that ends inside one batch,
+    or spans several, hands out the same results in the same order as one
+    pop of everything (IPInputCombo -> IPOutputCombo at BATCH 64,
+    double-buffered: 13 batches, some results popped between flushes)."""
+    from click_amd.elements import Chain
+    spec = [(c, conf + ", BATCH 64", n) for c, conf, n in COMBOS]
+    bufs = [np.empty(cap, t) for t in (np.uint64, np.int32, np.int32, np.uint32, np.uint32)]
+    runs = []
+    for small in (False, True):
+        arena, foff, flen = fake_frames(800)
+        els = make(ctx, spec)
+        ch = Chain(els)
+        base = arena.ctypes.data
+        got = [[] for _ in range(5)]
+        for i in range(len(foff)):
+            if ch.push_anno(base + int(foff[i]), int(flen[i]), -1, 0, i):
+                ch.flush_async()
+            if small and i % 300 == 299:          # one pop of part of what is queued
+                n = int(ch.lib.clk_chain_results(ch.h, *[x.ctypes.data_as(ctypes.c_void_p) for x in bufs], cap))
+                assert 0 < n <= cap
+                for k in range(5):
+                    got[k].extend(bufs[k][:n].tolist())
+        ch.flush()
+        r = ch.results(cap=cap) if small else ch.results()
+        for k in range(5):
+            got[k].extend(r[k].tolist())
+        assert len(ch.results()[0]) == 0
+        runs.append((got, arena))
+        ch.close()
+        for e in els:
+            e.close()
+    (a, arena_a), (b, arena_b) = runs
+    assert len(a[0]) >= 800 and a == b
+    assert sorted(set(a[0]))[:3] == [0, 1, 2]
+    assert np.array_equal(arena_a, arena_b)
