@@ -75,6 +75,14 @@ class Element:
             raise ValueError("clk_element_share_messages failed")
         return self
 
+    def hold_packets(self, on=True):
+        """The caller keeps each pushed packet unchanged until its result is
+        popped (clk_element_hold_packets): long spans may then be gathered
+        at the flush instead of in the push."""
+        if self.lib.clk_element_hold_packets(self.h, 1 if on else 0) != 0:
+            raise ValueError("clk_element_hold_packets failed")
+        return self
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.clk_element_destroy(self.h)

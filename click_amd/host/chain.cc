@@ -36,6 +36,8 @@
 #include <climits>
 #include <cstring>
 #include <deque>
+#include <iterator>
+#include <utility>
 #include <new>
 
 namespace clk {
@@ -766,11 +768,16 @@ int Chain::flush_async()
     }
     err_.clear();
     Batch &B = b_[cur_], &O = b_[cur_ ^ 1];
-    int r;
-    if (B.np && !B.started && (r = start(B)) != CLK_SUCCESS)
-        return r;
+    int r, rb = CLK_SUCCESS;
+    // a start that failed leaves B staged (failed_); one that ended B with a
+    // member's packets killed (kill_member: rb) still finishes O, so that
+    // everything pushed before B is routed when flush() returns
+    if (B.np && !B.started && (rb = start(B)) != CLK_SUCCESS && failed_)
+        return rb;
     if (O.started && (r = finish(O)) != CLK_SUCCESS)
         return r;
+    if (rb)
+        return rb;
     if (B.started) {
         cur_ ^= 1;                                   // pushes go to the other batch (O is free now)
         if ((r = step(B)) != CLK_SUCCESS)
@@ -788,14 +795,15 @@ int Chain::flush_async()
 // at that member (push() retries it first).
 int Chain::flush()
 {
-    int r = flush_async();
-    if (r)
-        return r;
+    const int ra = flush_async();
+    if (ra && failed_)
+        return ra;
+    int r;
     Batch &O = b_[cur_ ^ 1];
     if (O.started && (r = finish(O)) != CLK_SUCCESS)
         return r;
     failed_ = false;
-    return CLK_SUCCESS;
+    return ra;
 }
 
 // A member after the head that clones packets as they reach it (IPOutputCombo's
@@ -896,24 +904,40 @@ int Chain::copy_back(Batch &B, bool all)
     return CLK_SUCCESS;
 }
 
-// B's routed results so far join the ones handed out (the batch before B
-// was finished first: batches come out in order).  The batch's vector itself
-// is queued -- no copy -- and B goes on with a drained one's storage.
+// B's routed results so far join the ones handed out.  Batches come out in
+// push order: a batch's results wait (held_) while an older batch is still in
+// flight -- a batch decided wholly on the host can end inside start(), before
+// the batch ahead of it is finished -- and go out when it has ended
+// (release()).  The batch's vector itself is queued -- no copy -- and B goes
+// on with a drained one's storage.
 void Chain::publish(Batch &B)
 {
-    const Batch &X = &B == &b_[0] ? b_[1] : b_[0];
-    if (X.started && X.seq < B.seq)                  // the batch before it has results to come first
-        return;
-    if (B.out.empty())
-        return;
-    ready_.push_back(std::move(B.out));
-    if (!spare_.empty()) {
-        B.out = std::move(spare_.back());
-        spare_.pop_back();
-    } else {
-        B.out = std::vector<ChainExit>();
+    if (!B.out.empty()) {
+        auto it = held_.end();
+        while (it != held_.begin() && std::prev(it)->first > B.seq)
+            --it;
+        held_.emplace(it, B.seq, std::move(B.out));
+        if (!spare_.empty()) {
+            B.out = std::move(spare_.back());
+            spare_.pop_back();
+        } else {
+            B.out = std::vector<ChainExit>();
+        }
+        B.out.clear();
     }
-    B.out.clear();
+    release();
+}
+
+// Held results whose batches have no older batch in flight are handed out
+void Chain::release()
+{
+    while (!held_.empty()) {
+        const uint64_t s = held_.front().first;
+        if ((b_[0].started && b_[0].seq < s) || (b_[1].started && b_[1].seq < s))
+            break;
+        ready_.push_back(std::move(held_.front().second));
+        held_.pop_front();
+    }
 }
 
 void Chain::end_batch(Batch &B)
@@ -924,7 +948,8 @@ void Chain::end_batch(Batch &B)
     B.started = false;
     B.waiting = false;
     B.at = 0;
-    B.out.clear();
+    B.out.clear();                                   // (published: empty)
+    release();                                       // a newer batch's held results may go now
     if (!b_[0].np && !b_[1].np)
         for (BatchElement *e : m_)
             e->in_place_ = false, e->chain_ = false;

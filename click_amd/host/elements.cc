@@ -304,7 +304,7 @@ void BatchElement::chain_route_all(ChainWork &w)
 
 template <class SpanF>
 inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token,
-                                  uint32_t anno, bool single)
+                                  uint32_t anno, bool held)
 {
     Pending p{data, token, 0, length, nh_offset, 0, 0, 0, -1, (uint16_t)anno};
     uint32_t off = 0, len = 0;
@@ -359,7 +359,9 @@ inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length
             err_ = "out of pinned host memory";
             return CLK_EINVAL;
         }
-        if (single && CLK_STAGE_DEFER && copy >= CLK_STAGE_DEFER)   // copied by launch(), with the batch
+        // a caller that holds its packets (clk_element_hold_packets): a long
+        // span is copied by launch(), with the batch
+        if (held && CLK_STAGE_DEFER && copy >= CLK_STAGE_DEFER)
             g.gather.push_back(Stage::Gather{data + off, slot, copy, len});
         else
             stage_copy(g.h_arena + slot, data + off, copy, len);
@@ -386,7 +388,7 @@ inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length
 int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
 {
     return push_one([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); }, data,
-                    length, nh_offset, token, anno, true);
+                    length, nh_offset, token, anno, hold_);
 }
 
 template <class SpanF>
@@ -1907,6 +1909,14 @@ int clk_element_push(clk_element *w, uint8_t *data, uint32_t length, int32_t nh_
     if (!w || (!data && length))
         return CLK_EINVAL;
     return w->e->push(data, length, nh_offset, token);
+}
+
+int clk_element_hold_packets(clk_element *w, int on)
+{
+    if (!w)
+        return CLK_EINVAL;
+    w->e->hold_packets(on != 0);
+    return CLK_SUCCESS;
 }
 
 int clk_element_push_anno(clk_element *w, uint8_t *data, uint32_t length, int32_t nh_offset, uint32_t anno,

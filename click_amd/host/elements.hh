@@ -283,7 +283,7 @@ struct ChainWork {
         return push_one([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) CLK_INL {                 \
             bool r_; [[clang::always_inline]] r_ = this->C::span(p, o, l, c);                                   \
             return r_;                                                                                          \
-        }, d_, l_, nh_, t_, a_, true);                                                                          \
+        }, d_, l_, nh_, t_, a_, hold_);                                                                         \
     }                                                                                                           \
     int push_burst(uint8_t *const *d_, const uint32_t *l_, const int32_t *nh_, uint64_t t0_, uint32_t n_) override \
     {                                                                                                           \
@@ -345,6 +345,7 @@ class alignas(128) BatchElement {
     int64_t take_packet(uint32_t key, uint8_t *buf, size_t cap);
     virtual std::string read_handler(const std::string &h) const;
     std::string take_messages();
+    void hold_packets(bool on) { hold_ = on; }   // deferred gather allowed (clk_element_hold_packets)
     void share_messages(const BatchElement &with) { gate_ = with.gate_; }
     const std::string &name() const { return name_; }
     std::string declaration() const { return name_ + " :: " + class_name(); }
@@ -515,10 +516,11 @@ class alignas(128) BatchElement {
     // callables: the generic push() and route pass virtual calls; the final
     // classes pass qualified (inlined) ones through CLK_GLUE_LOOPS.
     template <class SpanF>
-    // one packet; `single`: pushed alone (its long span is gathered at
-    // launch), not from a burst (which prefetches the spans ahead itself)
+    // one packet; `held`: pushed alone by a caller that holds its packets
+    // (its long span is gathered at launch), not from a burst (which
+    // prefetches the spans ahead itself)
     int push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno,
-                 bool single);
+                 bool held);
     template <class SpanF>
     int burst_loop(SpanF &&span_f, uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets,
                    uint64_t first_token, uint32_t n);
@@ -554,6 +556,7 @@ class alignas(128) BatchElement {
     std::shared_ptr<std::atomic<uint64_t>> gate_ = std::make_shared<std::atomic<uint64_t>>(0);
     uint64_t gate_bump() { return gate_->fetch_add(1, std::memory_order_relaxed); }
     bool zerocopy_ = false;          // ZEROCOPY: packets read/written in registered host memory
+    bool hold_ = false;              // the caller holds its packets until popped (clk_element_hold_packets)
     bool in_place_ = false;          // routing a zero-copy batch: the kernel already wrote the packets
     // the launching stage's buffers (valid in run()) and the routing
     // stage's host results (valid in route())
@@ -1112,6 +1115,7 @@ class alignas(128) Chain {
     void drop_clones(Batch &B, size_t k, size_t q0, size_t q1);
     int copy_back(Batch &B, bool all);
     void publish(Batch &B);
+    void release();
     void end_batch(Batch &B);
     void free_batch(Batch &B);
     uint32_t extent(int32_t nh, uint32_t length)
@@ -1134,6 +1138,7 @@ class alignas(128) Chain {
     size_t zc_last_bytes_ = 0;
     uint8_t *zc_last_dev_ = nullptr;
     uint64_t zc_gen_ = 0;
+    std::deque<std::pair<uint64_t, std::vector<ChainExit>>> held_;   // published, behind an older batch (seq)
     std::deque<std::vector<ChainExit>> ready_;   // results handed out (pop), one vector per publish
     std::vector<std::vector<ChainExit>> spare_;  // drained vectors' storage, for the batches
     size_t head_ = 0;                         // into ready_.front()

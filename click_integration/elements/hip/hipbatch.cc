@@ -132,6 +132,7 @@ HIPBatchElement::ensure(PerThread &t, ErrorHandler *errh)
 	t.ctx = 0;
 	return r;
     }
+    clk_element_hold_packets(t.e, 1);	// the core holds each Packet until its result
     t.xmask = cls_extra_results() ? 1 : 0;	// primary() asked only for such a class
     // this thread's element speaks its once-only chatter (first drop...)
     // together with the home thread's, as the one reference element does
@@ -219,6 +220,7 @@ HIPBatchElement::ensure_chain(PerThread &t)
 	if (clk_element_create(t.ctx, y->glue_class(), y->_glue_conf.c_str(), y->name().c_str(),
 			       y->noutputs(), &me) != CLK_SUCCESS)
 	    break;
+	clk_element_hold_packets(me, 1);
 	if (y->_gate)
 	    clk_element_share_messages(me, y->_gate);
 	t.mem.push_back(me);

@@ -101,13 +101,20 @@ const char *clk_element_last_error(clk_element *e);
 /* Stage one host packet.  data/length = Packet::data()/length();
  * nh_offset = network_header_offset() (-1 = no network header: the IP
  * elements then use data(), as SetIPChecksum does, setipchecksum.cc:78).
- * Set elements write their result into `data` at flush(), and a long span
- * (>= 256 B) of a packet pushed alone is gathered at the flush (with the
- * batch), so the packet memory must stay valid and unchanged until then.
+ * Set elements write their result into `data` at flush(), so for them the
+ * packet memory must stay valid until then; the other elements copy what
+ * their kernel reads at the push (unless clk_element_hold_packets).
  * Returns 1 when the batch is full and should be flushed, 0 otherwise,
  * < 0 on error.                                                            */
 int clk_element_push(clk_element *e, uint8_t *data, uint32_t length, int32_t nh_offset,
                      uint64_t token);
+
+/* on != 0: the caller keeps every packet it pushes valid and unchanged
+ * until the packet's result is popped (the Click adapter holds its Packets
+ * so), and the element may then gather a long span (>= 256 B) of a packet
+ * pushed alone at the flush, with the batch, rather than in the push.
+ * Default off.  CLK_EINVAL for a null element.                            */
+int clk_element_hold_packets(clk_element *e, int on);
 
 /* Stage a burst of n host packets (an rte_eth_rx_burst-style array of
  * packet pointers; fromdpdkdevice.cc:98-115); token of packet k is

@@ -207,6 +207,7 @@ class Host {
                 std::fprintf(stderr, "create %s(%s): %s\n", glue_class, conf.c_str(), clk_last_error(st[k].ctx));
                 std::exit(3);
             }
+            clk_element_hold_packets(st[k].e, 1);       // the core holds its packets, as the adapter
         }
         char buf[64];
         clk_element_read_handler(st[0].e, "batch", buf, sizeof buf);

@@ -112,30 +112,35 @@ def run_separate(ctx, spec, arena, foff, flen, nh0, anno):
     return out, els
 
 
-def run_chain(ctx, spec, arena, foff, flen, nh0, anno, batch_flush=None, async_flush=False):
+def run_chain(ctx, spec, arena, foff, flen, nh0, anno, batch_flush=None, async_flush=False, flush_after=None):
     """The chain over the frames; a full batch (or every batch_flush
     packets) flushed with clk_chain_flush, or double-buffered with
-    clk_chain_flush_async (async_flush), then everything flushed."""
+    clk_chain_flush_async (async_flush), then everything flushed.
+    flush_after: {i: "sync" | "async"} -- a flush of that kind after packet
+    i as well (a partial batch: the adapter's deadline or stop)."""
     from click_amd.elements import Chain
     els = make(ctx, spec)
     ch = Chain(els)
     base = arena.ctypes.data
+    flush_after = flush_after or {}
     for i in range(len(foff)):
         if ch.push_anno(base + int(foff[i]), int(flen[i]), nh0, int(anno[i]), i) or \
                 (batch_flush and (i + 1) % batch_flush == 0):
             ch.flush_async() if async_flush else ch.flush()
+        if i in flush_after:
+            ch.flush_async() if flush_after[i] == "async" else ch.flush()
     ch.flush()
     tok, mem, port, length, aux = ch.results()
     return list(zip(tok.tolist(), mem.tolist(), port.tolist(), length.tolist(), aux.tolist())), els, ch
 
 
 def compare_chain(ctx, spec, arena, foff, flen, nh0=-1, anno=None, batch_flush=None,
-                  handlers=("drops", "fragments", "packets", "lost"), async_flush=False):
+                  handlers=("drops", "fragments", "packets", "lost"), async_flush=False, flush_after=None):
     from click_amd.elements import AUX_CLONE
     anno = np.zeros(len(foff), np.uint32) if anno is None else anno
     a1, a2 = arena.copy(), arena.copy()
     r1, e1 = run_separate(ctx, spec, a1, foff, flen, nh0, anno)
-    r2, e2, ch = run_chain(ctx, spec, a2, foff, flen, nh0, anno, batch_flush, async_flush)
+    r2, e2, ch = run_chain(ctx, spec, a2, foff, flen, nh0, anno, batch_flush, async_flush, flush_after)
     assert len(r1) == len(r2)
     # each member's results in its own (push) order, as the elements one by
     # one give them (a chain flush interleaves members batch by batch)
@@ -265,6 +270,37 @@ def test_chain_double_buffered(ctx, which):
     for async_flush in (False, True):
         compare_chain(ctx, spec, arena, foff, flen, anno=anno, async_flush=async_flush,
                       handlers=("drops", "packets", "lost"))
+
+
+def test_chain_host_only_batch_behind_gpu_batch(ctx):
+    """a batch decided wholly on the host (IPGWOptions
+    without options, FixIPSrc without the annotation) ends inside the flush
+    that starts it while the batch before it -- options, on the GPU -- is
+    still in flight.  Its results must come out after that batch's, none
+    lost.  Groups of fuzzed frames (options, annotations) and plain
+    fake-iprouter frames alternate; full batches are flushed double-buffered,
+    partial ones by a synchronous or a double-buffered flush (the adapter's
+    stop and deadline)."""
+    rng, a1, o1, l1 = fuzzed_frames(41, n=1500)
+    a2, o2, l2 = fake_frames(1500)
+    arena = np.concatenate([a1, a2])
+    o2 = o2 + np.uint64(len(a1))
+    groups = [(0, 0, 500, None), (1, 0, 300, "sync"), (0, 500, 1000, None), (1, 300, 500, "async"),
+              (1, 500, 800, "async"), (0, 1000, 1500, None), (1, 800, 1500, "sync")]
+    foff, flen, anno, flush_after = [], [], [], {}
+    fix = (rng.random(1500) < 0.3).astype(np.uint32)
+    for g, a, b, how in groups:
+        foff += list((o1 if g == 0 else o2)[a:b])
+        flen += list((l1 if g == 0 else l2)[a:b])
+        anno += list(fix[a:b]) if g == 0 else [0] * (b - a)
+        if how:
+            flush_after[len(foff) - 1] = how
+    foff, flen, anno = np.array(foff, np.uint64), np.array(flen, np.uint32), np.array(anno, np.uint32)
+    spec = [("IPGWOptions", MY_IP_TXT + ", BATCH 500", 2), ("FixIPSrc", MY_IP_TXT, 1)]
+    r = compare_chain(ctx, spec, arena, foff, flen, nh0=14, anno=anno, async_flush=True, flush_after=flush_after,
+                      handlers=("drops", "packets", "lost"))
+    toks = [t for t, m, p, _, _ in r]
+    assert sorted(set(toks)) == list(range(len(foff)))
 
 
 def test_fuzzed_combos_chain(ctx):

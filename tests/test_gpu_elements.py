@@ -149,6 +149,42 @@ def test_check_l4_element(ctx, proto, noutputs):
     assert e.messages() == expected_drop_messages(prefix, codes, reasons, False)
 
 
+@pytest.mark.parametrize("hold", [False, True])
+def test_push_copies_unless_held(ctx, hold):
+    """clk_element_push copies what the kernel reads at the push:
+    a caller may reuse its receive buffer at once, and the verdicts are the
+    packets' as pushed.  With clk_element_hold_packets the long spans are
+    gathered at the flush, so a buffer overwritten before it is what is
+    checked -- the caller's side of that contract (the adapter holds its
+    Packets)."""
+    from click_amd.elements import Element
+    rng = np.random.default_rng(77)
+    arena, foff, flen = frames(rng, 600, 17, max_total=1600)
+    codes, _ = oracle_lib.batch("check_udp", arena.copy(), len(foff), off=foff + 14, length=flen - 14)
+    e = Element(ctx, "CheckUDPHeader", "BATCH 4096", noutputs=2)
+    if hold:
+        e.hold_packets()
+    base = arena.ctypes.data
+    for i in range(len(foff)):
+        e.push_ptr(base + int(foff[i]), int(flen[i]), 14, token=i)
+    hl = [int(arena[int(o) + 14] & 15) * 4 for o in foff]
+    usum = [int(arena[int(foff[i]) + 14 + hl[i] + 6]) | int(arena[int(foff[i]) + 14 + hl[i] + 7]) << 8
+            if flen[i] - 14 >= hl[i] + 8 else 0 for i in range(len(foff))]
+    long_ = [i for i in range(len(foff)) if flen[i] - 14 - hl[i] >= 300 and codes[i] == 0 and usum[i]]
+    assert len(long_) > 50
+    for i in long_:                                  # the receive buffer reused before the flush
+        o = int(foff[i]) + 14 + hl[i] + 8            # UDP payload bytes
+        arena[o:o + 200] ^= 0x5A
+    e.flush()
+    tok, port, _ = e.results()
+    assert np.array_equal(tok, np.arange(len(foff)))
+    if not hold:
+        assert np.array_equal(port, np.where(codes == 0, 0, 1))
+    else:
+        assert all(port[i] == 1 for i in long_)      # the overwritten bytes were read at the flush
+    e.close()
+
+
 @pytest.mark.parametrize("proto,config,noutputs", [(17, "", 1), (17, "", 2), (6, "", 1), (6, "FIXOFF true", 1),
                                                    (6, "true", 1)])
 def test_set_l4_element(ctx, proto, config, noutputs):
