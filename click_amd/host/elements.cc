@@ -217,7 +217,7 @@ int BatchElement::configure(ConfArgs &args, std::string *err)
         return -1;
     }
     if (!args.kw.empty()) {
-        *err = "unknown keyword " + args.kw[0].first;
+        *err = args.kw[0].first + ": unknown argument";        // Args (args.cc:472)
         return -1;
     }
     return 0;
@@ -909,7 +909,7 @@ int CheckIPHeader::configure(ConfArgs &args, std::string *err)
     long off;
     if (args.take("OFFSET", &v)) {
         if (!parse_int(v, &off) || off < 0) {
-            *err = "OFFSET: expected unsigned integer";
+            *err = "OFFSET: invalid number";
             return -1;
         }
         offset_ = (uint32_t)off;
@@ -1002,7 +1002,7 @@ int IPInputCombo::configure(ConfArgs &args, std::string *err)
         args.pos.erase(args.pos.begin());
     }
     if (!parse_int(v, &color_)) {
-        *err = "COLOR: expected integer";
+        *err = "COLOR: invalid number";
         return -1;
     }
     if (!args.pos.empty()) {                                 // old-style BADSRC list
@@ -1478,7 +1478,7 @@ int IPOutputCombo::configure(ConfArgs &args, std::string *err)
     }
     long mtu;
     if (!parse_int(v[0], &color_)) {
-        *err = "COLOR: expected integer";
+        *err = "COLOR: invalid number";
         return -1;
     }
     if (!parse_ip(v[1], &my_ip_)) {
@@ -1486,7 +1486,7 @@ int IPOutputCombo::configure(ConfArgs &args, std::string *err)
         return -1;
     }
     if (!parse_int(v[2], &mtu) || mtu < 0 || mtu > 0xFFFFFFFFL) {
-        *err = "MTU: expected unsigned integer";
+        *err = "MTU: invalid number";
         return -1;
     }
     mtu_ = (uint32_t)mtu;
@@ -1584,7 +1584,7 @@ int IPFragmenter::configure(ConfArgs &args, std::string *err)
     }
     long mtu;
     if (!parse_int(v, &mtu) || mtu < 0 || mtu > 0xFFFFFFFFL) {
-        *err = "MTU: expected unsigned integer";
+        *err = "MTU: invalid number";
         return -1;
     }
     mtu_ = (uint32_t)mtu;
@@ -1603,7 +1603,7 @@ int IPFragmenter::configure(ConfArgs &args, std::string *err)
         }
     }
     if (args.take("HEADROOM", &v) && (!parse_int(v, &headroom_) || headroom_ < 0)) {   // Packet::make headroom: host side
-        *err = "HEADROOM: expected unsigned integer";
+        *err = "HEADROOM: invalid number";
         return -1;
     }
     if (!args.pos.empty()) {
@@ -1875,6 +1875,36 @@ int clk_element_create(clk_ctx *ctx, const char *class_name, const char *config,
     w->e = e;
     w->own_ctx = own;
     *out = w;
+    return CLK_SUCCESS;
+}
+
+int clk_element_check_config(const char *class_name, const char *config, const char *name, int noutputs)
+{
+    if (!class_name || noutputs < 1 || noutputs > 5)
+        return clk_ctx_set_error_internal(nullptr, "clk_element_check_config: bad arguments");
+    std::string nm = name ? name : class_name;
+    clk::host::ConfArgs args;
+    std::string err, v;
+    if (!clk::host::ConfArgs::split(config ? config : "", &args, &err)) {
+        clk_ctx_set_error_internal(nullptr, (nm + ": " + err).c_str());
+        return CLK_EINVAL;
+    }
+    long dev = 0;
+    if (args.take("DEVICE", &v) && (!clk::host::parse_int(v, &dev) || dev < 0)) {
+        clk_ctx_set_error_internal(nullptr, (nm + ": DEVICE: expected GPU number").c_str());
+        return CLK_EINVAL;
+    }
+    // configure() reads no context: the element is made without one, its
+    // keywords parsed, and destroyed (it never staged anything)
+    clk::host::BatchElement *e = clk::host::make_element(nullptr, class_name, nm, noutputs);
+    if (!e)
+        return clk_ctx_set_error_internal(nullptr, ("unknown element class " + std::string(class_name)).c_str());
+    const int r = e->configure(args, &err);
+    delete e;
+    if (r) {
+        clk_ctx_set_error_internal(nullptr, (nm + ": " + err).c_str());
+        return CLK_EINVAL;
+    }
     return CLK_SUCCESS;
 }
 

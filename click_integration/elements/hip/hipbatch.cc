@@ -107,6 +107,15 @@ HIPBatchElement::configure(Vector<String> &conf, ErrorHandler *errh)
     if (!batch)
 	conf.push_back(String("BATCH ") + String((int) ADAPTER_BATCH));
     _glue_conf = cp_unargvec(conf);
+    // the glue's keywords checked now, without a GPU, so a bad one is a
+    // configure-time error as in the reference element (Args' wording)
+    int nout = noutputs() < 1 ? 1 : (noutputs() > 5 ? 5 : noutputs());
+    if (clk_element_check_config(glue_class(), _glue_conf.c_str(), name().c_str(), nout) != CLK_SUCCESS) {
+	String m(clk_last_error(0)), pre = name() + ": ";
+	if (m.starts_with(pre))		// errh names the element already
+	    m = m.substring(pre.length());
+	return errh->error("%s", m.c_str());
+    }
     _core.set_latency(_latency_ms);
     _core.set_max_retries(_retries);
     return 0;
@@ -324,8 +333,9 @@ HIPBatchElement::cleanup(CleanupStage)
 {
     // nothing is pushed downstream: held, routed-but-undelivered and ready
     // packets are killed, the glue elements and contexts destroyed (the
-    // members' copies taken out of their handler sums first)
-    for (int k = 0; k <= _npt; k++) {
+    // members' copies taken out of their handler sums first); no states when
+    // configure() or an earlier element's initialize() failed
+    for (int k = 0; k < nstates(); k++) {
 	for (size_t m = 1; m < _pt[k].mem.size() && (int) m < _chain.size(); m++) {
 	    HIPBatchElement *y = _chain[m];
 	    y->_borrow_lock.acquire();
@@ -344,7 +354,7 @@ HIPBatchElement::cleanup(CleanupStage)
 String
 HIPBatchElement::glue_handler(const char *hname) const
 {
-    for (int k = 0; k <= _npt; k++)
+    for (int k = 0; k < nstates(); k++)
 	if (_pt[k].e) {
 	    char buf[4096];
 	    clk_element_read_handler(_pt[k].e, hname, buf, sizeof(buf));
@@ -362,7 +372,7 @@ HIPBatchElement::read_handler(Element *e, void *thunk)
     const char *hname = static_cast<const char *>(thunk);
     // this element's glue elements: its states' and its copies in chains
     Vector<clk_element *> els;
-    for (int k = 0; k <= he->_npt; k++)
+    for (int k = 0; k < he->nstates(); k++)
 	if (he->_pt[k].e)
 	    els.push_back(he->_pt[k].e);
     he->_borrow_lock.acquire();
@@ -417,5 +427,7 @@ HIPBatchElement::add_handlers()
 }
 
 CLICK_ENDDECLS
-ELEMENT_LIBS((-L$(CLICK_AMD)/click_amd -lclick_amd_cksum -L/opt/rocm/lib -lamdhip64))
+// (click-buildtool splits this line at ':' and ')': the library directories
+// come from LDFLAGS at configure time, tools/click_scratch_build.sh)
+ELEMENT_LIBS((-lclick_amd_cksum -lamdhip64))
 ELEMENT_PROVIDES(HIPBatchElement)

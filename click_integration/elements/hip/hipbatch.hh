@@ -186,6 +186,9 @@ class HIPBatchElement : public Element { public:
     // the router attachment naming a once-per-router message, if the
     // reference element has one (SetUDPChecksum); 0: once per element
     virtual const char *message_attachment() const	{ return 0; }
+    // the per-thread states made by initialize() (0 before it, or when
+    // configuration failed)
+    int nstates() const			{ return _pt ? _npt + 1 : 0; }
 
     String _glue_conf;
     int _device;		// -1: per thread

@@ -11,9 +11,7 @@
  * export those names, and hipparity.cc, which provides HIPParity).
  */
 #include <click/config.h>
-#include "hipcheck.hh"
-#include "hipset.hh"
-#include "hipoutput.hh"
+#include "hipdropin.hh"
 CLICK_DECLS
 CLICK_ENDDECLS
 ELEMENT_REQUIRES(HIPCheckImpl HIPSetImpl HIPOutputImpl)

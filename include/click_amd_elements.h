@@ -92,6 +92,13 @@ enum clk_port {
 int clk_element_create(clk_ctx *ctx, const char *class_name, const char *config,
                        const char *name, int noutputs, clk_element **out);
 int clk_element_destroy(clk_element *e);
+/* Configuration check without a GPU: the class's keywords parsed as
+ * clk_element_create parses them (DEVICE's value checked for form only),
+ * nothing allocated.  CLK_SUCCESS, or CLK_EINVAL with clk_last_error(NULL)
+ * set as clk_element_create would set it -- so an adapter reports a bad
+ * keyword at configure time, as the reference element does, on a host
+ * whatever its GPUs.                                                      */
+int clk_element_check_config(const char *class_name, const char *config, const char *name, int noutputs);
 /* Why the element's last flush / push failed.  A flush that fails (a HIP
  * runtime error, or a kernel's internal fault report) routes nothing: the
  * batch stays staged, exactly as pushed, and the next flush retries it

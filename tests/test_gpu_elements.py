@@ -169,8 +169,8 @@ def test_push_copies_unless_held(ctx, hold):
         e.push_ptr(base + int(foff[i]), int(flen[i]), 14, token=i)
     hl = [int(arena[int(o) + 14] & 15) * 4 for o in foff]
     usum = [int(arena[int(foff[i]) + 14 + hl[i] + 6]) | int(arena[int(foff[i]) + 14 + hl[i] + 7]) << 8
-            if flen[i] - 14 >= hl[i] + 8 else 0 for i in range(len(foff))]
-    long_ = [i for i in range(len(foff)) if flen[i] - 14 - hl[i] >= 300 and codes[i] == 0 and usum[i]]
+            if int(flen[i]) - 14 >= hl[i] + 8 else 0 for i in range(len(foff))]
+    long_ = [i for i in range(len(foff)) if int(flen[i]) - 14 - hl[i] >= 300 and codes[i] == 0 and usum[i]]
     assert len(long_) > 50
     for i in long_:                                  # the receive buffer reused before the flush
         o = int(foff[i]) + 14 + hl[i] + 8            # UDP payload bytes

@@ -66,6 +66,7 @@ int clk_element_flush_async(clk_element *e) { return flush_all(e); }
 uint64_t clk_element_abandon(clk_element *) { return 0; }
 int clk_element_share_messages(clk_element *, const clk_element *) { return CLK_SUCCESS; }
 int clk_element_hold_packets(clk_element *, int) { return CLK_SUCCESS; }
+int clk_element_check_config(const char *, const char *, const char *, int) { return CLK_SUCCESS; }
 uint64_t clk_element_results_aux(clk_element *e, uint64_t *tok, int32_t *port, uint32_t *len, uint32_t *aux,
                                  uint64_t cap)
 {
