@@ -998,37 +998,98 @@ def config1_cpu(n=C1_PACKETS):
     """The same chains on one host thread through the oracle restatement
     (the byte-touching elements only; Click's scheduler, Classifier and
     queues are not part of it): CheckIPHeader + IPGWOptions + FixIPSrc +
-    DecIPTTL + IPFragmenter(300), and IPInputCombo + IPOutputCombo; the
-    median of C1_RUNS runs, each on fresh frames, as the GPU legs."""
+    DecIPTTL + IPFragmenter(300), and IPInputCombo + IPOutputCombo.  The
+    thread is pinned to one core, the frames' arena and the flags are
+    allocated and first-touched there once, and the pristine frames are
+    copied back before each run, outside the clock (a fresh arena per run
+    left 22 or 40 Mpps to page placement, BENCH_r05); one warm-up, then
+    C1_RUNS timed runs: min / median / max."""
     import numpy as np
     from tests import oracle_lib
     frame = c1_frame()
     fl = len(frame)
-    res, walls = {}, {}
-    for name, run in [(nm, r) for nm in ("elements", "combos") for r in range(C1_RUNS)]:
-        arena = np.tile(np.frombuffer(frame, np.uint8), n)
+    prev = os.sched_getaffinity(0)
+    core = min(prev)
+    os.sched_setaffinity(0, {core})
+    try:
+        pristine = np.tile(np.frombuffer(frame, np.uint8), n)
+        arena = np.empty_like(pristine)
+        arena[:] = pristine                        # first touch on the pinned core
+        flags = np.zeros(n, np.uint8)
         l3 = arena[14:]
-        t0 = time.perf_counter()
-        codes, _ = oracle_lib.batch("check_ip", l3, n, stride=fl, fixed_len=fl - 14)
-        if name == "elements":
-            oracle_lib.ip_out_batch("ip_gw_options", l3, n, stride=fl, fixed_len=fl - 14, my_ip=0x18041A12)
-            oracle_lib.ip_out_batch("fix_ip_src", l3, n, stride=fl, fixed_len=fl - 14, my_ip=0x18041A12,
-                                    flags=np.zeros(n, np.uint8))
-            c2, _ = oracle_lib.batch("dec_ttl", l3, n, stride=fl, fixed_len=fl - 14)
-            fr = oracle_lib.ip_fragment(l3, n, 300, False, stride=fl, fixed_len=fl - 14)
-            fwd = int(((codes == 0) & (c2 == 0) & (fr["port"] == 0)).sum())
-        else:
-            port, _, _ = oracle_lib.ip_out_batch("ip_output_combo", l3, n, stride=fl, fixed_len=fl - 14,
-                                                 my_ip=0x18041A12, mtu=300)
-            fwd = int(((codes == 0) & (port == 0)).sum())
-        walls.setdefault(name, []).append(time.perf_counter() - t0)
-        dt = c1_median(walls[name])
-        res[name] = {"forwarded": fwd, "wall_s": round(dt, 4), "mpps": round(n / dt / 1e6, 2),
-                     "runs_mpps": [round(n / w / 1e6, 2) for w in walls[name]]}
-    return {"threads": 1, "kind": "port", "runs": C1_RUNS, **res,
-            "note": "oracle restatement of the byte-touching elements, one host thread; the reference's own "
-                    "`click -t conf/fake-iprouter.click` (Click runtime included) measured 4.3-6.7 Mpps on the "
-                    "survey VM (BASELINE.md §3)"}
+        res = {}
+        for name in ("elements", "combos"):
+            walls = []
+            for run in range(1 + C1_RUNS):
+                np.copyto(arena, pristine)
+                t0 = time.perf_counter()
+                codes, _ = oracle_lib.batch("check_ip", l3, n, stride=fl, fixed_len=fl - 14)
+                if name == "elements":
+                    oracle_lib.ip_out_batch("ip_gw_options", l3, n, stride=fl, fixed_len=fl - 14, my_ip=0x18041A12)
+                    oracle_lib.ip_out_batch("fix_ip_src", l3, n, stride=fl, fixed_len=fl - 14, my_ip=0x18041A12,
+                                            flags=flags)
+                    c2, _ = oracle_lib.batch("dec_ttl", l3, n, stride=fl, fixed_len=fl - 14)
+                    fr = oracle_lib.ip_fragment(l3, n, 300, False, stride=fl, fixed_len=fl - 14)
+                    fwd = int(((codes == 0) & (c2 == 0) & (fr["port"] == 0)).sum())
+                else:
+                    port, _, _ = oracle_lib.ip_out_batch("ip_output_combo", l3, n, stride=fl, fixed_len=fl - 14,
+                                                         my_ip=0x18041A12, mtu=300)
+                    fwd = int(((codes == 0) & (port == 0)).sum())
+                if run:
+                    walls.append(time.perf_counter() - t0)
+            dt = c1_median(walls)
+            rates = [round(n / w / 1e6, 2) for w in walls]
+            res[name] = {"forwarded": fwd, "wall_s": round(dt, 4), "mpps": round(n / dt / 1e6, 2),
+                         "min_med_max_mpps": [min(rates), round(n / dt / 1e6, 2), max(rates)], "runs_mpps": rates}
+    finally:
+        os.sched_setaffinity(0, prev)
+    return {"threads": 1, "kind": "port", "runs": C1_RUNS, "pinned_cpu": core, **res,
+            "note": "oracle restatement of the byte-touching elements, one pinned host thread, arena allocated and "
+                    "first-touched once; Click's own runtime on the same graph: drop_in.c1 (click-cpu)"}
+
+
+CLICK_LEGS = (("c1", 3000000, 1), ("c1", 3000000, 32), ("c3chk", 1000000, 32), ("c3set", 1000000, 32))
+
+
+def click_drop_in(reps=3, timeout=180):
+    """The GPU elements inside Click: the userlevel driver built with the GPU
+    group under the reference class names (click-dropin) against the stock
+    driver (click-cpu, the reference's CPU elements) on the same graph and
+    host, both built by tools/click_scratch_build.sh (tools/click_perf.py):
+    c1 = config 1's forwarding path (click_integration/conf/c1-forward.click,
+    InfiniteSource BURST 1 and 32), c3chk = 1500 B UDP frames through
+    CheckIPHeader -> CheckUDPHeader, c3set = SetUDPChecksum.  Mpps by the
+    graph's AverageCounter, median of `reps` processes; x_cpu = drop-in /
+    stock.  Also the adapter core's C3 push legs (tests/native/pull_bench c3:
+    staged and ZEROCOPY).  None if the binaries were not built."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import click_perf
+        from tests import click_run
+    except Exception as e:                       # reported, not fatal
+        return {"error": repr(e)}
+    if not (click_run.binary("cpu") and click_run.binary("dropin")):
+        return None
+    out = {}
+    for graph, limit, burst in CLICK_LEGS:
+        rec = {"packets": limit, "burst": burst}
+        for mode in ("cpu", "dropin"):
+            runs = [click_perf.run_one(mode, graph, "", limit, burst, timeout=timeout) for _ in range(reps)]
+            ok = sorted(r["mpps_counter"] for r in runs if "count" in r and r["count"] == limit)
+            rec[mode] = round(ok[len(ok) // 2], 2) if len(ok) == reps else None
+            rec[mode + "_runs"] = [round(r["mpps_counter"], 2) if "count" in r else r for r in runs]
+        rec["x_cpu"] = round(rec["dropin"] / rec["cpu"], 2) if rec["cpu"] and rec["dropin"] else None
+        out["%s_burst%d" % (graph, burst)] = rec
+    exe = os.path.join(ROOT, "tests", "native", "bin", "pull_bench")
+    if os.path.exists(exe):
+        try:
+            r = subprocess.run([exe, "2", "c3"], capture_output=True, text=True, timeout=timeout)
+            core = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+            out["core_c3_push"] = {x["leg"]: x.get("mpps") for x in core if "leg" in x} or core
+        except Exception as e:
+            out["core_c3_push"] = {"error": repr(e)}
+    return {"workload": "GPU elements in Click's userlevel driver (click-dropin) vs the stock elements (click-cpu), "
+                        "same graph and host; Mpps", **out}
 
 
 def comm_info(torch, dist, dev):
@@ -1084,6 +1145,10 @@ def bench_summary(line):
     if c1:
         out["C1 mpps"] = {k: c1[k]["mpps"] for k in c1 if isinstance(c1[k], dict) and "mpps" in c1[k]}
         out["C1 ok"] = c1.get("ok")
+    di = line.get("drop_in")
+    if isinstance(di, dict):
+        out["drop_in x_cpu"] = {k: [v.get("dropin"), v.get("cpu"), v.get("x_cpu")] for k, v in di.items()
+                                if isinstance(v, dict) and "x_cpu" in v}
     rs = line.get("root_scatter")
     if rs:
         out["root scatter GB/s"] = rs["GBps_out_of_rank0"]
@@ -1120,6 +1185,7 @@ def main():
     ap.add_argument("--packets", type=int, default=0, help="packets per GPU (default: the workload's)")
     ap.add_argument("--no-c2", action="store_true", help="skip the extra 64 B (C2) measurement")
     ap.add_argument("--no-c1", action="store_true", help="skip the config-1 (fake-iprouter) measurement")
+    ap.add_argument("--no-click", action="store_true", help="skip the GPU-elements-in-Click legs (drop_in)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-peak", action="store_true", help="skip the read-stream ceiling")
     ap.add_argument("--no-frag", action="store_true", help="skip the IPFragmenter measurement (C3)")
@@ -1211,6 +1277,9 @@ def main():
     c1 = None
     if rank == 0 and world == 1 and not args.no_c1:
         c1 = config1(ctx)
+    drop_in = None
+    if rank == 0 and world == 1 and not args.no_click:
+        drop_in = click_drop_in()
 
     # an input that starts on one GPU would first be scattered;
     # measured on a sample after the timed regions, never part of `value`
@@ -1269,6 +1338,8 @@ def main():
             line["fragmenter"] = frag
         if c1:
             line["c1_fake_iprouter"] = c1
+        if drop_in:
+            line["drop_in"] = drop_in
         if world == 1 and not args.no_cpu:
             try:
                 cb = cpu_baseline()

@@ -885,6 +885,8 @@ int CheckIPHeader::conf_addresses(ConfArgs &args, std::string *err)
 
 int CheckIPHeader::upload_addresses(std::string *err)
 {
+    if (!ctx_)                                   // configuration check only (clk_element_check_config)
+        return 0;
     if (!bad_src_.empty() || !good_dst_.empty()) {
         const size_t nb = bad_src_.size() + good_dst_.size();
         if (hipMalloc(&d_lists_, nb * 4) != hipSuccess) {
@@ -1367,8 +1369,9 @@ int IPGWOptions::configure(ConfArgs &args, std::string *err)
         *err = "too many arguments";
         return -1;
     }
-    if (hipMalloc(&d_addrs_, addrs_.size() * 4) != hipSuccess ||
-        hipMemcpy(d_addrs_, addrs_.data(), addrs_.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    if (ctx_ &&                                         // (no context: a configuration check only)
+        (hipMalloc(&d_addrs_, addrs_.size() * 4) != hipSuccess ||
+         hipMemcpy(d_addrs_, addrs_.data(), addrs_.size() * 4, hipMemcpyHostToDevice) != hipSuccess)) {
         *err = "out of device memory";
         return -1;
     }

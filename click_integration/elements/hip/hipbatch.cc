@@ -127,8 +127,10 @@ HIPBatchElement::ensure(PerThread &t, ErrorHandler *errh)
     if (t.e)
 	return 0;
     int ndev = clk_device_count();
-    if (ndev <= 0)
-	return errh ? errh->error("no gfx950 GPU: %s", clk_last_error(0)) : -1;
+    if (ndev <= 0) {
+	const char *why = clk_last_error(0);
+	return errh ? errh->error(why && *why ? "no gfx950 GPU: %s" : "no gfx950 GPU%s", why ? why : "") : -1;
+    }
     int dev = _device >= 0 ? _device : t.id % ndev;
     if (dev >= ndev)
 	return errh ? errh->error("DEVICE %d: no such GPU (%d gfx950 devices)", dev, ndev) : -1;

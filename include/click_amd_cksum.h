@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define CLK_ABI_VERSION 5
+#define CLK_ABI_VERSION 6
 
 /* ---- return codes -------------------------------------------------------- */
 #define CLK_SUCCESS 0

@@ -41,7 +41,7 @@ def test_library_exports_every_declared_symbol():
     for name in names:
         assert hasattr(lib, name), name
         assert name in _abi.SIGNATURES, "ctypes binding lacks " + name
-    assert lib.clk_abi_version() == 5
+    assert lib.clk_abi_version() == 6
 
 
 def test_codes_agree_with_header_and_oracle():
@@ -190,3 +190,22 @@ def test_click_adapters_keep_the_reference_processing():
         assert (m.group(1) if m else base) == proc, n
     cc = open(os.path.join(hip, "hipbatch.cc")).read()
     assert "_core.pull(*this, state())" in cc and "_core.push(*this, t, p)" in cc and "PerThread &t = state();" in cc
+
+
+@pytest.mark.parametrize("cls,conf,msg", [
+    ("CheckIPHeader", "INTERFACES 18.26.4.1/24 18.26.7.1/24, OFFSET 14", None),
+    ("IPGWOptions", "18.26.4.24", None), ("SetUDPChecksum", "", None), ("IPFragmenter", "300, HONOR_DF true", None),
+    ("CheckIPHeader", "FOO 3", "e0: FOO: unknown argument"), ("CheckIPHeader", "OFFSET x", "e0: OFFSET: invalid number"),
+    ("SetUDPChecksum", "3", "e0: too many arguments"), ("IPFragmenter", "MTU x", "e0: MTU: invalid number"),
+    ("CheckIPHeader", "BATCH 0", "e0: BATCH: expected positive integer"),
+    ("NoSuchElement", "", "unknown element class NoSuchElement")])
+def test_configuration_check_without_a_gpu(cls, conf, msg):
+    """clk_element_check_config parses a class's keywords with no context and
+    no device (the Click adapter's configure() calls it, so a bad keyword is
+    a configure-time error on any host, in the reference's Args wording)."""
+    lib = _abi.load()
+    r = lib.clk_element_check_config(cls.encode(), conf.encode(), b"e0", 2)
+    if msg is None:
+        assert r == 0, lib.clk_last_error(None)
+    else:
+        assert r == _abi.CLK_EINVAL and lib.clk_last_error(None).decode() == msg

@@ -37,8 +37,8 @@ def gpu():
 
 
 def test_parity_graph_ip():
-    rc, h, err = click_run.run("parity", "hip-parity-ip.click", handlers=("cmp.diffs", "cpu.drops", "gpu.drops",
-                                                                          "cmp.count"), timeout=120)
+    rc, h, err = click_run.run("parity", "hip-parity-ip.click", handlers=("cmp.diffs", "cpu.drops", "gpu.drops"),
+                               timeout=120)
     assert rc == 0, err
     assert h["cmp.diffs"] == "0", (h, err)
     assert h["cpu.drops"] == h["gpu.drops"] and int(h["cpu.drops"]) > 0, h
