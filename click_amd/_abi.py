@@ -172,6 +172,8 @@ SIGNATURES = {
     "clk_element_abandon": (ctypes.c_uint64, [_P]),
     "clk_element_share_messages": (ctypes.c_int, [_P, _P]),
     "clk_element_hold_packets": (ctypes.c_int, [_P, ctypes.c_int]),
+    "clk_element_push_th": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int32, ctypes.c_uint32,
+                                           ctypes.c_uint64]),
     "clk_element_check_config": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]),
     "clk_element_read_handler": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]),
     "clk_element_take_messages": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_size_t]),

@@ -105,6 +105,11 @@ class Element:
             raise ClickAmdError("push failed: %d" % rc)
         return rc == 1
 
+    def push_th(self, ptr, length, nh_offset, th_offset, token=0, anno=0):
+        """clk_element_push_th: th_offset = the transport header annotation's
+        offset from ptr (-2 none, -1 unknown).  Returns the raw status."""
+        return self.lib.clk_element_push_th(self.h, ctypes.c_void_p(ptr), length, nh_offset, th_offset, anno, token)
+
     def push_ptr(self, ptr, length, nh_offset=-1, token=0):
         rc = self.lib.clk_element_push(self.h, ctypes.c_void_p(ptr), length, nh_offset, token)
         if rc < 0:

@@ -304,9 +304,15 @@ void BatchElement::chain_route_all(ChainWork &w)
 
 template <class SpanF>
 inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token,
-                                  uint32_t anno, bool held)
+                                  uint32_t anno, bool held, int32_t th_offset)
 {
-    Pending p{data, token, 0, length, nh_offset, 0, 0, 0, -1, (uint16_t)anno};
+    Pending p{data, token, 0, length, nh_offset, 0, 0, 0, -1, (uint16_t)(anno & ~uint32_t(ANNO_CANON))};
+    if (reads_th_ && th_offset != -1 && nh_offset >= 0 && (uint32_t)nh_offset < length &&
+        th_offset != nh_offset + (int32_t)((data[nh_offset] & 15u) << 2)) {
+        const int r = push_irregular(p, th_offset);
+        if (r != ~0)
+            return r;
+    }
     uint32_t off = 0, len = 0;
     int32_t code = 0;
     if (!span_f(p, &off, &len, &code)) {
@@ -385,10 +391,61 @@ inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length
     return g.pend.size() >= batch_cap_ ? 1 : 0;
 }
 
-int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno)
+int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno,
+                       int32_t th_offset)
 {
     return push_one([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) { return span(p, o, l, c); }, data,
-                    length, nh_offset, token, anno, hold_);
+                    length, nh_offset, token, anno, hold_, th_offset);
+}
+
+int BatchElement::push_irregular(Pending &, int32_t)
+{
+    return ~0;
+}
+
+// A packet decided on the host (as span() returning false)
+int BatchElement::host_decided(Pending &p, int32_t code)
+{
+    p.host_code = (int16_t)code;
+    Stage &g = st_[cur_];
+    if (g.pend.capacity() < batch_cap_ && g.pend.empty())
+        g.pend.reserve(std::min<size_t>(batch_cap_, 1u << 20));
+    g.pend.push_back(p);
+    return g.pend.size() >= batch_cap_ ? 1 : 0;
+}
+
+// p's canonical copy into the staging arena (push_irregular): ip20 -- a
+// 20-byte IP header -- then seglen bytes of the segment; staged for the GPU
+// like any packet, its span the copy
+int BatchElement::stage_canonical(Pending &p, const uint8_t *ip20, const uint8_t *seg, uint32_t seglen)
+{
+    if (zerocopy_) {       // the kernels read ZEROCOPY packets where they lie: no room for a copy
+        err_ = "ZEROCOPY: a packet whose transport header annotation is not at ip_hl cannot be read in place";
+        return CLK_EINVAL;
+    }
+    Stage &g = st_[cur_];
+    const size_t slot = (g.h_used + 15) & ~size_t(15);
+    const uint32_t n = 20 + seglen;
+    if ((slot + n + 64 > g.h_arena_cap || g.ngpu >= g.h_n_cap) && grow_host(g, slot + n + 64, g.ngpu + 1)) {
+        err_ = "out of pinned host memory";
+        return CLK_EINVAL;
+    }
+    std::memcpy(g.h_arena + slot, ip20, 20);
+    std::memcpy(g.h_arena + slot + 20, seg, seglen);
+    g.h_used = slot + n;
+    p.slot = slot;
+    p.span_len = n;
+    p.anno |= ANNO_CANON;
+    p.index = (uint32_t)g.ngpu;
+    g.h_off[g.ngpu] = p.slot;
+    g.h_len[g.ngpu] = n;
+    g.h_anno[g.ngpu] = (uint8_t)p.anno;
+    g.maxlen = std::max(g.maxlen, n);
+    g.ngpu++;
+    if (g.pend.capacity() < batch_cap_ && g.pend.empty())
+        g.pend.reserve(std::min<size_t>(batch_cap_, 1u << 20));
+    g.pend.push_back(p);
+    return g.pend.size() >= batch_cap_ ? 1 : 0;
 }
 
 template <class SpanF>
@@ -1104,6 +1161,7 @@ static const char *const icmp_reasons[] = {"not ICMP", "bad packet length", "bad
 CheckL4Header::CheckL4Header(clk_ctx *ctx, const std::string &name, int noutputs, int proto)
     : CheckElement(ctx, name, noutputs), proto_(proto)
 {
+    reads_th_ = true;
 }
 
 const char *const *CheckL4Header::reason_texts() const
@@ -1142,6 +1200,81 @@ bool CheckL4Header::span(const Pending &p, uint32_t *off, uint32_t *len, int32_t
     return true;
 }
 
+// ---- packets whose transport header annotation is not at ip_hl -------------
+// (BatchElement::push_irregular).  The reference elements read the segment
+// at the annotation and everything else from the IP header bytes: the
+// lengths' ip_hl, ip_p, ip_len, and the pseudo-header's source and
+// destination (in_cksum.c:83-111, whose option walk uses ip_hl too).  Domain
+// guards, where the reference would read outside the packet: the header, the
+// transport fields it reads and the summed segment must lie inside it
+// (otherwise BAD_LENGTH / output 1 / kill, as a short packet), the option
+// walk stops at the packet's end, and an ip_len that the canonical copy
+// cannot carry is refused (CLK_EINVAL).
+
+// The 20-byte header the pseudo-header reads, with ip_hl 5: hdr is the IP
+// header as the reference sees it when it builds the pseudo-header (avail
+// bytes of it in the packet), its destination taken from the first
+// SSRR / LSRR option of length >= 7 (in_cksum.c:86-108) when ip_hl != 5.
+static void canonical_ip20(const uint8_t *hdr, uint32_t avail, uint8_t *ip20)
+{
+    std::memcpy(ip20, hdr, 20);
+    const uint32_t hl = std::min<uint32_t>((hdr[0] & 15u) << 2, avail);
+    if ((hdr[0] & 15u) != 5)
+        for (uint32_t o = 20; o < hl;) {
+            if (hdr[o] == 1) {                                   // IPOPT_NOP
+                o++;
+                continue;
+            }
+            if (hdr[o] == 0 || o + 1 >= hl || hdr[o + 1] < 2 || o + hdr[o + 1] > hl)
+                break;                                           // EOL, bad length
+            if ((hdr[o] == 137 || hdr[o] == 131) && hdr[o + 1] >= 7) {   // SSRR / LSRR
+                std::memcpy(ip20 + 16, hdr + o + hdr[o + 1] - 4, 4);
+                break;
+            }
+            o += hdr[o + 1];
+        }
+    ip20[0] = 0x45;
+}
+
+int CheckL4Header::push_irregular(Pending &p, int32_t th_off)
+{
+    const uint32_t L = p.length, nh = (uint32_t)p.nh_off;
+    if (th_off < 0 || nh + 20 > L)
+        return ~0;                                    // as a packet without the annotation / too short
+    const uint8_t *iph = p.data + nh, *th = p.data + th_off;
+    const uint32_t th_u = (uint32_t)th_off, hl = (iph[0] & 15u) << 2;
+    uint8_t ip20[20];
+    canonical_ip20(iph, L - nh, ip20);
+    if (iph[9] != proto_)                                       // NOT_UDP / NOT_TCP / NOT_ICMP
+        return host_decided(p, CLK_L4_NOT_PROTO);
+    uint32_t seg = 0;
+    if (proto_ == 17) {                                         // checkudpheader.cc:94-98
+        if (th_u + 8 > L)
+            return host_decided(p, CLK_L4_BAD_LENGTH);
+        seg = be16(th + 4);
+        if (seg < 8 || (uint64_t)L < (uint64_t)seg + hl + nh || th_u + seg > L)
+            return host_decided(p, CLK_L4_BAD_LENGTH);
+    } else if (proto_ == 6) {                                   // checktcpheader.cc:95-100
+        if (th_u + 13 > L)
+            return host_decided(p, CLK_L4_BAD_LENGTH);
+        seg = (be16(iph + 2) - hl) & 0xFFFFFFFFu;
+        const uint32_t thl = (uint32_t)(th[12] >> 4) << 2;
+        if (thl < 20 || seg < thl || (uint64_t)L < (uint64_t)seg + hl + nh || th_u + seg > L)
+            return host_decided(p, CLK_L4_BAD_LENGTH);
+        if (seg + 20 > 0xFFFF) {
+            err_ = "a TCP length past 65515 behind a transport header not at ip_hl";
+            return CLK_EINVAL;
+        }
+        ip20[2] = (uint8_t)((seg + 20) >> 8), ip20[3] = (uint8_t)(seg + 20);
+    } else {                                                    // checkicmpheader.cc:92-94
+        if (th_u > L || L - th_u < 8)
+            return host_decided(p, CLK_L4_BAD_LENGTH);
+        seg = L - th_u;
+    }
+    p.span_off = th_u;
+    return stage_canonical(p, ip20, th, seg);
+}
+
 int CheckL4Header::run(const clk_batch *b, uint8_t *d_codes, uint16_t *)
 {
     if (proto_ == 17)
@@ -1159,6 +1292,7 @@ void CheckL4Header::route(Pending &, int code, uint16_t, Result *r)
 SetL4Checksum::SetL4Checksum(clk_ctx *ctx, const std::string &name, int noutputs, int proto)
     : BatchElement(ctx, name, noutputs), proto_(proto)
 {
+    reads_th_ = true;
 }
 
 int SetL4Checksum::configure(ConfArgs &args, std::string *err)
@@ -1196,6 +1330,61 @@ bool SetL4Checksum::span(const Pending &p, uint32_t *off, uint32_t *len, int32_t
     return true;
 }
 
+int SetL4Checksum::push_irregular(Pending &p, int32_t th_off)
+{
+    const uint32_t L = p.length, nh = (uint32_t)p.nh_off;
+    if (th_off == -2 && proto_ == 6)                            // !has_transport_header() (settcpchecksum.cc:53)
+        return host_decided(p, CLK_SET_KILL);
+    if (th_off < 0 || nh + 20 > L)
+        return ~0;
+    const uint8_t *iph = p.data + nh, *th = p.data + th_off;
+    const uint32_t th_u = (uint32_t)th_off, hl = (iph[0] & 15u) << 2;
+    const uint32_t tlen = th_u <= L ? L - th_u : 0;              // transport_length() (< 0: too short)
+    const bool frag = (be16(iph + 6) & 0x3FFF) != 0;
+    uint32_t seg;
+    uint8_t b12 = 0;
+    bool fix = false;
+    if (proto_ == 17) {                                         // setudpchecksum.cc:48-61
+        if (frag || th_u > L || tlen < 8 || tlen < be16(th + 4))
+            return host_decided(p, CLK_SET_OUTPUT1);
+        seg = tlen;
+    } else {                                                    // settcpchecksum.cc:50-63
+        const uint32_t plen = (be16(iph + 2) - hl) & 0xFFFFFFFFu;
+        if (th_u > L || plen < 20 || plen > tlen)
+            return host_decided(p, CLK_SET_KILL);
+        if (plen + 20 > 0xFFFF) {
+            err_ = "a TCP length past 65515 behind a transport header not at ip_hl";
+            return CLK_EINVAL;
+        }
+        seg = plen;
+        if (fixoff_) {
+            const uint32_t off = (uint32_t)(th[12] >> 4) << 2;
+            fix = off < 20 || (off > plen && !frag);
+            b12 = (uint8_t)((th[12] & 0x0F) | ((off < 20 ? 5u : (plen >> 2) & 0xF) << 4));
+        }
+    }
+    // the header as the pseudo-header reads it: the reference has zeroed the
+    // checksum field (and FIXOFF rewritten th_off) first, and a transport
+    // header inside the IP header's first bytes changes them
+    const uint32_t have = std::min<uint32_t>(std::max<uint32_t>(hl, 20), L - nh);
+    uint8_t hdr[64];
+    std::memcpy(hdr, iph, have);
+    const uint32_t field = proto_ == 17 ? 6 : 16;
+    auto patch = [&](uint32_t at, uint8_t v) {                  // packet offset at, relative to data
+        if (at >= nh && at < nh + have)
+            hdr[at - nh] = v;
+    };
+    patch(th_u + field, 0), patch(th_u + field + 1, 0);
+    if (fix)
+        patch(th_u + 12, b12);
+    uint8_t ip20[20];
+    canonical_ip20(hdr, have, ip20);
+    if (proto_ == 6)
+        ip20[2] = (uint8_t)((seg + 20) >> 8), ip20[3] = (uint8_t)(seg + 20);
+    p.span_off = th_u;
+    return stage_canonical(p, ip20, th, seg);
+}
+
 int SetL4Checksum::run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums)
 {
     return proto_ == 17 ? clk_set_udp_checksum(ctx_, b, d_codes, d_sums)
@@ -1211,7 +1400,8 @@ void SetL4Checksum::route(Pending &p, int code, uint16_t sum, Result *r)
     if (code == CLK_SET_OK) {
         uint8_t *iph = p.data + p.nh_off;
         const uint32_t hl = (uint32_t)(iph[0] & 0xF) << 2;
-        uint8_t *th = iph + hl;
+        // the transport header: its annotation for a canonical copy
+        uint8_t *th = p.anno & ANNO_CANON ? p.data + p.span_off : iph + hl;
         if (proto_ == 6 && fixoff_) {                           // settcpchecksum.cc:57-63
             const uint32_t plen = be16(iph + 2) - hl;
             const uint32_t off = (uint32_t)(th[12] >> 4) << 2;
@@ -1958,6 +2148,14 @@ int clk_element_push_anno(clk_element *w, uint8_t *data, uint32_t length, int32_
     if (!w || (!data && length))
         return CLK_EINVAL;
     return w->e->push(data, length, nh_offset, token, anno);
+}
+
+int clk_element_push_th(clk_element *w, uint8_t *data, uint32_t length, int32_t nh_offset, int32_t th_offset,
+                        uint32_t anno, uint64_t token)
+{
+    if (!w || (!data && length) || th_offset < -2)
+        return CLK_EINVAL;
+    return w->e->push(data, length, nh_offset, token, anno, th_offset);
 }
 
 int clk_element_push_burst(clk_element *w, uint8_t *const *datas, const uint32_t *lengths,

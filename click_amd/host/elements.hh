@@ -278,12 +278,12 @@ struct ChainWork {
 // virtual call per packet).
 #define CLK_INL __attribute__((always_inline))
 #define CLK_GLUE_LOOPS(C)                                                                                       \
-    int push(uint8_t *d_, uint32_t l_, int32_t nh_, uint64_t t_, uint32_t a_ = 0) override                      \
+    int push(uint8_t *d_, uint32_t l_, int32_t nh_, uint64_t t_, uint32_t a_ = 0, int32_t th_ = -1) override    \
     {                                                                                                           \
         return push_one([this](const Pending &p, uint32_t *o, uint32_t *l, int32_t *c) CLK_INL {                 \
             bool r_; [[clang::always_inline]] r_ = this->C::span(p, o, l, c);                                   \
             return r_;                                                                                          \
-        }, d_, l_, nh_, t_, a_, hold_);                                                                         \
+        }, d_, l_, nh_, t_, a_, hold_, th_);                                                                    \
     }                                                                                                           \
     int push_burst(uint8_t *const *d_, const uint32_t *l_, const int32_t *nh_, uint64_t t0_, uint32_t n_) override \
     {                                                                                                           \
@@ -331,8 +331,11 @@ class alignas(128) BatchElement {
     virtual ~BatchElement();
     virtual const char *class_name() const = 0;
     virtual int configure(ConfArgs &args, std::string *err);
-    // one packet (the final classes run it with their span() inlined, CLK_GLUE_LOOPS)
-    virtual int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno = 0);
+    // one packet (the final classes run it with their span() inlined,
+    // CLK_GLUE_LOOPS); th_offset: the transport header annotation
+    // (clk_element_push_th), -1 unknown
+    virtual int push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno = 0,
+                     int32_t th_offset = -1);
     // a burst of packets (tokens first_token + k), flushing double-buffered
     // whenever the batch fills; the final classes run it with their span()
     // inlined (CLK_GLUE_LOOPS)
@@ -363,8 +366,11 @@ class alignas(128) BatchElement {
         uint32_t span_len;
         uint32_t index;      // position in the GPU batch (staged packets)
         int16_t host_code;   // >= 0: decided on the host (not staged)
-        uint16_t anno;       // CLK_ANNO_* bits
+        uint16_t anno;       // CLK_ANNO_* bits (and ANNO_CANON)
     };
+    // Pending::anno: staged as a canonical copy (push_irregular); span_off
+    // is then the transport header's offset from data
+    static constexpr uint16_t ANNO_CANON = 0x4;
     // Bytes the kernel needs, relative to data; return false to decide on the
     // host with *code (routed like a kernel result).
     virtual bool span(const Pending &p, uint32_t *off, uint32_t *len, int32_t *code) const = 0;
@@ -520,7 +526,21 @@ class alignas(128) BatchElement {
     // (its long span is gathered at launch), not from a burst (which
     // prefetches the spans ahead itself)
     int push_one(SpanF &&span_f, uint8_t *data, uint32_t length, int32_t nh_offset, uint64_t token, uint32_t anno,
-                 bool held);
+                 bool held, int32_t th_offset = -1);
+    // The L4 elements read the transport header where its annotation says,
+    // as udp_header() / tcp_header() / icmp_header() do (checkudpheader.cc:87,
+    // checktcpheader.cc:88, checkicmpheader.cc:85, setudpchecksum.cc:45,
+    // settcpchecksum.cc:49); the kernels find it at ip_hl.  A packet whose
+    // annotation is elsewhere (ip_hl rewritten after the header was marked)
+    // comes here (reads_th_): the host decides what the reference decides
+    // from the header and lengths, and the checksum runs on the GPU over a
+    // canonical copy -- the IP header with ip_hl 5 and the pseudo-header's
+    // destination (in_cksum.c:86-108) followed by the segment at the
+    // annotation (stage_canonical).  ~0: it is not irregular after all.
+    virtual int push_irregular(Pending &p, int32_t th_offset);
+    int stage_canonical(Pending &p, const uint8_t *ip20, const uint8_t *seg, uint32_t seglen);
+    int host_decided(Pending &p, int32_t code);
+    bool reads_th_ = false;
     template <class SpanF>
     int burst_loop(SpanF &&span_f, uint8_t *const *datas, const uint32_t *lengths, const int32_t *nh_offsets,
                    uint64_t first_token, uint32_t n);
@@ -699,6 +719,7 @@ class CheckL4Header : public CheckElement {
     const char *const *reason_texts() const override;
     int nreasons() const override { return 3; }
     std::string drop_message(const char *reason) const override;
+    int push_irregular(Pending &p, int32_t th_offset) override;
 
   private:
     int proto_;
@@ -717,6 +738,7 @@ class SetL4Checksum : public BatchElement {
     int run(const clk_batch *b, uint8_t *d_codes, uint16_t *d_sums) override;
     void route(Pending &p, int code, uint16_t sum, Result *r) override;
     bool wants_sums() const override { return true; }
+    int push_irregular(Pending &p, int32_t th_offset) override;
 
   private:
     int proto_;

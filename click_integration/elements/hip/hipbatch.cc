@@ -56,7 +56,7 @@ struct HIPChainGraph {
 	y->router()->visit_upstream(y, 0, &up);
 	return up.n == 1 ? gpu_backed(up.first) : 0;
     }
-    bool chain_conf(Node x) const	{ return x->_chain_conf; }
+    bool chain_conf(Node x) const	{ return x->_chain_conf && !x->cls_reads_transport(); }
     int device(Node x) const		{ return x->_device; }
     bool may_write(Node x) const	{ return x->cls_may_write(); }
     bool chain_last(Node x) const	{ return x->cls_chain_last(); }

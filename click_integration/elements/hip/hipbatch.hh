@@ -154,10 +154,16 @@ class HIPBatchElement : public Element { public:
     virtual bool cls_chain_last() const		{ return false; }
     virtual bool cls_chain_head_only() const	{ return false; }
     virtual bool cls_pass_effects() const	{ return false; }
+    // reads the transport header annotation (the L4 classes): runs alone,
+    // never in a chain, whose batches take no transport header
+    virtual bool cls_reads_transport() const	{ return false; }
 
     // ---- the core's host interface (hipcore.hh); m: the chain member ---------
     Packet *prepare(Packet *p, uint32_t *anno, Packet **extra);
     int32_t nh_offset(Packet *p)		{ return cls_nh_offset(p); }
+    int32_t th_offset(Packet *p) {		// udp_header() / tcp_header() / icmp_header()'s annotation
+	return !cls_reads_transport() ? -1 : p->has_transport_header() ? p->transport_header_offset() : -2;
+    }
     bool primary(int m, int32_t port, uint32_t aux) const	{ return _chain[m]->cls_primary(port, aux); }
     Packet *make_packet(int m, clk_element *e, uint32_t key)	{ return _chain[m]->cls_make_packet(e, key); }
     bool extra_results(int m) const	{ return _chain[m]->cls_extra_results(); }

@@ -39,6 +39,7 @@ class HIPIPInputCombo : public HIPClassElement<hipcore::IPInputComboClass<Packet
 
 class HIPCheckL4Header : public HIPBatchElement { public:
     const char *port_count() const	{ return PORTS_1_1X2; }
+    bool cls_reads_transport() const	{ return true; }
 };
 
 class HIPCheckUDPHeader : public HIPCheckL4Header { public:

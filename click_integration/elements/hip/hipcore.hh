@@ -76,6 +76,8 @@
  *        deliver_run() over member m's class, pushing on member m's outputs
  *        (checked_output_push); with `ready` (pull context, last member) the
  *        output-0 packets go there instead
+ *   int32_t th_offset(P *p)      the transport header annotation's offset
+ *        from data() (-2: none, -1: unknown), for clk_element_push_th
  *   uint8_t *data(P *p); uint32_t length(P *p)
  *   P *input_pull()                              input(0).pull(0)
  *   void kill(P *p)
@@ -459,8 +461,10 @@ template <class P, class Host, class L> class Core {
             t.counted = true;
             arm(h, t);
         }
+        // (the L4 classes read the transport header annotation: clk_element_push_th)
         int r = t.chain ? clk_chain_push_anno(t.chain, h.data(p), h.length(p), h.nh_offset(p), anno, t.next)
-                        : clk_element_push_anno(t.e, h.data(p), h.length(p), h.nh_offset(p), anno, t.next);
+                        : clk_element_push_th(t.e, h.data(p), h.length(p), h.nh_offset(p), h.th_offset(p), anno,
+                                              t.next);
         if (r < 0) {                     // not staged
             t.held.pop_back();
             h.kill(p);

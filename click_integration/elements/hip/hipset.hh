@@ -26,12 +26,14 @@ class HIPSetIPChecksum : public HIPSetChecksum { public:
 
 class HIPSetUDPChecksum : public HIPSetChecksum { public:
     const char *class_name() const	{ return "SetUDPChecksum"; }
+    bool cls_reads_transport() const	{ return true; }
     const char *message_attachment() const	{ return "HIPSetUDPChecksum_message"; }
     const char *port_count() const	{ return PORTS_1_1X2; }
 };
 
 class HIPSetTCPChecksum : public HIPSetChecksum { public:
     const char *class_name() const	{ return "SetTCPChecksum"; }
+    bool cls_reads_transport() const	{ return true; }
     const char *port_count() const	{ return PORTS_1_1; }
     const char *processing() const	{ return AGNOSTIC; }
 };

@@ -139,6 +139,20 @@ int clk_element_push_burst(clk_element *e, uint8_t *const *datas, const uint32_t
 int clk_element_push_anno(clk_element *e, uint8_t *data, uint32_t length, int32_t nh_offset,
                           uint32_t anno, uint64_t token);
 
+/* clk_element_push_anno with the packet's transport header annotation:
+ * th_offset = Packet::transport_header_offset(), -2 when the packet has
+ * none, -1 unknown (taken to be at ip_hl).  The L4 elements read the
+ * segment where the annotation says, as the reference's udp_header() /
+ * tcp_header() / icmp_header() do (checkudpheader.cc:87,
+ * checktcpheader.cc:88, checkicmpheader.cc:85, setudpchecksum.cc:45,
+ * settcpchecksum.cc:49), and the lengths' ip_hl from the header bytes: the
+ * two differ when ip_hl changed after the header was marked.  Such a packet
+ * is staged as a canonical copy (not with ZEROCOPY: CLK_EINVAL); SetTCPChecksum
+ * kills a packet with no transport header (settcpchecksum.cc:53).  The other
+ * classes ignore th_offset.                                               */
+int clk_element_push_th(clk_element *e, uint8_t *data, uint32_t length, int32_t nh_offset,
+                        int32_t th_offset, uint32_t anno, uint64_t token);
+
 /* Run the staged batch on the GPU and route it (synchronous).  Results are
  * appended to the element's result queue in push order.                  */
 int clk_element_flush(clk_element *e);

@@ -325,6 +325,122 @@ int oracle_check_icmp_header(const uint8_t *nh, uint32_t caplen)
     return CLK_OK;
 }
 
+/* ---- the L4 elements, transport header at its annotation -------------------
+ * Header fields (ip_p, ip_hl for the lengths, ip_len, ip_off) come from the
+ * IP header bytes, the segment from nh + th, as the reference reads them.
+ * Domain guards where the reference would read outside the packet: caplen <
+ * 20 as above; the transport fields read and the summed segment must lie in
+ * [0, caplen) (else BAD_LENGTH, output 1 or kill, as a short packet); the
+ * pseudo-header's option walk stops at caplen.  Test infrastructure: the
+ * checker of the glue's irregular-annotation path (clk_element_push_th). */
+static uint16_t pseudohdr_clamped(uint32_t csum, const uint8_t *iph, uint32_t caplen, int len)
+{
+    uint32_t dst = ld32(iph + 16);
+    uint32_t hl = (uint32_t)(iph[0] & 0xF) << 2;
+    if ((iph[0] & 0xF) != 5) {                              /* ip.h:156-159 -> in_cksum.c:83-108 */
+        uint32_t end = hl < caplen ? hl : caplen, o = 20;
+        while (o < end) {
+            if (iph[o] == 1) {
+                o++;
+                continue;
+            } else if (iph[o] == 0)
+                break;
+            if (o + 1 >= end || iph[o + 1] < 2 || o + iph[o + 1] > end)
+                break;
+            if ((iph[o] == 137 || iph[o] == 131) && iph[o + 1] >= 7) {
+                dst = ld32(iph + o + iph[o + 1] - 4);
+                break;
+            }
+            o += iph[o + 1];
+        }
+    }
+    return oracle_in_cksum_pseudohdr_raw(csum, ld32(iph + 12), dst, iph[9], len);
+}
+
+int oracle_check_l4_at(int proto, const uint8_t *nh, uint32_t caplen, uint32_t th)
+{
+    if (caplen < 20)
+        return CLK_L4_BAD_LENGTH;
+    if (nh[9] != proto)                                     /* NOT_UDP / NOT_TCP / NOT_ICMP */
+        return CLK_L4_NOT_PROTO;
+    uint32_t iph_len = (uint32_t)(nh[0] & 0xF) << 2;
+    const uint8_t *t = nh + th;
+    uint32_t len;
+    if (proto == 17) {                                      /* checkudpheader.cc:94-104 */
+        if (th + 8 > caplen)
+            return CLK_L4_BAD_LENGTH;
+        len = bswap16(ld16(t + 4));
+        if (len < 8 || (uint64_t)caplen < (uint64_t)len + iph_len || th + len > caplen)
+            return CLK_L4_BAD_LENGTH;
+        if (ld16(t + 6) == 0)
+            return CLK_OK;
+        return pseudohdr_clamped(oracle_in_cksum(t, (int)len), nh, caplen, (int)len) ? CLK_L4_BAD_CHECKSUM : CLK_OK;
+    }
+    if (proto == 6) {                                       /* checktcpheader.cc:95-104 */
+        if (th + 13 > caplen)
+            return CLK_L4_BAD_LENGTH;
+        len = (uint32_t)bswap16(ld16(nh + 2)) - iph_len;
+        uint32_t tcph_len = (uint32_t)(t[12] >> 4) << 2;
+        if (tcph_len < 20 || len < tcph_len || (uint64_t)caplen < (uint64_t)len + iph_len || th + len > caplen)
+            return CLK_L4_BAD_LENGTH;
+        return pseudohdr_clamped(oracle_in_cksum(t, (int)len), nh, caplen, (int)len) ? CLK_L4_BAD_CHECKSUM : CLK_OK;
+    }
+    /* checkicmpheader.cc:92-141 on the segment [th, caplen) */
+    if (th > caplen || caplen - th < 8)
+        return CLK_L4_BAD_LENGTH;
+    len = caplen - th;
+    switch (t[0]) {
+    case 3: case 11: case 12: case 4: case 5:
+        if (len < 8 + 28)
+            return CLK_L4_BAD_LENGTH;
+        break;
+    case 13: case 14:
+        if (len != 20)
+            return CLK_L4_BAD_LENGTH;
+        break;
+    case 15: case 16:
+        if (len != 8)
+            return CLK_L4_BAD_LENGTH;
+        break;
+    default:
+        break;
+    }
+    return oracle_in_cksum(t, (int)len) != 0 ? CLK_L4_BAD_CHECKSUM : CLK_OK;
+}
+
+int oracle_set_l4_at(int proto, uint8_t *nh, uint32_t caplen, uint32_t th, int has_th, int fixoff)
+{
+    if (caplen < 20)
+        return proto == 17 ? CLK_SET_OUTPUT1 : CLK_SET_KILL;
+    uint8_t *t = nh + th;
+    int isfrag = (bswap16(ld16(nh + 6)) & 0x3FFF) != 0;
+    if (proto == 17) {                                      /* setudpchecksum.cc:44-66 */
+        int tlen = th > caplen ? -1 : (int)(caplen - th);
+        int len;
+        if (isfrag || tlen < 8 || (len = bswap16(ld16(t + 4)), tlen < len))
+            return CLK_SET_OUTPUT1;
+        st16(t + 6, 0);
+        unsigned csum = oracle_in_cksum(t, len);
+        st16(t + 6, pseudohdr_clamped(csum, nh, caplen, len));
+        return CLK_OK;
+    }
+    uint32_t hl = (uint32_t)(nh[0] & 0xF) << 2;             /* settcpchecksum.cc:50-67 */
+    uint32_t plen = (uint32_t)bswap16(ld16(nh + 2)) - hl;
+    if (!has_th || th > caplen || plen < 20 || plen > caplen - th)
+        return CLK_SET_KILL;
+    if (fixoff) {
+        uint32_t off = (uint32_t)(t[12] >> 4) << 2;
+        if (off < 20)
+            t[12] = (uint8_t)((t[12] & 0x0F) | (5 << 4));
+        else if (off > plen && !isfrag)
+            t[12] = (uint8_t)((t[12] & 0x0F) | (((plen >> 2) & 0xF) << 4));
+    }
+    st16(t + 16, 0);
+    unsigned csum = oracle_in_cksum(t, (int)plen);
+    st16(t + 16, pseudohdr_clamped(csum, nh, caplen, (int)plen));
+    return CLK_OK;
+}
+
 /* elements/ip/decipttl.cc:45-77 with ACTIVE true (ACTIVE false returns the
  * packet before reading it; the caller does not launch).  multicast =
  * the MULTICAST keyword.  Returns CLK_OK (TTL decremented, ip_sum updated

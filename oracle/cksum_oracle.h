@@ -45,6 +45,15 @@ int oracle_check_tcp_header(const uint8_t *nh, uint32_t caplen);
 int oracle_set_tcp_checksum(uint8_t *nh, uint32_t caplen, int fixoff);
 int oracle_check_icmp_header(const uint8_t *nh, uint32_t caplen);
 int oracle_dec_ip_ttl(uint8_t *nh, uint32_t caplen, int multicast);
+/* The same L4 elements with the transport header where its annotation puts
+ * it, th bytes past the network header (udp_header(), tcp_header(),
+ * icmp_header(), transport_length(): checkudpheader.cc:84-107,
+ * setudpchecksum.cc:37-69, checktcpheader.cc:85-107,
+ * settcpchecksum.cc:44-75, checkicmpheader.cc:83-141); th = ip_hl*4 gives
+ * the functions above.  proto 17 / 6 / 1.  has_th = 0: no transport header
+ * (SetTCPChecksum kills, settcpchecksum.cc:53). */
+int oracle_check_l4_at(int proto, const uint8_t *nh, uint32_t caplen, uint32_t th);
+int oracle_set_l4_at(int proto, uint8_t *nh, uint32_t caplen, uint32_t th, int has_th, int fixoff);
 
 /* ---- IP output path (ipgwoptions.cc, fixipsrc.cc, ipoutputcombo.cc) ------
  * ts = the 4 bytes stored for Timestamp::now() (htonl(ms since midnight)). */

@@ -44,6 +44,7 @@ struct TPacket {
     uint8_t *raw = nullptr;          // buf->data(), kept in the packet as Click's Packet keeps its buffer
     size_t off = 0, len = 0;
     long nh = -1;                    // absolute offset of the network header in buf
+    long th = -1;                    // ... and of the transport header (set_ip_header); -1 unknown
     bool cloned = false;             // a clone of it was made, or it is one: uniqueify() asks the
                                      // buffer's count (Click keeps that count in the Packet itself)
     bool ring = false;               // owned by a measurement's receive ring (raw points into it;
@@ -142,7 +143,11 @@ struct TOps {
     static const uint8_t *network_header(TPacket *p) { return p->raw + p->nh; }
     static int32_t network_header_offset(TPacket *p) { return (int32_t)(p->nh - (long)p->off); }
     static int network_length(TPacket *p) { return (int)((long)(p->off + p->len) - p->nh); }
-    static void set_ip_header(TPacket *p, const uint8_t *ip, uint32_t) { p->nh = ip - p->raw; }
+    static void set_ip_header(TPacket *p, const uint8_t *ip, uint32_t hlen)
+    {
+        p->nh = ip - p->raw;
+        p->th = p->nh + hlen;        // Packet::set_ip_header marks both (packet.hh)
+    }
     static void take(TPacket *p, uint32_t n) { p->len -= n; }
     static void pull(TPacket *p, uint32_t n) { p->off += n, p->len -= n; }
     static void set_dst_ip_anno(TPacket *p, uint32_t a) { p->a.dst = a; }
@@ -225,6 +230,7 @@ class Host {
     // ---- the core's host interface (as HIPBatchElement / HIPClassElement) -----
     TPacket *prepare(TPacket *p, uint32_t *anno, TPacket **extra) { return cls.prepare(p, anno, extra); }
     int32_t nh_offset(TPacket *p) { return cls.nh_offset(p); }
+    int32_t th_offset(TPacket *p) { return p->th >= 0 ? (int32_t)(p->th - (long)p->off) : -1; }
     bool primary(int, int32_t port, uint32_t aux) { return cls.primary(port, aux); }
     TPacket *make_packet(int, clk_element *e, uint32_t key) { return cls.make_packet(e, key); }
     bool extra_results(int) const { return C::extra_results != 0; }
@@ -408,6 +414,7 @@ class ChainHost {
         return hipcore::chain_ready<TPacket, TOps>(p, writes, anno);
     }
     int32_t nh_offset(TPacket *p) { return m[0]->nh_offset(p); }
+    int32_t th_offset(TPacket *) { return -1; }         // (chains take no transport header)
     bool primary(int k, int32_t port, uint32_t aux) { return m[(size_t)k]->primary(port, aux); }
     TPacket *make_packet(int k, clk_element *e, uint32_t key) { return m[(size_t)k]->make_packet(e, key); }
     void deliver(int k, St &t, const hipcore::Chunk<TPacket> &c, uint32_t i, uint32_t j, std::vector<TPacket *> *ready)

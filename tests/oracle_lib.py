@@ -62,6 +62,10 @@ def load_oracle():
     L.oracle_ip_fragment_batch.restype = ctypes.c_int
     L.oracle_ip_fragment_batch.argtypes = [_P, _P, ctypes.c_uint64, _P, ctypes.c_uint32, ctypes.c_uint64,
                                            ctypes.c_uint32, ctypes.c_int, _P, _P, _P, _P, _P, _P, _P, _P, _P]
+    L.oracle_check_l4_at.restype = ctypes.c_int
+    L.oracle_check_l4_at.argtypes = [ctypes.c_int, _P, ctypes.c_uint32, ctypes.c_uint32]
+    L.oracle_set_l4_at.restype = ctypes.c_int
+    L.oracle_set_l4_at.argtypes = [ctypes.c_int, _P, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int]
     _lib = L
     return L
 

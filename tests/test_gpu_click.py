@@ -37,8 +37,8 @@ def gpu():
 
 
 def test_parity_graph_ip():
-    rc, h, err = click_run.run("parity", "hip-parity-ip.click", handlers=("cmp.diffs", "cpu.drops", "gpu.drops"),
-                               timeout=120)
+    rc, h, err = click_run.run("parity", "hip-parity-ip.click",
+                               handlers=("cmp.diffs", "cmp.diff_details", "cpu.drops", "gpu.drops"), timeout=120)
     assert rc == 0, err
     assert h["cmp.diffs"] == "0", (h, err)
     assert h["cpu.drops"] == h["gpu.drops"] and int(h["cpu.drops"]) > 0, h
@@ -46,7 +46,8 @@ def test_parity_graph_ip():
 
 def test_parity_graph_udp():
     rc, h, err = click_run.run("parity", "hip-parity-udp.click",
-                               handlers=("setcmp.diffs", "chkcmp.diffs", "cpucheck.drops", "gpucheck.drops"),
+                               handlers=("setcmp.diffs", "chkcmp.diffs", "setcmp.diff_details", "chkcmp.diff_details",
+                                         "cpucheck.drops", "gpucheck.drops"),
                                timeout=120)
     assert rc == 0, err
     assert h["setcmp.diffs"] == "0" and h["chkcmp.diffs"] == "0", (h, err)

@@ -3,6 +3,8 @@ batched elements route, count, trim, write back and chatter exactly as the
 reference elements would, packet by packet (the oracle decides each packet;
 the routing rules are the reference's: checkipheader.cc:143-159,
 setipchecksum.cc:88-93, setudpchecksum.cc:48-61, settcpchecksum.cc:71-74)."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -350,3 +352,82 @@ def test_shared_messages_speak_once(ctx, cls, config, noutputs, reasons, prefix)
         codes, _ = oracle_lib.batch("set_udp", ref, len(foff), off=foff + 14, length=flen - 14, arg=0)
         assert (codes[:half] != 0).any() and (codes[half:] != 0).any()
         assert msgs == [prefix]
+
+
+@pytest.mark.parametrize("cls,conf,proto,noutputs", [
+    ("CheckUDPHeader", "", 17, 2), ("CheckTCPHeader", "", 6, 2), ("CheckICMPHeader", "", 1, 2),
+    ("SetUDPChecksum", "", 17, 2), ("SetTCPChecksum", "", 6, 1), ("SetTCPChecksum", "FIXOFF true", 6, 1)])
+def test_transport_header_annotation(ctx, cls, conf, proto, noutputs):
+    """The L4 elements read the segment at the transport header annotation
+    (udp_header() / tcp_header() / icmp_header(), checkudpheader.cc:87,
+    setudpchecksum.cc:45, checktcpheader.cc:88, settcpchecksum.cc:49,
+    checkicmpheader.cc:85) and ip_hl from the header bytes.  Packets pushed
+    with clk_element_push_th: a third at ip_hl (the kernels' path), a third
+    with ip_hl rewritten after marking (a corrupted header: RandomBitErrors
+    in a graph), a third at an arbitrary offset; verdicts and every byte
+    against the oracle's annotation-aware restatement."""
+    from click_amd.elements import Element
+    L = oracle_lib.load_oracle()
+    rng = np.random.default_rng(300 + proto + len(conf))
+    arena, off3, cap3, _ = fuzz.make_batch(rng, 1500, proto, max_total=1200, mutate_frac=0.2)
+    n = len(off3)
+    th = np.zeros(n, np.int64)
+    for i in range(n):
+        o, c = int(off3[i]), int(cap3[i])
+        hl = int(arena[o] & 15) * 4 if c else 20
+        k = i % 3
+        if k == 0 or c < 20:
+            th[i] = hl
+        elif k == 1:
+            th[i] = hl
+            arena[o] = (arena[o] & 0xF0) | int(rng.choice([4, 6, 7, 9, 15, 2]))
+        else:
+            th[i] = int(rng.integers(0, min(c, 80) + 1))
+    ref = arena.copy()
+    set_ = cls.startswith("Set")
+    fix = 1 if "FIXOFF" in conf else 0
+    codes = []
+    for i in range(n):
+        o, c = int(off3[i]), int(cap3[i])
+        nh = ref.ctypes.data + o
+        if set_:
+            codes.append(L.oracle_set_l4_at(proto, nh, c, int(th[i]), 1, fix))
+        else:
+            codes.append(L.oracle_check_l4_at(proto, nh, c, int(th[i])))
+    codes = np.array(codes)
+    e = Element(ctx, cls, ", ".join(x for x in (conf, "BATCH 700") if x), noutputs=noutputs)
+    base = arena.ctypes.data
+    for i in range(n):
+        rc = e.push_th(base + int(off3[i]), int(cap3[i]), 0, int(th[i]), token=i)
+        assert rc >= 0, e.last_error()
+        if rc == 1:
+            e.flush()
+    e.flush()
+    tok, port, _ = e.results()
+    assert np.array_equal(tok, np.arange(n))
+    if set_:
+        from click_amd import _abi
+        exp = np.where(codes == 0, 0, np.where(codes == _abi.CLK_SET_OUTPUT1, 1 if noutputs == 2 else -1, -1))
+    else:
+        exp = np.where(codes == 0, 0, 1 if noutputs == 2 else -1)
+    bad = np.nonzero(port != exp)[0]
+    assert len(bad) == 0, [(int(i), int(codes[i]), int(port[i]), int(th[i]), int(cap3[i])) for i in bad[:8]]
+    if set_:
+        diff = np.nonzero(arena != ref)[0]
+        assert len(diff) == 0, diff[:10]
+    kinds = {(i % 3, int(codes[i] == 0)) for i in range(n)}
+    assert (1, 1) in kinds and (2, 1) in kinds and (1, 0) in kinds, kinds
+    e.close()
+
+
+def test_transport_header_annotation_zerocopy_refused(ctx):
+    """ZEROCOPY reads packets in place: a packet whose annotation is not at
+    ip_hl cannot be, and the push is refused (clk_element_push_th)."""
+    import ctypes as ct
+    from click_amd.elements import Element
+    pkt = np.zeros(64, np.uint8)
+    oracle_lib.gen(pkt, 1, stride=64, fixed_len=60, proto=17)
+    e = Element(ctx, "CheckUDPHeader", "ZEROCOPY true", noutputs=2)
+    assert e.push_th(pkt.ctypes.data, 60, 0, 24, token=0) < 0
+    assert "annotation" in e.last_error()
+    e.close()

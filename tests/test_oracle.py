@@ -6,6 +6,7 @@
    on randomized and fuzzed inputs, including the u32-wrap overflow case;
 3. the synthetic-traffic generator's invariants.
 """
+import ctypes
 import json
 import os
 import struct
@@ -423,3 +424,30 @@ def test_config1_fake_iprouter_plumbing_on_cpu():
         outs.append(ip)
     assert np.array_equal(outs[0], outs[1])
     assert int(outs[0].reshape(n, -1)[:, 8].astype(np.int64).sum()) == n * 63     # TTL 64 -> 63 on all 600000
+
+
+@pytest.mark.parametrize("proto", [17, 6, 1])
+def test_transport_annotation_restatement_at_ip_hl(proto):
+    """oracle_check_l4_at / oracle_set_l4_at (the segment at the transport
+    header annotation, as udp_header() / tcp_header() / icmp_header() read
+    it) with the annotation at ip_hl are the element restatements above:
+    same verdicts and, for the Set elements, the same bytes."""
+    L = oracle_lib.load_oracle()
+    rng = np.random.default_rng(40 + proto)
+    arena, off, cap, _ = fuzz.make_batch(rng, 1200, proto, max_total=900)
+    a2 = arena.copy()
+    base, base2 = arena.ctypes.data, a2.ctypes.data
+    check = {17: L.oracle_check_udp_header, 6: L.oracle_check_tcp_header, 1: L.oracle_check_icmp_header}[proto]
+    for f in (check, L.oracle_set_udp_checksum, L.oracle_set_tcp_checksum):
+        f.restype = ctypes.c_int
+    for i in range(len(off)):
+        o, c = int(off[i]), int(cap[i])
+        hl = int(arena[o] & 15) * 4 if c else 0
+        assert L.oracle_check_l4_at(proto, base + o, c, hl) == check(ctypes.c_void_p(base + o), c), i
+        if proto == 17:
+            assert L.oracle_set_l4_at(17, base + o, c, hl, 1, 0) == \
+                L.oracle_set_udp_checksum(ctypes.c_void_p(base2 + o), c), i
+        elif proto == 6:
+            assert L.oracle_set_l4_at(6, base + o, c, hl, 1, i & 1) == \
+                L.oracle_set_tcp_checksum(ctypes.c_void_p(base2 + o), c, i & 1), i
+    assert np.array_equal(arena, a2)

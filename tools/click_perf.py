@@ -107,11 +107,11 @@ def run_one(mode, graph, extra="", limit=None, burst=None, timeout=180):
     return {"count": n, "mpps_counter": float(h["out.rate"]) / 1e6, "mpps_wall": n / wall / 1e6, "wall_s": wall}
 
 
-def sweep(limit_c1=6000000, limit_c3=2000000, reps=3, variants=None):
+def sweep(limit_c1=6000000, limit_c3=2000000, reps=3, variants=None, bursts=(1, 32)):
     variants = variants if variants is not None else [("cpu", ""), ("dropin", "")]
     out = {}
     for graph, limit in (("c1", limit_c1), ("c3chk", limit_c3), ("c3set", limit_c3)):
-        for burst in (1, 32):
+        for burst in bursts:
             for mode, extra in variants:
                 key = "%s/burst%d/%s%s" % (graph, burst, mode, ("/" + extra.replace(" ", "")) if extra else "")
                 runs = [run_one(mode, graph, extra, limit, burst) for _ in range(reps)]
@@ -130,10 +130,11 @@ if __name__ == "__main__":
     ap.add_argument("--limit", type=int, default=6000000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out")
+    ap.add_argument("--bursts", default="1,32")
     ap.add_argument("--variants", default="cpu:;dropin:;dropin:LATENCY 20;dropin:BATCH 1024;dropin:BATCH 32768, LATENCY 50;dropin:CHAIN false, LATENCY 20")
     a = ap.parse_args()
     v = [tuple(x.split(":", 1)) for x in a.variants.split(";")]
-    res = sweep(a.limit, a.limit // 3, a.reps, v)
+    res = sweep(a.limit, a.limit // 3, a.reps, v, tuple(int(b) for b in a.bursts.split(",")))
     if a.out:
         with open(a.out, "w") as f:
             json.dump(res, f, indent=1)

@@ -12,6 +12,9 @@
 #                                         (--enable-skip-elements of the CPU ones)
 #   tools/click_scratch_build.sh parity   CPU classes + HIP-prefixed GPU classes
 #                                         (ComparePackets graphs)
+#   tools/click_scratch_build.sh dropin-pg  the drop-in compiled with -pg (gprof's
+#                                         samples of Click and the adapter; the
+#                                         glue library is not sampled), symbols kept
 #
 # Trees go to $CLICK_SCRATCH/<mode> (default /tmp/clickbuild); each build's
 # `click` is stripped and copied to click_integration/bin/click-<mode>
@@ -25,9 +28,18 @@ SCRATCH=${CLICK_SCRATCH:-/tmp/clickbuild}
 JOBS=${JOBS:-8}
 DROPIN_SKIP=CheckIPHeader,CheckIPHeader2,SetIPChecksum,CheckUDPHeader,SetUDPChecksum,CheckTCPHeader,SetTCPChecksum,CheckICMPHeader,DecIPTTL,IPInputCombo,IPGWOptions,FixIPSrc,IPOutputCombo,IPFragmenter,HIPParity
 
+pg=()
 case "$mode" in
 cpu) extra=() ;;
 dropin) extra=(--enable-hip "--enable-skip-elements=$DROPIN_SKIP") ;;
+dropin-pg) extra=(--enable-hip "--enable-skip-elements=$DROPIN_SKIP"); pg=(CXXFLAGS="-g -O2 -pg" CFLAGS="-g -O2 -pg") ;;
+dropin-prof)
+    # the drop-in with tools/core_profile/preload_sampler.c linked in: with
+    # SAMPLES=file it samples the main thread's PC (its own CPU-time timer,
+    # so HIP's threads do not take the signals, as they take gprof's)
+    extra=(--enable-hip "--enable-skip-elements=$DROPIN_SKIP")
+    gcc -O2 -c "$REPO/tools/core_profile/preload_sampler.c" -o "$SCRATCH/sampler.o"
+    pg=(LIBS="$SCRATCH/sampler.o -ldl -lrt") ;;
 parity) extra=(--enable-hip --enable-skip-elements=HIPCheckIPHeader) ;;
 *) echo "unknown mode $mode" >&2; exit 2 ;;
 esac
@@ -45,11 +57,15 @@ cd "$tree"
 {
     echo "== configure ($mode)"
     ./configure --disable-linuxmodule --disable-bsdmodule --enable-userlevel --disable-dynamic-linking \
-        "${extra[@]}" CPPFLAGS="-I$REPO/include" \
-        LDFLAGS="-L$REPO/click_amd -L/opt/rocm/lib -Wl,-rpath,/root/repo/click_amd -Wl,-rpath,/opt/rocm/lib"
+        "${extra[@]}" "${pg[@]}" CPPFLAGS="-I$REPO/include" \
+        LDFLAGS="$([ "$mode" = dropin-pg ] && echo "-pg ")-L$REPO/click_amd -L/opt/rocm/lib -Wl,-rpath,/root/repo/click_amd -Wl,-rpath,/opt/rocm/lib"
     echo "== make"
     make -j"$JOBS"
 } > "$log" 2>&1 || { tail -40 "$log"; exit 1; }
 mkdir -p "$REPO/click_integration/bin"
-strip -o "$REPO/click_integration/bin/click-$mode" userlevel/click
+if [ "$mode" = dropin-pg ] || [ "$mode" = dropin-prof ]; then
+    strip --strip-debug -o "$REPO/click_integration/bin/click-$mode" userlevel/click
+else
+    strip -o "$REPO/click_integration/bin/click-$mode" userlevel/click
+fi
 echo "$REPO/click_integration/bin/click-$mode"

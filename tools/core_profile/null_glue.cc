@@ -66,6 +66,10 @@ int clk_element_flush_async(clk_element *e) { return flush_all(e); }
 uint64_t clk_element_abandon(clk_element *) { return 0; }
 int clk_element_share_messages(clk_element *, const clk_element *) { return CLK_SUCCESS; }
 int clk_element_hold_packets(clk_element *, int) { return CLK_SUCCESS; }
+int clk_element_push_th(clk_element *e, uint8_t *d, uint32_t length, int32_t nh, int32_t, uint32_t a, uint64_t token)
+{
+    return clk_element_push_anno(e, d, length, nh, a, token);
+}
 int clk_element_check_config(const char *, const char *, const char *, int) { return CLK_SUCCESS; }
 uint64_t clk_element_results_aux(clk_element *e, uint64_t *tok, int32_t *port, uint32_t *len, uint32_t *aux,
                                  uint64_t cap)
