@@ -299,9 +299,6 @@ constexpr int FRAG_U = CLK_FRAG_U;       // 16 B payload loads in flight per lan
 #ifndef CLK_FRAG_WPE
 #define CLK_FRAG_WPE 4
 #endif
-#ifndef CLK_FRAG_SPLIT
-#define CLK_FRAG_SPLIT 0    // fused: headers / descriptors in one pass over the tile, payloads in a second
-#endif
 
 // Header dword gl (< 15) of a packet, 0 past caplen: the prefetch of the
 // next fragmenting packet's header (port 2 implies caplen > mtu >= hlen + 8).
@@ -699,19 +696,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
                 if (FUSED && CLK_FRAG_PRO && lhdr[j][0] != 0u)
                     frag_restore_header(ip, lhdr[j]);
                 (FUSED ? lb.out_port : (uint8_t *)port)[i] = FRAG_PORT_NOROOM;
-#if CLK_FRAG_SPLIT
-                if (FUSED && CLK_FRAG_PRO)
-                    lhdr[j][0] = 0u;                    // no payload pass for it
-#endif
             }
             j = jn;
             continue;
         }
-#if CLK_FRAG_SPLIT
-        constexpr bool split = FUSED && CLK_FRAG_PRO;
-#else
-        constexpr bool split = false;
-#endif
         // payload offsets are relative to ip (32-bit): fragment k's payload
         // starts at pay0 + k * step and ends at min(that + dlen_k, caplen)
         const uint32_t pay0 = hlen + (uint32_t)first_dlen;
@@ -766,17 +754,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
 #if CLK_FRAG_HDR_FIRST
         write_headers();
 #endif
-        if (split) {
-            // headers and descriptors now; the payload in the second pass,
-            // from the plan kept in this packet's (no longer needed) lhdr row
-            write_headers();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();            // every lane read lhdr[j] (write_headers)
-            if (gl == 0)
-                lhdr[split ? j : 0][0] = nextra ? (hlen | out_hlen << 8 | (uint32_t)rem << 16) : 0u;
-            j = jn;
-            continue;
-        }
         uint32_t ck = 0, cc = gl;                          // this lane's next (fragment, chunk)
         for (uint32_t c0 = 0; c0 == 0 || c0 < total; c0 += FRAG_G * FRAG_U) {
             u32x4 v[FRAG_U];
@@ -826,66 +803,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
         }
         j = jn;
     }
-#if CLK_FRAG_SPLIT
-    if (FUSED && CLK_FRAG_PRO) {
-        // second pass: the payloads.  Every fragment of these packets fits
-        // (the first pass marked the others CLK_FRAG_NOROOM and kept 0):
-        // per packet a fixed shape -- U 16 B loads per lane, then their
-        // stores -- with no header, descriptor or bounds store in between.
-        __syncthreads();                                // every packet's plan is in lhdr
-        for (uint32_t jj = next_j(grp); jj < lim; jj = next_j(jj + NG)) {
-            const uint32_t pp = lhdr[jj][0];
-            if (!pp)
-                continue;
-            const uint32_t hlen = pp & 0xFF, out_hlen = (pp >> 8) & 0xFF, rem = pp >> 16;
-            const uint32_t pay0 = hlen + ((f.mtu - hlen) & ~7u);
-            const uint32_t step = (f.mtu - out_hlen) & ~7u;
-            const uint32_t nextra = (rem + step - 1) / step;
-            const uint32_t last = rem - (nextra - 1) * step;
-            const uint32_t slot_f = slot16(out_hlen + step);
-            const uint32_t nch_f = (step + 15) / 16, nch_l = (last + 15) / 16;
-            const uint32_t total = (nextra - 1) * nch_f + nch_l;
-            const uint64_t i = tile + jj;
-            const uint8_t *ip = b.base + pkt_off(b, i);
-            const uint32_t caplen = pkt_len(b, i);
-            uint8_t *dst0 = f.arena + bbase + pb[jj] + out_hlen;
-            uint32_t ck = 0, cc = gl;
-            for (uint32_t c0 = 0; c0 < total; c0 += FRAG_G * FRAG_U) {
-                u32x4 v[FRAG_U];
-                uint32_t vat[FRAG_U], vend[FRAG_U];    // store offset from dst0 (~0u: none), its slot's end
-#pragma unroll
-                for (int u = 0; u < FRAG_U; u++) {
-                    while (ck + 1 < nextra && cc >= nch_f) {
-                        cc -= nch_f;
-                        ck++;
-                    }
-                    const bool ok = cc < (ck + 1 < nextra ? nch_f : nch_l);
-                    const uint32_t dlen = ck + 1 < nextra ? step : last;
-                    const uint32_t fs = pay0 + ck * step, fe = fs + dlen;
-                    v[u] = ok ? load16_rel(ip, fs + 16 * cc, fe < caplen ? fe : caplen) : u32x4{0, 0, 0, 0};
-                    vat[u] = ok ? ck * slot_f + 16 * cc : 0xFFFFFFFFu;
-                    vend[u] = ck * slot_f + slot16(out_hlen + dlen) - out_hlen;
-                    cc += FRAG_G;
-                }
-#pragma unroll
-                for (int u = 0; u < FRAG_U; u++) {
-                    const uint32_t at = vat[u];
-                    if (at == 0xFFFFFFFFu)
-                        continue;
-                    uint8_t *q = dst0 + at;
-                    if (at + 16 <= vend[u]) {
-                        *(__attribute__((address_space(1))) u32x4_a4 *)q = v[u];
-                    } else {
-#pragma unroll
-                        for (int d = 0; d < 4; d++)
-                            if (at + 4 * d < vend[u])
-                                st_u32(q + 4 * d, v[u][d]);
-                    }
-                }
-            }
-        }
-    }
-#endif
 }
 
 } // namespace clk

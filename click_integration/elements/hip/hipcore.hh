@@ -671,6 +671,10 @@ template <class P, class Host, class L> class Core {
                 t.leave();
                 deliver_chunk(h, t, c, 0, pull_ctx, last, ready);
                 t.enter();
+                if (!ready.empty()) {            // (pull context: queued now, whatever ends the loop)
+                    t.ready.insert(t.ready.end(), ready.begin(), ready.end());
+                    ready.clear();
+                }
                 continue;
             }
             if (!t.unrouted || !t.e)

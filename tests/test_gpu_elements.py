@@ -427,7 +427,8 @@ def test_transport_header_annotation_zerocopy_refused(ctx):
     from click_amd.elements import Element
     pkt = np.zeros(64, np.uint8)
     oracle_lib.gen(pkt, 1, stride=64, fixed_len=60, proto=17)
+    pkt[0] = 0x44                                    # ip_hl 4 written after the header was marked at 20
     e = Element(ctx, "CheckUDPHeader", "ZEROCOPY true", noutputs=2)
-    assert e.push_th(pkt.ctypes.data, 60, 0, 24, token=0) < 0
+    assert e.push_th(pkt.ctypes.data, 60, 0, 20, token=0) < 0
     assert "annotation" in e.last_error()
     e.close()

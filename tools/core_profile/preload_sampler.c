@@ -3,7 +3,7 @@
  * do not rebuild (Click's userlevel driver over the null glue).
  *   gcc -O2 -shared -fPIC preload_sampler.c -o /tmp/sampler.so -ldl -lrt
  *   SAMPLES=/tmp/s.txt LD_PRELOAD=/tmp/sampler.so click ...
- * One line per sample of the main thread (every 20 us of CPU time): the
+ * One line per sample of the main thread (every 50 us of wall time): the
  * object file and the PC's offset in it; tools/core_profile/fold.py turns
  * them into functions. */
 #define _GNU_SOURCE
@@ -41,8 +41,10 @@ __attribute__((constructor)) static void arm(void)
     ev.sigev_signo = SIGPROF;
     ev._sigev_un._tid = (pid_t)syscall(SYS_gettid);
     timer_t tm;
-    if (timer_create(CLOCK_THREAD_CPUTIME_ID, &ev, &tm) == 0) {
-        struct itimerspec its = {{0, 20000}, {0, 20000}};
+    /* wall-clock ticks (a thread CPU-time timer ticks at the scheduler's
+       granularity): a sample while the thread waits shows where it waits */
+    if (timer_create(CLOCK_MONOTONIC, &ev, &tm) == 0) {
+        struct itimerspec its = {{0, 50000}, {0, 50000}};
         timer_settime(tm, 0, &its, NULL);
     }
 }
@@ -53,7 +55,7 @@ __attribute__((destructor)) static void dump(void)
     if (!path)
         return;
     signal(SIGPROF, SIG_IGN);
-    FILE *f = fopen(path, "w");
+    FILE *f = fopen(path, "a");              /* (a program may link it twice) */
     if (!f)
         return;
     for (size_t k = 0; k < npc; k++) {

@@ -83,12 +83,7 @@ VARIANTS = {
     "ch4": ([], {"set_chunks": 4}),
     "ch8": ([], {"set_chunks": 8}),
     "ch16": ([], {"set_chunks": 16}),
-    "fsplit": (["-DCLK_FRAG_SPLIT=1"], {}),
-    "fsplit5": (["-DCLK_FRAG_SPLIT=1", "-DCLK_FRAG_WPE=5"], {}),
-    "fsplit6": (["-DCLK_FRAG_SPLIT=1", "-DCLK_FRAG_WPE=6"], {}),
     "fw5": (["-DCLK_FRAG_WPE=5"], {}),
-    "fsplit5u2": (["-DCLK_FRAG_SPLIT=1", "-DCLK_FRAG_WPE=5", "-DCLK_FRAG_U=2"], {}),
-    "fsplit5u8": (["-DCLK_FRAG_SPLIT=1", "-DCLK_FRAG_WPE=5", "-DCLK_FRAG_U=8"], {}),
     "fw5u2": (["-DCLK_FRAG_WPE=5", "-DCLK_FRAG_U=2"], {}),
     "fu2": (["-DCLK_FRAG_U=2"], {}),
     "fg32": (["-DCLK_FRAG_G=32"], {}),
