@@ -436,6 +436,44 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
             "note": "kernel time (one plan + look-back + write launch, after a small memset); first-fragment headers restored between steps"}
 
 
+COPY_SHAPES = {0: "gs4_ntst_8k", 1: "gs8_ntst_8k", 2: "gs4_st_8k", 3: "gs8_st_16k"}
+
+
+def copy_stream_peak(torch, ctx, nbytes=4 << 30, reps=3, launches=5, rounds=2):
+    """Measured HBM copy ceiling (clk_copy_stream): `nbytes` copied between
+    two device buffers, 16 B nontemporal loads, 4 or 8 in flight per lane,
+    nontemporal or plain stores, capped grids -- the traffic of equal read
+    and write streams (the fragmenter's); and shape 4, the IMIX Set's own
+    pattern without its arithmetic (the stream read once, one 64 B block in
+    six written back in place).  GB/s of read + written bytes, best of
+    `reps` x `launches`, the shapes in turn for `rounds` rounds.  Returns
+    ({shape: GB/s}, the best copy shape's GB/s, the Set pattern's GB/s)."""
+    src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    src.fill_(3)
+    dst.fill_(0)
+    out = torch.zeros(1, dtype=torch.int64, device="cuda")
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    names = dict(COPY_SHAPES, **{4: "set_blocks_1in6"})
+    best = {name: 1e30 for name in names.values()}
+    for _ in range(rounds):
+        for shape, name in names.items():
+            ctx.copy_stream(dst, src, shape=shape, out=out)
+            torch.cuda.synchronize()
+            for _ in range(reps):
+                s.record()
+                for _ in range(launches):
+                    ctx.copy_stream(dst, src, shape=shape, out=out)
+                e.record()
+                torch.cuda.synchronize()
+                best[name] = min(best[name], s.elapsed_time(e) / launches)
+    moved = {name: (2 * nbytes if shape < 4 else nbytes + (nbytes // 64 + 5) // 6 * 64) for shape, name in names.items()}
+    rates = {name: round(moved[name] / (ms * 1e-3) / 1e9, 1) for name, ms in best.items()}
+    del src, dst
+    torch.cuda.empty_cache()
+    return rates, max(rates[n] for n in COPY_SHAPES.values()), rates["set_blocks_1in6"]
+
+
 READ_SHAPES = {0: "gs8_nt_8k", 1: "gs4_nt_8k", 2: "gs16_nt_2k", 3: "wave8_nt_4k", 4: "rows1536_nt",
                5: "rows1536_nt_8k"}
 
@@ -1274,6 +1312,7 @@ def main():
                                   coll_dev=coll_dev)
     peak_shapes = {}
     peak_meas = None if args.no_peak else read_stream_peak(torch, ctx, detail=peak_shapes)
+    copy_meas = None if args.no_peak else copy_stream_peak(torch, ctx)
     c1 = None
     if rank == 0 and world == 1 and not args.no_c1:
         c1 = config1(ctx)
@@ -1307,6 +1346,11 @@ def main():
         # frac is against the 8 TB/s spec; this one against the read ceiling
         # measured in the same run (read_stream_kernel: the best probe shape)
         hs["roofline"]["frac_of_measured_read"] = round(hs["roofline"]["achieved"] / peak_meas, 4) if peak_meas else None
+        if copy_meas:
+            # the ceilings of the read+write kernels (IPFragmenter, the IMIX
+            # Set): a copy of equal streams, and the Set's own block pattern
+            hs["roofline"]["copy_stream_measured_GBs"] = copy_meas[1]
+            hs["roofline"]["copy_stream_shapes_GBs"] = copy_meas[0]
         line = {
             "metric": METRIC, "value": hs["value"], "unit": "GiB/s", "mpps": hs["mpps"],
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -1334,7 +1378,13 @@ def main():
         for sect, (wl, res) in extra.items():
             line[sect] = {"workload": WORKLOADS[wl]["desc"],
                           "elements": {e: summarize(r, args.steps, wl) for e, r in res.items()}}
+            if copy_meas and wl == "c4":
+                for e, r in line[sect]["elements"].items():
+                    if e.startswith("Set"):            # against the measured read + one-block-in-six pattern
+                        r["roofline"]["frac_of_set_pattern"] = round(r["roofline"]["achieved"] / copy_meas[2], 4)
         if frag:
+            if copy_meas:
+                frag["roofline"]["frac_of_measured_copy"] = round(frag["roofline"]["achieved"] / copy_meas[1], 4)
             line["fragmenter"] = frag
         if c1:
             line["c1_fake_iprouter"] = c1

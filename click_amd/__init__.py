@@ -381,6 +381,16 @@ class Context:
             self._check(self.lib.clk_gen_corrupt_span(self.h, ctypes.byref(cb), seed, first_idx or 0, rate_log2,
                                                       0xFFFFFFFF if lo is None else lo, hi))
 
+    def copy_stream(self, dst, src, shape=0, nbytes=None, out=None):
+        """clk_copy_stream (bench: the copy ceiling; shape 4 the IMIX Set's
+        read-all, write-one-block-in-six pattern, in place on src)."""
+        if out is None:
+            out = self._torch.zeros(1, dtype=self._torch.int64, device="cuda:%d" % self.device)
+        nbytes = src.numel() * src.element_size() if nbytes is None else nbytes
+        self._check(self.lib.clk_copy_stream(self.h, _ptr(dst) if dst is not None else None, _ptr(src), nbytes, shape,
+                                             _ptr(out)))
+        return out
+
     def read_stream(self, t, nbytes=None, out=None):
         if out is None:
             out = self._torch.zeros(1, dtype=self._torch.int64, device="cuda:%d" % self.device)

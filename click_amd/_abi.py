@@ -155,6 +155,7 @@ SIGNATURES = {
     "clk_gen_corrupt_span": (ctypes.c_int, [_P, _BP, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
                                             ctypes.c_uint32, ctypes.c_uint32]),
     "clk_read_stream": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P]),
+    "clk_copy_stream": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, ctypes.c_int, _P]),
     # include/click_amd_elements.h
     "clk_element_create": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                           ctypes.POINTER(_P)]),

@@ -909,4 +909,36 @@ int clk_read_stream(clk_ctx *ctx, const void *base, uint64_t bytes, uint64_t *ou
     return check_launch(ctx, "clk_read_stream");
 }
 
+int clk_copy_stream(clk_ctx *ctx, void *dst, const void *src, uint64_t bytes, int shape, uint64_t *out_sum)
+{
+    int r = enter(ctx);
+    if (r) return r;
+    if (!src || ((uint64_t)src & 15) || (shape < 4 && (!dst || ((uint64_t)dst & 15))) || (shape == 4 && !out_sum) ||
+        shape < 0 || shape > 4)
+        return fail(ctx, CLK_EINVAL, "clk_copy_stream: bad arguments");
+    const uint64_t n16 = bytes / 16;
+    if (n16 == 0) return CLK_SUCCESS;
+    const clk::u32x4 *s = (const clk::u32x4 *)src;
+    clk::u32x4 *d = (clk::u32x4 *)dst;
+    auto grid = [&](uint64_t cap, uint64_t per) { return (unsigned)std::min<uint64_t>(cap, std::max<uint64_t>(1, n16 / per)); };
+    switch (shape) {
+    case 0:
+        hipLaunchKernelGGL((clk::copy_stream_kernel<4, true>), dim3(grid(8192, 4 * BLOCK)), dim3(BLOCK), 0, ctx->cur, s, d, n16);
+        break;
+    case 1:
+        hipLaunchKernelGGL((clk::copy_stream_kernel<8, true>), dim3(grid(8192, 8 * BLOCK)), dim3(BLOCK), 0, ctx->cur, s, d, n16);
+        break;
+    case 2:
+        hipLaunchKernelGGL((clk::copy_stream_kernel<4, false>), dim3(grid(8192, 4 * BLOCK)), dim3(BLOCK), 0, ctx->cur, s, d, n16);
+        break;
+    case 3:
+        hipLaunchKernelGGL((clk::copy_stream_kernel<8, false>), dim3(grid(16384, 8 * BLOCK)), dim3(BLOCK), 0, ctx->cur, s, d, n16);
+        break;
+    default:    // the C4 Set pattern: read all, one 64 B block in six written back
+        hipLaunchKernelGGL(clk::read_write_blocks_kernel<8>, dim3(grid(8192, 8 * BLOCK)), dim3(BLOCK), 0, ctx->cur,
+                           (clk::u32x4 *)s, n16, 6u, (unsigned long long *)out_sum);
+    }
+    return check_launch(ctx, "clk_copy_stream");
+}
+
 } // extern "C"

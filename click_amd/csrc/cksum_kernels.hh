@@ -1960,4 +1960,62 @@ __global__ void __launch_bounds__(256) read_rows_kernel(const u32x4 *p, uint64_t
         atomicAdd(out, (unsigned long long)acc);
 }
 
+// The measured copy ceiling (bench only): grid-stride, U nontemporal 16 B
+// loads per lane in flight, then their U stores (NTS: nontemporal), on a
+// capped grid -- equal read and write streams, the fragmenter's traffic.
+template <int U, bool NTS>
+__global__ void __launch_bounds__(256) copy_stream_kernel(const u32x4 *src, u32x4 *dst, uint64_t n16)
+{
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (U - 1) * nthreads < n16; i += U * nthreads) {
+        u32x4 a[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            a[u] = __builtin_nontemporal_load(src + i + u * nthreads);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (NTS)
+                __builtin_nontemporal_store(a[u], dst + i + u * nthreads);
+            else
+                dst[i + u * nthreads] = a[u];
+        }
+    }
+    for (; i < n16; i += nthreads)
+        dst[i] = src[i];
+}
+
+// ... and the IMIX Set's traffic without its arithmetic: the stream read as
+// read_stream_kernel<U> reads it, and one whole 64 B block in every `every`
+// written back in place (nontemporal; C4 SetUDPChecksum writes the block
+// holding each packet's field, one per 354 B on average)
+template <int U>
+__global__ void __launch_bounds__(256) read_write_blocks_kernel(u32x4 *p, uint64_t n16, uint32_t every,
+                                                                unsigned long long *out)
+{
+    const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t acc = 0;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + (U - 1) * nthreads < n16; i += U * nthreads) {
+        u32x4 a[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            a[u] = __builtin_nontemporal_load(p + i + u * nthreads);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            acc += a[u][0] ^ a[u][1] ^ a[u][2] ^ a[u][3];
+            if (((i + u * nthreads) >> 2) % every == 0)
+                __builtin_nontemporal_store(a[u], p + i + u * nthreads);
+        }
+    }
+    for (; i < n16; i += nthreads) {
+        const u32x4 a0 = p[i];
+        acc += a0[0] ^ a0[1] ^ a0[2] ^ a0[3];
+    }
+    for (int m = 32; m >= 1; m >>= 1)
+        acc += __shfl_xor(acc, m, 64);
+    if ((threadIdx.x & 63) == 0 && acc)
+        atomicAdd(out, (unsigned long long)acc);
+}
+
 } // namespace clk

@@ -391,6 +391,13 @@ int clk_gen_corrupt_span(clk_ctx *ctx, const clk_batch *batch, uint64_t seed, ui
  * measured HBM read-stream ceiling for the roofline (bench only).          */
 int clk_read_stream(clk_ctx *ctx, const void *base, uint64_t bytes, uint64_t *out_sum);
 
+/* The measured copy ceiling (bench only): `bytes` from device src to dst as
+ * 16-byte nontemporal loads, shape 0-3 = 4 / 8 loads in flight per lane,
+ * nontemporal / plain stores; shape 4 = the IMIX Set's traffic, src read
+ * once and one 64-byte block in six written back in place (dst unused,
+ * out_sum as clk_read_stream's).  16-byte aligned.                         */
+int clk_copy_stream(clk_ctx *ctx, void *dst, const void *src, uint64_t bytes, int shape, uint64_t *out_sum);
+
 #ifdef __cplusplus
 }
 #endif
