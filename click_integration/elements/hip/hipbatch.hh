@@ -75,7 +75,10 @@ struct ClickPacketOps {
  *   CHAIN    bool join the GPU-backed elements after this one into one batch
  *                 (default true; see Chains below)
  * Glue keywords passed through: BATCH (default here ADAPTER_BATCH = 8192,
- * where the glue's own default is 65536), ZEROCOPY, and the element's own.
+ * where the glue's own default is 65536; in push context a batch is
+ * launched after at most hipcore::Core::INFLIGHT = 8192 packets whatever
+ * BATCH, so that held packets stay in the host caches), ZEROCOPY, and the
+ * element's own.
  *
  * Threads (click -j N): one hipcore::State (context, glue element, held
  * packets) per RouterThread, chosen by click_current_cpu_id()
