@@ -310,7 +310,7 @@ inline int BatchElement::push_one(SpanF &&span_f, uint8_t *data, uint32_t length
     if (reads_th_ && th_offset != -1 && nh_offset >= 0 && (uint32_t)nh_offset < length &&
         th_offset != nh_offset + (int32_t)((data[nh_offset] & 15u) << 2)) {
         const int r = push_irregular(p, th_offset);
-        if (r != ~0)
+        if (r != NOT_IRREGULAR)
             return r;
     }
     uint32_t off = 0, len = 0;
@@ -400,7 +400,7 @@ int BatchElement::push(uint8_t *data, uint32_t length, int32_t nh_offset, uint64
 
 int BatchElement::push_irregular(Pending &, int32_t)
 {
-    return ~0;
+    return NOT_IRREGULAR;
 }
 
 // A packet decided on the host (as span() returning false)
@@ -1240,7 +1240,7 @@ int CheckL4Header::push_irregular(Pending &p, int32_t th_off)
 {
     const uint32_t L = p.length, nh = (uint32_t)p.nh_off;
     if (th_off < 0 || nh + 20 > L)
-        return ~0;                                    // as a packet without the annotation / too short
+        return NOT_IRREGULAR;                         // as a packet without the annotation / too short
     const uint8_t *iph = p.data + nh, *th = p.data + th_off;
     const uint32_t th_u = (uint32_t)th_off, hl = (iph[0] & 15u) << 2;
     uint8_t ip20[20];
@@ -1336,7 +1336,7 @@ int SetL4Checksum::push_irregular(Pending &p, int32_t th_off)
     if (th_off == -2 && proto_ == 6)                            // !has_transport_header() (settcpchecksum.cc:53)
         return host_decided(p, CLK_SET_KILL);
     if (th_off < 0 || nh + 20 > L)
-        return ~0;
+        return NOT_IRREGULAR;
     const uint8_t *iph = p.data + nh, *th = p.data + th_off;
     const uint32_t th_u = (uint32_t)th_off, hl = (iph[0] & 15u) << 2;
     const uint32_t tlen = th_u <= L ? L - th_u : 0;              // transport_length() (< 0: too short)

@@ -536,7 +536,8 @@ class alignas(128) BatchElement {
     // from the header and lengths, and the checksum runs on the GPU over a
     // canonical copy -- the IP header with ip_hl 5 and the pseudo-header's
     // destination (in_cksum.c:86-108) followed by the segment at the
-    // annotation (stage_canonical).  ~0: it is not irregular after all.
+    // annotation (stage_canonical).  NOT_IRREGULAR: handle it as any packet.
+    static constexpr int NOT_IRREGULAR = -1000;
     virtual int push_irregular(Pending &p, int32_t th_offset);
     int stage_canonical(Pending &p, const uint8_t *ip20, const uint8_t *seg, uint32_t seglen);
     int host_decided(Pending &p, int32_t code);

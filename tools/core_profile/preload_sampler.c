@@ -43,8 +43,13 @@ __attribute__((constructor)) static void arm(void)
     timer_t tm;
     /* wall-clock ticks (a thread CPU-time timer ticks at the scheduler's
        granularity): a sample while the thread waits shows where it waits */
+    /* SAMPLES_DELAY_MS (default 0): the first sample that long after start --
+       a program initialising HIP is left alone until then (a signal in the
+       middle of its first ioctls made the runtime report no device) */
+    const char *dl = getenv("SAMPLES_DELAY_MS");
+    const long delay_ms = dl ? atol(dl) : 0;
     if (timer_create(CLOCK_MONOTONIC, &ev, &tm) == 0) {
-        struct itimerspec its = {{0, 50000}, {0, 50000}};
+        struct itimerspec its = {{0, 50000}, {delay_ms / 1000, delay_ms % 1000 * 1000000 + (delay_ms ? 0 : 50000)}};
         timer_settime(tm, 0, &its, NULL);
     }
 }
