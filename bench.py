@@ -454,7 +454,7 @@ def copy_stream_peak(torch, ctx, nbytes=4 << 30, reps=3, launches=5, rounds=2):
     dst.fill_(0)
     out = torch.zeros(1, dtype=torch.int64, device="cuda")
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    names = dict(COPY_SHAPES, **{4: "set_blocks_1in6"})
+    names = {**COPY_SHAPES, 4: "set_blocks_1in6"}
     best = {name: 1e30 for name in names.values()}
     for _ in range(rounds):
         for shape, name in names.items():

@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <new>
+#include <malloc.h>
 CLICK_DECLS
 
 namespace {
@@ -158,6 +159,19 @@ HIPBatchElement::initialize(ErrorHandler *errh)
     // one state per RouterThread, driven by that thread alone (no lock:
     // hipcore State::shared), plus a locked catch-all state for a push from
     // a thread id past them
+    // A state holds up to three batches of packets (hipcore INFLIGHT), past
+    // what Click's packet pool keeps (packet.cc:238, 1000 per thread): the
+    // clones and copies beyond it come from malloc and go back with free,
+    // and glibc returned the heap's top to the kernel at every such free and
+    // took it back at the next malloc -- a third of the samples of a drop-in
+    // Click in malloc, free and brk (profiles/r06/click_samples_*_r06h.txt).
+    // Freed memory stays in the heap instead (once per process).
+    static bool heap_kept = false;
+    if (!heap_kept) {
+	mallopt(M_TRIM_THRESHOLD, 256 << 20);
+	mallopt(M_TOP_PAD, 64 << 20);
+	heap_kept = true;
+    }
     _npt = click_max_cpu_ids();
     _pt = new PerThread[_npt + 1];
     for (int k = 0; k < _npt; k++)

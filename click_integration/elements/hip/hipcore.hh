@@ -89,8 +89,10 @@
  *   void message(int m, const char *line)        member m's chatter lines from the glue
  *
  * Latency flush on the state's own thread: a state that holds packets has a
- * deadline (LATENCY after its batch started); poll(t), run by the thread's
- * Task, flushes and delivers once it has passed.  So every packet of thread
+ * deadline (LATENCY after its last flush); poll(t), run by the thread's
+ * Task, launches what was staged since (double-buffered) and delivers the
+ * batch before once it has passed, and at the next deadline with nothing
+ * new staged waits for the rest.  So every packet of thread
  * k is staged, flushed and pushed downstream on thread k (the reference's
  * per-thread model; a Timer would run on the element's home thread,
  * timer.cc:245-246).
@@ -316,7 +318,14 @@ template <class P, class Host, class L> class Core {
             t.leave();
             return true;
         }
-        flush(h, t, true);
+        // packets staged since the last flush: launch them and route the
+        // batch before (double-buffered, as a full batch); only what is
+        // already in flight: wait for it.  At rates under INFLIGHT packets
+        // per LATENCY the deadline, not a full batch, launches every batch,
+        // and a waiting flush each time stalled the thread on the GPU
+        // (Click, C3 CheckUDPHeader: a quarter of the samples in HIP's
+        // event wait, profiles/r06/click_samples_c3chk_r06h.txt)
+        flush(h, t, t.fresh == 0);
         t.leave();
         drain(h, t, false);
         t.enter();

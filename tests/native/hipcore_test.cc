@@ -500,7 +500,10 @@ void push_check_ip()
     CHECK(h.poll());                                   // before the deadline: nothing flushed
     CHECK(h.out[0].size() + h.out[1].size() == 1000);  // (batch 2 in flight, 500 staged)
     std::this_thread::sleep_for(std::chrono::milliseconds(210));
-    CHECK(!h.poll());                                  // past it: flushed, nothing left
+    CHECK(h.poll());                                   // past it: the 500 staged launched, batch 2 routed
+    CHECK(h.out[0].size() + h.out[1].size() == 2000 && h.runcount == 1);
+    std::this_thread::sleep_for(std::chrono::milliseconds(210));
+    CHECK(!h.poll());                                  // past the next, nothing new: the rest waited for
     CHECK(h.runcount == 0 && !h.armed());
     CHECK(h.out[0].size() + h.out[1].size() == (size_t)n);
     long last0 = -1, last1 = -1;

@@ -118,4 +118,4 @@ def test_dropin_config1_pcap_bytes(tmp_path):
         for k, (x, y) in enumerate(zip(a, b)):
             assert x == y, (o, k, x[:3], y[:3], x[3].hex(), y[3].hex())
         seen += len(a) > 0
-    assert seen >= 5
+    assert seen >= 4                                # forwarded, bad headers, option problems, TTLs
