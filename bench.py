@@ -1098,7 +1098,9 @@ def click_drop_in(reps=3, timeout=180):
     InfiniteSource BURST 1 and 32), c3chk = 1500 B UDP frames through
     CheckIPHeader -> CheckUDPHeader, c3set = SetUDPChecksum.  Mpps by the
     graph's AverageCounter, median of `reps` processes; x_cpu = drop-in /
-    stock.  Also the adapter core's C3 push legs (tests/native/pull_bench c3:
+    stock.  Both run with glibc's tcache deepened (click_perf.TCACHE: the
+    packets a GPU element holds outrun Click's 1000-packet pool, and freed
+    chunks then stay per-thread; the stock build's rate does not change).  Also the adapter core's C3 push legs (tests/native/pull_bench c3:
     staged and ZEROCOPY).  None if the binaries were not built."""
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     try:
@@ -1112,7 +1114,8 @@ def click_drop_in(reps=3, timeout=180):
     for graph, limit, burst in CLICK_LEGS:
         rec = {"packets": limit, "burst": burst}
         for mode in ("cpu", "dropin"):
-            runs = [click_perf.run_one(mode, graph, "", limit, burst, timeout=timeout) for _ in range(reps)]
+            runs = [click_perf.run_one(mode, graph, "", limit, burst, timeout=timeout, extra_env=click_perf.TCACHE)
+                    for _ in range(reps)]
             ok = sorted(r["mpps_counter"] for r in runs if "count" in r and r["count"] == limit)
             rec[mode] = round(ok[len(ok) // 2], 2) if len(ok) == reps else None
             rec[mode + "_runs"] = [round(r["mpps_counter"], 2) if "count" in r else r for r in runs]

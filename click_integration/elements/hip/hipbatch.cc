@@ -97,9 +97,9 @@ HIPBatchElement::configure(Vector<String> &conf, ErrorHandler *errh)
 	.consume() < 0)
 	return -1;
     // BATCH: the glue's (65536, sized for the device batch) unless given;
-    // the adapter's default is smaller, so a batch's packets stay in the
-    // host caches between staging and delivery (config 1
-    // through the core, 2.8 Mpps at 65536, 4.4 at 8192)
+    // the adapter's default is the core's in-flight cap, so a batch's
+    // packets stay in the host caches between staging and delivery
+    // (hipcore.hh Core::INFLIGHT; profiles/r06/click_batch_tcache_r06l.json)
     bool batch = false;
     for (int i = 0; i < conf.size(); i++) {
 	String w = cp_uncomment(conf[i]);

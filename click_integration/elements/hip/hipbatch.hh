@@ -74,9 +74,9 @@ struct ClickPacketOps {
  *                 (default 3)
  *   CHAIN    bool join the GPU-backed elements after this one into one batch
  *                 (default true; see Chains below)
- * Glue keywords passed through: BATCH (default here ADAPTER_BATCH = 8192,
+ * Glue keywords passed through: BATCH (default here ADAPTER_BATCH = 2048,
  * where the glue's own default is 65536; in push context a batch is
- * launched after at most hipcore::Core::INFLIGHT = 8192 packets whatever
+ * launched after at most hipcore::Core::INFLIGHT = 2048 packets whatever
  * BATCH, so that held packets stay in the host caches), ZEROCOPY, and the
  * element's own.
  *
@@ -121,7 +121,7 @@ struct ClickPush {
 
 class HIPBatchElement : public Element { public:
 
-    enum { ADAPTER_BATCH = 8192 };
+    enum { ADAPTER_BATCH = 2048 };	// = hipcore::Core::INFLIGHT
 
     typedef hipcore::State<Packet, Spinlock> PerThread;
     typedef hipcore::Routed<Packet> Routed;

@@ -270,11 +270,13 @@ template <class P, class Host, class L> class Core {
 
     // push context launches a batch once INFLIGHT packets are staged, whatever
     // BATCH: with two batches in flight and the one being staged, a state
-    // then holds at most 3 x INFLIGHT packets, whose Packet structures and
-    // the glue's per-packet records stay in the host caches between staging
-    // and delivery (Click config 1 through the core: BATCH 32768 ran at
-    // 0.55 x BATCH 8192, profiles/r06/click_batch_sweep_r06d.json)
-    enum { INFLIGHT = 8192 };
+    // then holds at most 3 x INFLIGHT packets, whose Packet structures, data
+    // and the glue's per-packet records stay in the host caches between
+    // staging and delivery.  In Click (profiles/r06/click_batch_tcache_r06l.json,
+    // Mpps at 512 / 1024 / 2048 / 4096 / 8192): C3 SetUDPChecksum 5.4 / 6.3 /
+    // 6.4 / 4.6 / 3.6 (its uniqueified copies), CheckUDPHeader 5.9 / 7.6 /
+    // 8.4 / 8.8 / 7.3, config 1 3.8 / 4.7 / 5.1 / 5.6 / 5.0
+    enum { INFLIGHT = 2048 };
 
     Core() : _batch(65536), _latency_ms(1), _max_retries(3) { }
 

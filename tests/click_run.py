@@ -20,14 +20,14 @@ def binary(mode):
     return p if os.access(p, os.X_OK) else None
 
 
-def env():
-    e = dict(os.environ)
+def env(extra=None):
+    e = dict(os.environ, **(extra or {}))
     libs = [os.path.join(ROOT, "click_amd"), "/opt/rocm/lib"]
     e["LD_LIBRARY_PATH"] = ":".join(libs + ([e["LD_LIBRARY_PATH"]] if e.get("LD_LIBRARY_PATH") else []))
     return e
 
 
-def run(mode, conf=None, defines=None, handlers=(), expr=None, timeout=300, cwd=None):
+def run(mode, conf=None, defines=None, handlers=(), expr=None, timeout=300, cwd=None, extra_env=None):
     """Run click-<mode> on a config file (or -e expr) with NAME=value
     defines; returns (returncode, {handler: text}, stderr)."""
     cmd = [binary(mode)]
@@ -39,7 +39,7 @@ def run(mode, conf=None, defines=None, handlers=(), expr=None, timeout=300, cwd=
         cmd.append("%s=%s" % (k, v))
     for h in handlers:
         cmd += ["-h", h]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env(), cwd=cwd)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env(extra_env), cwd=cwd)
     vals = {}
     # click -h prints "NAME:\nVALUE" blocks (one line values: "NAME: VALUE")
     lines = p.stdout.splitlines()

@@ -9,7 +9,7 @@
 // next batch and routes the one before, hipcore.hh).
 //   pull_bench [SCALE]     packet counts divided by SCALE
 //   pull_bench SCALE chain REPS   the push_c1 chain leg only, REPS times
-//                                 (BATCH 8192, the Click adapter's default)
+//                                 (BATCH 2048, the Click adapter's default)
 //   pull_bench SCALE pull         the pull legs only
 #include <algorithm>
 #include <x86intrin.h>
@@ -17,7 +17,7 @@
 
 namespace {
 
-const uint32_t ADAPTER_BATCH = 8192;                    // hipbatch.hh HIPBatchElement::ADAPTER_BATCH
+const uint32_t ADAPTER_BATCH = 2048;                    // hipbatch.hh HIPBatchElement::ADAPTER_BATCH
 
 uint16_t fold_sum(const uint8_t *b, uint32_t n, uint32_t acc)   // RFC 1071 over n bytes
 {

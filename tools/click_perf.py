@@ -85,7 +85,12 @@ def conf_text(graph):
     return c3_conf(graph)
 
 
-def run_one(mode, graph, extra="", limit=None, burst=None, timeout=180):
+# glibc's per-thread cache of freed chunks, deep enough for the packets a
+# GPU element holds (Click's own pool keeps 1000, packet.cc:238)
+TCACHE = {"GLIBC_TUNABLES": "glibc.malloc.tcache_count=65535"}
+
+
+def run_one(mode, graph, extra="", limit=None, burst=None, timeout=180, extra_env=None):
     text = conf_text(graph)
     if mode != "cpu":
         text = with_gpu_conf(text, extra)
@@ -98,7 +103,7 @@ def run_one(mode, graph, extra="", limit=None, burst=None, timeout=180):
     if burst:
         d["BURST"] = burst
     t0 = time.perf_counter()
-    rc, h, err = click_run.run(mode, path, d, ("out.count", "out.rate"), timeout=timeout)
+    rc, h, err = click_run.run(mode, path, d, ("out.count", "out.rate"), timeout=timeout, extra_env=extra_env)
     wall = time.perf_counter() - t0
     os.unlink(path)
     if rc != 0:
@@ -114,7 +119,9 @@ def sweep(limit_c1=6000000, limit_c3=2000000, reps=3, variants=None, bursts=(1, 
         for burst in bursts:
             for mode, extra in variants:
                 key = "%s/burst%d/%s%s" % (graph, burst, mode, ("/" + extra.replace(" ", "")) if extra else "")
-                runs = [run_one(mode, graph, extra, limit, burst) for _ in range(reps)]
+                ex = extra.replace("@tcache", "").strip(" ,")
+                runs = [run_one(mode, graph, ex, limit, burst, extra_env=TCACHE if "@tcache" in extra else None)
+                        for _ in range(reps)]
                 ok = [r for r in runs if "count" in r]
                 rec = {"runs": runs}
                 if ok:
