@@ -1105,11 +1105,13 @@ void converging_outputs(uint32_t batch)
     }
     ch.timer();
     // the contract: batch by batch (the flushes' batches: BATCH packets in
-    // push order), member 0's drops in push order, then member 3's
+    // push order, at most the core's in-flight cap), member 0's drops in
+    // push order, then member 3's
+    const uint32_t eb = std::min<uint32_t>(batch, (uint32_t)ChainHost::Core::INFLIGHT);
     std::vector<std::pair<int, long> > want, ref;
-    for (int b0 = 0; b0 < n; b0 += (int)batch)
+    for (int b0 = 0; b0 < n; b0 += (int)eb)
         for (int k : {0, 3})
-            for (int i = b0; i < n && i < b0 + (int)batch; i++)
+            for (int i = b0; i < n && i < b0 + (int)eb; i++)
                 if (drop_at[i] == k)
                     want.emplace_back(k, i);
     for (int i = 0; i < n; i++)                      // the reference's depth-first order
