@@ -436,7 +436,8 @@ def measure_fragmenter(torch, ctx, dist, rank, world, steps, warmup, mtu=576, se
             "note": "kernel time (one plan + look-back + write launch, after a small memset); first-fragment headers restored between steps"}
 
 
-COPY_SHAPES = {0: "gs4_ntst_8k", 1: "gs8_ntst_8k", 2: "gs4_st_8k", 3: "gs8_st_16k"}
+COPY_SHAPES = {0: "gs4_ntst_8k", 1: "gs8_ntst_8k", 2: "gs4_st_8k", 3: "gs8_st_16k", 5: "gs16_st_4k",
+               6: "wave8_st_4k", 7: "flat4_st"}
 
 
 def copy_stream_peak(torch, ctx, nbytes=4 << 30, reps=3, launches=5, rounds=2):
@@ -467,7 +468,7 @@ def copy_stream_peak(torch, ctx, nbytes=4 << 30, reps=3, launches=5, rounds=2):
                 e.record()
                 torch.cuda.synchronize()
                 best[name] = min(best[name], s.elapsed_time(e) / launches)
-    moved = {name: (2 * nbytes if shape < 4 else nbytes + (nbytes // 64 + 5) // 6 * 64) for shape, name in names.items()}
+    moved = {name: (2 * nbytes if shape != 4 else nbytes + (nbytes // 64 + 5) // 6 * 64) for shape, name in names.items()}
     rates = {name: round(moved[name] / (ms * 1e-3) / 1e9, 1) for name, ms in best.items()}
     del src, dst
     torch.cuda.empty_cache()
@@ -1037,13 +1038,16 @@ def config1_cpu(n=C1_PACKETS):
     (the byte-touching elements only; Click's scheduler, Classifier and
     queues are not part of it): CheckIPHeader + IPGWOptions + FixIPSrc +
     DecIPTTL + IPFragmenter(300), and IPInputCombo + IPOutputCombo.  The
-    thread is pinned to one core, the frames' arena and the flags are
-    allocated and first-touched there once, and the pristine frames are
-    copied back before each run, outside the clock (a fresh arena per run
-    left 22 or 40 Mpps to page placement, BENCH_r05); one warm-up, then
+    thread is pinned to one core; the frames' arena and every output array
+    are allocated and first-touched there once, outside the clock (oracle_lib's
+    helpers allocate per call, and the fragmenter helper copies the whole
+    arena for a sizing pass: BENCH_r05's 22-or-40 Mpps runs), and the
+    pristine frames are copied back before each run; one warm-up, then
     C1_RUNS timed runs: min / median / max."""
     import numpy as np
     from tests import oracle_lib
+    L = oracle_lib.load_oracle()
+    P = oracle_lib._np_ptr
     frame = c1_frame()
     fl = len(frame)
     prev = os.sched_getaffinity(0)
@@ -1053,26 +1057,42 @@ def config1_cpu(n=C1_PACKETS):
         pristine = np.tile(np.frombuffer(frame, np.uint8), n)
         arena = np.empty_like(pristine)
         arena[:] = pristine                        # first touch on the pinned core
-        flags = np.zeros(n, np.uint8)
         l3 = arena[14:]
+        flags = np.zeros(n, np.uint8)
+        codes, c2, port, prob = (np.zeros(n, np.uint8) for _ in range(4))
+        sums = np.zeros(n, np.uint16)
+        first = np.zeros(n, np.uint32)
+        ffirst = np.zeros(n, np.uint64)
+        totals = np.zeros(2, np.uint64)
+        fcap = 4 * n                               # room for the fragments (fake-iprouter's frames make none)
+        fout = np.zeros(fcap * 64, np.uint8)
+        foff, flen, fsrc = np.zeros(fcap, np.uint64), np.zeros(fcap, np.uint32), np.zeros(fcap, np.uint32)
+        ops, iops = oracle_lib.OPS, oracle_lib.IP_OUT_OPS
+        stride, flen3, my_ip = fl, fl - 14, 0x18041A12
+
+        def out_op(op, fl_=None, mtu=0xFFFFFFFF, dst=codes):
+            assert L.oracle_ip_out_batch(iops[op], P(l3), None, stride, None, flen3, n, P(fl_), my_ip, None, 0, 0,
+                                         mtu, P(dst), P(prob), P(sums)) == 0
+
         res = {}
         for name in ("elements", "combos"):
             walls = []
             for run in range(1 + C1_RUNS):
                 np.copyto(arena, pristine)
                 t0 = time.perf_counter()
-                codes, _ = oracle_lib.batch("check_ip", l3, n, stride=fl, fixed_len=fl - 14)
+                assert L.oracle_batch(ops["check_ip"], P(l3), None, stride, None, flen3, n, 1, P(codes), P(sums)) == 0
                 if name == "elements":
-                    oracle_lib.ip_out_batch("ip_gw_options", l3, n, stride=fl, fixed_len=fl - 14, my_ip=0x18041A12)
-                    oracle_lib.ip_out_batch("fix_ip_src", l3, n, stride=fl, fixed_len=fl - 14, my_ip=0x18041A12,
-                                            flags=flags)
-                    c2, _ = oracle_lib.batch("dec_ttl", l3, n, stride=fl, fixed_len=fl - 14)
-                    fr = oracle_lib.ip_fragment(l3, n, 300, False, stride=fl, fixed_len=fl - 14)
-                    fwd = int(((codes == 0) & (c2 == 0) & (fr["port"] == 0)).sum())
+                    ok = codes == 0
+                    out_op("ip_gw_options", dst=port)
+                    out_op("fix_ip_src", fl_=flags, dst=port)
+                    assert L.oracle_batch(ops["dec_ttl"], P(l3), None, stride, None, flen3, n, 1, P(c2), P(sums)) == 0
+                    L.oracle_ip_fragment_batch(P(l3), None, stride, None, flen3, n, 300, 0, None, P(port), P(first),
+                                               P(ffirst), P(fout), P(foff), P(flen), P(fsrc), P(totals))
+                    fwd = int((ok & (c2 == 0) & (port == 0)).sum())
                 else:
-                    port, _, _ = oracle_lib.ip_out_batch("ip_output_combo", l3, n, stride=fl, fixed_len=fl - 14,
-                                                         my_ip=0x18041A12, mtu=300)
-                    fwd = int(((codes == 0) & (port == 0)).sum())
+                    ok = codes == 0
+                    out_op("ip_output_combo", mtu=300, dst=port)
+                    fwd = int((ok & (port == 0)).sum())
                 if run:
                     walls.append(time.perf_counter() - t0)
             dt = c1_median(walls)
@@ -1082,8 +1102,8 @@ def config1_cpu(n=C1_PACKETS):
     finally:
         os.sched_setaffinity(0, prev)
     return {"threads": 1, "kind": "port", "runs": C1_RUNS, "pinned_cpu": core, **res,
-            "note": "oracle restatement of the byte-touching elements, one pinned host thread, arena allocated and "
-                    "first-touched once; Click's own runtime on the same graph: drop_in.c1 (click-cpu)"}
+            "note": "oracle restatement of the byte-touching elements, one pinned host thread, every buffer allocated "
+                    "and first-touched once; Click's own runtime on the same graph: drop_in.c1 (click-cpu)"}
 
 
 CLICK_LEGS = (("c1", 3000000, 1), ("c1", 3000000, 32), ("c3chk", 1000000, 32), ("c3set", 1000000, 32))

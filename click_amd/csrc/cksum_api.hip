@@ -913,8 +913,8 @@ int clk_copy_stream(clk_ctx *ctx, void *dst, const void *src, uint64_t bytes, in
 {
     int r = enter(ctx);
     if (r) return r;
-    if (!src || ((uint64_t)src & 15) || (shape < 4 && (!dst || ((uint64_t)dst & 15))) || (shape == 4 && !out_sum) ||
-        shape < 0 || shape > 4)
+    if (!src || ((uint64_t)src & 15) || (shape != 4 && (!dst || ((uint64_t)dst & 15))) || (shape == 4 && !out_sum) ||
+        shape < 0 || shape > 7)
         return fail(ctx, CLK_EINVAL, "clk_copy_stream: bad arguments");
     const uint64_t n16 = bytes / 16;
     if (n16 == 0) return CLK_SUCCESS;
@@ -933,6 +933,15 @@ int clk_copy_stream(clk_ctx *ctx, void *dst, const void *src, uint64_t bytes, in
         break;
     case 3:
         hipLaunchKernelGGL((clk::copy_stream_kernel<8, false>), dim3(grid(16384, 8 * BLOCK)), dim3(BLOCK), 0, ctx->cur, s, d, n16);
+        break;
+    case 5:
+        hipLaunchKernelGGL((clk::copy_stream_kernel<16, false>), dim3(grid(4096, 16 * BLOCK)), dim3(BLOCK), 0, ctx->cur, s, d, n16);
+        break;
+    case 6:
+        hipLaunchKernelGGL(clk::copy_wave_kernel<8>, dim3(grid(4096, 8 * BLOCK)), dim3(BLOCK), 0, ctx->cur, s, d, n16);
+        break;
+    case 7:     // one step per thread: the grid covers the buffer
+        hipLaunchKernelGGL((clk::copy_stream_kernel<4, false>), dim3(grid(1u << 30, 4 * BLOCK)), dim3(BLOCK), 0, ctx->cur, s, d, n16);
         break;
     default:    // the C4 Set pattern: read all, one 64 B block in six written back
         hipLaunchKernelGGL(clk::read_write_blocks_kernel<8>, dim3(grid(8192, 8 * BLOCK)), dim3(BLOCK), 0, ctx->cur,

@@ -1985,6 +1985,30 @@ __global__ void __launch_bounds__(256) copy_stream_kernel(const u32x4 *src, u32x
         dst[i] = src[i];
 }
 
+// ... each wave copying U KiB contiguous per step (lane l: 16 B at l*16 +
+// u*1 KiB), the steps dealt round-robin to the waves; the tail grid-strided
+template <int U>
+__global__ void __launch_bounds__(256) copy_wave_kernel(const u32x4 *src, u32x4 *dst, uint64_t n16)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    const uint64_t w0 = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const uint64_t nsteps = n16 / (64 * U);
+    for (uint64_t s = w0; s < nsteps; s += nwaves) {
+        const uint64_t q = s * 64 * U + lane;
+        u32x4 a[U];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            a[u] = __builtin_nontemporal_load(src + q + 64 * u);
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            dst[q + 64 * u] = a[u];
+    }
+    for (uint64_t i = nsteps * 64 * U + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[i];
+}
+
 // ... and the IMIX Set's traffic without its arithmetic: the stream read as
 // read_stream_kernel<U> reads it, and one whole 64 B block in every `every`
 // written back in place (nontemporal; C4 SetUDPChecksum writes the block

@@ -393,9 +393,11 @@ int clk_read_stream(clk_ctx *ctx, const void *base, uint64_t bytes, uint64_t *ou
 
 /* The measured copy ceiling (bench only): `bytes` from device src to dst as
  * 16-byte nontemporal loads, shape 0-3 = 4 / 8 loads in flight per lane,
- * nontemporal / plain stores; shape 4 = the IMIX Set's traffic, src read
- * once and one 64-byte block in six written back in place (dst unused,
- * out_sum as clk_read_stream's).  16-byte aligned.                         */
+ * nontemporal / plain stores; 5 = 16 in flight, plain; 6 = each wave 8 KiB
+ * contiguous per step; 7 = one step per thread over a grid covering the
+ * buffer; shape 4 = the IMIX Set's traffic, src read once and one 64-byte
+ * block in six written back in place (dst unused, out_sum as
+ * clk_read_stream's).  16-byte aligned.                                    */
 int clk_copy_stream(clk_ctx *ctx, void *dst, const void *src, uint64_t bytes, int shape, uint64_t *out_sum);
 
 #ifdef __cplusplus
