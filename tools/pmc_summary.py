@@ -73,13 +73,14 @@ def main():
     res["trace_ms"] = {k: {"calls": len(v), "mean_ms": statistics.mean(v), "min_ms": min(v)}
                        for k, v in durs.items()}
     counters = {}
-    for cname, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+    for cname, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write"), ("TCC_EA0_WRREQ_sum", "wrreq"),
+                       ("TCC_EA0_WRREQ_64B_sum", "wrreq")):
         p = find(os.path.join(out, sub), "*counter_collection.csv")
         if not p:
             continue
         per = {}
         for r in rows(p):
-            if r.get("Counter_Name") != cname:
+            if r.get("Counter_Name") not in (cname, cname.replace("_sum", "")):
                 continue
             n = short(r["Kernel_Name"])
             per.setdefault(n, []).append(float(r["Counter_Value"]))
@@ -100,6 +101,12 @@ def main():
             e["fetch_bytes_corrected"] = 2 * f * 1024
             e["write_bytes"] = w * 1024
             e["hbm_bytes_per_launch"] = 2 * f * 1024 + w * 1024
+        if "TCC_EA0_WRREQ_sum" in counters and "TCC_EA0_WRREQ_64B_sum" in counters:
+            q = sum(counters["TCC_EA0_WRREQ_sum"].get(k, 0.0) for k in ks)
+            q64 = sum(counters["TCC_EA0_WRREQ_64B_sum"].get(k, 0.0) for k in ks)
+            e["write_requests"] = q
+            e["write_requests_64B"] = q64
+            e["write_requests_partial"] = q - q64     # (MI355X_MICROARCH.md: partial-line writes cost a read-modify-write)
         res["elements"][el] = e
     with open(os.path.join(pdir, "%s_pmc.json" % wl), "w") as fh:
         json.dump(res, fh, indent=1)

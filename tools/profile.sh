@@ -20,4 +20,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch"
     python3 bench.py --steps 3 --warmup 1 $ARGS > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- \
     python3 bench.py --steps 3 --warmup 1 $ARGS > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
+# 4. the write requests by class (whole 64 B vs partial), own pass
+timeout -k 10 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d "$OUT/wrreq" -o run -- \
+    python3 bench.py --steps 3 --warmup 1 $ARGS > "$OUT/bench_wrreq.json" 2> "$OUT/bench_wrreq.err"
 python3 tools/pmc_summary.py "$OUT" "$TAG" "$WL" gpurun_out/profiles 20
