@@ -27,10 +27,11 @@ def env(extra=None):
     return e
 
 
-def run(mode, conf=None, defines=None, handlers=(), expr=None, timeout=300, cwd=None, extra_env=None):
+def run(mode, conf=None, defines=None, handlers=(), expr=None, timeout=300, cwd=None, extra_env=None, threads=0):
     """Run click-<mode> on a config file (or -e expr) with NAME=value
-    defines; returns (returncode, {handler: text}, stderr)."""
-    cmd = [binary(mode)]
+    defines (threads: click -j N); returns (returncode, {handler: text},
+    stderr)."""
+    cmd = [binary(mode)] + (["-j", str(threads)] if threads else [])
     if expr is not None:
         cmd += ["-e", expr]
     else:

@@ -12,6 +12,8 @@
 #                                         (--enable-skip-elements of the CPU ones)
 #   tools/click_scratch_build.sh parity   CPU classes + HIP-prefixed GPU classes
 #                                         (ComparePackets graphs)
+#   tools/click_scratch_build.sh cpu-mt / dropin-mt  the same with
+#                                         --enable-user-multithread (click -j N)
 #   tools/click_scratch_build.sh dropin-pg  the drop-in compiled with -pg (gprof's
 #                                         samples of Click and the adapter; the
 #                                         glue library is not sampled), symbols kept
@@ -33,6 +35,8 @@ case "$mode" in
 cpu) extra=() ;;
 dropin) extra=(--enable-hip "--enable-skip-elements=$DROPIN_SKIP") ;;
 dropin-pg) extra=(--enable-hip "--enable-skip-elements=$DROPIN_SKIP"); pg=(CXXFLAGS="-g -O2 -pg" CFLAGS="-g -O2 -pg") ;;
+cpu-mt) extra=(--enable-user-multithread) ;;
+dropin-mt) extra=(--enable-user-multithread --enable-hip "--enable-skip-elements=$DROPIN_SKIP") ;;
 dropin-prof)
     # the drop-in with tools/core_profile/preload_sampler.c linked in: with
     # SAMPLES=file it samples the main thread's PC (its own CPU-time timer,
@@ -49,7 +53,7 @@ log="$SCRATCH/$mode.log"
 mkdir -p "$SCRATCH"
 rm -rf "$tree"
 cp -r "$REF" "$tree"
-if [ "$mode" != cpu ]; then
+if [ "${mode#cpu}" = "$mode" ]; then
     [ -f "$REPO/click_amd/libclick_amd_cksum.so" ] || python3 -m click_amd.build
     cp -r "$REPO/click_integration/elements/hip" "$tree/elements/hip"
 fi
