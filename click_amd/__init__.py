@@ -176,8 +176,9 @@ class Context:
     def tune(self, **knobs):
         """Speed-only tuning (clk_ctx_tune): max_blocks, scatter_blocks,
         set_mode (-1 auto, 0 fused, 1 two-phase), stream_min, group,
-        set_chunks, read_shape (clk_read_stream, bench).  No setting changes
-        a result."""
+        set_chunks, read_shape (clk_read_stream, bench), frag_flat_min
+        (clk_ip_fragment's flat payload pass from this batch size).  No
+        setting changes a result."""
         for k, v in knobs.items():
             self._check(self.lib.clk_ctx_tune(self.h, _abi.TUNE[k], int(v)))
         return self

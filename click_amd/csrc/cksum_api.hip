@@ -27,6 +27,7 @@ struct clk_ctx {
     int scatter_blocks;  // grid cap of field_scatter_kernel: fewer, longer-lived waves
                          // (C3 scatter 0.57 vs 0.67 ms at 16K vs 64K blocks)
     uint64_t stream_min; // len[] batches of >= stream_min packets run by the packet-stream kernel
+    uint64_t frag_flat_min; // clk_ip_fragment: batches of >= this many packets use the flat payload pass
     int set_chunks;      // two-phase Set: packet ranges whose scatter overlaps the next range's compute
     int read_shape;      // clk_read_stream's load shape (CLK_TUNE_READ_SHAPE)
     hipStream_t side;    // the scatters' stream (created on first use)
@@ -384,6 +385,7 @@ int clk_ctx_create(int device, clk_ctx **out)
     c->ev_pass = c->ev_side = nullptr;
     c->scatter_blocks = 16384;
     c->stream_min = 65536;
+    c->frag_flat_min = 8192;
     c->force_group = 0;
     e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -471,6 +473,10 @@ int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value)
     case CLK_TUNE_READ_SHAPE:
         if (value < 0 || value > 5) break;
         ctx->read_shape = (int)value;
+        return CLK_SUCCESS;
+    case CLK_TUNE_FRAG_FLAT_MIN:
+        if (value < 0) break;
+        ctx->frag_flat_min = (uint64_t)value;
         return CLK_SUCCESS;
     case CLK_TUNE_GROUP:
         if (!(value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16 || value == 32 ||
@@ -716,7 +722,13 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, u
     const size_t pl = (b->n * 4 + 255) & ~size_t(255);
     const size_t tb = (((size_t)ntiles * 16 + 255) & ~size_t(255));
     const size_t ts_end = fused ? 256 + tb : 2 * pl + tb;
-    if ((r = ensure_scratch(ctx, ts_end + (out_frag_first ? 0 : b->n * 8)))) return r;
+    // FLAT: the fragments of plain-header packets written by frag_flat_kernel,
+    // from one 16 B record per fragment, [FragFlat x max_frags] at fx_at
+    const bool flat = fused && CLK_FRAG_FLAT && b->n >= ctx->frag_flat_min && out->max_frags &&
+                      out->max_frags <= (1ull << 32);
+    const size_t fx_at = (ts_end + (out_frag_first ? 0 : b->n * 8) + 255) & ~size_t(255);
+    if ((r = ensure_scratch(ctx, flat ? fx_at + out->max_frags * sizeof(clk::FragFlat)
+                                      : ts_end + (out_frag_first ? 0 : b->n * 8)))) return r;
     uint8_t *sc = (uint8_t *)ctx->scratch;
     uint32_t *pl_n = (uint32_t *)sc, *pl_b = (uint32_t *)(sc + pl);
     uint64_t *tile_sums = (uint64_t *)(sc + 2 * pl);
@@ -731,6 +743,7 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, u
     f.frag_len = out->frag_len;
     f.frag_src = out->frag_src;
     f.max_frags = out->frag_off ? out->max_frags : 0;
+    f.fx = flat ? (clk::FragFlat *)(sc + fx_at) : nullptr;
     if (fused) {
         clk::FragLookback lb;
         lb.ticket = (uint32_t *)sc;
@@ -744,9 +757,21 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, u
         e = hipMemsetAsync(sc, 0, 256 + (size_t)ntiles * 16, ctx->cur);
         if (e != hipSuccess)
             return hip_fail(ctx, e, "hipMemsetAsync");
-        hipLaunchKernelGGL(clk::frag_write_kernel<true>, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f,
-                           (const uint8_t *)nullptr, (const uint32_t *)nullptr, (const uint32_t *)nullptr,
-                           (const uint64_t *)nullptr, ffirst, lb);
+        if (!flat) {
+            hipLaunchKernelGGL((clk::frag_write_kernel<true, false>), dim3(ntiles), dim3(BLOCK), 0, ctx->cur,
+                               args_of(b), f, (const uint8_t *)nullptr, (const uint32_t *)nullptr,
+                               (const uint32_t *)nullptr, (const uint64_t *)nullptr, ffirst, lb);
+            return check_launch(ctx, "clk_ip_fragment");
+        }
+        hipLaunchKernelGGL((clk::frag_write_kernel<true, true>), dim3(ntiles), dim3(BLOCK), 0, ctx->cur,
+                           args_of(b), f, (const uint8_t *)nullptr, (const uint32_t *)nullptr,
+                           (const uint32_t *)nullptr, (const uint64_t *)nullptr, ffirst, lb);
+        const uint64_t nblk = ((out->max_frags + clk::FLAT_F - 1) / clk::FLAT_F + 3) / 4;   // 4 waves per block
+        if (nblk > 0x7FFFFFFFull)
+            return fail(ctx, CLK_EINVAL, "clk_ip_fragment: max_frags too large");
+        hipLaunchKernelGGL(clk::frag_flat_kernel, dim3((uint32_t)nblk), dim3(BLOCK), 0, ctx->cur, args_of(b),
+                           f.arena, f.arena_bytes, (const clk::FragFlat *)f.fx, f.max_frags,
+                           (const uint64_t *)totals);
         return check_launch(ctx, "clk_ip_fragment");
     }
     hipLaunchKernelGGL(clk::frag_plan_kernel, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f, out_port,

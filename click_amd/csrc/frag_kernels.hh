@@ -21,6 +21,13 @@
 //                      four unaligned 16 B loads per lane in flight, all
 //                      issued before the packet's stores; the next
 //                      packet's header is prefetched meanwhile.
+// FLAT (default when fragments are written): frag_write_kernel<true, true>
+// plans, scans and rewrites the first fragments' headers as above, but for
+// the packets without options it writes only the descriptors and a 16 B
+// record per appended fragment; frag_flat_kernel then writes those
+// fragments, headers included, as one flat copy over the arena (every line
+// written by one wave, 16 B-aligned stores).  Packets with options keep the
+// 16-lane group path.
 // Appended fragments are packed in packet order, as the reference pushes
 // them, so the arena layout equals the oracle's (oracle_ip_fragment_batch).
 #pragma once
@@ -45,7 +52,20 @@ struct FragArgs {
     uint32_t *frag_len;
     uint32_t *frag_src;
     uint64_t max_frags;
+    struct FragFlat *fx;        // FLAT: per appended fragment, the payload pass's record
 };
+
+// FLAT: what frag_flat_kernel needs of one appended fragment (16 B).  The
+// write kernel fills one for every fragment index below min(total,
+// max_frags): dlen 0 marks a fragment the write kernel wrote itself (copied
+// options) or that has no room; its arena offset keeps the records ordered.
+struct FragFlat {
+    uint64_t bp_dlen;           // arena offset (bits 0..47) | payload bytes << 48
+    uint32_t pkt;               // packet index
+    uint16_t fo;                // the fragment's ip_off, host order (ipfragmenter.cc:145-147)
+    uint16_t src;               // its payload's offset in the packet
+};
+constexpr uint64_t FLAT_BP = (1ull << 48) - 1;
 
 struct FragPlan {
     uint32_t port, first_len, hlen, out_hlen, step, nextra, bytes;
@@ -229,6 +249,9 @@ __device__ __forceinline__ u32x4 load16_guarded(uint64_t p, uint64_t hi)
 #ifndef CLK_FRAG_FUSED
 #define CLK_FRAG_FUSED 1       // one launch (plan + look-back scan + write) when fragments are written
 #endif
+#ifndef CLK_FRAG_FLAT
+#define CLK_FRAG_FLAT 1        // fused: plain-header packets' fragments written by frag_flat_kernel
+#endif
 #ifndef CLK_FRAG_HDR_FIRST
 #define CLK_FRAG_HDR_FIRST 0
 #endif
@@ -359,7 +382,7 @@ __device__ __forceinline__ void lb_store(uint64_t *p, uint64_t v)
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <bool FUSED>
+template <bool FUSED, bool FLAT = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FRAG_WPE))) frag_write_kernel(BatchArgs b, FragArgs f, const uint8_t *port,
                                                          const uint32_t *pl_n, const uint32_t *pl_b,
                                                          const uint64_t *tile_sums, uint64_t *out_frag_first,
@@ -585,6 +608,53 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
     for (uint32_t j = threadIdx.x; j < FRAG_TILE && tile + j < b.n; j += blockDim.x)
         out_frag_first[tile + j] = fbase + pn[j];
     const uint32_t lim = b.n - tile < FRAG_TILE ? (uint32_t)(b.n - tile) : FRAG_TILE;
+    if (FLAT) {
+        // the plain-header packets (first-fragment header rewritten by the
+        // prologue, original words in lhdr), a thread per packet: their
+        // descriptors and frag_flat_kernel's records; the 16-lane groups
+        // below take only the packets with options.  Packet t + 256k, so a
+        // wave's stores cover consecutive records
+#pragma unroll
+        for (int k = 0; k < FRAG_PER; k++) {
+            const uint32_t pk = threadIdx.x + 256u * k;
+            if (pk >= lim || lhdr[pk][0] == 0u)
+                continue;
+            const uint64_t i = tile + pk;
+            uint8_t *ip = b.base + pkt_off(b, i);
+            const uint32_t h0 = lhdr[pk][0], h1 = lhdr[pk][1];
+            const FragPlan p = frag_plan_words(ip, pkt_len(b, i), f.mtu, f.honor_df, h0, h1);   // hlen 20: no option read
+            const uint64_t fidx = fbase + pn[pk], bpos = bbase + pb[pk];
+            const uint32_t slot_f = slot16(20 + p.step);
+            lport[pk] = 0;                                 // not for the groups
+            if (!(fidx + p.nextra <= f.max_frags && bpos + p.bytes <= f.arena_bytes)) {
+                frag_restore_header(ip, lhdr[pk]);         // port CLK_FRAG_NOROOM, bytes kept
+                lb.out_port[i] = FRAG_PORT_NOROOM;
+                for (uint32_t q = 0; q < p.nextra && fidx + q < f.max_frags; q++)
+                    f.fx[fidx + q] = FragFlat{(bpos + (uint64_t)q * slot_f) & FLAT_BP, 0u, 0, 0};
+                continue;
+            }
+            // ntohs(ip_off) of the first fragment: MF set, DF cleared (112-118)
+            const uint32_t off_first = bswap16((((h1 >> 16) & ~0x40u) | 0x20u) & 0xFFFF);
+            const bool had_mf = (h1 >> 16) & 0x20;
+            const uint32_t pay0 = 20 + (uint32_t)p.first_dlen;
+            const int rem = p.in_dlen - p.first_dlen;
+            const uint32_t last = (uint32_t)rem - (p.nextra - 1) * p.step;
+            for (uint32_t q = 0; q < p.nextra; q++) {
+                const int off = p.first_dlen + (int)(q * p.step);
+                const uint32_t dlen = q + 1 < p.nextra ? p.step : last;
+                const uint64_t bp = bpos + (uint64_t)q * slot_f;
+                uint32_t fo = (off_first + ((uint32_t)off >> 3)) & 0xFFFF;                 // 145
+                if ((int)dlen + off >= p.in_dlen && !had_mf)                              // 146-147
+                    fo &= ~0x2000u;
+                f.frag_off[fidx + q] = bp;
+                f.frag_len[fidx + q] = 20 + dlen;
+                f.frag_src[fidx + q] = (uint32_t)i;
+                f.fx[fidx + q] = FragFlat{bp | (uint64_t)dlen << 48, (uint32_t)i, (uint16_t)fo,
+                                          (uint16_t)(pay0 + q * p.step)};
+            }
+        }
+        __syncthreads();                                   // lport
+    }
     auto next_j = [&](uint32_t j) {
         while (j < lim && lport[j] != 2)
             j += NG;
@@ -697,6 +767,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
                     frag_restore_header(ip, lhdr[j]);
                 (FUSED ? lb.out_port : (uint8_t *)port)[i] = FRAG_PORT_NOROOM;
             }
+            if (FLAT)                                      // nothing for the payload pass
+                for (uint32_t k = gl; k < nextra && fidx + k < f.max_frags; k += FRAG_G)
+                    f.fx[fidx + k] = FragFlat{(bpos + (uint64_t)k * slot_f) & FLAT_BP, 0u, 0, 0};
             j = jn;
             continue;
         }
@@ -741,6 +814,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
                 if (gl == 2)
                     h |= s << 16;                                           // 150
                 if (fits) {
+                    if (FLAT && gl == (k & (FRAG_G - 1)))
+                        f.fx[fidx + k] = FragFlat{bp & FLAT_BP, 0u, 0, 0};   // written here
                     if (gl < qw)
                         st_u32(f.arena + bp + 4 * gl, h);
                     if (gl == (k & (FRAG_G - 1))) {
@@ -802,6 +877,119 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
             }
         }
         j = jn;
+    }
+}
+
+// FLAT payload pass: the appended fragments of the plain-header packets,
+// headers included, as a flat copy of the arena.  One wave = FLAT_F
+// consecutive fragment records, whose slots are consecutive in the arena;
+// lane k < FLAT_F loads record k, the slot starts go to scalar registers,
+// and the wave's lanes take the 16 B chunks of the range in order (one
+// store instruction = 1 KB of contiguous arena, every store 16 B-aligned),
+// each chunk's record found by FLAT_F - 1 scalar compares and its fields
+// fetched from that record's lane.  No LDS, no barrier: a wave waits only
+// on its own records and loads.  Chunk 0 of a slot is header bytes 0-15
+// (the packet's rewritten first-fragment header with the fragment's
+// ip_len, ip_off, ip_sum: ipfragmenter.cc:140-150), chunk 1 the header's
+// last dword and the payload's first 12 bytes; bytes past the payload up to
+// the slot's end are 0, as frag_write_kernel writes them.
+#ifndef CLK_FRAG_FLAT_F
+#define CLK_FRAG_FLAT_F 8
+#endif
+#ifndef CLK_FRAG_FLAT_U
+#define CLK_FRAG_FLAT_U 4
+#endif
+constexpr uint32_t FLAT_F = CLK_FRAG_FLAT_F;     // fragment records per wave (<= 64)
+constexpr int FLAT_U = CLK_FRAG_FLAT_U;           // chunks per lane in flight
+static_assert(FLAT_F >= 1 && FLAT_F <= 64, "records per wave");
+
+__global__ void __launch_bounds__(256) frag_flat_kernel(BatchArgs b, uint8_t *arena, uint64_t arena_bytes,
+                                                        const FragFlat *fx, uint64_t max_frags,
+                                                        const uint64_t *totals)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t tot = totals[0];
+    const uint64_t nf = tot < max_frags ? tot : max_frags;
+    const uint64_t f0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64 * FLAT_F;
+    if (f0 >= nf)
+        return;                                       // wave-uniform
+    const uint32_t cnt = nf - f0 < FLAT_F ? (uint32_t)(nf - f0) : FLAT_F;
+    uint64_t bp = 0, ipa = 0;
+    uint32_t dlen = 0, src = 0, hi = 0, fo = 0;
+    if (lane < cnt) {
+        const FragFlat e = fx[f0 + lane];
+        bp = e.bp_dlen & FLAT_BP;
+        dlen = (uint32_t)(e.bp_dlen >> 48);
+        src = e.src;
+        fo = e.fo;
+        if (dlen && e.pkt < b.n) {
+            const uint32_t caplen = pkt_len(b, e.pkt);
+            const uint32_t fe = src + dlen;
+            ipa = (uint64_t)(b.base + pkt_off(b, e.pkt));
+            hi = fe < caplen ? fe : caplen;
+        }
+    }
+    const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bp >> 32), 0) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bp, 0);
+    const uint32_t slot = slot16(20 + dlen);
+    // a record this call did not write (a tile whose look-back failed)
+    // cannot send a store out of the arena
+    const bool ok = ipa != 0 && bp >= base && bp + slot <= arena_bytes;
+    const uint32_t stc = lane < cnt ? (uint32_t)((bp - base) >> 4) : 0xFFFFFFFFu;
+    const uint32_t endc = lane < cnt ? stc + (ok ? slot >> 4 : 0u) : 0u;
+    const uint32_t nchunks = (uint32_t)__builtin_amdgcn_readlane((int)endc, (int)cnt - 1);   // records in arena order
+    uint32_t sk[FLAT_F];
+#pragma unroll
+    for (uint32_t k = 1; k < FLAT_F; k++)
+        sk[k] = (uint32_t)__builtin_amdgcn_readlane((int)stc, (int)k);
+    typedef __attribute__((address_space(1))) u32x4_a4 g4;
+    // wave-uniform trip count: every lane takes part in the shuffles
+    for (uint32_t p0 = 0; p0 < nchunks; p0 += 64 * FLAT_U) {
+        const uint32_t c0 = p0 + lane;
+        u32x4 v[FLAT_U];
+        uint32_t x[FLAT_U], ss[FLAT_U], qq[FLAT_U];   // header dword 4; byte in the slot (~0u: none); ip_len | ip_off
+#pragma unroll
+        for (int u = 0; u < FLAT_U; u++) {
+            const uint32_t c = c0 + 64u * u;
+            uint32_t j = 0;
+#pragma unroll
+            for (uint32_t k = 1; k < FLAT_F; k++)
+                j += sk[k] <= c;
+            const uint64_t ip = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ipa >> 32), (int)j, 64) << 32) |
+                                (uint32_t)__shfl((int)(uint32_t)ipa, (int)j, 64);
+            const uint32_t st_j = (uint32_t)__shfl((int)stc, (int)j, 64);
+            const uint32_t end_j = (uint32_t)__shfl((int)endc, (int)j, 64);
+            const uint32_t src_j = (uint32_t)__shfl((int)src, (int)j, 64);
+            const uint32_t hi_j = (uint32_t)__shfl((int)hi, (int)j, 64);
+            qq[u] = (uint32_t)__shfl((int)(fo << 16 | (20 + dlen)), (int)j, 64);
+            const bool live = c < nchunks && c < end_j;
+            const uint32_t sb = 16 * (c - st_j);
+            ss[u] = live ? sb : 0xFFFFFFFFu;
+            x[u] = live && sb <= 16 ? ld_u32_unaligned((const uint8_t *)ip + 16) : 0u;
+            v[u] = !live ? u32x4{0, 0, 0, 0}
+                         : sb == 0 ? load16_rel((const uint8_t *)ip, 0, 20)
+                                   : load16_rel((const uint8_t *)ip, src_j + sb - 20, hi_j);
+        }
+#pragma unroll
+        for (int u = 0; u < FLAT_U; u++) {
+            if (ss[u] == 0xFFFFFFFFu)
+                continue;
+            u32x4 w = v[u];
+            if (ss[u] == 0) {
+                const uint32_t q = qq[u];
+                w[0] = (w[0] & 0xFFFF) | (bswap16(q & 0xFFFF) << 16);           // ip_len (148)
+                w[1] = (w[1] & 0xFFFF) | (bswap16(q >> 16) << 16);             // ip_off (145-147)
+                w[2] &= 0xFFFF;                                                 // ip_sum (149-150)
+                uint32_t sum = (x[u] & 0xFFFF) + (x[u] >> 16);
+#pragma unroll
+                for (int d = 0; d < 4; d++)
+                    sum += (w[d] & 0xFFFF) + (w[d] >> 16);
+                w[2] |= in_cksum_fold(sum) << 16;
+            } else if (ss[u] == 16) {
+                w[0] = x[u];
+            }
+            *(g4 *)(arena + base + 16ull * (c0 + 64u * u)) = w;
+        }
     }
 }
 

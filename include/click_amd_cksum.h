@@ -113,7 +113,7 @@ enum clk_tune_knob {
     CLK_TUNE_SET_CHUNKS = 6,          /* two-phase Set in this many packet ranges, each
                                          range's scatter on a side stream overlapping the
                                          next range's compute pass (1: one of each)       */
-    CLK_TUNE_READ_SHAPE = 7           /* clk_read_stream's load shape: 0 grid-stride, 8
+    CLK_TUNE_READ_SHAPE = 7,          /* clk_read_stream's load shape: 0 grid-stride, 8
                                          16 B loads per lane in flight, 8K workgroups;
                                          1 the same with 4 loads; 2 with 16 loads, 2K
                                          workgroups; 3 each wave 8 KiB contiguous per
@@ -123,6 +123,9 @@ enum clk_tune_knob {
                                          workgroup; 5 the same on 8K workgroups
                                          (bench: the best is the measured read
                                          ceiling)                                    */
+    CLK_TUNE_FRAG_FLAT_MIN = 8        /* clk_ip_fragment: batches of >= this many packets
+                                         write the fragments of plain-header packets in
+                                         a flat second pass (8192; 0: always)            */
 };
 int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value);
 /* Last error text for `ctx` (or for the calling thread when ctx == NULL). */

@@ -2,7 +2,9 @@
 the C ABI: the reference's own IPFragmenter-01/02 outputs, fuzzed batches
 against the oracle (ports, first-fragment rewrite in place, every appended
 fragment byte, descriptors), capacity limits, and a full-size batch whose
-fragments all pass CheckIPHeader and reassemble to the original payload."""
+fragments all pass CheckIPHeader and reassemble to the original payload.
+Every test runs on both write paths: the flat payload pass and the 16-lane
+groups (CLK_TUNE_FRAG_FLAT_MIN)."""
 import json
 import os
 
@@ -22,10 +24,12 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module")
-def ctx(torch):
+@pytest.fixture(scope="module", params=["flat", "groups"])
+def ctx(torch, request):
+    """Both write paths at every size: the flat payload pass
+    (frag_flat_kernel) for every batch, and the 16-lane groups only."""
     import click_amd
-    c = click_amd.Context(0)
+    c = click_amd.Context(0).tune(frag_flat_min=0 if request.param == "flat" else 1 << 62)
     yield c
     c.close()
 

@@ -88,6 +88,14 @@ VARIANTS = {
     "fu2": (["-DCLK_FRAG_U=2"], {}),
     "fg32": (["-DCLK_FRAG_G=32"], {}),
     "fw5u3": (["-DCLK_FRAG_WPE=5", "-DCLK_FRAG_U=3"], {}),
+    "flat0": (["-DCLK_FRAG_FLAT=0"], {}),            # payloads in frag_write_kernel (round 5)
+    "flatf16": (["-DCLK_FRAG_FLAT_F=16"], {}),
+    "flatf4": (["-DCLK_FRAG_FLAT_F=4"], {}),
+    "flatu2": (["-DCLK_FRAG_FLAT_U=2"], {}),
+    "flatu8": (["-DCLK_FRAG_FLAT_U=8"], {}),
+    "flatf16u8": (["-DCLK_FRAG_FLAT_F=16", "-DCLK_FRAG_FLAT_U=8"], {}),
+    "flatf16u8t512": (["-DCLK_FRAG_FLAT_F=16", "-DCLK_FRAG_FLAT_U=8", "-DCLK_FRAG_TILE=512"], {}),
+    "flatf32u8": (["-DCLK_FRAG_FLAT_F=32", "-DCLK_FRAG_FLAT_U=8"], {}),
 }
 
 
