@@ -769,8 +769,7 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, u
         const uint64_t nblk = ((out->max_frags + clk::FLAT_F - 1) / clk::FLAT_F + 3) / 4;   // 4 waves per block
         if (nblk > 0x7FFFFFFFull)
             return fail(ctx, CLK_EINVAL, "clk_ip_fragment: max_frags too large");
-        hipLaunchKernelGGL(clk::frag_flat_kernel, dim3((uint32_t)nblk), dim3(BLOCK), 0, ctx->cur, args_of(b),
-                           f.arena, f.arena_bytes, (const clk::FragFlat *)f.fx, f.max_frags,
+        hipLaunchKernelGGL(clk::frag_flat_kernel, dim3((uint32_t)nblk), dim3(BLOCK), 0, ctx->cur, args_of(b), f,
                            (const uint64_t *)totals);
         return check_launch(ctx, "clk_ip_fragment");
     }

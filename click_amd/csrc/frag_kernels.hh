@@ -252,6 +252,12 @@ __device__ __forceinline__ u32x4 load16_guarded(uint64_t p, uint64_t hi)
 #ifndef CLK_FRAG_FLAT
 #define CLK_FRAG_FLAT 1        // fused: plain-header packets' fragments written by frag_flat_kernel
 #endif
+#ifndef CLK_FRAG_FLAT_DESC
+#define CLK_FRAG_FLAT_DESC 0   // 1: the flat pass writes its fragments' descriptors (r06x: 1.5 % slower overall)
+#endif
+#ifndef CLK_FRAG_HDR_X4
+#define CLK_FRAG_HDR_X4 1      // fused plan: a packet's 20 header bytes in two loads, not five
+#endif
 #ifndef CLK_FRAG_HDR_FIRST
 #define CLK_FRAG_HDR_FIRST 0
 #endif
@@ -424,9 +430,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
             cl[k] = i < b.n ? pkt_len(b, i) : 0u;
             const bool rd = i < b.n && frag_reads_header(cl[k], f.mtu);   // caplen >= 20
             const uint8_t *ip = b.base + (i < b.n ? pkt_off(b, i) : 0);
+            if (HW == 5 && CLK_FRAG_HDR_X4) {          // bytes 0-15 in one load (unaligned mode), then 16-19
+                typedef u32x4 u32x4_a1 __attribute__((aligned(1)));
+                const u32x4 q = rd ? *(const __attribute__((address_space(1))) u32x4_a1 *)ip : u32x4{0, 0, 0, 0};
 #pragma unroll
-            for (int d = 0; d < HW; d++)
-                hw[k][d] = rd ? ld_u32_unaligned(ip + 4 * d) : 0u;
+                for (int d = 0; d < 4; d++)
+                    hw[k][d] = q[d];
+                hw[k][HW - 1] = rd ? ld_u32_unaligned(ip + 16) : 0u;
+            } else {
+#pragma unroll
+                for (int d = 0; d < HW; d++)
+                    hw[k][d] = rd ? ld_u32_unaligned(ip + 4 * d) : 0u;
+            }
         }
 #pragma unroll
         for (int k = 0; k < FRAG_PER; k++) {
@@ -646,9 +661,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
                 uint32_t fo = (off_first + ((uint32_t)off >> 3)) & 0xFFFF;                 // 145
                 if ((int)dlen + off >= p.in_dlen && !had_mf)                              // 146-147
                     fo &= ~0x2000u;
-                f.frag_off[fidx + q] = bp;
-                f.frag_len[fidx + q] = 20 + dlen;
-                f.frag_src[fidx + q] = (uint32_t)i;
+                if (!CLK_FRAG_FLAT_DESC) {                 // else frag_flat_kernel writes them
+                    f.frag_off[fidx + q] = bp;
+                    f.frag_len[fidx + q] = 20 + dlen;
+                    f.frag_src[fidx + q] = (uint32_t)i;
+                }
                 f.fx[fidx + q] = FragFlat{bp | (uint64_t)dlen << 48, (uint32_t)i, (uint16_t)fo,
                                           (uint16_t)(pay0 + q * p.step)};
             }
@@ -903,10 +920,11 @@ constexpr uint32_t FLAT_F = CLK_FRAG_FLAT_F;     // fragment records per wave (<
 constexpr int FLAT_U = CLK_FRAG_FLAT_U;           // chunks per lane in flight
 static_assert(FLAT_F >= 1 && FLAT_F <= 64, "records per wave");
 
-__global__ void __launch_bounds__(256) frag_flat_kernel(BatchArgs b, uint8_t *arena, uint64_t arena_bytes,
-                                                        const FragFlat *fx, uint64_t max_frags,
-                                                        const uint64_t *totals)
+__global__ void __launch_bounds__(256) frag_flat_kernel(BatchArgs b, FragArgs f, const uint64_t *totals)
 {
+    uint8_t *const arena = f.arena;
+    const uint64_t arena_bytes = f.arena_bytes, max_frags = f.max_frags;
+    const FragFlat *const fx = f.fx;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t tot = totals[0];
     const uint64_t nf = tot < max_frags ? tot : max_frags;
@@ -923,6 +941,11 @@ __global__ void __launch_bounds__(256) frag_flat_kernel(BatchArgs b, uint8_t *ar
         src = e.src;
         fo = e.fo;
         if (dlen && e.pkt < b.n) {
+            if (CLK_FRAG_FLAT_DESC) {                      // the descriptors: fragment q, pushed at ipfragmenter.cc:154
+                f.frag_off[f0 + lane] = bp;
+                f.frag_len[f0 + lane] = 20 + dlen;
+                f.frag_src[f0 + lane] = e.pkt;
+            }
             const uint32_t caplen = pkt_len(b, e.pkt);
             const uint32_t fe = src + dlen;
             ipa = (uint64_t)(b.base + pkt_off(b, e.pkt));

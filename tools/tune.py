@@ -96,6 +96,10 @@ VARIANTS = {
     "flatf16u8": (["-DCLK_FRAG_FLAT_F=16", "-DCLK_FRAG_FLAT_U=8"], {}),
     "flatf16u8t512": (["-DCLK_FRAG_FLAT_F=16", "-DCLK_FRAG_FLAT_U=8", "-DCLK_FRAG_TILE=512"], {}),
     "flatf32u8": (["-DCLK_FRAG_FLAT_F=32", "-DCLK_FRAG_FLAT_U=8"], {}),
+    "hx4off": (["-DCLK_FRAG_HDR_X4=0"], {}),
+    "hx4t512": (["-DCLK_FRAG_TILE=512"], {}),
+    "hx4w5": (["-DCLK_FRAG_WPE=5"], {}),
+    "descB": (["-DCLK_FRAG_FLAT_DESC=1"], {}),
 }
 
 
