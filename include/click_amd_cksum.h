@@ -330,7 +330,10 @@ int clk_ip_output_combo(clk_ctx *ctx, const clk_batch *batch, const clk_ip_out_c
  * fragments and arena bytes the batch needs; a packet whose fragments would
  * pass out->max_frags or out->arena_bytes is left whole (CLK_FRAG_NOROOM).
  * Domain guards (as the oracle): len_i < 20 with len_i > MTU -> port 1;
- * fragment bytes past len_i (ip_len > network_length) are written as 0. */
+ * fragment bytes past len_i (ip_len > network_length) are written as 0.
+ * Batches of at least CLK_TUNE_FRAG_FLAT_MIN packets (8192) that write
+ * fragments run two kernels (plan/scan, then the flat payload pass) and
+ * grow the context's device scratch by 16 B per out->max_frags. */
 #define CLK_FRAG_NOROOM 3
 #define CLK_FRAG_FAULT 0xFF
 typedef struct clk_frag_cfg {
