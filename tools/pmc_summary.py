@@ -36,7 +36,8 @@ ELEMENT_KERNELS = {
     "SetIPChecksum": ["ip_header_kernel<2"],
     "DecIPTTL": ["dec_ttl_kernel"],
     "IPOutputCombo": ["ip_out_kernel<2"],
-    "IPFragmenter": ["frag_plan_kernel", "frag_scan_kernel", "frag_write_kernel"],   # one launch (frag_write_kernel<true>) or three
+    # one launch (frag_write_kernel<true, false>), two (<true, true> + the flat pass) or three
+    "IPFragmenter": ["frag_plan_kernel", "frag_scan_kernel", "frag_write_kernel", "frag_flat_kernel"],
 }
 
 
@@ -107,6 +108,13 @@ def main():
             e["write_requests"] = q
             e["write_requests_64B"] = q64
             e["write_requests_partial"] = q - q64     # (MI355X_MICROARCH.md: partial-line writes cost a read-modify-write)
+        if len(ks) > 1:                          # each kernel's share
+            e["per_kernel"] = {k: {"duration_ms": statistics.mean(durs[k]),
+                                   "hbm_bytes": (2 * counters.get("FETCH_SIZE", {}).get(k, 0.0)
+                                                 + counters.get("WRITE_SIZE", {}).get(k, 0.0)) * 1024,
+                                   "write_requests_partial": (counters.get("TCC_EA0_WRREQ_sum", {}).get(k, 0.0)
+                                                              - counters.get("TCC_EA0_WRREQ_64B_sum", {}).get(k, 0.0))}
+                               for k in ks}
         res["elements"][el] = e
     with open(os.path.join(pdir, "%s_pmc.json" % wl), "w") as fh:
         json.dump(res, fh, indent=1)
