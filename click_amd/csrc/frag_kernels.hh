@@ -252,9 +252,6 @@ __device__ __forceinline__ u32x4 load16_guarded(uint64_t p, uint64_t hi)
 #ifndef CLK_FRAG_FLAT
 #define CLK_FRAG_FLAT 1        // fused: plain-header packets' fragments written by frag_flat_kernel
 #endif
-#ifndef CLK_FRAG_FLAT_DESC
-#define CLK_FRAG_FLAT_DESC 0   // 1: the flat pass writes its fragments' descriptors (r06x: 1.5 % slower overall)
-#endif
 #ifndef CLK_FRAG_HDR_X4
 #define CLK_FRAG_HDR_X4 1      // fused plan: a packet's 20 header bytes in two loads, not five
 #endif
@@ -661,11 +658,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
                 uint32_t fo = (off_first + ((uint32_t)off >> 3)) & 0xFFFF;                 // 145
                 if ((int)dlen + off >= p.in_dlen && !had_mf)                              // 146-147
                     fo &= ~0x2000u;
-                if (!CLK_FRAG_FLAT_DESC) {                 // else frag_flat_kernel writes them
-                    f.frag_off[fidx + q] = bp;
-                    f.frag_len[fidx + q] = 20 + dlen;
-                    f.frag_src[fidx + q] = (uint32_t)i;
-                }
+                f.frag_off[fidx + q] = bp;                 // (from the flat pass: 1.5 % slower overall, r06x)
+                f.frag_len[fidx + q] = 20 + dlen;
+                f.frag_src[fidx + q] = (uint32_t)i;
                 f.fx[fidx + q] = FragFlat{bp | (uint64_t)dlen << 48, (uint32_t)i, (uint16_t)fo,
                                           (uint16_t)(pay0 + q * p.step)};
             }
@@ -941,11 +936,6 @@ __global__ void __launch_bounds__(256) frag_flat_kernel(BatchArgs b, FragArgs f,
         src = e.src;
         fo = e.fo;
         if (dlen && e.pkt < b.n) {
-            if (CLK_FRAG_FLAT_DESC) {                      // the descriptors: fragment q, pushed at ipfragmenter.cc:154
-                f.frag_off[f0 + lane] = bp;
-                f.frag_len[f0 + lane] = 20 + dlen;
-                f.frag_src[f0 + lane] = e.pkt;
-            }
             const uint32_t caplen = pkt_len(b, e.pkt);
             const uint32_t fe = src + dlen;
             ipa = (uint64_t)(b.base + pkt_off(b, e.pkt));

@@ -99,7 +99,6 @@ VARIANTS = {
     "hx4off": (["-DCLK_FRAG_HDR_X4=0"], {}),
     "hx4t512": (["-DCLK_FRAG_TILE=512"], {}),
     "hx4w5": (["-DCLK_FRAG_WPE=5"], {}),
-    "descB": (["-DCLK_FRAG_FLAT_DESC=1"], {}),
 }
 
 
