@@ -36,7 +36,7 @@ CLK_GWOPT_OK = 0
 CLK_GWOPT_ERROR = 1
 # clk_tune_knob
 TUNE = {"max_blocks": 1, "scatter_blocks": 2, "set_mode": 3, "stream_min": 4, "group": 5, "set_chunks": 6,
-        "read_shape": 7, "frag_flat_min": 8}
+        "read_shape": 7, "frag_flat_min": 8, "frag_chunks": 9}
 
 
 class clk_batch(ctypes.Structure):

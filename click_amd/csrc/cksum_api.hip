@@ -28,6 +28,7 @@ struct clk_ctx {
                          // (C3 scatter 0.57 vs 0.67 ms at 16K vs 64K blocks)
     uint64_t stream_min; // len[] batches of >= stream_min packets run by the packet-stream kernel
     uint64_t frag_flat_min; // clk_ip_fragment: batches of >= this many packets use the flat payload pass
+    int frag_chunks;        // ... in this many tile ranges, each range's flat pass overlapping the next one's plan
     int set_chunks;      // two-phase Set: packet ranges whose scatter overlaps the next range's compute
     int read_shape;      // clk_read_stream's load shape (CLK_TUNE_READ_SHAPE)
     hipStream_t side;    // the scatters' stream (created on first use)
@@ -386,6 +387,7 @@ int clk_ctx_create(int device, clk_ctx **out)
     c->scatter_blocks = 16384;
     c->stream_min = 65536;
     c->frag_flat_min = 8192;
+    c->frag_chunks = 1;
     c->force_group = 0;
     e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -477,6 +479,10 @@ int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value)
     case CLK_TUNE_FRAG_FLAT_MIN:
         if (value < 0) break;
         ctx->frag_flat_min = (uint64_t)value;
+        return CLK_SUCCESS;
+    case CLK_TUNE_FRAG_CHUNKS:
+        if (value < 1 || value > 64) break;
+        ctx->frag_chunks = (int)value;
         return CLK_SUCCESS;
     case CLK_TUNE_GROUP:
         if (!(value == 0 || value == 1 || value == 2 || value == 4 || value == 8 || value == 16 || value == 32 ||
@@ -763,14 +769,41 @@ int clk_ip_fragment(clk_ctx *ctx, const clk_batch *b, const clk_frag_cfg *cfg, u
                                (const uint32_t *)nullptr, (const uint64_t *)nullptr, ffirst, lb);
             return check_launch(ctx, "clk_ip_fragment");
         }
-        hipLaunchKernelGGL((clk::frag_write_kernel<true, true>), dim3(ntiles), dim3(BLOCK), 0, ctx->cur,
-                           args_of(b), f, (const uint8_t *)nullptr, (const uint32_t *)nullptr,
-                           (const uint32_t *)nullptr, (const uint64_t *)nullptr, ffirst, lb);
-        const uint64_t nblk = ((out->max_frags + clk::FLAT_F - 1) / clk::FLAT_F + 3) / 4;   // 4 waves per block
-        if (nblk > 0x7FFFFFFFull)
-            return fail(ctx, CLK_EINVAL, "clk_ip_fragment: max_frags too large");
-        hipLaunchKernelGGL(clk::frag_flat_kernel, dim3((uint32_t)nblk), dim3(BLOCK), 0, ctx->cur, args_of(b), f,
-                           (const uint64_t *)totals);
+        // blocks of the flat pass for `frags` records: 4 waves of FLAT_F each
+        auto flat_blocks = [](uint64_t frags) {
+            const uint64_t nb = ((frags + clk::FLAT_F - 1) / clk::FLAT_F + 3) / 4;
+            return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(nb, 1u << 30));   // the kernel strides past it
+        };
+        const uint32_t nch = (uint32_t)std::min<uint64_t>(ctx->frag_chunks, ntiles / 2);
+        if (nch <= 1) {
+            hipLaunchKernelGGL((clk::frag_write_kernel<true, true>), dim3(ntiles), dim3(BLOCK), 0, ctx->cur,
+                               args_of(b), f, (const uint8_t *)nullptr, (const uint32_t *)nullptr,
+                               (const uint32_t *)nullptr, (const uint64_t *)nullptr, ffirst, lb);
+            hipLaunchKernelGGL(clk::frag_flat_kernel, dim3(flat_blocks(out->max_frags)), dim3(BLOCK), 0, ctx->cur,
+                               args_of(b), f, (const uint64_t *)nullptr, (const uint64_t *)totals);
+            return check_launch(ctx, "clk_ip_fragment");
+        }
+        // in tile ranges: range c's plan on this stream (its tiles take the
+        // next tickets and look back into the ranges before it), then its
+        // flat pass on the side stream, over the fragments between the
+        // inclusive prefixes of the tiles before and at its end, while range
+        // c + 1's plan runs here
+        if ((r = ensure_side(ctx))) return r;
+        const uint32_t per = (ntiles + nch - 1) / nch;
+        for (uint32_t t0 = 0; t0 < ntiles; t0 += per) {
+            const uint32_t t1 = std::min(ntiles, t0 + per);
+            hipLaunchKernelGGL((clk::frag_write_kernel<true, true>), dim3(t1 - t0), dim3(BLOCK), 0, ctx->cur,
+                               args_of(b), f, (const uint8_t *)nullptr, (const uint32_t *)nullptr,
+                               (const uint32_t *)nullptr, (const uint64_t *)nullptr, ffirst, lb);
+            (void)hipEventRecord(ctx->ev_pass, ctx->cur);
+            (void)hipStreamWaitEvent(ctx->side, ctx->ev_pass, 0);
+            const uint64_t est = (out->max_frags * (t1 - t0) + ntiles - 1) / ntiles;
+            hipLaunchKernelGGL(clk::frag_flat_kernel, dim3(flat_blocks(est)), dim3(BLOCK), 0, ctx->side, args_of(b), f,
+                               t0 ? (const uint64_t *)(lb.word + 2 * (t0 - 1)) : (const uint64_t *)nullptr,
+                               t1 < ntiles ? (const uint64_t *)(lb.word + 2 * (t1 - 1)) : (const uint64_t *)totals);
+        }
+        (void)hipEventRecord(ctx->ev_side, ctx->side);
+        (void)hipStreamWaitEvent(ctx->cur, ctx->ev_side, 0);
         return check_launch(ctx, "clk_ip_fragment");
     }
     hipLaunchKernelGGL(clk::frag_plan_kernel, dim3(ntiles), dim3(BLOCK), 0, ctx->cur, args_of(b), f, out_port,

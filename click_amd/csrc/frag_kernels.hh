@@ -915,17 +915,13 @@ constexpr uint32_t FLAT_F = CLK_FRAG_FLAT_F;     // fragment records per wave (<
 constexpr int FLAT_U = CLK_FRAG_FLAT_U;           // chunks per lane in flight
 static_assert(FLAT_F >= 1 && FLAT_F <= 64, "records per wave");
 
-__global__ void __launch_bounds__(256) frag_flat_kernel(BatchArgs b, FragArgs f, const uint64_t *totals)
+// Records [f0, f0 + FLAT_F) of [.., nf), by one wave.
+__device__ __forceinline__ void frag_flat_wave(const BatchArgs &b, const FragArgs &f, uint64_t f0, uint64_t nf)
 {
     uint8_t *const arena = f.arena;
-    const uint64_t arena_bytes = f.arena_bytes, max_frags = f.max_frags;
+    const uint64_t arena_bytes = f.arena_bytes;
     const FragFlat *const fx = f.fx;
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t tot = totals[0];
-    const uint64_t nf = tot < max_frags ? tot : max_frags;
-    const uint64_t f0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64 * FLAT_F;
-    if (f0 >= nf)
-        return;                                       // wave-uniform
     const uint32_t cnt = nf - f0 < FLAT_F ? (uint32_t)(nf - f0) : FLAT_F;
     uint64_t bp = 0, ipa = 0;
     uint32_t dlen = 0, src = 0, hi = 0, fo = 0;
@@ -1003,6 +999,24 @@ __global__ void __launch_bounds__(256) frag_flat_kernel(BatchArgs b, FragArgs f,
             }
             *(g4 *)(arena + base + 16ull * (c0 + 64u * u)) = w;
         }
+    }
+}
+
+// Records [lo, min(hi, max_frags)), lo and hi read from device words (a
+// tile's look-back word or totals; their tag bits masked): a wave per
+// FLAT_F records, the grid striding when the range is larger than it.
+__global__ void __launch_bounds__(256) frag_flat_kernel(BatchArgs b, FragArgs f, const uint64_t *lo_p,
+                                                        const uint64_t *hi_p)
+{
+    const uint64_t lo = lo_p ? (lo_p[0] & LB_VAL) : 0;
+    const uint64_t hv = hi_p[0] & LB_VAL;
+    const uint64_t nf = hv < f.max_frags ? hv : f.max_frags;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;; w += nwaves) {
+        const uint64_t f0 = lo + w * FLAT_F;
+        if (f0 >= nf)
+            return;                                   // wave-uniform
+        frag_flat_wave(b, f, f0, nf);
     }
 }
 

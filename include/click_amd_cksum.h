@@ -123,9 +123,12 @@ enum clk_tune_knob {
                                          workgroup; 5 the same on 8K workgroups
                                          (bench: the best is the measured read
                                          ceiling)                                    */
-    CLK_TUNE_FRAG_FLAT_MIN = 8        /* clk_ip_fragment: batches of >= this many packets
+    CLK_TUNE_FRAG_FLAT_MIN = 8,       /* clk_ip_fragment: batches of >= this many packets
                                          write the fragments of plain-header packets in
                                          a flat second pass (8192; 0: always)            */
+    CLK_TUNE_FRAG_CHUNKS = 9          /* ... in this many tile ranges, each range's flat
+                                         pass on a side stream overlapping the next
+                                         range's plan (1)                                 */
 };
 int clk_ctx_tune(clk_ctx *ctx, int knob, int64_t value);
 /* Last error text for `ctx` (or for the calling thread when ctx == NULL). */

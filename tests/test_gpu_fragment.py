@@ -3,8 +3,9 @@ the C ABI: the reference's own IPFragmenter-01/02 outputs, fuzzed batches
 against the oracle (ports, first-fragment rewrite in place, every appended
 fragment byte, descriptors), capacity limits, and a full-size batch whose
 fragments all pass CheckIPHeader and reassemble to the original payload.
-Every test runs on both write paths: the flat payload pass and the 16-lane
-groups (CLK_TUNE_FRAG_FLAT_MIN)."""
+Every test runs on each write path: the flat payload pass, the 16-lane
+groups (CLK_TUNE_FRAG_FLAT_MIN), and the flat pass in tile ranges on two
+streams (CLK_TUNE_FRAG_CHUNKS)."""
 import json
 import os
 
@@ -24,12 +25,14 @@ def torch():
     return t
 
 
-@pytest.fixture(scope="module", params=["flat", "groups"])
+@pytest.fixture(scope="module", params=["flat", "groups", "flat_ranges"])
 def ctx(torch, request):
-    """Both write paths at every size: the flat payload pass
-    (frag_flat_kernel) for every batch, and the 16-lane groups only."""
+    """Every write path at every size: the flat payload pass
+    (frag_flat_kernel) for every batch, the 16-lane groups only, and the
+    flat pass in 5 tile ranges overlapping the plans (batches of 10+ tiles)."""
     import click_amd
-    c = click_amd.Context(0).tune(frag_flat_min=0 if request.param == "flat" else 1 << 62)
+    c = click_amd.Context(0).tune(frag_flat_min=1 << 62 if request.param == "groups" else 0,
+                                  frag_chunks=5 if request.param == "flat_ranges" else 1)
     yield c
     c.close()
 
