@@ -16,6 +16,8 @@ reference's class names, and its results are compared with the stock build's
 Skipped when the binaries were not built."""
 import os
 
+import struct
+
 import numpy as np
 import pytest
 
@@ -52,6 +54,76 @@ def test_parity_graph_udp():
     assert rc == 0, err
     assert h["setcmp.diffs"] == "0" and h["chkcmp.diffs"] == "0", (h, err)
     assert h["cpucheck.drops"] == h["gpucheck.drops"] and int(h["cpucheck.drops"]) > 0, h
+
+
+def inet_cksum(b):
+    """RFC 1071 checksum of bytes (the value to store; test helper)."""
+    if len(b) & 1:
+        b += b"\0"
+    s = sum(struct.unpack(">%dH" % (len(b) // 2), b))
+    s = (s & 0xFFFF) + (s >> 16)
+    s += s >> 16
+    return ~s & 0xFFFF
+
+
+def icmp_pcap(path, seed, n):
+    """Ethernet frames of IPv4 packets for CheckICMPHeader's rules
+    (checkicmpheader.cc:89-138): ICMP types of each length class at lengths
+    around its bound (8, 36, exactly 20, exactly 8), other types at any
+    length including under 8, NOP options before the ICMP header on some,
+    a bad checksum on some, bytes past ip_len on some, a few not ICMP."""
+    rng = np.random.default_rng(seed)
+    bounds = {3: 36, 4: 36, 5: 36, 11: 36, 12: 36, 13: 20, 14: 20, 15: 8, 16: 8}
+    types = list(bounds) + [0, 8, 9, 10, 17, 18, 30, 255]
+    frames = []
+    for k in range(n):
+        t = types[int(rng.integers(len(types)))]
+        b = bounds.get(t, 8)
+        ilen = int(rng.choice([b - 1, b, b + 1, b + int(rng.integers(2, 120)), int(rng.integers(0, 8))]))
+        ilen = max(ilen, 0)
+        hl = 5 if rng.random() < 0.85 else int(rng.integers(6, 9))
+        icmp = bytearray(rng.integers(0, 256, ilen, dtype=np.uint8).tobytes())
+        if ilen >= 1:
+            icmp[0] = t
+        if ilen >= 4:
+            icmp[2:4] = b"\0\0"
+            if rng.random() < 0.85:
+                icmp[2:4] = struct.pack(">H", inet_cksum(bytes(icmp)))
+        ip = bytearray(4 * hl)
+        ip[0] = 0x40 | hl
+        ip[2:4] = struct.pack(">H", 4 * hl + ilen)
+        ip[8] = 64
+        ip[9] = 1 if rng.random() < 0.95 else 17
+        ip[12:16] = bytes([10, 0, 0, 1])
+        ip[16:20] = bytes([10, 0, 0, 2])
+        ip[20:] = b"\x01" * (4 * hl - 20)               # NOPs
+        ip[10:12] = struct.pack(">H", inet_cksum(bytes(ip)))
+        tail = rng.integers(0, 256, int(rng.integers(1, 6)), dtype=np.uint8).tobytes() if rng.random() < 0.1 else b""
+        eth = bytes.fromhex("0000c0ae67ef") + bytes(6) + b"\x08\x00"
+        frames.append(eth + bytes(ip) + bytes(icmp) + tail)
+    click_run.write_pcap(path, frames)
+
+
+def test_parity_graph_icmp(tmp_path):
+    """CheckICMPHeader's length classes and checksum on the GPU against the
+    reference element in one router: ComparePackets sees no difference, and
+    both drop the same packets for the same reasons (parity pinned by Click
+    itself, where the reference's tests hold no ICMP bytes)."""
+    n = 30000
+    icmp_pcap(str(tmp_path / "icmp.pcap"), 23, n)
+    rc, h, err = click_run.run("parity", "hip-parity-icmp.click", {"IN": str(tmp_path / "icmp.pcap"), "N": n},
+                               handlers=("cmp.diffs", "cmp.diff_details", "cpu.drops", "gpu.drops",
+                                         "cpu.drop_details", "gpu.drop_details"), timeout=120)
+    assert rc == 0, err
+    assert h["cmp.diffs"] == "0", (h, err)
+    assert h["cpu.drops"] == h["gpu.drops"] and 0 < int(h["cpu.drops"]) < n, h
+    said = {ln.split(" :: ")[0]: ln.split("failed: ")[-1] for ln in err.splitlines() if "header check failed" in ln}
+    assert said.get("cpu") and said.get("cpu") == said.get("gpu"), err    # the first drop's reason
+    # the reference's drop_details counters start uninitialised
+    # (checkicmpheader.cc:58, new atomic_uint32_t[NREASONS]): only the GPU
+    # element's are read, each reason seen, summing to the drops
+    det = [int(ln.split()[0]) for ln in h["gpu.drop_details"].splitlines()]
+    assert len(det) == 3 and all(x > 0 for x in det) and sum(det) == int(h["gpu.drops"]), h
 
 
 C1_HANDLERS = ("out.count", "local.count", "other.count", "bad.count", "redirect.count", "gw.drops", "ttl.drops",
