@@ -126,6 +126,82 @@ def test_parity_graph_icmp(tmp_path):
     assert len(det) == 3 and all(x > 0 for x in det) and sum(det) == int(h["gpu.drops"]), h
 
 
+def mix_pcap(path, seed, n):
+    """Ethernet frames of fuzzed IPv4 packets for hip-parity-mix.click: TCP
+    (th_off 0-15, payload 0-600 B), UDP, ICMP and protocol 47, ip_hl 5-7 with
+    NOP options, the IP, TCP and UDP checksums right on most, ip_len equal to,
+    above or below the captured length, some packets shorter than 40 B."""
+    rng = np.random.default_rng(seed)
+    frames = []
+    for k in range(n):
+        proto = int(rng.choice([6, 6, 6, 17, 1, 47]))
+        hl = 5 if rng.random() < 0.8 else int(rng.integers(6, 8))
+        if proto == 6:
+            doff = int(rng.integers(5, 11)) if rng.random() < 0.9 else int(rng.integers(0, 16))
+            l4 = bytearray(rng.integers(0, 256, max(4 * doff, 20) + int(rng.integers(0, 600)), dtype=np.uint8).tobytes())
+            l4[12] = (doff << 4) | (l4[12] & 0x0F)
+            sum_at = 16
+        elif proto == 17:
+            l4 = bytearray(rng.integers(0, 256, 8 + int(rng.integers(0, 400)), dtype=np.uint8).tobytes())
+            l4[4:6] = struct.pack(">H", len(l4))
+            sum_at = 6
+        else:
+            l4 = bytearray(rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8).tobytes())
+            sum_at = None
+        ip = bytearray(4 * hl)
+        ip[0] = 0x40 | hl
+        total = 4 * hl + len(l4)
+        ip[2:4] = struct.pack(">H", total)
+        ip[6] = 0x40 if rng.random() < 0.5 else 0
+        ip[8] = int(rng.integers(1, 255))
+        ip[9] = proto
+        ip[12:16] = bytes([10, 0, int(rng.integers(0, 4)), int(rng.integers(1, 255))])
+        ip[16:20] = bytes([192, 168, int(rng.integers(0, 4)), int(rng.integers(1, 255))])
+        ip[20:] = b"\x01" * (4 * hl - 20)
+        if sum_at is not None and len(l4) >= sum_at + 2:
+            l4[sum_at:sum_at + 2] = b"\0\0"
+            if rng.random() < 0.85:
+                ph = bytes(ip[12:20]) + bytes([0, proto]) + struct.pack(">H", len(l4))
+                c = inet_cksum(ph + bytes(l4))
+                l4[sum_at:sum_at + 2] = struct.pack(">H", c if (c or proto != 17) else 0xFFFF)
+        r = rng.random()
+        if r < 0.05:                                          # ip_len above the packet
+            ip[2:4] = struct.pack(">H", total + int(rng.integers(1, 40)))
+        elif r < 0.10 and len(l4) > 4:                        # ip_len below the packet
+            ip[2:4] = struct.pack(">H", total - int(rng.integers(1, min(len(l4), 40))))
+        ip[10:12] = b"\0\0"
+        if rng.random() < 0.9:
+            ip[10:12] = struct.pack(">H", inet_cksum(bytes(ip)))
+        pkt = bytes(ip) + bytes(l4)
+        if rng.random() < 0.03:                               # short packets
+            pkt = pkt[:4 * hl + int(rng.integers(0, 20))]     # (MarkIPHeader needs the IP header)
+        eth = bytes.fromhex("0000c0ae67ef") + bytes(6) + b"\x08\x00"
+        frames.append(eth + pkt)
+    click_run.write_pcap(path, frames)
+
+
+MIX_PAIRS = ("tcpchk", "tcpset", "ipset", "ip2", "combo")
+
+
+def test_parity_graph_mix(tmp_path):
+    """CheckTCPHeader, SetTCPChecksum(FIXOFF), SetIPChecksum, CheckIPHeader2
+    and IPInputCombo beside their GPU versions in one router over 20000
+    fuzzed packets: every pair's outputs equal packet by packet, in number,
+    bytes and annotations (ComparePackets)."""
+    n = 20000
+    mix_pcap(str(tmp_path / "mix.pcap"), 29, n)
+    hs = tuple("%s.diffs" % c for c in MIX_PAIRS) + tuple("k%d.count" % k for k in range(10))
+    rc, h, err = click_run.run("parity", "hip-parity-mix.click", {"IN": str(tmp_path / "mix.pcap"), "N": n},
+                               handlers=hs, timeout=120)
+    assert rc == 0, err[-2000:]
+    for c in MIX_PAIRS:
+        assert h["%s.diffs" % c] == "0", (c, h)
+    for k in range(0, 10, 2):
+        assert h["k%d.count" % k] == h["k%d.count" % (k + 1)], (k, h)
+        assert 0 < int(h["k%d.count" % k]) <= n, (k, h)
+    assert sum(int(h["k%d.count" % k]) < n for k in range(0, 10, 2)) >= 4, h   # drops seen on four of the five
+
+
 C1_HANDLERS = ("out.count", "local.count", "other.count", "bad.count", "redirect.count", "gw.drops", "ttl.drops",
                "frag.fragments", "frag.drops", "chk.drops")
 
