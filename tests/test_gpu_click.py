@@ -180,17 +180,19 @@ def mix_pcap(path, seed, n):
     click_run.write_pcap(path, frames)
 
 
-MIX_PAIRS = ("tcpchk", "tcpset", "ipset", "ip2", "combo")
+MIX_PAIRS = ("tcpchk", "tcpset", "ipset", "ip2", "combo", "outc")
 
 
 def test_parity_graph_mix(tmp_path):
-    """CheckTCPHeader, SetTCPChecksum(FIXOFF), SetIPChecksum, CheckIPHeader2
-    and IPInputCombo beside their GPU versions in one router over 20000
-    fuzzed packets: every pair's outputs equal packet by packet, in number,
-    bytes and annotations (ComparePackets)."""
+    """CheckTCPHeader, SetTCPChecksum(FIXOFF), SetIPChecksum, CheckIPHeader2,
+    IPInputCombo and IPOutputCombo beside their GPU versions in one router
+    over 20000 fuzzed packets: every pair's outputs equal packet by packet,
+    in number, bytes and header offsets (ComparePackets), IPOutputCombo's
+    other four outputs equal in number."""
     n = 20000
     mix_pcap(str(tmp_path / "mix.pcap"), 29, n)
-    hs = tuple("%s.diffs" % c for c in MIX_PAIRS) + tuple("k%d.count" % k for k in range(10))
+    hs = (tuple("%s.diffs" % c for c in MIX_PAIRS) + tuple("k%d.count" % k for k in range(10))
+          + tuple("o%d.count" % k for k in range(10)))
     rc, h, err = click_run.run("parity", "hip-parity-mix.click", {"IN": str(tmp_path / "mix.pcap"), "N": n},
                                handlers=hs, timeout=120)
     assert rc == 0, err[-2000:]
@@ -200,6 +202,9 @@ def test_parity_graph_mix(tmp_path):
         assert h["k%d.count" % k] == h["k%d.count" % (k + 1)], (k, h)
         assert 0 < int(h["k%d.count" % k]) <= n, (k, h)
     assert sum(int(h["k%d.count" % k]) < n for k in range(0, 10, 2)) >= 4, h   # drops seen on four of the five
+    for k in range(0, 10, 2):                            # IPOutputCombo's five outputs
+        assert h["o%d.count" % k] == h["o%d.count" % (k + 1)], (k, h)
+    assert all(int(h["o%d.count" % k]) > 0 for k in (0, 2, 6, 8)), h   # forwarded/fragments, PaintTee, TTL, DF
 
 
 C1_HANDLERS = ("out.count", "local.count", "other.count", "bad.count", "redirect.count", "gw.drops", "ttl.drops",
