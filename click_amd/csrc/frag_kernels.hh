@@ -911,6 +911,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CLK_FR
 #ifndef CLK_FRAG_FLAT_U
 #define CLK_FRAG_FLAT_U 4
 #endif
+#ifndef CLK_FRAG_FLAT_NT
+#define CLK_FRAG_FLAT_NT 1      // nontemporal arena stores (r06ag: the pass 6.71 vs 6.82 ms)
+#endif
 constexpr uint32_t FLAT_F = CLK_FRAG_FLAT_F;     // fragment records per wave (<= 64)
 constexpr int FLAT_U = CLK_FRAG_FLAT_U;           // chunks per lane in flight
 static_assert(FLAT_F >= 1 && FLAT_F <= 64, "records per wave");
@@ -997,7 +1000,10 @@ __device__ __forceinline__ void frag_flat_wave(const BatchArgs &b, const FragArg
             } else if (ss[u] == 16) {
                 w[0] = x[u];
             }
-            *(g4 *)(arena + base + 16ull * (c0 + 64u * u)) = w;
+            if (CLK_FRAG_FLAT_NT)
+                __builtin_nontemporal_store(w, (g4 *)(arena + base + 16ull * (c0 + 64u * u)));
+            else
+                *(g4 *)(arena + base + 16ull * (c0 + 64u * u)) = w;
         }
     }
 }

@@ -99,6 +99,7 @@ VARIANTS = {
     "hx4off": (["-DCLK_FRAG_HDR_X4=0"], {}),
     "hx4t512": (["-DCLK_FRAG_TILE=512"], {}),
     "hx4w5": (["-DCLK_FRAG_WPE=5"], {}),
+    "flatnt0": (["-DCLK_FRAG_FLAT_NT=0"], {}),
     "fch2": ([], {"frag_chunks": 2}),
     "fch4": ([], {"frag_chunks": 4}),
     "fch8": ([], {"frag_chunks": 8}),
