@@ -100,6 +100,7 @@ VARIANTS = {
     "hx4t512": (["-DCLK_FRAG_TILE=512"], {}),
     "hx4w5": (["-DCLK_FRAG_WPE=5"], {}),
     "flatnt0": (["-DCLK_FRAG_FLAT_NT=0"], {}),
+    "hdrnt": (["-DCLK_FRAG_HDR_NT=1"], {}),
     "fch2": ([], {"frag_chunks": 2}),
     "fch4": ([], {"frag_chunks": 4}),
     "fch8": ([], {"frag_chunks": 8}),
