@@ -191,3 +191,18 @@ def test_fragment_full_size(torch, ctx):
     assert torch.equal(orig[:, 1104:1480], p2)
     del arena, out
     torch.cuda.empty_cache()
+
+
+def test_fragment_tune_knobs_range(torch):
+    """CLK_TUNE_FRAG_CHUNKS takes 1..64 and CLK_TUNE_FRAG_FLAT_MIN any
+    count; anything else is CLK_EINVAL and leaves the setting as it was."""
+    import click_amd
+    from click_amd import ClickAmdError
+    c = click_amd.Context(0)
+    try:
+        c.tune(frag_chunks=64, frag_flat_min=0)
+        for bad in ({"frag_chunks": 0}, {"frag_chunks": 65}, {"frag_flat_min": -1}):
+            with pytest.raises(ClickAmdError):
+                c.tune(**bad)
+    finally:
+        c.close()
