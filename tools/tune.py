@@ -100,6 +100,8 @@ VARIANTS = {
     "hx4t512": (["-DCLK_FRAG_TILE=512"], {}),
     "hx4w5": (["-DCLK_FRAG_WPE=5"], {}),
     "flatnt0": (["-DCLK_FRAG_FLAT_NT=0"], {}),
+    "flatf12u6": (["-DCLK_FRAG_FLAT_F=12", "-DCLK_FRAG_FLAT_U=6"], {}),
+    "flatf6u3": (["-DCLK_FRAG_FLAT_F=6", "-DCLK_FRAG_FLAT_U=3"], {}),
     "hdrnt": (["-DCLK_FRAG_HDR_NT=1"], {}),
     "fch2": ([], {"frag_chunks": 2}),
     "fch4": ([], {"frag_chunks": 4}),
